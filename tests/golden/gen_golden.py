@@ -1,0 +1,221 @@
+"""Generate golden fixtures by running the REFERENCE implementation (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+Imports /root/reference/{models,train_eval}.py (read-only, never copied) with inert
+stub modules for the CPU/data/plot libraries it imports at module level but never
+uses on the training path (cv2, skimage, pycocotools, torchvision, seaborn).  The
+stubs fetch nothing.  Outputs small .npz fixtures next to this script; the GPU box
+and the product never read /root/reference.
+
+Fixtures (all with formula weights, oracle/weights.py):
+  fwd_c3k3.npz     reference EnhancedUNet (SMP-absent fallback, base 64, in 3, K 3):
+                   train-mode logits, BN running stats after, eval-mode logits
+  fwd_c3k2.npz     same with num_classes=2
+  in1_equiv.npz    1-channel input via the (x,0,0) equivalence (in 3 model, K 2)
+  loss_k3.npz      Trainer._compute_combined_loss (+parts) and d loss / d logits, K=3
+  loss_k2.npz      K=2 via a -inf third logit fed to the reference loss
+  step_c3k3.npz    one Trainer.train_epoch (warmup-stepped LR, clip, AdamW) on a B=2 batch
+  lr_traj.npz      train_model's per-epoch LR for E in {6, 50}
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+
+from oracle.weights import formula_state_dict  # noqa: E402
+from oracle.eunet_ref import state_spec  # noqa: E402
+
+
+def _install_stubs():
+    def mod(name, **attrs):
+        m = types.ModuleType(name)
+        for k, v in attrs.items():
+            setattr(m, k, v)
+        sys.modules[name] = m
+        return m
+
+    class _Any:
+        def __init__(self, *a, **k):
+            pass
+
+        def __getattr__(self, item):
+            return _Any()
+
+        def __call__(self, *a, **k):
+            return _Any()
+
+    mod("cv2")
+    sk = mod("skimage")
+    sk.measure = mod("skimage.measure")
+    sk.feature = mod("skimage.feature", peak_local_max=lambda *a, **k: None)
+    pc = mod("pycocotools")
+    pc.mask = mod("pycocotools.mask")
+    pc.coco = mod("pycocotools.coco", COCO=_Any)
+    pc.cocoeval = mod("pycocotools.cocoeval", COCOeval=_Any)
+    tv = mod("torchvision")
+    tv.transforms = mod("torchvision.transforms", Compose=_Any, ToTensor=_Any, Normalize=_Any)
+    mod("seaborn")
+
+
+def _import_reference():
+    _install_stubs()
+    sys.path.insert(0, REF)
+    import models as ref_models  # noqa
+    import train_eval as ref_te  # noqa
+    assert not ref_models.SMP_AVAILABLE, "fixtures pin the SMP-absent fallback"
+    return ref_models, ref_te
+
+
+def _load_formula(model, base, in_ch, K, dtype=torch.float32):
+    sd = formula_state_dict(state_spec(base, in_ch, K))
+    ref_sd = model.state_dict()
+    assert list(ref_sd.keys()) == list(sd.keys()), "state_dict schema mismatch"
+    new = {}
+    for k, v in sd.items():
+        if k.endswith("num_batches_tracked"):
+            new[k] = torch.tensor(0, dtype=torch.long)
+        else:
+            new[k] = torch.from_numpy(np.asarray(v)).to(dtype).reshape(ref_sd[k].shape)
+    model.load_state_dict(new)
+
+
+def _inputs(B, C, H, W, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, C, H, W, generator=g)
+    m = torch.randint(0, K, (B, H, W), generator=g)
+    return x, m
+
+
+def _bn_stats(model):
+    return {k: v.detach().numpy().copy() for k, v in model.state_dict().items()
+            if k.endswith("running_mean") or k.endswith("running_var")}
+
+
+def gen_forward(ref_models, K, fname):
+    torch.manual_seed(0)
+    model = ref_models.get_model("enhanced_unet", num_classes=K, device="cpu")
+    _load_formula(model, 64, 3, K)
+    x, _ = _inputs(2, 3, 32, 32, K, seed=11)
+    model.train()
+    with torch.no_grad():
+        out_train = model(x)
+    stats = _bn_stats(model)
+    model.eval()
+    with torch.no_grad():
+        out_eval = model(x)
+    np.savez_compressed(os.path.join(HERE, fname), x=x.numpy(), out_train=out_train.numpy(),
+                        out_eval=out_eval.numpy(),
+                        **{"bn:" + k: v for k, v in stats.items()})
+
+
+def gen_in1(ref_models):
+    model = ref_models.get_model("enhanced_unet", num_classes=2, device="cpu")
+    _load_formula(model, 64, 3, 2)
+    g = torch.Generator().manual_seed(21)
+    x1 = torch.rand(2, 1, 32, 32, generator=g)
+    x3 = torch.cat([x1, torch.zeros_like(x1), torch.zeros_like(x1)], 1)
+    model.train()
+    with torch.no_grad():
+        out = model(x3)
+    np.savez_compressed(os.path.join(HERE, "in1_equiv.npz"), x1=x1.numpy(), out_train=out.numpy())
+
+
+def gen_loss(ref_te, K, fname):
+    tr = ref_te.Trainer(torch.nn.Linear(1, 1), "cpu", "enhanced_unet", total_epochs=50)
+    g = torch.Generator().manual_seed(31 + K)
+    logits = (torch.randn(K, 24, 20, generator=g) * 2.0).requires_grad_(True)
+    target = torch.randint(0, K, (24, 20), generator=g)
+    if K == 3:
+        feed = logits
+    else:  # K=2 semantics: third logit at -inf
+        feed = torch.cat([logits, torch.full((1, 24, 20), float("-inf"))], 0)
+    lg = feed.unsqueeze(0)
+    tg = target.unsqueeze(0)
+    focal = tr.focal_loss(lg, tg)
+    dice = tr.dice_loss(lg, tg, num_classes=3)
+    tv = tr.tversky_loss(lg, tg, num_classes=3)
+    total = tr._compute_combined_loss(feed, target)
+    total.backward()
+    np.savez_compressed(os.path.join(HERE, fname), logits=logits.detach().numpy(),
+                        target=target.numpy(), total=total.item(), focal=focal.item(),
+                        dice=dice.item(), tversky=tv.item(), grad=logits.grad.numpy())
+
+
+def gen_step(ref_models, ref_te):
+    model = ref_models.get_model("enhanced_unet", num_classes=3, device="cpu")
+    _load_formula(model, 64, 3, 3)
+    x, m = _inputs(2, 3, 32, 32, 3, seed=41)
+    batch = {"images": x, "batch_items": [{"semantic_mask": m[i]} for i in range(2)]}
+    tr = ref_te.Trainer(model, "cpu", "enhanced_unet", total_epochs=50)
+    tr.warmup_scheduler.step()  # train_model epoch 0 (train_eval.py:1104-1105)
+    lr = tr.optimizer.param_groups[0]["lr"]
+    loss = tr.train_epoch([batch])
+    sd = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    grads = {k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
+    np.savez_compressed(os.path.join(HERE, "step_c3k3.npz"), x=x.numpy(), m=m.numpy(), lr=lr,
+                        loss=loss, **_summaries("post", sd), **_summaries("grad", grads))
+
+
+def _summaries(tag, tensors, full_below=8192, n_sample=64):
+    """Full tensor when small; else sum / L2 norm / 64 samples at fixed indices."""
+    out = {}
+    for k, v in tensors.items():
+        v = np.asarray(v, dtype=np.float64)
+        if v.size <= full_below:
+            out[f"{tag}:{k}"] = v
+        else:
+            flat = v.reshape(-1)
+            idx = sample_indices(k, flat.size, n_sample)
+            out[f"{tag}_sum:{k}"] = flat.sum()
+            out[f"{tag}_norm:{k}"] = np.sqrt((flat * flat).sum())
+            out[f"{tag}_idx:{k}"] = idx
+            out[f"{tag}_val:{k}"] = flat[idx]
+    return out
+
+
+def sample_indices(key, n, k):
+    from oracle.weights import uniform01
+    return np.unique((uniform01("idx:" + key, k) * n).astype(np.int64))
+
+
+def gen_lr(ref_te):
+    out = {}
+    for E in (6, 50):
+        tr = ref_te.Trainer(torch.nn.Linear(1, 1), "cpu", "enhanced_unet", total_epochs=E)
+        lrs = []
+        for epoch in range(E):
+            if epoch < tr.warmup_epochs:
+                tr.warmup_scheduler.step()
+            else:
+                tr.scheduler.step()
+            lrs.append(tr.optimizer.param_groups[0]["lr"])
+        out[f"E{E}"] = np.array(lrs)
+    np.savez_compressed(os.path.join(HERE, "lr_traj.npz"), **out)
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    ref_models, ref_te = _import_reference()
+    gen_forward(ref_models, 3, "fwd_c3k3.npz")
+    gen_forward(ref_models, 2, "fwd_c3k2.npz")
+    gen_in1(ref_models)
+    gen_loss(ref_te, 3, "loss_k3.npz")
+    gen_loss(ref_te, 2, "loss_k2.npz")
+    gen_step(ref_models, ref_te)
+    gen_lr(ref_te)
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
