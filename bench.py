@@ -1,0 +1,166 @@
+"""Benchmark of the MI355X Enhanced-UNet training step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Workload (BASELINE.json configs[2], the metric's config): base_ch=64,
+1x1024x1024 synthetic bright-field tiles, 1-ch -> 2-class, batch 4 per GPU,
+bf16 activations / MFMA (fp32 params, BN stats, loss, AdamW).  A "step" is one
+full Trainer step (forward, fused loss, backward, bucketed RCCL all-reduce when
+N>1, clip_grad_norm_, AdamW, loss.item()).  Inputs are resident in HBM before
+the timed region.  value = images processed by all ranks / max-over-ranks time.
+
+Also reported on the same JSON line:
+  roofline     -- the dominant kernel family (conv3x3 implicit-GEMM fwd/dgrad),
+                  algorithmic FLOPs / its summed launch time, measured with HIP
+                  events on the launch stream over the timed region, vs the
+                  gfx950 dense MFMA peak of the dtype;
+  cpu_baseline -- the oracle (PyTorch CPU restatement of the reference step)
+                  on the host cores, bounded sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "enhanced-unet_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training images/sec at 1024×1024 1-ch→2-cls, 1/2/4/8 MI355X; Dice vs CPU ref"
+PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X_MICROARCH.md dense MFMA peaks
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=4, help="images per GPU")
+    ap.add_argument("--base", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-size", type=int, default=1024, help="CPU baseline sample: one B=1 step at this size")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Oracle train step on the host CPU: one image, B=1 (bounded ~10-30 s)."""
+    from oracle import eunet_ref as R
+    from eunet import synth
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    S = R.formula_weights(args.base, 1, 2, dtype=torch.float32)
+    tr = R.OracleTrainer(S, total_epochs=50)
+    xw, mw = synth.batch(1, 64, 64, start_index=0)
+    tr.step(xw, mw)  # warm-up (allocator / oneDNN init), not timed
+    x, m = synth.batch(1, args.cpu_size, args.cpu_size, start_index=0)
+    t0 = time.perf_counter()
+    tr.step(x, m)
+    dt = time.perf_counter() - t0
+    scale = (args.cpu_size / args.size) ** 2  # images of the benchmark size per sample
+    return {"value": round(scale / dt, 5), "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"1 oracle train step (PyTorch CPU fp32 restatement of Trainer.train_epoch), B=1, "
+                      f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from eunet import synth, kprof
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+
+    torch.manual_seed(0)
+    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=args.base, dtype=args.dtype).to(dev)
+    tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
+    tr.epoch_lr_step(0)
+    if world > 1:
+        from eunet.dp import DataParallel
+        tr.dp = DataParallel(model)
+    x, m = synth.batch(args.batch, args.size, args.size, start_index=rank * args.batch, num_classes=2,
+                       in_channels=1, device=dev)
+    for _ in range(args.warmup):
+        tr.step(x, m)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    with kprof.KernelTimer() as timer:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.step(x, m)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ks = timer.summary()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    imgs = world * args.batch * args.steps
+    fam = ks.get("conv3x3_fwd", {"ms": float("nan"), "flops": 0.0, "launches": 0})
+    achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12 if fam["ms"] else None
+    peak = PEAK_TFLOPS[args.dtype]
+    roof = {"kernel": "conv3x3_fwd_kernel (implicit-GEMM MFMA, fwd + dgrad launches)", "bound": "mfma",
+            "achieved": round(achieved, 2) if achieved else None, "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+            "launches_per_step": fam["launches"] // max(1, args.steps),
+            "kernel_ms_per_step": round(fam["ms"] / args.steps, 3)}
+    if "conv3x3_wgrad" in ks:
+        wg = ks["conv3x3_wgrad"]
+        roof["wgrad_tflops"] = round(wg["flops"] / (wg["ms"] * 1e-3) / 1e12, 2)
+        roof["wgrad_ms_per_step"] = round(wg["ms"] / args.steps, 3)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    from oracle.eunet_ref import flops_per_pixel
+    step_flops = flops_per_pixel(args.base, 1, 2) * args.size * args.size * args.batch
+    line = {
+        "metric": METRIC,
+        "value": round(imgs / elapsed, 3),
+        "unit": "img/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic bright-field tiles (eunet.synth, seeded), random-init weights",
+        "config": {"workload": f"base_ch={args.base}, 1x{args.size}x{args.size} 1-ch->2-cls, batch "
+                               f"{args.batch}/GPU, {args.dtype} (BASELINE configs[2]; configs[3] at N=8)",
+                   "global_batch": world * args.batch, "image_size": args.size, "parallelism": f"dp{world}"},
+        "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,894 @@
+// Memory-bound kernels of the hot path (HBM-bound; NHWC, 16-byte vectors):
+//   enc1.0 direct conv (Cin <= 4), BatchNorm statistics finalisation,
+//   BN+ReLU fused into MaxPool / bilinear Upsample / dec1 1x1 consumers,
+//   and their backward counterparts.
+// Reference sites: models.py:203 (enc1.0), 214-215 (pool, upsample),
+// 212/236 (dec1), 220-224 (BN+ReLU), autograd of all of them.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int STH = 8, STW = 32;  // same pixel tiling as conv3x3 (stats rows agree)
+
+bool act_ok(const eunet_act* a) {
+  return a && a->ptr && a->n > 0 && a->h > 0 && a->w > 0 && a->c > 0 && a->coff >= 0 &&
+         a->coff + a->c <= a->ctot && (a->dtype == EUNET_F32 || a->dtype == EUNET_BF16);
+}
+int e16(int dt) { return dt == EUNET_BF16 ? 8 : 4; }
+bool vec_ok(const eunet_act* a) {
+  const int E = e16(a->dtype);
+  return a->c % E == 0 && a->ctot % E == 0 && a->coff % E == 0;
+}
+
+// ---------------------------------------------------------------------------
+// enc1.0: direct 3x3 conv for Cin <= 4, 64 output channels per block.y
+// ---------------------------------------------------------------------------
+struct SmallArgs {
+  const void* x; int N, H, W, xct, xco, cin;
+  const float* w; const float* b;
+  void* y; int yct, yco, cout;
+  float* stats; int tx, ty, ntiles;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
+  __shared__ float xs[(STH + 2) * (STW + 2) * 4];
+  __shared__ float ws[64 * 4 * 9];
+  __shared__ float red[4][64];
+  __shared__ float meanb[64], sums[64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tile = blockIdx.x, tpi = a.tx * a.ty;
+  const int n = tile / tpi, trem = tile - n * tpi;
+  const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
+  const int co0 = blockIdx.y * 64;
+  const int cin = a.cin;
+  for (int i = tid; i < (STH + 2) * (STW + 2) * cin; i += NT) {
+    const int hp = i / cin, ci = i - hp * cin;
+    const int hy = hp / (STW + 2), hx = hp - hy * (STW + 2);
+    const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+    float v = 0.f;
+    if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+      v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
+    xs[hp * 4 + ci] = v;
+  }
+  for (int i = tid; i < 64 * cin * 9; i += NT) {
+    const int co = i / (cin * 9), r = i - co * cin * 9;
+    ws[co * 36 + r] = (co0 + co < a.cout) ? a.w[(long long)(co0 + co) * cin * 9 + r] : 0.f;
+  }
+  __syncthreads();
+  const int r = tid / STW, c = tid - r * STW;
+  const int yy = y0 + r, xx = x0 + c;
+  const bool pv = yy < a.H && xx < a.W;
+  float acc[64];
+#pragma unroll
+  for (int co = 0; co < 64; ++co) acc[co] = (a.b != nullptr && co0 + co < a.cout) ? a.b[co0 + co] : 0.f;
+  for (int ci = 0; ci < cin; ++ci) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - ky * 3;
+      const float v = xs[((r + ky) * (STW + 2) + c + kx) * 4 + ci];
+#pragma unroll
+      for (int co = 0; co < 64; ++co) acc[co] = fmaf(ws[co * 36 + ci * 9 + t], v, acc[co]);
+    }
+  }
+  if (pv) {
+    T* yp = (T*)a.y + ((long long)(n * a.H + yy) * a.W + xx) * a.yct + a.yco + co0;
+    const int nco = min(64, a.cout - co0);
+    constexpr int E = Vec16<T>::N;
+    if (nco == 64 && ((a.yct | a.yco) % E) == 0) {
+#pragma unroll
+      for (int u = 0; u < 64 / E; ++u) *(uint4*)(yp + u * E) = Vec16<T>::pack(acc + u * E);
+    } else {
+      for (int co = 0; co < nco; ++co) Elem<T>::st(yp + co, acc[co]);
+    }
+  }
+  if (a.stats == nullptr) return;
+  float v[64];
+#pragma unroll
+  for (int co = 0; co < 64; ++co) v[co] = pv ? acc[co] : 0.f;
+  float s = wave_transpose_reduce64(v);
+  red[wv][lane] = s;
+  __syncthreads();
+  const float cnt = (float)(min(STH, a.H - y0) * min(STW, a.W - x0));
+  if (tid < 64) {
+    sums[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    meanb[tid] = sums[tid] / cnt;
+  }
+  __syncthreads();
+  const float sum_tile = sums[lane];
+#pragma unroll
+  for (int co = 0; co < 64; ++co) {
+    const float d = acc[co] - meanb[co];
+    v[co] = pv ? d * d : 0.f;
+  }
+  s = wave_transpose_reduce64(v);
+  __syncthreads();
+  red[wv][lane] = s;
+  __syncthreads();
+  if (tid < 64 && co0 + tid < a.cout) {
+    a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum_tile;
+    a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+    if (blockIdx.y == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
+  }
+}
+
+struct SmallWgArgs {
+  const void* x; int N, H, W, xct, xco, cin;
+  const void* dy; int dct, dco, cout;
+  float* dw; float* db;
+  int tx, ty, ntiles, per_split;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
+  __shared__ float xs[(STH + 2) * (STW + 2) * 4];
+  __shared__ float ds[STH * STW][65];
+  const int tid = threadIdx.x, co = tid & 63, tg = tid >> 6;
+  const int split = blockIdx.x, co0 = blockIdx.y * 64;
+  const int t_begin = split * a.per_split, t_end = min(a.ntiles, t_begin + a.per_split);
+  const int tpi = a.tx * a.ty, cin = a.cin;
+  float acc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  float dbacc = 0.f;
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
+    __syncthreads();
+    for (int i = tid; i < (STH + 2) * (STW + 2) * cin; i += NT) {
+      const int hp = i / cin, ci = i - hp * cin;
+      const int hy = hp / (STW + 2), hx = hp - hy * (STW + 2);
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      float v = 0.f;
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+        v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
+      xs[hp * 4 + ci] = v;
+    }
+    for (int i = tid; i < STH * STW * 64; i += NT) {
+      const int px = i >> 6, cc = i & 63;
+      const int r = px / STW, c = px - r * STW;
+      const int yy = y0 + r, xx = x0 + c;
+      float v = 0.f;
+      if (yy < a.H && xx < a.W && co0 + cc < a.cout)
+        v = Elem<T>::ld((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co0 + cc);
+      ds[px][cc] = v;
+    }
+    __syncthreads();
+    for (int px = 0; px < STH * STW; ++px) {
+      const float g = ds[px][co];
+      const int r = px / STW, c = px - r * STW;
+      if (tg == 0) dbacc += g;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int t = tg + 4 * k;
+        if (t < 9) {
+          const int ky = t / 3, kx = t - ky * 3;
+          const float* xp = xs + ((r + ky) * (STW + 2) + c + kx) * 4;
+#pragma unroll
+          for (int ci = 0; ci < 4; ++ci)
+            if (ci < cin) acc[k][ci] = fmaf(g, xp[ci], acc[k][ci]);
+        }
+      }
+    }
+  }
+  if (co0 + co >= a.cout) return;
+  float* out = a.dw + (long long)split * a.cout * 9 * cin;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int t = tg + 4 * k;
+    if (t < 9)
+      for (int ci = 0; ci < cin; ++ci) out[((long long)(co0 + co) * 9 + t) * cin + ci] = acc[k][ci];
+  }
+  if (a.db != nullptr && tg == 0) a.db[(long long)split * a.cout + co0 + co] = dbacc;
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm statistics: Chan-combine per-tile (sum, M2, count) in fp64
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void bn_finalize_kernel(const float* st, int tiles, int C, const float* gamma,
+                                                         const float* beta, float eps, float mom, float* rm,
+                                                         float* rv, float* mean_o, float* invstd_o, float* scale_o,
+                                                         float* shift_o) {
+  __shared__ double sh[NT];
+  __shared__ double shb[2];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const float* cnt = st + (long long)2 * C * tiles;
+  double n = 0.0, s = 0.0;
+  for (int t = tid; t < tiles; t += NT) {
+    n += (double)cnt[t];
+    s += (double)st[((long long)t * 2) * C + c];
+  }
+  auto block_sum = [&](double v) -> double {
+    sh[tid] = v;
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+      if (tid < o) sh[tid] += sh[tid + o];
+      __syncthreads();
+    }
+    double r = sh[0];
+    __syncthreads();
+    return r;
+  };
+  n = block_sum(n);
+  s = block_sum(s);
+  const double mean = s / n;
+  double m2 = 0.0;
+  for (int t = tid; t < tiles; t += NT) {
+    const double nb = (double)cnt[t];
+    if (nb > 0.0) {
+      const double mb = (double)st[((long long)t * 2) * C + c] / nb;
+      m2 += (double)st[((long long)t * 2 + 1) * C + c] + nb * (mb - mean) * (mb - mean);
+    }
+  }
+  m2 = block_sum(m2);
+  (void)shb;
+  if (tid == 0) {
+    const double var_b = m2 / n;
+    const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
+    const double istd = 1.0 / sqrt(var_b + (double)eps);
+    const double sc = (double)gamma[c] * istd;
+    if (mean_o) mean_o[c] = (float)mean;
+    if (invstd_o) invstd_o[c] = (float)istd;
+    if (scale_o) scale_o[c] = (float)sc;
+    if (shift_o) shift_o[c] = (float)((double)beta[c] - mean * sc);
+    if (rm) rm[c] = (float)((1.0 - mom) * (double)rm[c] + mom * mean);
+    if (rv) rv[c] = (float)((1.0 - mom) * (double)rv[c] + mom * var_u);
+  }
+}
+
+__global__ void bn_eval_affine_kernel(int C, const float* g, const float* b, const float* rm, const float* rv,
+                                      float eps, float* sc, float* sh) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float s = g[c] / sqrtf(rv[c] + eps);
+  sc[c] = s;
+  sh[c] = b[c] - rm[c] * s;
+}
+
+// ---------------------------------------------------------------------------
+// BN+ReLU -> (skip activation) + MaxPool2d(2)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void bnrelu_pool_kernel(const T* y, int N, int H, int W, int C, int yct, int yco, const float* sc,
+                                   const float* sh, T* act, int act_ct, int act_co, T* pool, int pct, int pco) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, Ho = H / 2, Wo = W / 2;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)N * Ho * Wo * U;
+  if (id >= total) return;
+  const int u = (int)(id % U);
+  long long p = id / U;
+  const int xo = (int)(p % Wo); p /= Wo;
+  const int yo = (int)(p % Ho);
+  const int n = (int)(p / Ho);
+  const int c = u * E;
+  float s[E], t[E], m[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s[j] = sc[c + j]; t[j] = sh[c + j]; m[j] = -INFINITY; }
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const long long pix = (long long)(n * H + 2 * yo + dy) * W + 2 * xo + dx;
+      float f[E];
+      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), f);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        f[j] = fmaxf(fmaf(f[j], s[j], t[j]), 0.f);
+        m[j] = fmaxf(m[j], f[j]);
+      }
+      if (act != nullptr) *(uint4*)(act + pix * act_ct + act_co + c) = Vec16<T>::pack(f);
+    }
+  const long long po = (long long)(n * Ho + yo) * Wo + xo;
+  *(uint4*)(pool + po * pct + pco + c) = Vec16<T>::pack(m);
+}
+
+// BN+ReLU -> bilinear x2 upsample (align_corners=False)
+template <typename T>
+__global__ void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco, const float* sc,
+                                 const float* sh, T* out, int oct, int oco) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)N * H2 * W2 * U;
+  if (id >= total) return;
+  const int u = (int)(id % U);
+  long long p = id / U;
+  const int ox = (int)(p % W2); p /= W2;
+  const int oy = (int)(p % H2);
+  const int n = (int)(p / H2);
+  const int c = u * E;
+  int y0, y1, x0, x1;
+  float ly, lx;
+  up2_src(oy, h, y0, y1, ly);
+  up2_src(ox, w, x0, x1, lx);
+  const int ys[2] = {y0, y1}, xs[2] = {x0, x1};
+  const float wy[2] = {1.f - ly, ly}, wx[2] = {1.f - lx, lx};
+  float s[E], t[E], acc[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s[j] = sc[c + j]; t[j] = sh[c + j]; acc[j] = 0.f; }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    float row[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) row[j] = 0.f;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float f[E];
+      const long long pix = (long long)(n * h + ys[a]) * w + xs[b];
+      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), f);
+#pragma unroll
+      for (int j = 0; j < E; ++j) row[j] = fmaf(wx[b], fmaxf(fmaf(f[j], s[j], t[j]), 0.f), row[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) acc[j] = fmaf(wy[a], row[j], acc[j]);
+  }
+  const long long po = (long long)(n * H2 + oy) * W2 + ox;
+  *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(acc);
+}
+
+// BN+ReLU -> 1x1 conv (C -> K <= 3), fp32 NHWC output
+template <typename T>
+__global__ void bnrelu_conv1x1_kernel(const T* y, long long P, int C, int yct, int yco, const float* sc,
+                                      const float* sh, const float* w, const float* b, int K, float* z) {
+  constexpr int E = Vec16<T>::N;
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float acc[3] = {0.f, 0.f, 0.f};
+  for (int c = 0; c < C; c += E) {
+    float f[E];
+    Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float a = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < K) acc[k] = fmaf(w[k * C + c + j], a, acc[k]);
+    }
+  }
+  for (int k = 0; k < K; ++k) z[p * K + k] = acc[k] + b[k];
+}
+
+// ---------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------
+constexpr int BWD_PIX = 1024;  // pixels per reduction tile
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
+                                                           long long P, int C, const float* mean, const float* istd,
+                                                           const float* gamma, const float* beta, float* part) {
+  constexpr int E = Vec16<T>::N;
+  __shared__ float red[2][NT][E];
+  const int U = C / E;
+  const int tid = threadIdx.x;
+  const int slots = NT / U;  // U <= NT required (C <= 2048 bf16)
+  const int u = tid % U, sl = tid / U;
+  const int c = u * E;
+  float s1[E], s2[E], mu[E], is[E], ga[E], be[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    s1[j] = 0.f; s2[j] = 0.f;
+    if (sl < slots) { mu[j] = mean[c + j]; is[j] = istd[c + j]; ga[j] = gamma[c + j]; be[j] = beta[c + j]; }
+  }
+  const long long p0 = (long long)blockIdx.x * BWD_PIX;
+  const long long p1 = min(P, p0 + BWD_PIX);
+  if (sl < slots) {
+    for (long long p = p0 + sl; p < p1; p += slots) {
+      float gf[E], yf[E];
+      Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
+      Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), yf);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float xh = (yf[j] - mu[j]) * is[j];
+        const float gg = (fmaf(ga[j], xh, be[j]) > 0.f) ? gf[j] : 0.f;
+        s1[j] += gg;
+        s2[j] = fmaf(gg, xh, s2[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) { red[0][tid][j] = s1[j]; red[1][tid][j] = s2[j]; }
+  __syncthreads();
+  if (sl == 0) {
+    for (int k = 1; k < slots; ++k) {
+#pragma unroll
+      for (int j = 0; j < E; ++j) { s1[j] += red[0][k * U + u][j]; s2[j] += red[1][k * U + u][j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      part[((long long)blockIdx.x * 2 + 0) * C + c + j] = s1[j];
+      part[((long long)blockIdx.x * 2 + 1) * C + c + j] = s2[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void colsum_kernel(const float* part, int rows, int cols, int ld, float* out) {
+  __shared__ double sh[4][64];
+  const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (col < cols)
+    for (int r = rg; r < rows; r += 4) s += (double)part[(long long)r * ld + col];
+  sh[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && col < cols) out[col] = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
+}
+
+template <typename T, typename TO>
+__global__ void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco, long long P, int C,
+                                    const float* mean, const float* istd, const float* gamma, const float* beta,
+                                    const float* dbeta, const float* dgamma, TO* gy, int oct, int oco) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= P * U) return;
+  const int u = (int)(id % U);
+  const long long p = id / U;
+  const int c = u * E;
+  const float inv_n = 1.f / (float)P;
+  float gf[E], yf[E], o[E];
+  Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
+  Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), yf);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const float xh = (yf[j] - mean[c + j]) * istd[c + j];
+    const float gg = (fmaf(gamma[c + j], xh, beta[c + j]) > 0.f) ? gf[j] : 0.f;
+    o[j] = gamma[c + j] * istd[c + j] * (gg - dbeta[c + j] * inv_n - xh * dgamma[c + j] * inv_n);
+  }
+  *(uint4*)(gy + p * oct + oco + c) = Vec16<T>::pack(o);
+}
+
+template <typename T>
+__global__ void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct, int gpco,
+                                    const T* gs, int gsct, int gsco, T* go, int goct, int goco, int N, int H, int W,
+                                    int C) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, Ho = H / 2, Wo = W / 2;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * Ho * Wo * U) return;
+  const int u = (int)(id % U);
+  long long p = id / U;
+  const int xo = (int)(p % Wo); p /= Wo;
+  const int yo = (int)(p % Ho);
+  const int n = (int)(p / Ho);
+  const int c = u * E;
+  float a[4][E], best[E], gpv[E];
+  int arg[E];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long pix = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+    Vec16<T>::unpack(*(const uint4*)(act + pix * act_ct + act_co + c), a[k]);
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    best[j] = a[0][j];
+    arg[j] = 0;
+  }
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < E; ++j)
+      if (a[k][j] > best[j] || (a[k][j] != a[k][j])) { best[j] = a[k][j]; arg[j] = k; }
+  Vec16<T>::unpack(*(const uint4*)(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c), gpv);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const long long pix = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+    float o[E];
+    if (gs != nullptr) Vec16<T>::unpack(*(const uint4*)(gs + pix * gsct + gsco + c), o);
+    else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) o[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
+    *(uint4*)(go + pix * goct + goco + c) = Vec16<T>::pack(o);
+  }
+}
+
+// adjoint of the x2 bilinear taps; per low-res row y the contributing
+// high-res rows are 2y-1 .. 2y+2
+__device__ __forceinline__ float up2_adj_w(int o, int in, int i) {
+  int i0, i1;
+  float l1;
+  up2_src(o, in, i0, i1, l1);
+  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+template <typename T, typename TO>
+__global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N, int h, int w, int C) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * h * w * U) return;
+  const int u = (int)(id % U);
+  long long p = id / U;
+  const int x = (int)(p % w); p /= w;
+  const int y = (int)(p % h);
+  const int n = (int)(p / h);
+  const int c = u * E;
+  float acc[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) acc[j] = 0.f;
+  for (int oy = 2 * y - 1; oy <= 2 * y + 2; ++oy) {
+    if (oy < 0 || oy >= H2) continue;
+    const float wy = up2_adj_w(oy, h, y);
+    if (wy == 0.f) continue;
+    for (int ox = 2 * x - 1; ox <= 2 * x + 2; ++ox) {
+      if (ox < 0 || ox >= W2) continue;
+      const float wx = up2_adj_w(ox, w, x);
+      if (wx == 0.f) continue;
+      float f[E];
+      Vec16<T>::unpack(*(const uint4*)(g + ((long long)(n * H2 + oy) * W2 + ox) * gct + gco + c), f);
+      const float ww = wy * wx;
+#pragma unroll
+      for (int j = 0; j < E; ++j) acc[j] = fmaf(ww, f[j], acc[j]);
+    }
+  }
+  *(uint4*)(o + ((long long)(n * h + y) * w + x) * oct + oco + c) = Vec16<TO>::pack(acc);
+}
+
+// fp32 K-channel (K <= 4) upsample backward for the head: g [N,2h,2w,K] -> o [N,h,w,K]
+__global__ void up_bwd_small_kernel(const float* g, float* o, int N, int h, int w, int K) {
+  const int H2 = 2 * h, W2 = 2 * w;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * h * w) return;
+  const int x = (int)(id % w);
+  const int y = (int)((id / w) % h);
+  const int n = (int)(id / ((long long)w * h));
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int oy = 2 * y - 1; oy <= 2 * y + 2; ++oy) {
+    if (oy < 0 || oy >= H2) continue;
+    const float wy = up2_adj_w(oy, h, y);
+    if (wy == 0.f) continue;
+    for (int ox = 2 * x - 1; ox <= 2 * x + 2; ++ox) {
+      if (ox < 0 || ox >= W2) continue;
+      const float wx = up2_adj_w(ox, w, x);
+      if (wx == 0.f) continue;
+      const float* gp = g + ((long long)(n * H2 + oy) * W2 + ox) * K;
+      for (int k = 0; k < K; ++k) acc[k] = fmaf(wy * wx, gp[k], acc[k]);
+    }
+  }
+  for (int k = 0; k < K; ++k) o[id * K + k] = acc[k];
+}
+
+// dec1 backward: gact = W^T gz; per-tile partials of gW [K][C] and gb [K]
+template <typename T>
+__global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P, int C, int yct, int yco,
+                                                         const float* sc, const float* sh, const float* w, int K,
+                                                         const float* gz, T* ga, int gct, int gco, float* part) {
+  constexpr int E = Vec16<T>::N;
+  __shared__ float acc_s[3 * 256 + 3];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int stride = K * C + K;
+  for (int i = tid; i < stride; i += NT) acc_s[i] = 0.f;
+  __syncthreads();
+  const long long p = (long long)blockIdx.x * NT + tid;
+  const bool pv = p < P;
+  float g[3] = {0.f, 0.f, 0.f};
+  if (pv)
+    for (int k = 0; k < K; ++k) g[k] = gz[p * K + k];
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    float a[64];
+#pragma unroll
+    for (int u = 0; u < 64 / E; ++u) {
+      const int c = c0 + u * E;
+      float f[E];
+      if (pv && c < C) {
+        Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+#pragma unroll
+        for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) f[j] = 0.f;
+      }
+      float go[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        a[u * E + j] = f[j];
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) s = fmaf(w[k * C + c + j], g[k], s);
+        go[j] = s;
+      }
+      if (pv && c < C) *(uint4*)(ga + p * gct + gco + c) = Vec16<T>::pack(go);
+    }
+    for (int k = 0; k < K; ++k) {
+      float v[64];
+#pragma unroll
+      for (int j = 0; j < 64; ++j) v[j] = a[j] * g[k];
+      const float s = wave_transpose_reduce64(v);
+      if (c0 + lane < C) atomicAdd(&acc_s[k * C + c0 + lane], s);
+    }
+  }
+  for (int k = 0; k < K; ++k) {
+    const float s = wave_sum(g[k]);
+    if (lane == 0) atomicAdd(&acc_s[K * C + k], s);
+  }
+  __syncthreads();
+  for (int i = tid; i < stride; i += NT) part[(long long)blockIdx.x * stride + i] = acc_s[i];
+}
+
+}  // namespace
+
+// ===========================================================================
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, hipStream_t s) {
+  EUNET_REQUIRE(part && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
+  colsum_kernel<<<cdiv(cols, 64), NT, 0, s>>>(part, rows, cols, ld, out);
+  EUNET_LAUNCH_CHECK("colsum");
+  return EUNET_OK;
+}
+
+extern "C" {
+
+int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
+
+int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, const eunet_act* y, float* stats,
+                         void* stream) {
+  EUNET_REQUIRE(act_ok(x) && act_ok(y) && w, "conv_small_fwd: bad args");
+  EUNET_REQUIRE(x->c <= 4 && x->dtype == y->dtype, "conv_small_fwd: Cin <= 4 and equal dtypes required");
+  EUNET_REQUIRE(x->n == y->n && x->h == y->h && x->w == y->w, "conv_small_fwd: spatial mismatch");
+  SmallArgs a;
+  a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
+  a.w = w; a.b = bias;
+  a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
+  a.stats = stats; a.tx = cdiv(x->w, STW); a.ty = cdiv(x->h, STH); a.ntiles = x->n * a.tx * a.ty;
+  dim3 grid(a.ntiles, cdiv(y->c, 64));
+  if (x->dtype == EUNET_BF16)
+    conv_small_fwd_kernel<bf16_t><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  else
+    conv_small_fwd_kernel<float><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  EUNET_LAUNCH_CHECK("conv_small_fwd");
+  return EUNET_OK;
+}
+
+int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
+  EUNET_REQUIRE(act_ok(dy) && nsplit, "conv_small_wgrad_splits: bad args");
+  const int ntiles = dy->n * cdiv(dy->h, STH) * cdiv(dy->w, STW);
+  int s = cdiv(1024, cdiv(dy->c, 64));
+  s = s > ntiles ? ntiles : (s < 1 ? 1 : s);
+  const int per = cdiv(ntiles, s);
+  *nsplit = cdiv(ntiles, per);
+  return EUNET_OK;
+}
+
+int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
+                           void* stream) {
+  EUNET_REQUIRE(act_ok(x) && act_ok(dy) && dw_part && nsplit > 0, "conv_small_wgrad: bad args");
+  EUNET_REQUIRE(x->c <= 4 && x->dtype == dy->dtype, "conv_small_wgrad: Cin <= 4, equal dtypes");
+  SmallWgArgs a;
+  a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
+  a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
+  a.dw = dw_part; a.db = db_part;
+  a.tx = cdiv(x->w, STW); a.ty = cdiv(x->h, STH); a.ntiles = x->n * a.tx * a.ty;
+  a.per_split = cdiv(a.ntiles, nsplit);
+  EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv_small_wgrad: nsplit mismatch");
+  dim3 grid(nsplit, cdiv(dy->c, 64));
+  if (x->dtype == EUNET_BF16)
+    conv_small_wgrad_kernel<bf16_t><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  else
+    conv_small_wgrad_kernel<float><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  EUNET_LAUNCH_CHECK("conv_small_wgrad");
+  return EUNET_OK;
+}
+
+int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, const float* beta, float eps,
+                      float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
+                      float* shift, void* stream) {
+  EUNET_REQUIRE(stats && tiles > 0 && c > 0 && gamma && beta, "bn_finalize: bad args");
+  bn_finalize_kernel<<<c, NT, 0, (hipStream_t)stream>>>(stats, tiles, c, gamma, beta, eps, momentum, run_mean,
+                                                        run_var, mean, invstd, scale, shift);
+  EUNET_LAUNCH_CHECK("bn_finalize");
+  return EUNET_OK;
+}
+
+int eunet_bn_eval_affine(int c, const float* gamma, const float* beta, const float* run_mean, const float* run_var,
+                         float eps, float* scale, float* shift, void* stream) {
+  EUNET_REQUIRE(c > 0 && gamma && beta && run_mean && run_var && scale && shift, "bn_eval_affine: bad args");
+  bn_eval_affine_kernel<<<cdiv(c, 256), 256, 0, (hipStream_t)stream>>>(c, gamma, beta, run_mean, run_var, eps,
+                                                                        scale, shift);
+  EUNET_LAUNCH_CHECK("bn_eval_affine");
+  return EUNET_OK;
+}
+
+int eunet_bnrelu_pool(const eunet_act* y, const float* scale, const float* shift, const eunet_act* act,
+                      const eunet_act* pooled, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(pooled) && scale && shift && vec_ok(y) && vec_ok(pooled),
+                "bnrelu_pool: bad args");
+  EUNET_REQUIRE(y->h % 2 == 0 && y->w % 2 == 0, "bnrelu_pool: H and W must be even");
+  EUNET_REQUIRE(pooled->h == y->h / 2 && pooled->w == y->w / 2 && pooled->c == y->c && pooled->n == y->n,
+                "bnrelu_pool: pooled shape");
+  if (act) EUNET_REQUIRE(act_ok(act) && vec_ok(act) && act->h == y->h && act->w == y->w && act->c == y->c,
+                         "bnrelu_pool: act shape");
+  const int E = e16(y->dtype);
+  const long long total = (long long)y->n * (y->h / 2) * (y->w / 2) * (y->c / E);
+  const unsigned g = (unsigned)((total + 255) / 256);
+  if (y->dtype == EUNET_BF16)
+    bnrelu_pool_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)y->ptr, y->n, y->h, y->w, y->c, y->ctot, y->coff, scale, shift,
+        act ? (bf16_t*)act->ptr : nullptr, act ? act->ctot : 0, act ? act->coff : 0, (bf16_t*)pooled->ptr,
+        pooled->ctot, pooled->coff);
+  else
+    bnrelu_pool_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>(
+        (const float*)y->ptr, y->n, y->h, y->w, y->c, y->ctot, y->coff, scale, shift,
+        act ? (float*)act->ptr : nullptr, act ? act->ctot : 0, act ? act->coff : 0, (float*)pooled->ptr,
+        pooled->ctot, pooled->coff);
+  EUNET_LAUNCH_CHECK("bnrelu_pool");
+  return EUNET_OK;
+}
+
+int eunet_bnrelu_upsample(const eunet_act* y, const float* scale, const float* shift, const eunet_act* out,
+                          void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(out) && scale && shift && vec_ok(y) && vec_ok(out), "bnrelu_upsample: bad args");
+  EUNET_REQUIRE(out->h == 2 * y->h && out->w == 2 * y->w && out->c == y->c && out->n == y->n &&
+                    out->dtype == y->dtype,
+                "bnrelu_upsample: shape");
+  const int E = e16(y->dtype);
+  const long long total = (long long)out->n * out->h * out->w * (y->c / E);
+  const unsigned g = (unsigned)((total + 255) / 256);
+  if (y->dtype == EUNET_BF16)
+    bnrelu_up_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, y->n, y->h, y->w, y->c,
+                                                                   y->ctot, y->coff, scale, shift,
+                                                                   (bf16_t*)out->ptr, out->ctot, out->coff);
+  else
+    bnrelu_up_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)y->ptr, y->n, y->h, y->w, y->c,
+                                                                  y->ctot, y->coff, scale, shift, (float*)out->ptr,
+                                                                  out->ctot, out->coff);
+  EUNET_LAUNCH_CHECK("bnrelu_upsample");
+  return EUNET_OK;
+}
+
+int eunet_bnrelu_conv1x1(const eunet_act* y, const float* scale, const float* shift, const float* w, const float* b,
+                         int k, float* z, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && vec_ok(y) && scale && shift && w && b && z && k >= 1 && k <= 3,
+                "bnrelu_conv1x1: bad args");
+  const long long P = (long long)y->n * y->h * y->w;
+  const unsigned g = (unsigned)((P + 255) / 256);
+  if (y->dtype == EUNET_BF16)
+    bnrelu_conv1x1_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
+                                                                        y->coff, scale, shift, w, b, k, z);
+  else
+    bnrelu_conv1x1_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
+                                                                       y->coff, scale, shift, w, b, k, z);
+  EUNET_LAUNCH_CHECK("bnrelu_conv1x1");
+  return EUNET_OK;
+}
+
+int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles) {
+  EUNET_REQUIRE(act_ok(y) && tiles, "bn_bwd_tiles: bad args");
+  const long long P = (long long)y->n * y->h * y->w;
+  *tiles = (int)((P + BWD_PIX - 1) / BWD_PIX);
+  return EUNET_OK;
+}
+
+int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
+                        const float* gamma, const float* beta, float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(g) && act_ok(y) && vec_ok(g) && vec_ok(y) && mean && invstd && gamma && beta && part,
+                "bn_bwd_reduce: bad args");
+  EUNET_REQUIRE(g->dtype == y->dtype && g->c == y->c && g->n == y->n && g->h == y->h && g->w == y->w,
+                "bn_bwd_reduce: shape mismatch");
+  EUNET_REQUIRE(y->c / e16(y->dtype) <= NT, "bn_bwd_reduce: too many channels");
+  const long long P = (long long)y->n * y->h * y->w;
+  const unsigned tiles = (unsigned)((P + BWD_PIX - 1) / BWD_PIX);
+  if (y->dtype == EUNET_BF16)
+    bn_bwd_reduce_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
+        gamma, beta, part);
+  else
+    bn_bwd_reduce_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>(
+        (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
+        gamma, beta, part);
+  EUNET_LAUNCH_CHECK("bn_bwd_reduce");
+  return EUNET_OK;
+}
+
+int eunet_colsum(const float* part, int rows, int cols, float* out, void* stream) {
+  EUNET_REQUIRE(part && out && rows > 0 && cols > 0, "colsum: bad args");
+  return eunet_colsum_ld(part, rows, cols, cols, out, (hipStream_t)stream);
+}
+
+int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
+                       const float* gamma, const float* beta, const float* dbeta, const float* dgamma,
+                       const eunet_act* gy, void* stream) {
+  EUNET_REQUIRE(act_ok(g) && act_ok(y) && act_ok(gy) && vec_ok(g) && vec_ok(y) && vec_ok(gy),
+                "bn_bwd_apply: bad tensors");
+  EUNET_REQUIRE(mean && invstd && gamma && beta && dbeta && dgamma, "bn_bwd_apply: null stats");
+  EUNET_REQUIRE(g->dtype == y->dtype && gy->dtype == y->dtype && g->c == y->c && gy->c == y->c,
+                "bn_bwd_apply: mismatch");
+  const long long P = (long long)y->n * y->h * y->w;
+  const long long total = P * (y->c / e16(y->dtype));
+  const unsigned gr = (unsigned)((total + 255) / 256);
+  if (y->dtype == EUNET_BF16)
+    bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
+        gamma, beta, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff);
+  else
+    bn_bwd_apply_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
+        (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
+        gamma, beta, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff);
+  EUNET_LAUNCH_CHECK("bn_bwd_apply");
+  return EUNET_OK;
+}
+
+int eunet_pool_bwd_add(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip, const eunet_act* gout,
+                       void* stream) {
+  EUNET_REQUIRE(act_ok(act) && act_ok(gpool) && act_ok(gout) && vec_ok(act) && vec_ok(gpool) && vec_ok(gout),
+                "pool_bwd_add: bad tensors");
+  if (gskip) EUNET_REQUIRE(act_ok(gskip) && vec_ok(gskip) && gskip->c == act->c, "pool_bwd_add: gskip");
+  EUNET_REQUIRE(gpool->h * 2 == act->h && gpool->w * 2 == act->w && gout->h == act->h && gout->w == act->w &&
+                    gpool->c == act->c && gout->c == act->c,
+                "pool_bwd_add: shapes");
+  const int E = e16(act->dtype);
+  const long long total = (long long)act->n * (act->h / 2) * (act->w / 2) * (act->c / E);
+  const unsigned gr = (unsigned)((total + 255) / 256);
+#define PBA(T)                                                                                                  \
+  pool_bwd_add_kernel<T><<<gr, 256, 0, (hipStream_t)stream>>>(                                                  \
+      (const T*)act->ptr, act->ctot, act->coff, (const T*)gpool->ptr, gpool->ctot, gpool->coff,                 \
+      gskip ? (const T*)gskip->ptr : nullptr, gskip ? gskip->ctot : 0, gskip ? gskip->coff : 0, (T*)gout->ptr, \
+      gout->ctot, gout->coff, act->n, act->h, act->w, act->c)
+  if (act->dtype == EUNET_BF16) PBA(bf16_t);
+  else PBA(float);
+#undef PBA
+  EUNET_LAUNCH_CHECK("pool_bwd_add");
+  return EUNET_OK;
+}
+
+int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream) {
+  EUNET_REQUIRE(act_ok(ghi) && act_ok(glo), "upsample_bwd: bad tensors");
+  EUNET_REQUIRE(ghi->h == 2 * glo->h && ghi->w == 2 * glo->w && ghi->c == glo->c && ghi->n == glo->n,
+                "upsample_bwd: shapes");
+  if (ghi->dtype == EUNET_F32 && glo->dtype == EUNET_F32 && ghi->ctot == ghi->c && glo->ctot == glo->c &&
+      ghi->c <= 4 && ghi->coff == 0 && glo->coff == 0) {
+    const long long total = (long long)glo->n * glo->h * glo->w;
+    up_bwd_small_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+        (const float*)ghi->ptr, (float*)glo->ptr, glo->n, glo->h, glo->w, glo->c);
+    EUNET_LAUNCH_CHECK("upsample_bwd_small");
+    return EUNET_OK;
+  }
+  EUNET_REQUIRE(vec_ok(ghi) && vec_ok(glo) && ghi->dtype == glo->dtype, "upsample_bwd: vector layout");
+  const int E = e16(ghi->dtype);
+  const long long total = (long long)glo->n * glo->h * glo->w * (glo->c / E);
+  const unsigned gr = (unsigned)((total + 255) / 256);
+  if (ghi->dtype == EUNET_BF16)
+    up_bwd_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
+        glo->w, glo->c);
+  else
+    up_bwd_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>((const float*)ghi->ptr, ghi->ctot, ghi->coff,
+                                                                     (float*)glo->ptr, glo->ctot, glo->coff, glo->n,
+                                                                     glo->h, glo->w, glo->c);
+  EUNET_LAUNCH_CHECK("upsample_bwd");
+  return EUNET_OK;
+}
+
+int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles) {
+  EUNET_REQUIRE(act_ok(y) && tiles, "conv1x1_bwd_tiles: bad args");
+  *tiles = (int)(((long long)y->n * y->h * y->w + NT - 1) / NT);
+  return EUNET_OK;
+}
+
+int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift, const float* w, int k,
+                      const float* gz, const eunet_act* gact, float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(gact) && vec_ok(y) && vec_ok(gact) && scale && shift && w && gz && part,
+                "conv1x1_bwd: bad args");
+  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 256 && gact->c == y->c && gact->dtype == y->dtype,
+                "conv1x1_bwd: K<=3, C<=256");
+  const long long P = (long long)y->n * y->h * y->w;
+  const unsigned tiles = (unsigned)((P + NT - 1) / NT);
+  if (y->dtype == EUNET_BF16)
+    conv1x1_bwd_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
+                                                                        y->coff, scale, shift, w, k, gz,
+                                                                        (bf16_t*)gact->ptr, gact->ctot, gact->coff,
+                                                                        part);
+  else
+    conv1x1_bwd_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
+                                                                       y->coff, scale, shift, w, k, gz,
+                                                                       (float*)gact->ptr, gact->ctot, gact->coff,
+                                                                       part);
+  EUNET_LAUNCH_CHECK("conv1x1_bwd");
+  return EUNET_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+// Shared device/host helpers for libeunet_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/eunet.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // storage type for bf16 activations
+
+__device__ __forceinline__ bf16x8 cat_bf16x4(s16x4 lo, s16x4 hi) {
+  const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// ---------------------------------------------------------------------------
+// host-side error plumbing (C-ABI returns int codes; message via eunet_last_error)
+// ---------------------------------------------------------------------------
+namespace eunet {
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+}  // namespace eunet
+
+#define EUNET_REQUIRE(cond, ...)                    \
+  do {                                              \
+    if (!(cond)) {                                  \
+      eunet::set_error(__VA_ARGS__);                \
+      return EUNET_ERR_INVALID;                     \
+    }                                               \
+  } while (0)
+
+#define EUNET_LAUNCH_CHECK(name) \
+  do {                           \
+    int _rc = eunet::check_launch(name); \
+    if (_rc) return _rc;         \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// element conversion
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+  static constexpr int per16 = 4;  // elements per 16-byte unit
+};
+template <> struct Elem<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+  static constexpr int per16 = 8;
+};
+
+// 16-byte unit <-> 8 (bf16) or 4 (f32) floats
+template <typename T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  static __device__ __forceinline__ void unpack(uint4 u, float* f) {
+    f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y);
+    f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+template <> struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void unpack(uint4 u, float* f) {
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+    }
+  }
+  static __device__ __forceinline__ uint4 pack(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Butterfly transpose-reduce: every lane holds v[0..63] (one value per channel);
+// afterwards lane l holds sum over the 64 lanes of channel l.  63 shuffles/lane.
+__device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const bool upper = (lane & s) != 0;
+#pragma unroll
+    for (int i = 0; i < s; ++i) {
+      // keep half [upper ? s+i : i], send the other half to partner lane^s
+      float keep = upper ? v[i + s] : v[i];
+      float send = upper ? v[i] : v[i + s];
+      float recv = __shfl_xor(send, s, 64);
+      v[i] = keep + recv;
+    }
+  }
+  return v[0];
+}
+
+// bilinear x2 (align_corners=False) source index/weight, PyTorch's
+// area_pixel_compute_source_index for scale 1/2 (F.interpolate, nn.Upsample)
+__device__ __forceinline__ void up2_src(int o, int in, int& i0, int& i1, float& l1) {
+  float s = 0.5f * ((float)o + 0.5f) - 0.5f;
+  s = s < 0.f ? 0.f : s;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+}
+
+// kernels with > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+template <typename K>
+inline void allow_lds(K* kernel, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+__host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// activation view accessors
+__host__ __device__ inline long long act_pix(const eunet_act& a, int n, int y, int x) {
+  return ((long long)(n * a.h + y) * a.w + x);
+}

@@ -1,0 +1,111 @@
+"""ctypes binding of libeunet_hip.so (the C-ABI in include/eunet.h).
+
+The product path has exactly one implementation: the HIP library.  If it is
+missing or cannot be loaded, every op raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_size_t, c_void_p, c_char_p, c_int64
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeunet_hip.so")
+
+EUNET_F32 = 0
+EUNET_BF16 = 1
+
+
+class Act(ctypes.Structure):
+    """eunet_act: NHWC view (ptr, n, h, w, c, ctot, coff, dtype)."""
+    _fields_ = [("ptr", c_void_p), ("n", c_int), ("h", c_int), ("w", c_int), ("c", c_int),
+                ("ctot", c_int), ("coff", c_int), ("dtype", c_int)]
+
+
+_P = POINTER(Act)
+_f = c_void_p  # float* / void* device pointers are passed as integers
+
+# name -> argtypes (restype is always c_int except the two string getters)
+SIGNATURES = {
+    "eunet_nchw_to_nhwc": [_f, _P, c_void_p],
+    "eunet_conv3x3_packed_bytes": [c_int, c_int, c_int, POINTER(c_size_t)],
+    "eunet_conv3x3_pack": [_f, c_int, c_int, c_int, _f, c_int, c_void_p],
+    "eunet_conv3x3_tiles": [_P, POINTER(c_int)],
+    "eunet_conv3x3_fwd": [_P, _f, _f, _f, _f, _P, _f, c_void_p],
+    "eunet_conv3x3_wgrad_splits": [_P, c_int, c_int, POINTER(c_int)],
+    "eunet_conv3x3_wgrad": [_P, _f, _f, _P, _f, _f, c_int, c_void_p],
+    "eunet_wgrad_reduce": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, c_void_p],
+    "eunet_conv_small_fwd": [_P, _f, _f, _P, _f, c_void_p],
+    "eunet_conv_small_wgrad_splits": [_P, POINTER(c_int)],
+    "eunet_conv_small_wgrad": [_P, _P, _f, _f, c_int, c_void_p],
+    "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_bn_eval_affine": [c_int, _f, _f, _f, _f, c_float, _f, _f, c_void_p],
+    "eunet_bnrelu_pool": [_P, _f, _f, _P, _P, c_void_p],
+    "eunet_bnrelu_upsample": [_P, _f, _f, _P, c_void_p],
+    "eunet_bnrelu_conv1x1": [_P, _f, _f, _f, _f, c_int, _f, c_void_p],
+    "eunet_head_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],
+    "eunet_head_fwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, c_int, c_float, c_float,
+                       _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_head_bwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
+                       _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_loss_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],
+    "eunet_loss_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, c_void_p],
+    "eunet_loss_bwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, c_void_p],
+    "eunet_bn_bwd_tiles": [_P, POINTER(c_int)],
+    "eunet_bn_bwd_reduce": [_P, _P, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_colsum": [_f, c_int, c_int, _f, c_void_p],
+    "eunet_bn_bwd_apply": [_P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
+    "eunet_pool_bwd_add": [_P, _P, _P, _P, c_void_p],
+    "eunet_upsample_bwd": [_P, _P, c_void_p],
+    "eunet_conv1x1_bwd_tiles": [_P, POINTER(c_int)],
+    "eunet_conv1x1_bwd": [_P, _f, _f, _f, c_int, _f, _P, _f, c_void_p],
+}
+STRING_FNS = ("eunet_version", "eunet_last_error")
+
+
+class EunetError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and type the library.  Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EunetError(f"libeunet_hip.so not found at {path}: build it with "
+                         f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = ctypes.CDLL(path)
+    for name in STRING_FNS:
+        fn = getattr(lib, name)
+        fn.restype = c_char_p
+        fn.argtypes = []
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = c_int
+        fn.argtypes = argt
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.eunet_last_error().decode(errors="replace")
+        raise EunetError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def exported_symbols():
+    return list(SIGNATURES) + list(STRING_FNS)
+
+
+def version() -> str:
+    return load().eunet_version().decode()
+
+
+__all__ = ["Act", "load", "call", "EunetError", "EUNET_F32", "EUNET_BF16", "exported_symbols",
+           "c_int", "c_size_t", "c_float", "c_int64"]

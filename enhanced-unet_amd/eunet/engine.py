@@ -1,0 +1,324 @@
+"""Explicit forward/backward schedule of the Enhanced-UNet hot path over libeunet_hip.
+
+Reference structure (models.py:199-240, 304-339):
+    e1 = enc1(x); e2 = enc2(pool(e1)); e3 = enc3(pool(e2)); e4 = enc4(pool(e3))
+    d4 = dec4(cat[up(e4), e3]); d3 = dec3(cat[up(d4), e2]); d2 = dec2(cat[up(d3), e1])
+    out = u + enhance(u),  u = dec1(up(d2))  (== up(dec1(d2)), computed that way)
+
+Data layout in HBM (NHWC, dtype = fp32 or bf16):
+  * each DoubleConv keeps only its two PRE-BatchNorm conv outputs y_a, y_b;
+    BN+ReLU of y_a is applied inside the operand load of conv b (and of the
+    wgrad that needs it); BN+ReLU of y_b is applied by its single consumer
+    (pool / upsample / dec1 kernel), so no post-ReLU tensor of a block is
+    written except the skip activations;
+  * the skip activations e1..e3 and the upsampled decoder inputs are written
+    straight into their concat buffers cat2/cat3/cat4 (torch.cat never runs);
+  * the 2H tail is fused in the head kernels (never materialised).
+Backward mirrors it; every parameter gradient is written into a slot handed
+out by a GradSink (the data-parallel sink launches bucketed all-reduces as
+soon as a bucket is complete, overlapping RCCL with the rest of backward).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import ops
+from ._lib import EunetError
+
+BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+class GradSink:
+    """Default sink: a fresh fp32 tensor per parameter gradient."""
+
+    def __init__(self, device):
+        self.device = device
+        self.grads: Dict[str, torch.Tensor] = {}
+
+    def slot(self, name: str, shape) -> torch.Tensor:
+        t = torch.empty(shape, dtype=torch.float32, device=self.device)
+        self.grads[name] = t
+        return t
+
+    def ready(self, names):  # hook point for data-parallel overlap
+        pass
+
+    def finish(self):
+        return self.grads
+
+
+def _e(shape, dtype, device):
+    return torch.empty(shape, dtype=dtype, device=device)
+
+
+class UNetEngine:
+    def __init__(self, model):
+        self.m = model
+        self.base = model.base_ch
+        self.K = model.num_classes
+        self.cin = model.in_channels
+        self.dtype = model.compute_dtype
+
+    # ------------------------------------------------------------------ utils
+    def _P(self):
+        return dict(self.m.named_parameters())
+
+    def _B(self):
+        return dict(self.m.named_buffers())
+
+    def _bn(self, prefix, stats, tiles, C, training, P, B):
+        dev = P[prefix + ".weight"].device
+        scale, shift = _e(C, torch.float32, dev), _e(C, torch.float32, dev)
+        if training:
+            mean, invstd = _e(C, torch.float32, dev), _e(C, torch.float32, dev)
+            ops.bn_finalize(stats, tiles, C, P[prefix + ".weight"], P[prefix + ".bias"], BN_EPS, BN_MOMENTUM,
+                            B[prefix + ".running_mean"], B[prefix + ".running_var"], mean, invstd, scale, shift)
+            B[prefix + ".num_batches_tracked"].add_(1)
+            return dict(mean=mean, invstd=invstd, scale=scale, shift=shift)
+        ops.bn_eval_affine(P[prefix + ".weight"], P[prefix + ".bias"], B[prefix + ".running_mean"],
+                           B[prefix + ".running_var"], BN_EPS, scale, shift)
+        return dict(mean=None, invstd=None, scale=scale, shift=shift)
+
+    def _stats_buf(self, y):
+        tiles = ops.conv3x3_tiles(ops.act(y))
+        C = y.shape[3]
+        return _e(tiles * (2 * C + 1), torch.float32, y.device), tiles
+
+    def _block_fwd(self, nm, X: ops.Act, training, P, B, small: bool):
+        p = f"model.{nm}"
+        N, H, W = X.n, X.h, X.w
+        C = P[p + ".0.weight"].shape[0]
+        dev = P[p + ".0.weight"].device
+        ya = _e((N, H, W, C), self.dtype, dev)
+        yb = _e((N, H, W, C), self.dtype, dev)
+        st, tiles = self._stats_buf(ya) if training else (None, 0)
+        if small:
+            ops.conv_small_fwd(X, P[p + ".0.weight"], P[p + ".0.bias"], ops.act(ya), st)
+        else:
+            wp = ops.conv3x3_pack(P[p + ".0.weight"], self.dtype, flip=False)
+            ops.conv3x3_fwd(X, wp, ops.act(ya), bias=P[p + ".0.bias"], stats=st)
+        bna = self._bn(p + ".1", st, tiles, C, training, P, B)
+        wp = ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
+        ops.conv3x3_fwd(ops.act(ya), wp, ops.act(yb), bias=P[p + ".3.bias"], scale=bna["scale"],
+                        shift=bna["shift"], stats=st)
+        bnb = self._bn(p + ".4", st, tiles, C, training, P, B)
+        return dict(ya=ya, yb=yb, bna=bna, bnb=bnb, X=X)
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x: torch.Tensor, training: bool, want: str = "logits"):
+        """x [N,Cin,H,W] fp32 -> logits [N,K,H,W] ('logits', the 2x2 mean of the
+        2H output) or out2h [N,K,2H,2W] ('out2h', the reference forward)."""
+        if not x.is_cuda:
+            raise EunetError("EnhancedUNet (eunet) runs on the GPU only; no CPU fallback")
+        N, Cin, H, W = x.shape
+        if Cin != self.cin:
+            raise ValueError(f"expected {self.cin} input channels, got {Cin}")
+        if H % 8 or W % 8:
+            raise ValueError("H and W must be multiples of 8 (the reference pads to /32)")
+        P, B = self._P(), self._B()
+        dt, dev, b, K = self.dtype, x.device, self.base, self.K
+        ch = [b, 2 * b, 4 * b, 8 * b]
+        lv = [(H >> i, W >> i) for i in range(4)]
+        S = {}
+        xin = _e((N, H, W, Cin), dt, dev)
+        ops.nchw_to_nhwc(x.contiguous().float(), xin)
+        cat4 = _e((N, *lv[2], ch[3] + ch[2]), dt, dev)
+        cat3 = _e((N, *lv[1], ch[2] + ch[1]), dt, dev)
+        cat2 = _e((N, *lv[0], ch[1] + ch[0]), dt, dev)
+        p1 = _e((N, *lv[1], ch[0]), dt, dev)
+        p2 = _e((N, *lv[2], ch[1]), dt, dev)
+        p3 = _e((N, *lv[3], ch[2]), dt, dev)
+        S.update(xin=xin, cat4=cat4, cat3=cat3, cat2=cat2, p1=p1, p2=p2, p3=p3)
+
+        def consume_pool(nm, cat, coff, pooled):
+            s = S[nm]
+            ops.bnrelu_pool(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
+                            ops.act(cat, coff, s["yb"].shape[3]), ops.act(pooled))
+
+        def consume_up(nm, cat):
+            s = S[nm]
+            ops.bnrelu_upsample(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
+                                ops.act(cat, 0, s["yb"].shape[3]))
+
+        S["enc1"] = self._block_fwd("enc1", ops.act(xin), training, P, B, small=True)
+        consume_pool("enc1", cat2, ch[1], p1)
+        S["enc2"] = self._block_fwd("enc2", ops.act(p1), training, P, B, small=False)
+        consume_pool("enc2", cat3, ch[2], p2)
+        S["enc3"] = self._block_fwd("enc3", ops.act(p2), training, P, B, small=False)
+        consume_pool("enc3", cat4, ch[3], p3)
+        S["enc4"] = self._block_fwd("enc4", ops.act(p3), training, P, B, small=False)
+        consume_up("enc4", cat4)
+        S["dec4"] = self._block_fwd("dec4", ops.act(cat4), training, P, B, small=False)
+        consume_up("dec4", cat3)
+        S["dec3"] = self._block_fwd("dec3", ops.act(cat3), training, P, B, small=False)
+        consume_up("dec3", cat2)
+        S["dec2"] = self._block_fwd("dec2", ops.act(cat2), training, P, B, small=False)
+        s = S["dec2"]
+        z = _e((N, H, W, K), torch.float32, dev)
+        ops.bnrelu_conv1x1(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
+                           P["model.dec1.weight"].reshape(K, b).contiguous(), P["model.dec1.bias"], K, z)
+        S["z"] = z
+        hws = _e(ops.head_workspace_bytes(N, H, W, K), torch.uint8, dev)
+        hmean = _e(64, torch.float32, dev) if training else None
+        hinv = _e(64, torch.float32, dev) if training else None
+        out2h = _e((N, K, 2 * H, 2 * W), torch.float32, dev) if want == "out2h" else None
+        logits = _e((N, K, H, W), torch.float32, dev) if want == "logits" else None
+        ops.head_fwd(z, N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
+                     P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), P["enhance.3.bias"],
+                     training, BN_EPS, BN_MOMENTUM, B["enhance.1.running_mean"], B["enhance.1.running_var"],
+                     hmean, hinv, out2h, logits, hws)
+        if training:
+            B["enhance.1.num_batches_tracked"].add_(1)
+        S.update(hmean=hmean, hinv=hinv, N=N, H=H, W=W, want=want)
+        return (logits if want == "logits" else out2h), S
+
+    # --------------------------------------------------------------- backward
+    def _block_bwd(self, nm, G: torch.Tensor, S, P, sink: GradSink, need_gx: bool, small: bool):
+        p = f"model.{nm}"
+        s = S[nm]
+        ya, yb, bna, bnb, X = s["ya"], s["yb"], s["bna"], s["bnb"], s["X"]
+        N, H, W, C = yb.shape
+        dev, dt = yb.device, self.dtype
+        red = _e(2 * C, torch.float32, dev)
+
+        def bn_back(prefix, g, y, bn):
+            tiles = ops.bn_bwd_tiles(ops.act(y))
+            part = _e(tiles * 2 * C, torch.float32, dev)
+            ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
+                              P[prefix + ".bias"], part)
+            ops.colsum(part, tiles, 2 * C, red)
+            sink.slot(prefix + ".bias", (C,)).copy_(red[:C])
+            sink.slot(prefix + ".weight", (C,)).copy_(red[C:])
+            gy = torch.empty_like(y)
+            ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
+                             P[prefix + ".bias"], red[:C], red[C:], ops.act(gy))
+            return gy
+
+        def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False):
+            cin = xa.c
+            gya = ops.act(gy)
+            if small_conv:
+                ns = ops.conv_small_wgrad_splits(gya)
+            else:
+                ns = ops.conv3x3_wgrad_splits(gya, cin, dt)
+            dwp = _e(ns * C * 9 * cin, torch.float32, dev)
+            dbp = _e(ns * C, torch.float32, dev)
+            if small_conv:
+                ops.conv_small_wgrad(xa, gya, dwp, dbp, ns)
+            else:
+                ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=scale, shift=shift)
+            dw = sink.slot(conv + ".weight", (C, cin, 3, 3))
+            db = sink.slot(conv + ".bias", (C,))
+            ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
+
+        gyb = bn_back(p + ".4", G, yb, bnb)
+        wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
+        wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
+        gaa = torch.empty_like(ya)
+        ops.conv3x3_fwd(ops.act(gyb), wpt, ops.act(gaa))
+        del gyb
+        gya = bn_back(p + ".1", gaa, ya, bna)
+        del gaa
+        wgrad(p + ".0", X, gya, small_conv=small)
+        sink.ready([f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")])
+        if not need_gx:
+            return None
+        wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
+        gx = _e((N, H, W, X.c), dt, dev)
+        ops.conv3x3_fwd(ops.act(gya), wpt, ops.act(gx))
+        return gx
+
+    def backward(self, S, g_out: torch.Tensor, sink: Optional[GradSink] = None):
+        P = self._P()
+        N, H, W, K, b = S["N"], S["H"], S["W"], self.K, self.base
+        dev, dt = g_out.device, self.dtype
+        ch = [b, 2 * b, 4 * b, 8 * b]
+        sink = sink or GradSink(dev)
+        g_out = g_out.contiguous().float()
+        # ---- 2H head -> gz
+        gz = _e((N, H, W, K), torch.float32, dev)
+        hws = _e(ops.head_workspace_bytes(N, H, W, K), torch.uint8, dev)
+        gw1 = sink.slot("enhance.0.weight", (64, K, 3, 3))
+        gb1 = sink.slot("enhance.0.bias", (64,))
+        gg = sink.slot("enhance.1.weight", (64,))
+        gbt = sink.slot("enhance.1.bias", (64,))
+        gw2 = sink.slot("enhance.3.weight", (K, 64, 1, 1))
+        gb2 = sink.slot("enhance.3.bias", (K,))
+        glog = g_out if S["want"] == "logits" else None
+        gout2h = g_out if S["want"] == "out2h" else None
+        ops.head_bwd(S["z"], N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
+                     P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), S["hmean"], S["hinv"],
+                     glog, gout2h, gz, gw1, gb1, gg, gbt, gw2, gb2, hws)
+        sink.ready(["enhance.0.weight", "enhance.0.bias", "enhance.1.weight", "enhance.1.bias",
+                    "enhance.3.weight", "enhance.3.bias"])
+        # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))
+        s2 = S["dec2"]
+        gd2 = torch.empty_like(s2["yb"])
+        yb_act = ops.act(s2["yb"])
+        tiles = ops.conv1x1_bwd_tiles(yb_act)
+        part = _e(tiles * (K * b + K), torch.float32, dev)
+        ops.conv1x1_bwd(yb_act, s2["bnb"]["scale"], s2["bnb"]["shift"], P["model.dec1.weight"].reshape(K, b).contiguous(),
+                        K, gz, ops.act(gd2), part)
+        red = _e(K * b + K, torch.float32, dev)
+        ops.colsum(part, tiles, K * b + K, red)
+        sink.slot("model.dec1.weight", (K, b, 1, 1)).copy_(red[:K * b].view(K, b, 1, 1))
+        sink.slot("model.dec1.bias", (K,)).copy_(red[K * b:])
+        sink.ready(["model.dec1.weight", "model.dec1.bias"])
+        # ---- decoder
+        g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False)
+        del gd2
+        g_d3 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
+        ops.upsample_bwd(ops.act(g_cat2, 0, ch[1]), ops.act(g_d3))
+        g_cat3 = self._block_bwd("dec3", g_d3, S, P, sink, need_gx=True, small=False)
+        del g_d3
+        g_d4 = _e((N, H >> 2, W >> 2, ch[2]), dt, dev)
+        ops.upsample_bwd(ops.act(g_cat3, 0, ch[2]), ops.act(g_d4))
+        g_cat4 = self._block_bwd("dec4", g_d4, S, P, sink, need_gx=True, small=False)
+        del g_d4
+        g_e4 = _e((N, H >> 3, W >> 3, ch[3]), dt, dev)
+        ops.upsample_bwd(ops.act(g_cat4, 0, ch[3]), ops.act(g_e4))
+        # ---- encoder (skip gradients + max-pool backward)
+        g_p3 = self._block_bwd("enc4", g_e4, S, P, sink, need_gx=True, small=False)
+        del g_e4
+        g_e3 = _e((N, H >> 2, W >> 2, ch[2]), dt, dev)
+        ops.pool_bwd_add(ops.act(S["cat4"], ch[3], ch[2]), ops.act(g_p3), ops.act(g_cat4, ch[3], ch[2]),
+                         ops.act(g_e3))
+        del g_p3, g_cat4
+        g_p2 = self._block_bwd("enc3", g_e3, S, P, sink, need_gx=True, small=False)
+        del g_e3
+        g_e2 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
+        ops.pool_bwd_add(ops.act(S["cat3"], ch[2], ch[1]), ops.act(g_p2), ops.act(g_cat3, ch[2], ch[1]),
+                         ops.act(g_e2))
+        del g_p2, g_cat3
+        g_p1 = self._block_bwd("enc2", g_e2, S, P, sink, need_gx=True, small=False)
+        del g_e2
+        g_e1 = _e((N, H, W, ch[0]), dt, dev)
+        ops.pool_bwd_add(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]),
+                         ops.act(g_e1))
+        del g_p1, g_cat2
+        self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True)
+        return sink.finish()
+
+
+class UNetFunction(torch.autograd.Function):
+    """autograd boundary: forward/backward of the whole network in one node."""
+
+    @staticmethod
+    def forward(ctx, x, want, engine, sink_factory, *params):
+        out, S = engine.forward(x, training=True, want=want)
+        ctx.S = S
+        ctx.engine = engine
+        ctx.sink_factory = sink_factory
+        ctx.names = [n for n, _ in engine.m.named_parameters()]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        sink = ctx.sink_factory() if ctx.sink_factory is not None else None
+        grads = ctx.engine.backward(ctx.S, g, sink)
+        ctx.S = None
+        return (None, None, None, None) + tuple(grads.get(n) for n in ctx.names)

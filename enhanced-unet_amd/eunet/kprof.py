@@ -1,0 +1,71 @@
+"""Live per-kernel timing with HIP events on the launch stream (used by bench.py).
+
+When a KernelTimer is active, ops.* launches of the named kernel families are
+bracketed by events recorded on torch's current stream -- the same stream the
+C-ABI launches on -- and credited with their algorithmic FLOPs / bytes.
+"""
+from __future__ import annotations
+
+import torch
+
+_active = None
+
+
+class KernelTimer:
+    def __init__(self):
+        self.records = {}  # family -> list of (ev0, ev1, flops, bytes)
+
+    def __enter__(self):
+        global _active
+        _active = self
+        return self
+
+    def __exit__(self, *exc):
+        global _active
+        _active = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for fam, recs in self.records.items():
+            ms = sum(a.elapsed_time(b) for a, b, _, _ in recs)
+            out[fam] = dict(launches=len(recs), ms=ms, flops=sum(r[2] for r in recs),
+                            bytes=sum(r[3] for r in recs))
+        return out
+
+
+def timed(family: str, flops: float, nbytes: float = 0.0):
+    """Context manager used around a launch; no-op when no timer is active."""
+    t = _active
+    if t is None:
+        return _Null
+    return _Rec(t, family, flops, nbytes)
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_Null = _NullCtx()
+
+
+class _Rec:
+    __slots__ = ("t", "fam", "flops", "nbytes", "e0")
+
+    def __init__(self, t, fam, flops, nbytes):
+        self.t, self.fam, self.flops, self.nbytes = t, fam, flops, nbytes
+
+    def __enter__(self):
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.t.records.setdefault(self.fam, []).append((self.e0, e1, self.flops, self.nbytes))
+        return False

@@ -1,0 +1,208 @@
+"""Thin torch-tensor wrappers over the C-ABI (one function per entry point).
+
+Tensors are device memory only (torch is the allocator); every call is
+enqueued on torch's current HIP stream.  Activations are NHWC tensors
+[N, H, W, Ctot]; a channel slice is expressed by (coff, c).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib, kprof
+from ._lib import Act, call, c_int, c_size_t
+
+DTYPES = {torch.float32: _lib.EUNET_F32, torch.bfloat16: _lib.EUNET_BF16}
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise _lib.EunetError("eunet ops need device tensors (no CPU fallback)")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def act(t: torch.Tensor, coff: int = 0, c: int | None = None) -> Act:
+    """NHWC view of a contiguous [N,H,W,Ctot] tensor, channels [coff, coff+c)."""
+    if t.dim() != 4 or not t.is_contiguous():
+        raise _lib.EunetError(f"act(): need a contiguous NHWC tensor, got {tuple(t.shape)}")
+    if not t.is_cuda:
+        raise _lib.EunetError("act(): tensor must live on the GPU")
+    n, h, w, ct = t.shape
+    return Act(t.data_ptr(), n, h, w, ct - coff if c is None else c, ct, coff, DTYPES[t.dtype])
+
+
+def _ref(a):
+    return None if a is None else ctypes.byref(a)
+
+
+def nchw_to_nhwc(x: torch.Tensor, out: torch.Tensor):
+    call("eunet_nchw_to_nhwc", _ptr(x), ctypes.byref(act(out)), _stream())
+
+
+def conv3x3_packed_bytes(cout, cin, dtype):
+    b = c_size_t()
+    call("eunet_conv3x3_packed_bytes", cout, cin, DTYPES[dtype], ctypes.byref(b))
+    return b.value
+
+
+def conv3x3_pack(w: torch.Tensor, dtype, flip: bool) -> torch.Tensor:
+    cout, cin = w.shape[0], w.shape[1]
+    nbytes = conv3x3_packed_bytes(cin if flip else cout, cout if flip else cin, dtype)
+    wp = torch.empty(nbytes // (2 if dtype == torch.bfloat16 else 4), dtype=dtype, device=w.device)
+    call("eunet_conv3x3_pack", _ptr(w.contiguous()), cout, cin, int(flip), _ptr(wp), DTYPES[dtype], _stream())
+    return wp
+
+
+def conv3x3_tiles(y_act: Act) -> int:
+    t = c_int()
+    call("eunet_conv3x3_tiles", ctypes.byref(y_act), ctypes.byref(t))
+    return t.value
+
+
+def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None):
+    flops = 2.0 * 9 * x.c * y.c * x.n * x.h * x.w
+    with kprof.timed("conv3x3_fwd", flops):
+        call("eunet_conv3x3_fwd", ctypes.byref(x), _ptr(scale), _ptr(shift), _ptr(wp), _ptr(bias),
+             ctypes.byref(y), _ptr(stats), _stream())
+
+
+def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
+    s = c_int()
+    call("eunet_conv3x3_wgrad_splits", ctypes.byref(dy), cin, DTYPES[dtype], ctypes.byref(s))
+    return s.value
+
+
+def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=None):
+    flops = 2.0 * 9 * x.c * dy.c * x.n * x.h * x.w
+    with kprof.timed("conv3x3_wgrad", flops):
+        call("eunet_conv3x3_wgrad", ctypes.byref(x), _ptr(scale), _ptr(shift), ctypes.byref(dy), _ptr(dw_part),
+             _ptr(db_part), nsplit, _stream())
+
+
+def wgrad_reduce(dw_part, db_part, nsplit, cout, cin, taps, dw, db):
+    call("eunet_wgrad_reduce", _ptr(dw_part), _ptr(db_part), nsplit, cout, cin, taps, _ptr(dw), _ptr(db),
+         _stream())
+
+
+def conv_small_fwd(x: Act, w, bias, y: Act, stats=None):
+    call("eunet_conv_small_fwd", ctypes.byref(x), _ptr(w), _ptr(bias), ctypes.byref(y), _ptr(stats), _stream())
+
+
+def conv_small_wgrad_splits(dy: Act) -> int:
+    s = c_int()
+    call("eunet_conv_small_wgrad_splits", ctypes.byref(dy), ctypes.byref(s))
+    return s.value
+
+
+def conv_small_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit):
+    call("eunet_conv_small_wgrad", ctypes.byref(x), ctypes.byref(dy), _ptr(dw_part), _ptr(db_part), nsplit,
+         _stream())
+
+
+def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, scale, shift):
+    call("eunet_bn_finalize", _ptr(stats), tiles, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+         _ptr(run_mean), _ptr(run_var), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _stream())
+
+
+def bn_eval_affine(gamma, beta, run_mean, run_var, eps, scale, shift):
+    call("eunet_bn_eval_affine", gamma.numel(), _ptr(gamma), _ptr(beta), _ptr(run_mean), _ptr(run_var),
+         float(eps), _ptr(scale), _ptr(shift), _stream())
+
+
+def bnrelu_pool(y: Act, scale, shift, act_out: Act | None, pooled: Act):
+    call("eunet_bnrelu_pool", ctypes.byref(y), _ptr(scale), _ptr(shift), _ref(act_out), ctypes.byref(pooled),
+         _stream())
+
+
+def bnrelu_upsample(y: Act, scale, shift, out: Act):
+    call("eunet_bnrelu_upsample", ctypes.byref(y), _ptr(scale), _ptr(shift), ctypes.byref(out), _stream())
+
+
+def bnrelu_conv1x1(y: Act, scale, shift, w, b, k, z):
+    call("eunet_bnrelu_conv1x1", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), _ptr(b), k, _ptr(z),
+         _stream())
+
+
+def head_workspace_bytes(n, h, w, k):
+    b = c_size_t()
+    call("eunet_head_workspace_bytes", n, h, w, k, ctypes.byref(b))
+    return b.value
+
+
+def head_fwd(z, n, h, w, k, w1, b1, gamma, beta, w2, b2, training, eps, momentum, run_mean, run_var, mean,
+             invstd, out2h, logits, ws):
+    call("eunet_head_fwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2), _ptr(b2),
+         int(training), float(eps), float(momentum), _ptr(run_mean), _ptr(run_var), _ptr(mean), _ptr(invstd),
+         _ptr(out2h), _ptr(logits), _ptr(ws), _stream())
+
+
+def head_bwd(z, n, h, w, k, w1, b1, gamma, beta, w2, mean, invstd, g_logits, g_out2h, gz, gw1, gb1, ggamma,
+             gbeta, gw2, gb2, ws):
+    call("eunet_head_bwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2),
+         _ptr(mean), _ptr(invstd), _ptr(g_logits), _ptr(g_out2h), _ptr(gz), _ptr(gw1), _ptr(gb1), _ptr(ggamma),
+         _ptr(gbeta), _ptr(gw2), _ptr(gb2), _ptr(ws), _stream())
+
+
+def loss_workspace_bytes(n, k, h, w):
+    b = c_size_t()
+    call("eunet_loss_workspace_bytes", n, k, h, w, ctypes.byref(b))
+    return b.value
+
+
+def loss_fwd(logits, target, sums, loss, parts, ws):
+    n, k, h, w = logits.shape
+    call("eunet_loss_fwd", _ptr(logits), _ptr(target), n, k, h, w, _ptr(sums), _ptr(loss), _ptr(parts), _ptr(ws),
+         _stream())
+
+
+def loss_bwd(logits, target, sums, gloss, glogits):
+    n, k, h, w = logits.shape
+    call("eunet_loss_bwd", _ptr(logits), _ptr(target), n, k, h, w, _ptr(sums), _ptr(gloss), _ptr(glogits),
+         _stream())
+
+
+def bn_bwd_tiles(y: Act) -> int:
+    t = c_int()
+    call("eunet_bn_bwd_tiles", ctypes.byref(y), ctypes.byref(t))
+    return t.value
+
+
+def bn_bwd_reduce(g: Act, y: Act, mean, invstd, gamma, beta, part):
+    call("eunet_bn_bwd_reduce", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma),
+         _ptr(beta), _ptr(part), _stream())
+
+
+def colsum(part, rows, cols, out):
+    call("eunet_colsum", _ptr(part), rows, cols, _ptr(out), _stream())
+
+
+def bn_bwd_apply(g: Act, y: Act, mean, invstd, gamma, beta, dbeta, dgamma, gy: Act):
+    call("eunet_bn_bwd_apply", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma),
+         _ptr(beta), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
+
+
+def pool_bwd_add(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act):
+    call("eunet_pool_bwd_add", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), ctypes.byref(gout),
+         _stream())
+
+
+def upsample_bwd(ghi: Act, glo: Act):
+    call("eunet_upsample_bwd", ctypes.byref(ghi), ctypes.byref(glo), _stream())
+
+
+def conv1x1_bwd_tiles(y: Act) -> int:
+    t = c_int()
+    call("eunet_conv1x1_bwd_tiles", ctypes.byref(y), ctypes.byref(t))
+    return t.value
+
+
+def conv1x1_bwd(y: Act, scale, shift, w, k, gz, gact: Act, part):
+    call("eunet_conv1x1_bwd", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),
+         ctypes.byref(gact), _ptr(part), _stream())

@@ -1,0 +1,138 @@
+"""Drop-in training loop of reference train_eval.py for the Enhanced-UNet path.
+
+Trainer keeps the reference constructor, hyper-parameters and attributes
+(train_eval.py:63-132): AdamW(lr 4e-3, wd 1e-4, betas (0.9, 0.999)), warmup
+LinearLR(0.001 -> 1, max(1, min(5, E//6)) epochs) + CosineAnnealingWarmRestarts
+(T_0 = max(10, E//3), T_mult 2, eta_min 1e-7), loss weights 2.5/2.5/1.0.
+train_epoch(dataloader) -> mean loss, same batch dict as dataset.collate_fn
+(dataset.py:355-361): {'images': [B,C,H,W] float in [0,1],
+'batch_items': [{'semantic_mask': [H,W] int}, ...]}.
+
+Differences that are implementation, not semantics:
+  * the per-sample loss loop (train_eval.py:262-335) runs as one batched HIP
+    kernel (per-sample sums are kept per sample);
+  * the 2H->H bilinear resize of the logits (train_eval.py:306-310) is fused
+    into the network tail as the exact 2x2 mean it is;
+  * clip_grad_norm_ / AdamW stay PyTorch (foreach/fused kernels).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .losses import combined_loss
+from .models import EnhancedUNet
+
+
+class FocalLoss(nn.Module):
+    """API mirror of train_eval.FocalLoss (train_eval.py:28-60) for the Enhanced-UNet
+    configuration (alpha [1,8,5], gamma 5, CE weights [1,20,10]); computed by the
+    fused loss kernel.  inputs [N,K,H,W], targets [N,H,W] -> mean focal term."""
+
+    def forward(self, inputs, targets):
+        _, parts = combined_loss(inputs, targets, return_parts=True)
+        return parts[:, 0].mean()
+
+
+class Trainer:
+    def __init__(self, model, device, model_name, total_epochs: int = 50):
+        self.model = model
+        self.device = device
+        self.model_name = model_name
+        self.total_epochs = max(1, total_epochs)
+        if model_name != "enhanced_unet":
+            raise ValueError("this build implements the enhanced_unet training path only")
+        self.dice_loss_weight = 2.5
+        self.focal_loss_weight = 2.5
+        self.tversky_loss_weight = 1.0
+        self.aux_branch_weights = {"unetpp": 0.6, "deeplab": 0.5}
+        self.consistency_weight = 0.4
+        base_lr = 4e-3
+        params = [p for p in model.parameters()]
+        try:
+            self.optimizer = torch.optim.AdamW(params, lr=base_lr, weight_decay=1e-4, betas=(0.9, 0.999),
+                                               fused=True)
+        except (RuntimeError, TypeError):
+            self.optimizer = torch.optim.AdamW(params, lr=base_lr, weight_decay=1e-4, betas=(0.9, 0.999),
+                                               foreach=True)
+        self.warmup_epochs = max(1, min(5, self.total_epochs // 6))
+        self.scheduler = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(
+            self.optimizer, T_0=max(10, self.total_epochs // 3), T_mult=2, eta_min=1e-7)
+        self.warmup_scheduler = torch.optim.lr_scheduler.LinearLR(
+            self.optimizer, start_factor=0.001, end_factor=1.0, total_iters=self.warmup_epochs)
+        self.dp = None  # eunet.dp.DataParallel when training on several GPUs
+
+    # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
+    def _compute_combined_loss(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        return combined_loss(logits.unsqueeze(0), target.long().to(logits.device).unsqueeze(0))
+
+    def dice_loss(self, pred, target, num_classes=3):
+        return combined_loss(pred, target, return_parts=True)[1][:, 1].mean()
+
+    def tversky_loss(self, pred, target, num_classes=3, alpha=0.7):
+        return combined_loss(pred, target, return_parts=True)[1][:, 2].mean()
+
+    # ---- the hot loop ----------------------------------------------------------
+    @staticmethod
+    def _masks(batch, device, h_pad, w_pad):
+        ms = []
+        for item in batch["batch_items"]:
+            m = item["semantic_mask"]
+            if m.dim() != 2:
+                m = m.squeeze()
+                if m.dim() != 2:
+                    raise ValueError(f"gt_mask should be 2D after squeeze, got {tuple(m.shape)}")
+            ms.append(m)
+        m = torch.stack(ms).to(device, non_blocking=True).long()
+        if h_pad or w_pad:
+            m = F.pad(m, (0, w_pad, 0, h_pad), mode="constant", value=0)
+        return m
+
+    def step(self, images: torch.Tensor, masks: torch.Tensor, sync_loss: bool = True):
+        """One optimisation step on device-resident images [B,C,H,W] / masks [B,H,W]."""
+        self.model.train()
+        _, _, h, w = images.shape
+        h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
+        if h_pad or w_pad:  # train_eval.py:248-253
+            images = F.pad(images, (0, w_pad, 0, h_pad), mode="reflect")
+            masks = F.pad(masks, (0, w_pad, 0, h_pad), mode="constant", value=0)
+        self.optimizer.zero_grad(set_to_none=True)
+        if self.dp is not None:
+            self.dp.before_forward()
+        if isinstance(self.model, EnhancedUNet):
+            logits = self.model.forward_lowres(images)
+        else:
+            out = self.model(images)
+            logits = F.interpolate(out, size=masks.shape[-2:], mode="bilinear", align_corners=False)
+        loss = combined_loss(logits, masks)
+        loss.backward()
+        if self.dp is not None:
+            self.dp.after_backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1.0, foreach=True)
+        self.optimizer.step()
+        return loss.item() if sync_loss else loss.detach()
+
+    def train_epoch(self, dataloader):
+        self.model.train()
+        total = 0.0
+        n = 0
+        for batch in dataloader:
+            images = batch["images"].to(self.device, non_blocking=True)
+            _, _, h, w = images.shape
+            h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
+            masks = self._masks(batch, self.device, 0, 0)
+            total += self.step(images, masks)
+            n += 1
+        return total / max(1, n)
+
+    def epoch_lr_step(self, epoch: int) -> float:
+        """train_model's per-epoch stepping (train_eval.py:1104-1111)."""
+        if epoch < self.warmup_epochs:
+            self.warmup_scheduler.step()
+        else:
+            self.scheduler.step()
+        return self.optimizer.param_groups[0]["lr"]

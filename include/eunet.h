@@ -1,0 +1,170 @@
+/*
+ * libeunet_hip -- C-ABI of the MI355X-native Enhanced-UNet training hot path.
+ *
+ * Conventions
+ *   - Every entry point returns 0 on success or a negative EUNET_ERR_* code;
+ *     eunet_last_error() returns the message (thread-local).
+ *   - The library never allocates, frees or synchronises: all buffers and
+ *     workspaces are owned by the caller (the torch caching allocator in the
+ *     Python host); every launch is enqueued on the `stream` argument only
+ *     (a hipStream_t passed as void*), so RCCL/DDP stream ordering stays valid.
+ *   - Activations are NHWC views (eunet_act); dtype EUNET_F32 or EUNET_BF16.
+ *     BatchNorm statistics, losses, weights-for-the-optimizer and all
+ *     reductions are fp32 (partials combined in fp64).
+ *   - Stateless and re-entrant.
+ *
+ * The reference exposes this path only as Python (no FFI): each entry point
+ * below names the reference call site it replaces (file:line in
+ * whh1747012859/Enhanced-UNet).  INTEGRATION.md shows the ctypes binding.
+ */
+#ifndef EUNET_H
+#define EUNET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EUNET_OK 0
+#define EUNET_ERR_INVALID (-1)
+#define EUNET_ERR_HIP (-2)
+
+enum { EUNET_F32 = 0, EUNET_BF16 = 1 };
+
+/* NHWC view: element (n,y,x,c) lives at ptr + ((n*h + y)*w + x)*ctot + coff + c */
+typedef struct {
+  void* ptr;
+  int n, h, w;  /* batch, rows, cols */
+  int c;        /* channels in this view */
+  int ctot;     /* channel stride of the underlying buffer (>= coff + c) */
+  int coff;     /* first channel of the view inside the buffer */
+  int dtype;    /* EUNET_F32 | EUNET_BF16 */
+} eunet_act;
+
+const char* eunet_version(void);
+const char* eunet_last_error(void);
+
+/* ---- layout conversion ----------------------------------------------------
+ * images.to(device) + NCHW->NHWC (train_eval.py:242); x [N,C,H,W] fp32 */
+int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
+
+/* ---- Conv2d 3x3, padding 1 (models.py:219,222 / autograd) -----------------
+ * Weights are re-packed every step from the fp32 torch parameter
+ * [Cout][Cin][3][3] into the MFMA-ready layout.  transpose_flip=1 packs the
+ * dgrad operand W'[ci][co][8-t] so dgrad runs through the forward kernel. */
+int eunet_conv3x3_packed_bytes(int cout, int cin, int dtype, size_t* bytes);
+int eunet_conv3x3_pack(const float* w, int cout, int cin, int transpose_flip, void* wp, int dtype,
+                       void* stream);
+/* number of pixel tiles = rows of the BatchNorm statistics partial buffer */
+int eunet_conv3x3_tiles(const eunet_act* y, int* tiles);
+/* y = conv(t(x)) + bias, t = relu(x*in_scale+in_shift) per input channel when
+ * in_scale != NULL (the preceding BN+ReLU fused into the operand load, zero
+ * padding applied after the transform).  stats (nullable): [tiles][2][cout]
+ * per-tile (sum, M2) plus [tiles] counts appended after 2*cout*tiles floats. */
+int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in_shift,
+                      const void* wp, const float* bias, const eunet_act* y, float* stats,
+                      void* stream);
+/* wgrad (split over pixel tiles): dw_part [nsplit][cout][9][cin] and
+ * db_part [nsplit][cout] (db only when db_part != NULL) */
+int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit);
+int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* in_shift,
+                        const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
+                        void* stream);
+/* reduce split partials -> torch layout dw [cout][cin][taps], db [cout] (fp64 combine) */
+int eunet_wgrad_reduce(const float* dw_part, const float* db_part, int nsplit, int cout, int cin,
+                       int taps, float* dw, float* db, void* stream);
+
+/* ---- first conv (models.py:203 enc1.0, Cin = in_channels <= 4): direct ---- */
+int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias,
+                         const eunet_act* y, float* stats, void* stream);
+int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit);
+int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part,
+                           float* db_part, int nsplit, void* stream);
+
+/* ---- BatchNorm2d train-mode statistics (models.py:220,223; eps 1e-5, momentum 0.1)
+ * combine per-tile (sum, M2, count) partials (Chan, fp64); update running
+ * stats with the UNBIASED variance; emit mean, invstd and the fused affine
+ * scale = gamma*invstd, shift = beta - mean*scale. */
+int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, const float* beta,
+                      float eps, float momentum, float* run_mean, float* run_var, float* mean,
+                      float* invstd, float* scale, float* shift, void* stream);
+/* eval-mode affine from running stats */
+int eunet_bn_eval_affine(int c, const float* gamma, const float* beta, const float* run_mean,
+                         const float* run_var, float eps, float* scale, float* shift, void* stream);
+
+/* ---- fused BN-apply + ReLU consumers ----------------------------------------
+ * pool: MaxPool2d(2) (models.py:214, 229-231); act (nullable) receives the
+ * full-resolution activation (the skip tensor, written into its concat slot,
+ * models.py:233-235). */
+int eunet_bnrelu_pool(const eunet_act* y, const float* scale, const float* shift,
+                      const eunet_act* act, const eunet_act* pooled, void* stream);
+/* Upsample x2 bilinear, align_corners=False (models.py:215, 233-236) */
+int eunet_bnrelu_upsample(const eunet_act* y, const float* scale, const float* shift,
+                          const eunet_act* out, void* stream);
+/* dec1 1x1 conv (models.py:212,236), commuted before the upsample:
+ * z[p][k] = b[k] + sum_c w[k][c] * relu(bn(y))[p][c]; z fp32 NHWC [N,H,W,K] */
+int eunet_bnrelu_conv1x1(const eunet_act* y, const float* scale, const float* shift,
+                         const float* w, const float* b, int k, float* z, void* stream);
+
+/* ---- enhance head at 2H + residual + 2x2 mean (models.py:308-313,336-337;
+ *      train_eval.py:306-310 resize == 2x2 mean) ------------------------------
+ * z: [N,H,W,K] fp32. out2h (nullable) [N,K,2H,2W] fp32 NCHW, logits
+ * (nullable) [N,K,H,W] fp32 NCHW.  Head BN stats saved in mean/invstd (64). */
+int eunet_head_workspace_bytes(int n, int h, int w, int k, size_t* bytes);
+int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1,
+                   const float* gamma, const float* beta, const float* w2, const float* b2,
+                   int training, float eps, float momentum, float* run_mean, float* run_var,
+                   float* mean, float* invstd, float* out2h, float* logits, void* ws,
+                   void* stream);
+/* backward from g_logits (or g_out2h when g_logits == NULL).  Writes gz and the
+ * head parameter gradients gw1 [64][K][3][3], gb1, ggamma, gbeta, gw2 [K][64], gb2. */
+int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1,
+                   const float* gamma, const float* beta, const float* w2, const float* mean,
+                   const float* invstd, const float* g_logits, const float* g_out2h, float* gz,
+                   float* gw1, float* gb1, float* ggamma, float* gbeta, float* gw2, float* gb2,
+                   void* ws, void* stream);
+
+/* ---- combined loss (train_eval.py:28-60, 134-197, 262-337) ----------------
+ * logits [N,K,H,W] fp32 NCHW, target [N,H,W] int64; K <= 3.
+ * loss = (1/N) sum_n [2.5 focal_n + 2.5 dice_n + 1.0 tversky_n].
+ * sums (caller-owned, saved for backward): [N][1+3K] fp32; loss: 1 fp32 on device.
+ * parts (nullable): [N][3] focal/dice/tversky per sample. */
+int eunet_loss_workspace_bytes(int n, int k, int h, int w, size_t* bytes);
+int eunet_loss_fwd(const float* logits, const int64_t* target, int n, int k, int h, int w,
+                   float* sums, float* loss, float* parts, void* ws, void* stream);
+/* glogits = d loss / d logits * (*gloss) (gloss: device scalar) */
+int eunet_loss_bwd(const float* logits, const int64_t* target, int n, int k, int h, int w,
+                   const float* sums, const float* gloss, float* glogits, void* stream);
+
+/* ---- backward helpers ----------------------------------------------------
+ * BN(+ReLU) backward (autograd of models.py:220-224): g is the gradient w.r.t.
+ * the ReLU output, y the pre-BN conv output.  reduce -> part [tiles][2][c]
+ * (sum g', sum g'*xhat); colsum -> (dbeta, dgamma); apply -> gy. */
+int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles);
+int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mean,
+                        const float* invstd, const float* gamma, const float* beta, float* part,
+                        void* stream);
+int eunet_colsum(const float* part, int rows, int cols, float* out, void* stream);
+int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean,
+                       const float* invstd, const float* gamma, const float* beta,
+                       const float* dbeta, const float* dgamma, const eunet_act* gy,
+                       void* stream);
+/* MaxPool2d backward (first max in row-major order wins, recomputed from the
+ * saved activation) + the skip-path gradient: gout = gskip + scatter(gpool) */
+int eunet_pool_bwd_add(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
+                       const eunet_act* gout, void* stream);
+/* Upsample x2 backward (adjoint of the bilinear taps) */
+int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream);
+/* dec1 1x1 backward: gact = W^T gz (w.r.t. relu(bn(y))), part [tiles][K*C + K]
+ * = per-tile (gW, gb) partials */
+int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles);
+int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift,
+                      const float* w, int k, const float* gz, const eunet_act* gact, float* part,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EUNET_H */

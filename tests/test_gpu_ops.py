@@ -1,0 +1,342 @@
+"""Per-kernel numerics through the C-ABI vs plain PyTorch fp64 references (GPU only).
+
+fp32 kernels (exact-fp32 MFMA / VALU) are held to 1e-4 relative; bf16
+kernels (bf16 operands, fp32 accumulation) to 2e-2 relative of the output scale.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from eunet import ops
+    return ops
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("transform", [False, True])
+def test_conv3x3_fwd_stats(dt, transform):
+    ops = _ops()
+    g = torch.Generator().manual_seed(1)
+    N, H, W, Cin, Cout, CT, CO = 2, 20, 36, 32, 80, 48, 8
+    buf = torch.randn(N, H, W, CT, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 17.0
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    sc = torch.rand(Cin, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(Cin, generator=g, dtype=torch.float64) * 0.3
+    xd = buf.to(DEV, dt)
+    xq = xd.double().cpu()[..., CO:CO + Cin]  # rounded input the kernel sees
+    xt = nchw(xq)
+    if transform:
+        xt = torch.relu(xt * sc[None, :, None, None] + sh[None, :, None, None])
+        if dt == torch.bfloat16:
+            xt = xt.to(torch.bfloat16).double()
+    wq = w.to(dt).double()
+    ref = nhwc(F.conv2d(xt, wq, b, padding=1))
+    y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
+    tiles = ops.conv3x3_tiles(ops.act(y))
+    st = torch.empty(tiles * (2 * Cout + 1), dtype=torch.float32, device=DEV)
+    ops.conv3x3_fwd(ops.act(xd, CO, Cin), wp, ops.act(y), bias=b.float().to(DEV),
+                    scale=sc.float().to(DEV) if transform else None,
+                    shift=sh.float().to(DEV) if transform else None, stats=st)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < TOL[dt]
+    # BN statistics via finalize
+    gamma = torch.ones(Cout, device=DEV)
+    beta = torch.zeros(Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mean, inv = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    s1, s2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, rm, rv, mean, inv, s1, s2)
+    torch.cuda.synchronize()
+    yr = y.double().cpu() if dt == torch.float32 else ref
+    m_ref = yr.mean(dim=(0, 1, 2))
+    v_ref = yr.var(dim=(0, 1, 2), unbiased=False)
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert rel(mean, m_ref) < tol
+    assert rel(1.0 / inv ** 2 - 1e-5, v_ref) < tol * 10
+    n = N * H * W
+    assert rel(rv, 0.9 + 0.1 * v_ref * n / (n - 1)) < tol * 10
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_dgrad_wgrad(dt):
+    ops = _ops()
+    g = torch.Generator().manual_seed(2)
+    N, H, W, Cin, Cout = 2, 16, 40, 48, 64
+    x = torch.randn(N, H, W, Cin, generator=g, dtype=torch.float64).to(dt).double()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 20).to(dt).double()
+    gy = torch.randn(N, H, W, Cout, generator=g, dtype=torch.float64).to(dt).double()
+    sc = torch.rand(Cin, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(Cin, generator=g, dtype=torch.float64) * 0.3
+    xt = nchw(x).requires_grad_(True)
+    xa = torch.relu(xt * sc[None, :, None, None] + sh[None, :, None, None])
+    xa_q = xa.to(dt).double() if dt == torch.bfloat16 else xa
+    wt = w.clone().requires_grad_(True)
+    y = F.conv2d(xa_q.detach() if dt == torch.bfloat16 else xa, wt, None, padding=1)
+    y.backward(nchw(gy))
+    # dgrad (w.r.t. the conv input, i.e. before the transform): kernel computes W^T gy
+    gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w, padding=1))
+    gxd = torch.empty(N, H, W, Cin, dtype=dt, device=DEV)
+    wpt = ops.conv3x3_pack(w.float().to(DEV), dt, flip=True)
+    ops.conv3x3_fwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gxd))
+    # wgrad with fused transform
+    dyd = gy.to(DEV, dt)
+    ns = ops.conv3x3_wgrad_splits(ops.act(dyd), Cin, dt)
+    dwp = torch.empty(ns * Cout * 9 * Cin, device=DEV)
+    dbp = torch.empty(ns * Cout, device=DEV)
+    ops.conv3x3_wgrad(ops.act(x.to(DEV, dt)), ops.act(dyd), dwp, dbp, ns, scale=sc.float().to(DEV),
+                      shift=sh.float().to(DEV))
+    dw = torch.empty(Cout, Cin, 3, 3, device=DEV)
+    db = torch.empty(Cout, device=DEV)
+    ops.wgrad_reduce(dwp, dbp, ns, Cout, Cin, 9, dw, db)
+    torch.cuda.synchronize()
+    assert rel(gxd, gx_ref) < TOL[dt]
+    assert rel(dw, wt.grad) < TOL[dt]
+    assert rel(db, gy.sum(dim=(0, 1, 2))) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin", [1, 3])
+def test_conv_small(dt, cin):
+    ops = _ops()
+    g = torch.Generator().manual_seed(3)
+    N, H, W, Cout = 2, 24, 40, 64
+    x = torch.rand(N, H, W, cin, generator=g, dtype=torch.float64).to(dt).double()
+    w = torch.randn(Cout, cin, 3, 3, generator=g, dtype=torch.float64) / 3
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    ref = nhwc(F.conv2d(nchw(x), w, b, padding=1))
+    y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    tiles = ops.conv3x3_tiles(ops.act(y))
+    st = torch.empty(tiles * (2 * Cout + 1), device=DEV)
+    ops.conv_small_fwd(ops.act(x.to(DEV, dt)), w.float().to(DEV), b.float().to(DEV), ops.act(y), st)
+    gy = torch.randn(N, H, W, Cout, generator=g, dtype=torch.float64).to(dt).double()
+    ns = ops.conv_small_wgrad_splits(ops.act(gy.to(DEV, dt)))
+    dwp = torch.empty(ns * Cout * 9 * cin, device=DEV)
+    dbp = torch.empty(ns * Cout, device=DEV)
+    ops.conv_small_wgrad(ops.act(x.to(DEV, dt)), ops.act(gy.to(DEV, dt)), dwp, dbp, ns)
+    dw = torch.empty(Cout, cin, 3, 3, device=DEV)
+    db = torch.empty(Cout, device=DEV)
+    ops.wgrad_reduce(dwp, dbp, ns, Cout, cin, 9, dw, db)
+    wt = w.clone().requires_grad_(True)
+    F.conv2d(nchw(x), wt, None, padding=1).backward(nchw(gy))
+    torch.cuda.synchronize()
+    assert rel(y, ref) < TOL[dt]
+    assert rel(dw, wt.grad) < 1e-4
+    assert rel(db, gy.sum(dim=(0, 1, 2))) < 1e-4
+    gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    mean, inv = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, None, None, mean, inv, None, None)
+    torch.cuda.synchronize()
+    yr = y.double().cpu()
+    assert rel(mean, yr.mean(dim=(0, 1, 2))) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bnrelu_pool_up_conv1x1(dt):
+    ops = _ops()
+    g = torch.Generator().manual_seed(4)
+    N, H, W, C = 2, 12, 20, 32
+    y = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).to(dt).double()
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(C, generator=g, dtype=torch.float64) * 0.3
+    a = torch.relu(y * sc + sh)
+    yd = y.to(DEV, dt)
+    scd, shd = sc.float().to(DEV), sh.float().to(DEV)
+    # pool (+ act into a concat slot)
+    cat = torch.zeros(N, H, W, C + 16, dtype=dt, device=DEV)
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=dt, device=DEV)
+    ops.bnrelu_pool(ops.act(yd), scd, shd, ops.act(cat, 16, C), ops.act(pooled))
+    # upsample into a slot
+    up = torch.zeros(N, 2 * H, 2 * W, C + 8, dtype=dt, device=DEV)
+    ops.bnrelu_upsample(ops.act(yd), scd, shd, ops.act(up, 0, C))
+    # dec1 1x1
+    K = 3
+    w = torch.randn(K, C, generator=g, dtype=torch.float64) / 5
+    b = torch.randn(K, generator=g, dtype=torch.float64)
+    z = torch.empty(N, H, W, K, device=DEV)
+    ops.bnrelu_conv1x1(ops.act(yd), scd, shd, w.float().to(DEV), b.float().to(DEV), K, z)
+    torch.cuda.synchronize()
+    tol = TOL[dt]
+    assert rel(cat[..., 16:], a) < tol
+    assert float(cat[..., :16].abs().max()) == 0.0
+    assert rel(pooled, nhwc(F.max_pool2d(nchw(a), 2))) < tol
+    up_ref = nhwc(F.interpolate(nchw(a), scale_factor=2, mode="bilinear", align_corners=False))
+    assert rel(up[..., :C], up_ref) < tol
+    assert float(up[..., C:].abs().max()) == 0.0
+    assert rel(z, a @ w.t() + b) < tol
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_backward_helpers(dt):
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    N, H, W, C = 2, 8, 16, 32
+    # --- BN + ReLU backward
+    y = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).to(dt).double()
+    gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, generator=g, dtype=torch.float64) * 0.2
+    go = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).to(dt).double()
+    yt = nchw(y).requires_grad_(True)
+    gt, bt = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    out = torch.relu(F.batch_norm(yt, None, None, gt, bt, True, 0.1, 1e-5))
+    out.backward(nchw(go))
+    mean = y.mean(dim=(0, 1, 2))
+    inv = 1.0 / torch.sqrt(y.var(dim=(0, 1, 2), unbiased=False) + 1e-5)
+    gd, yd = go.to(DEV, dt), y.to(DEV, dt)
+    f = lambda t: t.float().to(DEV)
+    tiles = ops.bn_bwd_tiles(ops.act(yd))
+    part = torch.empty(tiles * 2 * C, device=DEV)
+    ops.bn_bwd_reduce(ops.act(gd), ops.act(yd), f(mean), f(inv), f(gamma), f(beta), part)
+    red = torch.empty(2 * C, device=DEV)
+    ops.colsum(part, tiles, 2 * C, red)
+    gy = torch.empty_like(yd)
+    ops.bn_bwd_apply(ops.act(gd), ops.act(yd), f(mean), f(inv), f(gamma), f(beta), red[:C], red[C:], ops.act(gy))
+    torch.cuda.synchronize()
+    assert rel(red[:C], bt.grad) < 1e-4
+    assert rel(red[C:], gt.grad) < 1e-4
+    assert rel(gy, nhwc(yt.grad)) < TOL[dt]
+    # --- max-pool backward + skip add (with ties)
+    act = torch.relu(torch.randn(N, H, W, C, generator=g, dtype=torch.float64)).to(dt).double()
+    act[0, 0, 0, :] = act[0, 0, 1, :]  # tie inside a window
+    gp = torch.randn(N, H // 2, W // 2, C, generator=g, dtype=torch.float64).to(dt).double()
+    gs = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).to(dt).double()
+    at = nchw(act).requires_grad_(True)
+    F.max_pool2d(at, 2).backward(nchw(gp))
+    out_ref = nhwc(at.grad) + gs
+    cat = torch.zeros(N, H, W, C + 8, dtype=dt, device=DEV)
+    cat[..., 8:] = act.to(DEV, dt)
+    gcat = torch.zeros(N, H, W, C + 8, dtype=dt, device=DEV)
+    gcat[..., 8:] = gs.to(DEV, dt)
+    gout = torch.empty(N, H, W, C, dtype=dt, device=DEV)
+    ops.pool_bwd_add(ops.act(cat, 8, C), ops.act(gp.to(DEV, dt)), ops.act(gcat, 8, C), ops.act(gout))
+    # --- upsample backward from a channel slice
+    gh = torch.randn(N, 2 * H, 2 * W, C + 16, generator=g, dtype=torch.float64).to(dt).double()
+    lo = torch.zeros(N, H, W, C, dtype=torch.float64).requires_grad_(True)
+    F.interpolate(nchw(lo), scale_factor=2, mode="bilinear", align_corners=False).backward(nchw(gh[..., :C]))
+    glo = torch.empty(N, H, W, C, dtype=dt, device=DEV)
+    ops.upsample_bwd(ops.act(gh.to(DEV, dt), 0, C), ops.act(glo))
+    torch.cuda.synchronize()
+    assert rel(gout, out_ref) < TOL[dt]
+    assert rel(glo, lo.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv1x1_bwd(dt):
+    ops = _ops()
+    g = torch.Generator().manual_seed(6)
+    N, H, W, C, K = 2, 8, 24, 64, 2
+    y = torch.randn(N, H, W, C, generator=g, dtype=torch.float64).to(dt).double()
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(C, generator=g, dtype=torch.float64) * 0.3
+    w = torch.randn(K, C, generator=g, dtype=torch.float64) / 4
+    gz = torch.randn(N, H, W, K, generator=g, dtype=torch.float64)
+    a = torch.relu(y * sc + sh)
+    yd = y.to(DEV, dt)
+    gact = torch.empty_like(yd)
+    tiles = ops.conv1x1_bwd_tiles(ops.act(yd))
+    part = torch.empty(tiles * (K * C + K), device=DEV)
+    ops.conv1x1_bwd(ops.act(yd), sc.float().to(DEV), sh.float().to(DEV), w.float().to(DEV), K, gz.float().to(DEV),
+                    ops.act(gact), part)
+    red = torch.empty(K * C + K, device=DEV)
+    ops.colsum(part, tiles, K * C + K, red)
+    torch.cuda.synchronize()
+    assert rel(gact, gz @ w) < TOL[dt]
+    gw_ref = torch.einsum("nhwk,nhwc->kc", gz, a)
+    assert rel(red[:K * C].view(K, C), gw_ref) < TOL[dt]
+    assert rel(red[K * C:], gz.sum(dim=(0, 1, 2))) < 1e-4
+
+
+def _head_ref(z, w1, b1, gamma, beta, w2, b2):
+    u = F.interpolate(z, scale_factor=2, mode="bilinear", align_corners=False)
+    h = F.conv2d(u, w1, b1, padding=1)
+    a = torch.relu(F.batch_norm(h, None, None, gamma, beta, True, 0.1, 1e-5))
+    return u + F.conv2d(a, w2, b2)
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_head_fwd_bwd(K):
+    ops = _ops()
+    g = torch.Generator().manual_seed(7)
+    N, H, W = 2, 12, 20
+    z = torch.randn(N, K, H, W, generator=g, dtype=torch.float64)
+    w1 = torch.randn(64, K, 3, 3, generator=g, dtype=torch.float64) / 4
+    b1 = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
+    gamma = torch.rand(64, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
+    w2 = torch.randn(K, 64, 1, 1, generator=g, dtype=torch.float64) / 8
+    b2 = torch.randn(K, generator=g, dtype=torch.float64) * 0.1
+    leaves = [t.clone().requires_grad_(True) for t in (z, w1, b1, gamma, beta, w2, b2)]
+    out = _head_ref(*leaves)
+    logit_ref = F.avg_pool2d(out, 2)
+    glog = torch.randn(N, K, H, W, generator=g, dtype=torch.float64)
+    logit_ref.backward(glog)
+    f = lambda t: t.float().contiguous().to(DEV)
+    zd = f(nhwc(z))
+    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K), dtype=torch.uint8, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    mean, inv = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    out2h = torch.empty(N, K, 2 * H, 2 * W, device=DEV)
+    logits = torch.empty(N, K, H, W, device=DEV)
+    ops.head_fwd(zd, N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2.reshape(K, 64)), f(b2), True, 1e-5, 0.1,
+                 rm, rv, mean, inv, out2h, logits, ws)
+    gz = torch.empty(N, H, W, K, device=DEV)
+    gw1, gb1 = torch.empty(64, K, 3, 3, device=DEV), torch.empty(64, device=DEV)
+    gg, gbt = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    gw2, gb2 = torch.empty(K, 64, device=DEV), torch.empty(K, device=DEV)
+    ops.head_bwd(zd, N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2.reshape(K, 64)), mean, inv, f(glog), None,
+                 gz, gw1, gb1, gg, gbt, gw2, gb2, ws)
+    torch.cuda.synchronize()
+    assert rel(out2h, out) < 1e-4
+    assert rel(logits, logit_ref) < 1e-4
+    assert rel(gz, nhwc(leaves[0].grad)) < 1e-4
+    assert rel(gw1, leaves[1].grad) < 1e-4
+    assert rel(gg, leaves[3].grad) < 1e-4
+    assert rel(gbt, leaves[4].grad) < 1e-4
+    assert rel(gw2, leaves[5].grad.reshape(K, 64)) < 1e-4
+    assert rel(gb2, leaves[6].grad) < 1e-4
+    assert float(gb1.abs().max()) < 1e-3 * float(gw1.abs().max()) + 1e-5  # pre-BN bias: ~0
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_loss_fwd_bwd(K):
+    from oracle import eunet_ref as R
+    ops = _ops()
+    g = torch.Generator().manual_seed(8)
+    N, H, W = 3, 20, 28
+    logits = torch.randn(N, K, H, W, generator=g, dtype=torch.float64) * 2
+    target = torch.randint(0, K, (N, H, W), generator=g)
+    lt = logits.clone().requires_grad_(True)
+    ref = sum(R.combined_loss(lt[i], target[i]) for i in range(N)) / N
+    ref.backward()
+    from eunet.losses import combined_loss
+    ld = logits.float().to(DEV).requires_grad_(True)
+    loss, parts = combined_loss(ld, target.to(DEV), return_parts=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
+    assert rel(ld.grad, lt.grad) < 1e-4
+    p0 = R.combined_loss(logits[0], target[0], parts=True)[1]
+    assert abs(parts[0, 0].item() - p0["focal"].item()) < 1e-5 * abs(p0["focal"].item()) + 1e-7
