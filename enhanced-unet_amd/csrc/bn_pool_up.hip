@@ -406,13 +406,30 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, 
   }
 }
 
-__global__ __launch_bounds__(NT) void colsum_kernel(const float* part, int rows, int cols, int ld, float* out) {
+// deterministic two-stage column sum of a [rows][ld] fp32 partial matrix:
+// stage 1 -> fp64 partials [RB][cols] (fixed row chunks), stage 2 -> out[cols]
+constexpr int COLSUM_RB_MAX = 256;
+__global__ __launch_bounds__(NT) void colsum_stage1(const float* part, int rows, int cols, int ld, int chunk,
+                                                    double* ws) {
+  __shared__ double sh[4][64];
+  const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  double s = 0.0;
+  if (col < cols)
+    for (int r = r0 + rg; r < r1; r += 4) s += (double)part[(long long)r * ld + col];
+  sh[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && col < cols) ws[(long long)blockIdx.y * cols + col] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
+}
+
+__global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, int cols, float* out) {
   __shared__ double sh[4][64];
   const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int col = blockIdx.x * 64 + cl;
   double s = 0.0;
   if (col < cols)
-    for (int r = rg; r < rows; r += 4) s += (double)part[(long long)r * ld + col];
+    for (int r = rg; r < rb; r += 4) s += ws[(long long)r * cols + col];
   sh[rg][cl] = s;
   __syncthreads();
   if (rg == 0 && col < cols) out[col] = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
@@ -614,9 +631,19 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
 }  // namespace
 
 // ===========================================================================
-int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, hipStream_t s) {
-  EUNET_REQUIRE(part && out && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
-  colsum_kernel<<<cdiv(cols, 64), NT, 0, s>>>(part, rows, cols, ld, out);
+static int colsum_rb(int rows) {
+  int rb = (rows + 63) / 64;
+  return rb < 1 ? 1 : (rb > COLSUM_RB_MAX ? COLSUM_RB_MAX : rb);
+}
+
+size_t eunet_colsum_ws(int rows, int cols) { return (size_t)colsum_rb(rows) * cols * sizeof(double); }
+
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s) {
+  EUNET_REQUIRE(part && out && ws && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
+  const int rb = colsum_rb(rows);
+  const int chunk = cdiv(rows, rb);
+  colsum_stage1<<<dim3(cdiv(cols, 64), rb), NT, 0, s>>>(part, rows, cols, ld, chunk, (double*)ws);
+  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, out);
   EUNET_LAUNCH_CHECK("colsum");
   return EUNET_OK;
 }
@@ -784,9 +811,14 @@ int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mea
   return EUNET_OK;
 }
 
-int eunet_colsum(const float* part, int rows, int cols, float* out, void* stream) {
-  EUNET_REQUIRE(part && out && rows > 0 && cols > 0, "colsum: bad args");
-  return eunet_colsum_ld(part, rows, cols, cols, out, (hipStream_t)stream);
+int eunet_colsum_ws_bytes(int rows, int cols, size_t* bytes) {
+  EUNET_REQUIRE(bytes && rows > 0 && cols > 0, "colsum_ws_bytes: bad args");
+  *bytes = eunet_colsum_ws(rows, cols);
+  return EUNET_OK;
+}
+
+int eunet_colsum(const float* part, int rows, int cols, float* out, void* ws, void* stream) {
+  return eunet_colsum_ld(part, rows, cols, cols, out, ws, (hipStream_t)stream);
 }
 
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,

@@ -80,70 +80,84 @@ __device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int
   *(uint4*)(lds + (q * HPXP + hp) * 16) = v;
 }
 
+// v2: 512 threads = 8 waves (2 per SIMD); wave w computes output row w of the
+// 8x32 tile (32 px x 64 co = 2x4 MFMA tiles).  LDS is double-buffered: the next
+// chunk's global loads go to registers before the MFMAs of the current chunk
+// and are written (with the BN+ReLU transform) into the other buffer right
+// after them, so there is ONE barrier per K-chunk.  The epilogue stages the
+// tile through LDS and stores whole 16-byte vectors.
+constexpr int FT = 512;
+constexpr int FA_ITERS = (A_UNITS + FT - 1) / FT;  // 3
+constexpr int FB_ITERS = B_UNITS / FT;             // 4 full rounds ...
+constexpr int FB_TAIL = B_UNITS - FB_ITERS * FT;   // ... + 256 units for threads 0..255
+constexpr int STAGE_BYTES = A_LDS_BYTES + B_LDS_BYTES;  // 59392
+constexpr int OUT_LD = 68;                              // fp32 row stride of the output staging tile
+constexpr int FWD_LDS = 2 * STAGE_BYTES;                // 118784 (>= 256*68*4 + 2*8*64*4)
+
 template <typename T>
-__global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(FT, 1) void conv3x3_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* As = smem;
-  char* Bs = smem + A_LDS_BYTES;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int tile = blockIdx.x;
   const int tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
   const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
   const int co0 = blockIdx.y * BN;
+  const int q = lane >> 4, li = lane & 15;
 
-  f32x4 acc[4][4];
+  f32x4 acc[2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[A_ITERS];
-  bool rok[A_ITERS];
-  uint4 rb[B_ITERS];
-  const uint4* wp = (const uint4*)a.wp;
+  uint4 ra[FA_ITERS];
+  bool rok[FA_ITERS];
+  u32x4 rb[FB_ITERS];
+  u32x4 rbt = (u32x4){0u, 0u, 0u, 0u};
+  const u32x4* wp = (const u32x4*)a.wp;
+  const bool tail = tid < FB_TAIL;
 
+#define CONV_BUNIT(ID_, KC_) \
+  wp[((long long)((KC_) * 4 + (ID_) / (BN * 9)) * a.cout_pad + co0) * 9 + (ID_) % (BN * 9)]
 #define CONV_GLOAD(KC_)                                                                       \
   do {                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < A_ITERS; ++i)                                       \
-        ra[i] = load_halo_unit<T>(a, n, y0, x0, tid + i * NTHR, (KC_), rok[i]);               \
-    _Pragma("unroll") for (int i = 0; i < B_ITERS; ++i) {                                     \
-      const int id_ = tid + i * NTHR;                                                         \
-      const int q_ = id_ / (BN * 9), r_ = id_ - q_ * (BN * 9);                                \
-      rb[i] = wp[((long long)((KC_) * 4 + q_) * a.cout_pad + co0) * 9 + r_];                  \
-    }                                                                                         \
+    _Pragma("unroll") for (int i = 0; i < FA_ITERS; ++i)                                      \
+        ra[i] = load_halo_unit<T>(a, n, y0, x0, tid + i * FT, (KC_), rok[i]);                 \
+    _Pragma("unroll") for (int i = 0; i < FB_ITERS; ++i) rb[i] = CONV_BUNIT(tid + i * FT, KC_); \
+    if (tail) rbt = CONV_BUNIT(tid + FB_ITERS * FT, KC_);                                     \
   } while (0)
-#define CONV_LWRITE(KC_)                                                                      \
+#define CONV_LWRITE(KC_, BUF_)                                                                \
   do {                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < A_ITERS; ++i)                                       \
-        store_halo_unit<T>(a, As, tid + i * NTHR, (KC_), ra[i], rok[i]);                      \
-    _Pragma("unroll") for (int i = 0; i < B_ITERS; ++i)                                       \
-        *(uint4*)(Bs + (tid + i * NTHR) * 16) = rb[i];                                         \
+    char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
+    char* Bs_ = As_ + A_LDS_BYTES;                                                            \
+    _Pragma("unroll") for (int i = 0; i < FA_ITERS; ++i)                                      \
+        store_halo_unit<T>(a, As_, tid + i * FT, (KC_), ra[i], rok[i]);                       \
+    _Pragma("unroll") for (int i = 0; i < FB_ITERS; ++i) *(u32x4*)(Bs_ + (tid + i * FT) * 16) = rb[i]; \
+    if (tail) *(u32x4*)(Bs_ + (tid + FB_ITERS * FT) * 16) = rbt;                              \
   } while (0)
 
   CONV_GLOAD(0);
-  CONV_LWRITE(0);
+  CONV_LWRITE(0, 0);
   __syncthreads();
-  const int q = lane >> 4, li = lane & 15;
   for (int kc = 0; kc < a.nkc; ++kc) {
+    const int cur = kc & 1;
     if (kc + 1 < a.nkc) CONV_GLOAD(kc + 1);
+    const char* As = smem + cur * STAGE_BYTES;
+    const char* Bs = As + A_LDS_BYTES;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int ky = t / 3, kx = t - ky * 3;
-      uint4 fa[4], fb[4];
+      uint4 fa[2], fb[4];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int r = 2 * wv + (mt >> 1), c = (mt & 1) * 16 + li;
-        const int hp = (r + ky) * HW_ + c + kx;
+      for (int mt = 0; mt < 2; ++mt) {
+        const int hp = (wv + ky) * HW_ + mt * 16 + li + kx;
         fa[mt] = *(const uint4*)(As + (q * HPXP + hp) * 16);
       }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int co = nt * 16 + li;
-        fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + co * 9 + t) * 16);
-      }
+      for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           if constexpr (sizeof(T) == 2) {
@@ -158,104 +172,110 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           }
         }
     }
+    if (kc + 1 < a.nkc) CONV_LWRITE(kc + 1, cur ^ 1);
     __syncthreads();
-    if (kc + 1 < a.nkc) {
-      CONV_LWRITE(kc + 1);
-      __syncthreads();
-    }
   }
+#undef CONV_GLOAD
+#undef CONV_LWRITE
+#undef CONV_BUNIT
 
-  // ---- epilogue: bias, store, BN partials ---------------------------------
+  // ---- epilogue: bias, BN partials, LDS-staged vector stores ---------------
   const int vh = min(TH, a.H - y0), vw = min(TW, a.W - x0);
-  float bias_v[4];
+  const bool rv = wv < vh;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int co = co0 + nt * 16 + li;
-    bias_v[nt] = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
-  }
-  T* yp = (T*)a.y;
+    const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int r = 2 * wv + (mt >> 1);
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[mt][nt][i] += bv;
+  }
+  float* stage = (float*)smem;                              // [256 px][OUT_LD]
+  float* red = (float*)(smem + TH * TW * OUT_LD * 4);       // [8][64] x 2
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = (mt & 1) * 16 + q * 4 + i;
-      const bool pv = r < vh && c < vw;
-      const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
+      const int px = wv * TW + mt * 16 + q * 4 + i;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int co = co0 + nt * 16 + li;
-        acc[mt][nt][i] += bias_v[nt];
-        if (pv && co < a.cout) Elem<T>::st(yp + pix * a.yct + a.yco + co, acc[mt][nt][i]);
-      }
+      for (int nt = 0; nt < 4; ++nt) stage[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
     }
-  }
-  if (a.stats == nullptr) return;
-  // per-channel (sum, M2) over the valid pixels of this tile
-  float* red = (float*)smem;  // reuse: [4 waves][64]
-  __syncthreads();
-  float s[4];
+  if (a.stats != nullptr) {
+    float s[4];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    float v = 0.f;
+    for (int nt = 0; nt < 4; ++nt) {
+      float v = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int r = 2 * wv + (mt >> 1);
+      for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = (mt & 1) * 16 + q * 4 + i;
-        v += (r < vh && c < vw) ? acc[mt][nt][i] : 0.f;
-      }
+        for (int i = 0; i < 4; ++i) v += (rv && mt * 16 + q * 4 + i < vw) ? acc[mt][nt][i] : 0.f;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      s[nt] = v;
     }
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    s[nt] = v;
-  }
-  if (q == 0) {
+    if (q == 0)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) red[wv * 64 + nt * 16 + li] = s[nt];
-  }
-  __syncthreads();
-  const float cnt = (float)(vh * vw);
-  float mean_b[4];
+      for (int nt = 0; nt < 4; ++nt) red[wv * 64 + nt * 16 + li] = s[nt];
+    __syncthreads();
+    const float cnt = (float)(vh * vw);
+    float mb[4];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int cl = nt * 16 + li;
-    mean_b[nt] = (red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl]) / cnt;
-  }
-  float sum_tile = 0.f;
-  if (tid < 64) sum_tile = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-  __syncthreads();
+    for (int nt = 0; nt < 4; ++nt) {
+      float t = 0.f;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    float v = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int r = 2 * wv + (mt >> 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = (mt & 1) * 16 + q * 4 + i;
-        const float d = acc[mt][nt][i] - mean_b[nt];
-        v += (r < vh && c < vw) ? d * d : 0.f;
-      }
+      for (int w = 0; w < 8; ++w) t += red[w * 64 + nt * 16 + li];
+      mb[nt] = t / cnt;
     }
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    s[nt] = v;
-  }
-  if (q == 0) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) red[256 + wv * 64 + nt * 16 + li] = s[nt];
-  }
-  __syncthreads();
-  if (tid < 64) {
-    const int co = co0 + tid;
-    const float m2 = red[256 + tid] + red[320 + tid] + red[384 + tid] + red[448 + tid];
-    if (co < a.cout) {
-      a.stats[((long long)tile * 2 + 0) * a.cout + co] = sum_tile;
-      a.stats[((long long)tile * 2 + 1) * a.cout + co] = m2;
+    for (int nt = 0; nt < 4; ++nt) {
+      float v = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float d = acc[mt][nt][i] - mb[nt];
+          v += (rv && mt * 16 + q * 4 + i < vw) ? d * d : 0.f;
+        }
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      s[nt] = v;
+    }
+    if (q == 0)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) red[512 + wv * 64 + nt * 16 + li] = s[nt];
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.cout) {
+      float sum = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        sum += red[w * 64 + tid];
+        m2 += red[512 + w * 64 + tid];
+      }
+      a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
+      a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
     }
     if (blockIdx.y == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
+  } else {
+    __syncthreads();
+  }
+  constexpr int E = Vec16<T>::N;
+  constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
+  T* yp = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TH * TW * UPX / FT; ++j) {
+    const int id = tid + j * FT;
+    const int px = id / UPX, u = id - px * UPX;
+    const int r = px / TW, c = px - r * TW;
+    const int co = co0 + u * E;
+    if (r < vh && c < vw && co < a.cout) {
+      const float* sp = stage + px * OUT_LD + u * E;
+      float f[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) f[e] = sp[e];
+      const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
+      *(uint4*)(yp + pix * a.yct + a.yco + co) = Vec16<T>::pack(f);
+    }
   }
 }
 
@@ -495,12 +515,16 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.bias = bias;
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
   a.stats = stats; a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
+  EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
+                "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   dim3 grid(a.ntiles, a.cout_pad / BN);
-  const size_t lds = A_LDS_BYTES + B_LDS_BYTES;
-  if (x->dtype == EUNET_BF16)
-    conv3x3_fwd_kernel<bf16_t><<<grid, NTHR, lds, (hipStream_t)stream>>>(a);
-  else
-    conv3x3_fwd_kernel<float><<<grid, NTHR, lds, (hipStream_t)stream>>>(a);
+  if (x->dtype == EUNET_BF16) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else {
+    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
+    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  }
   EUNET_LAUNCH_CHECK("conv3x3_fwd");
   return EUNET_OK;
 }

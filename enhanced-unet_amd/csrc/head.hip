@@ -5,28 +5,35 @@
 // train_eval.py:306-310 (bilinear 2H->H resize, == exact 2x2 mean).
 //
 // dec1 commutes with the upsample, so the host passes z = dec1(d2) at H
-// (K channels).  Everything at 2H -- u = up(z), the 64-channel conv output h,
-// BN, ReLU, the 1x1, the residual and the 2x2 mean -- is recomputed per 16x16
-// tile from z and never stored: the largest tensor of the network (64 ch at
-// 2H) costs no HBM traffic.  Passes: fwd = stats, out; bwd = bwd1 (1x1 and BN
-// reductions), bwd2 (g_h, gW1, and g_u = W1^T g_h + g_o) + upsample adjoint.
-// All fp32 (vector ALU; ~1.5 % of the step FLOPs).
+// (K channels).  u = up(z), the 64-channel conv output h, BN, ReLU, the 1x1,
+// the residual and the 2x2 mean are recomputed per 16x16 tile (at 2H) from z;
+// the 64-channel forward tensors at 2H are never stored.
+// Kernels (persistent grids of <= 1024 blocks; one partial row per block):
+//   fwd : stats (Chan-combined per-block BN partials) -> bn_finalize -> out
+//   bwd : bwd1  -> gW2, gb2, dbeta, dgamma (BN backward sums)
+//         gh    -> g_h (dtype T, stored once) and the per-tap products
+//                  v[p][k][t] = sum_c W1[c][k][t] g_h[p][c]
+//         gu    -> g_u[q] = g_o[q] + sum_t v[q - d_t][t]   (conv3x3 dgrad as a stencil)
+//         wgrad -> gW1, gb1 via MFMA (K = pixels; im2col of u built in LDS)
+//         upsample adjoint g_u -> g_z.
 #include "common.h"
 
 namespace {
 constexpr int NT = 256;
 constexpr int T2 = 16;  // tile side at 2H
 constexpr int MID = 64;
+constexpr int HEAD_BLOCKS = 1024;
 
 struct HeadArgs {
   const float* z; int N, h, w, K;
   const float* w1; const float* b1;
   const float* gamma; const float* beta; const float* w2; const float* b2;
-  const float* mean; const float* istd;   // bwd
-  const float* scale; const float* shift; // fwd out
+  const float* mean; const float* istd;    // bwd
+  const float* scale; const float* shift;  // fwd out
   const float* glog; const float* gout2h;
-  const float* dbeta; const float* dgamma; // bwd2
-  float* stats; float* out2h; float* logits; float* part; float* gu;
+  const float* dbeta; const float* dgamma;  // bwd gh
+  float* stats; float* out2h; float* logits; float* part;
+  void* gh; float* v; float* gu;
   int tx, ty, ntiles;
 };
 
@@ -41,36 +48,17 @@ __device__ __forceinline__ float up_val(const HeadArgs& a, int n, int oy, int ox
   return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
 }
 
-// fill su[(R x R) region starting at (oy0-off, ox0-off)][K], zero outside the image
-__device__ void fill_u(const HeadArgs& a, float* su, int n, int oy0, int ox0, int R, int off) {
+// su[(18 x 18) region starting at (oy0-1, ox0-1)][3], zero outside the image
+__device__ void fill_u(const HeadArgs& a, float* su, int n, int oy0, int ox0) {
   const int H2 = 2 * a.h, W2 = 2 * a.w;
-  for (int i = threadIdx.x; i < R * R; i += NT) {
-    const int hy = i / R, hx = i - hy * R;
-    const int oy = oy0 + hy - off, ox = ox0 + hx - off;
+  for (int i = threadIdx.x; i < 18 * 18; i += NT) {
+    const int hy = i / 18, hx = i - hy * 18;
+    const int oy = oy0 + hy - 1, ox = ox0 + hx - 1;
     const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
     for (int k = 0; k < a.K; ++k) su[i * 3 + k] = in ? up_val(a, n, oy, ox, k) : 0.f;
   }
 }
 
-// h[c] for the pixel whose 3x3 window starts at su cell (sy, sx) (region width R)
-template <int K>
-__device__ __forceinline__ void conv_h(const float* su, const float* w1s, const float* b1s, int sy, int sx, int R,
-                                       float (&h)[MID]) {
-  float uk[K * 9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int ky = t / 3, kx = t - ky * 3;
-#pragma unroll
-    for (int k = 0; k < K; ++k) uk[k * 9 + t] = su[((sy + ky) * R + sx + kx) * 3 + k];
-  }
-#pragma unroll
-  for (int c = 0; c < MID; ++c) {
-    float s = b1s[c];
-#pragma unroll
-    for (int j = 0; j < K * 9; ++j) s = fmaf(w1s[c * K * 9 + j], uk[j], s);
-    h[c] = s;
-  }
-}
 
 __device__ __forceinline__ void tile_coords(const HeadArgs& a, int tile, int& n, int& oy0, int& ox0) {
   const int tpi = a.tx * a.ty;
@@ -80,299 +68,528 @@ __device__ __forceinline__ void tile_coords(const HeadArgs& a, int tile, int& n,
   ox0 = (r % a.tx) * T2;
 }
 
-// thread -> pixel inside a 16x16 tile, 2x2 quads on lanes 4j..4j+3
-__device__ __forceinline__ void quad_pixel(int tid, int& r, int& c) {
-  const int blk = tid >> 2, sub = tid & 3;
-  r = 2 * (blk >> 3) + (sub >> 1);
-  c = 2 * (blk & 7) + (sub & 1);
-}
-
-template <int K>
-__global__ __launch_bounds__(NT) void head_stats_kernel(HeadArgs a) {
-  __shared__ float w1s[MID * K * 9], b1s[MID], su[18 * 18 * 3];
-  __shared__ float red[4][MID], meanb[MID], sums[MID];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  int n, oy0, ox0;
-  tile_coords(a, blockIdx.x, n, oy0, ox0);
-  for (int i = tid; i < MID * K * 9; i += NT) w1s[i] = a.w1[i];
-  if (tid < MID) b1s[tid] = a.b1[tid];
-  fill_u(a, su, n, oy0, ox0, 18, 1);
-  __syncthreads();
-  const int r = tid / T2, c = tid % T2;
-  const bool pv = oy0 + r < 2 * a.h && ox0 + c < 2 * a.w;
-  float h[MID];
-  conv_h<K>(su, w1s, b1s, r, c, 18, h);
-  float v[MID];
-#pragma unroll
-  for (int i = 0; i < MID; ++i) v[i] = pv ? h[i] : 0.f;
-  red[wv][lane] = wave_transpose_reduce64(v);
-  __syncthreads();
-  const float cnt = (float)(min(T2, 2 * a.h - oy0) * min(T2, 2 * a.w - ox0));
-  if (tid < MID) {
-    sums[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    meanb[tid] = sums[tid] / cnt;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < MID; ++i) {
-    const float d = h[i] - meanb[i];
-    v[i] = pv ? d * d : 0.f;
-  }
-  const float m2 = wave_transpose_reduce64(v);
-  __syncthreads();
-  red[wv][lane] = m2;
-  __syncthreads();
-  if (tid < MID) {
-    a.stats[((long long)blockIdx.x * 2 + 0) * MID + tid] = sums[tid];
-    a.stats[((long long)blockIdx.x * 2 + 1) * MID + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    if (tid == 0) a.stats[(long long)2 * MID * a.ntiles + blockIdx.x] = cnt;
-  }
-}
-
-template <int K>
-__global__ __launch_bounds__(NT) void head_out_kernel(HeadArgs a) {
-  __shared__ float w1s[MID * K * 9], b1s[MID], su[18 * 18 * 3], sc[MID], sh[MID], w2s[K * MID];
-  const int tid = threadIdx.x;
-  int n, oy0, ox0;
-  tile_coords(a, blockIdx.x, n, oy0, ox0);
-  for (int i = tid; i < MID * K * 9; i += NT) w1s[i] = a.w1[i];
-  for (int i = tid; i < K * MID; i += NT) w2s[i] = a.w2[i];
-  if (tid < MID) {
-    b1s[tid] = a.b1[tid];
-    sc[tid] = a.scale[tid];
-    sh[tid] = a.shift[tid];
-  }
-  fill_u(a, su, n, oy0, ox0, 18, 1);
-  __syncthreads();
-  int r, c;
-  quad_pixel(tid, r, c);
-  const int H2 = 2 * a.h, W2 = 2 * a.w;
-  const int oy = oy0 + r, ox = ox0 + c;
-  const bool pv = oy < H2 && ox < W2;
-  float h[MID];
-  conv_h<K>(su, w1s, b1s, r, c, 18, h);
-  float o[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) o[k] = a.b2[k];
-#pragma unroll
-  for (int i = 0; i < MID; ++i) {
-    const float act = fmaxf(fmaf(h[i], sc[i], sh[i]), 0.f);
-#pragma unroll
-    for (int k = 0; k < K; ++k) o[k] = fmaf(w2s[k * MID + i], act, o[k]);
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const float u = su[((r + 1) * 18 + c + 1) * 3 + k];
-    const float val = u + o[k];
-    if (pv && a.out2h) a.out2h[(((long long)n * K + k) * H2 + oy) * W2 + ox] = val;
-    float s = val + __shfl_xor(val, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if (pv && a.logits && (tid & 3) == 0)
-      a.logits[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)] = 0.25f * s;
-  }
-}
-
 __device__ __forceinline__ float g_out(const HeadArgs& a, int K, int n, int k, int oy, int ox) {
   if (a.glog) return 0.25f * a.glog[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)];
   return a.gout2h[(((long long)n * K + k) * (2 * a.h) + oy) * (2 * a.w) + ox];
 }
 
-// pass 1: gW2, gb2 and the BN backward sums (dbeta = sum g_bn, dgamma = sum g_bn*xhat)
+// Thread mapping: 8 lanes per pixel, lane group g = lane & 7 owns channels 8g..8g+7;
+// a 256-thread block covers 32 pixels per pass, 8 passes per 16x16 tile.
+// Quad order (pixel slots 4q..4q+3 = one 2x2 quad) so the 2x2 mean is a
+// lane reduction (xor 8, 16).
+__device__ __forceinline__ void pass_pixel(int pass, int tid, int& r, int& c) {
+  const int ps = tid >> 3;  // pixel slot 0..31
+  const int q = pass * 8 + (ps >> 2), sub = ps & 3;
+  r = 2 * (q >> 3) + (sub >> 1);
+  c = 2 * (q & 7) + (sub & 1);
+}
+
+// W1 transposed in LDS: w1t[j][64], j = k*9 + t; b1s[64]
+template <int K>
+__device__ __forceinline__ void load_w1t(const HeadArgs& a, float* w1t, float* b1s) {
+  for (int i = threadIdx.x; i < MID * K * 9; i += NT) {
+    const int c = i / (K * 9), j = i - c * (K * 9);
+    w1t[j * MID + c] = a.w1[i];
+  }
+  if (threadIdx.x < MID) b1s[threadIdx.x] = a.b1[threadIdx.x];
+}
+
+// h[e] = conv3x3(u) for channels 8g+e of the pixel whose 3x3 window starts at su (r, c)
+template <int K>
+__device__ __forceinline__ void conv_h8(const float* su, const float* w1t, const float* b1s, int r, int c, int g,
+                                        float (&h)[8]) {
+  const float4 b0 = *(const float4*)(b1s + 8 * g), b1 = *(const float4*)(b1s + 8 * g + 4);
+  h[0] = b0.x; h[1] = b0.y; h[2] = b0.z; h[3] = b0.w; h[4] = b1.x; h[5] = b1.y; h[6] = b1.z; h[7] = b1.w;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t / 3, kx = t - ky * 3;
+      const float u = su[((r + ky) * 18 + c + kx) * 3 + k];
+      const float4 w0 = *(const float4*)(w1t + (k * 9 + t) * MID + 8 * g);
+      const float4 w1 = *(const float4*)(w1t + (k * 9 + t) * MID + 8 * g + 4);
+      h[0] = fmaf(w0.x, u, h[0]); h[1] = fmaf(w0.y, u, h[1]); h[2] = fmaf(w0.z, u, h[2]); h[3] = fmaf(w0.w, u, h[3]);
+      h[4] = fmaf(w1.x, u, h[4]); h[5] = fmaf(w1.y, u, h[5]); h[6] = fmaf(w1.z, u, h[6]); h[7] = fmaf(w1.w, u, h[7]);
+    }
+}
+
+__device__ __forceinline__ void load8(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// sum over the 8 pixel slots of a wave (lanes with equal g)
+__device__ __forceinline__ float sum_pixels(float v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+// sum over the 8 channel groups of one pixel
+__device__ __forceinline__ float sum_groups(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// forward statistics: per-thread Welford over its pixels (8 channels), Chan
+// combine across lanes / waves, one (sum, M2, count) row per block
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(NT) void head_stats_kernel(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float w1t[K * 9 * MID];
+  __shared__ __attribute__((aligned(16))) float b1s[MID];
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float wn_s[4], wm_s[4][MID], wq_s[4][MID];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7;
+  load_w1t<K>(a, w1t, b1s);
+  float n = 0.f, mean[8], m2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int nn, oy0, ox0;
+    tile_coords(a, tile, nn, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, nn, oy0, ox0);
+    __syncthreads();
+    for (int pass = 0; pass < 8; ++pass) {
+      int r, c;
+      pass_pixel(pass, tid, r, c);
+      if (oy0 + r >= 2 * a.h || ox0 + c >= 2 * a.w) continue;
+      float h[8];
+      conv_h8<K>(su, w1t, b1s, r, c, g, h);
+      n += 1.f;
+      const float inv = 1.f / n;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = h[e] - mean[e];
+        mean[e] = fmaf(d, inv, mean[e]);
+        m2[e] = fmaf(d, h[e] - mean[e], m2[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 8; off <= 32; off <<= 1) {
+    const float nb = __shfl_xor(n, off, 64);
+    const float nt = n + nb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float mb = __shfl_xor(mean[e], off, 64), qb = __shfl_xor(m2[e], off, 64);
+      const float d = mb - mean[e];
+      if (nt > 0.f) {
+        mean[e] += d * nb / nt;
+        m2[e] += qb + d * d * n * nb / nt;
+      }
+    }
+    n = nt;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      wm_s[wv][8 * g + e] = mean[e];
+      wq_s[wv][8 * g + e] = m2[e];
+    }
+    if (lane == 0) wn_s[wv] = n;
+  }
+  __syncthreads();
+  if (tid < MID) {
+    double bn = 0.0, bm = 0.0, bq = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      const double nb = wn_s[w];
+      if (nb <= 0.0) continue;
+      const double d = (double)wm_s[w][tid] - bm, nt = bn + nb;
+      bm += d * nb / nt;
+      bq += (double)wq_s[w][tid] + d * d * bn * nb / nt;
+      bn = nt;
+    }
+    a.stats[((long long)blockIdx.x * 2 + 0) * MID + tid] = (float)(bm * bn);
+    a.stats[((long long)blockIdx.x * 2 + 1) * MID + tid] = (float)bq;
+    if (tid == 0) a.stats[(long long)2 * MID * gridDim.x + blockIdx.x] = (float)bn;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(NT) void head_out_kernel(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float w1t[K * 9 * MID];
+  __shared__ __attribute__((aligned(16))) float b1s[MID], sc[MID], sh[MID], w2s[K * MID];
+  __shared__ float su[18 * 18 * 3];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane & 7;
+  load_w1t<K>(a, w1t, b1s);
+  for (int i = tid; i < K * MID; i += NT) w2s[i] = a.w2[i];
+  if (tid < MID) {
+    sc[tid] = a.scale[tid];
+    sh[tid] = a.shift[tid];
+  }
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+    for (int pass = 0; pass < 8; ++pass) {
+      int r, c;
+      pass_pixel(pass, tid, r, c);
+      const int oy = oy0 + r, ox = ox0 + c;
+      const bool pv = oy < H2 && ox < W2;
+      float h[8], s8[8], t8[8];
+      conv_h8<K>(su, w1t, b1s, r, c, g, h);
+      load8(sc + 8 * g, s8);
+      load8(sh + 8 * g, t8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) h[e] = fmaxf(fmaf(h[e], s8[e], t8[e]), 0.f);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float w8[8];
+        load8(w2s + k * MID + 8 * g, w8);
+        float o = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o = fmaf(w8[e], h[e], o);
+        o = sum_groups(o);
+        const float val = su[((r + 1) * 18 + c + 1) * 3 + k] + a.b2[k] + o;
+        if (pv && g == 0 && a.out2h) a.out2h[(((long long)n * K + k) * H2 + oy) * W2 + ox] = val;
+        float q = val + __shfl_xor(val, 8, 64);
+        q += __shfl_xor(q, 16, 64);
+        if (pv && g == 0 && ((lane >> 3) & 3) == 0 && a.logits)
+          a.logits[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)] = 0.25f * q;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward pass 1: gW2, gb2, dbeta = sum g_bn, dgamma = sum g_bn * xhat
+// (per-thread register accumulators over the block's pixels)
+// ---------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(NT) void head_bwd1_kernel(HeadArgs a) {
-  __shared__ float w1s[MID * K * 9], b1s[MID], su[18 * 18 * 3], ga[MID], be[MID], mu[MID], is[MID], w2s[K * MID];
-  __shared__ float acc_s[(K + 2) * MID + K];
-  const int tid = threadIdx.x, lane = tid & 63;
-  int n, oy0, ox0;
-  tile_coords(a, blockIdx.x, n, oy0, ox0);
-  for (int i = tid; i < MID * K * 9; i += NT) w1s[i] = a.w1[i];
+  constexpr int STRIDE = (K + 2) * MID + K;
+  __shared__ __attribute__((aligned(16))) float w1t[K * 9 * MID];
+  __shared__ __attribute__((aligned(16))) float b1s[MID], ga[MID], be[MID], mu[MID], is[MID], w2s[K * MID];
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float red[4][STRIDE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7;
+  load_w1t<K>(a, w1t, b1s);
   for (int i = tid; i < K * MID; i += NT) w2s[i] = a.w2[i];
-  for (int i = tid; i < (K + 2) * MID + K; i += NT) acc_s[i] = 0.f;
   if (tid < MID) {
-    b1s[tid] = a.b1[tid];
     ga[tid] = a.gamma[tid];
     be[tid] = a.beta[tid];
     mu[tid] = a.mean[tid];
     is[tid] = a.istd[tid];
   }
-  fill_u(a, su, n, oy0, ox0, 18, 1);
+  float aw2[K][8], agb[8], agx[8], ab2[K];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    agb[e] = 0.f;
+    agx[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) aw2[k][e] = 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) ab2[k] = 0.f;
   __syncthreads();
-  int r, c;
-  quad_pixel(tid, r, c);
-  const int oy = oy0 + r, ox = ox0 + c;
-  const bool pv = oy < 2 * a.h && ox < 2 * a.w;
-  float h[MID];
-  conv_h<K>(su, w1s, b1s, r, c, 18, h);
-  float go[K];
+  float ga8[8], be8[8], mu8[8], is8[8];
+  load8(ga + 8 * g, ga8);
+  load8(be + 8 * g, be8);
+  load8(mu + 8 * g, mu8);
+  load8(is + 8 * g, is8);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+    for (int pass = 0; pass < 8; ++pass) {
+      int r, c;
+      pass_pixel(pass, tid, r, c);
+      const int oy = oy0 + r, ox = ox0 + c;
+      if (oy >= 2 * a.h || ox >= 2 * a.w) continue;
+      float h[8];
+      conv_h8<K>(su, w1t, b1s, r, c, g, h);
+      float go[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
-  float v[MID];
+      for (int k = 0; k < K; ++k) {
+        go[k] = g_out(a, K, n, k, oy, ox);
+        ab2[k] += (g == 0) ? go[k] : 0.f;
+      }
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (h[e] - mu8[e]) * is8[e];
+        const float pre = fmaf(ga8[e], xh, be8[e]);
+        const float act = fmaxf(pre, 0.f);
+        float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < MID; ++i) {
-      const float xh = (h[i] - mu[i]) * is[i];
-      v[i] = go[k] * fmaxf(fmaf(ga[i], xh, be[i]), 0.f);
+        for (int k = 0; k < K; ++k) {
+          aw2[k][e] = fmaf(go[k], act, aw2[k][e]);
+          s = fmaf(w2s[k * MID + 8 * g + e], go[k], s);
+        }
+        const float gbn = pre > 0.f ? s : 0.f;
+        agb[e] += gbn;
+        agx[e] = fmaf(gbn, xh, agx[e]);
+      }
     }
-    atomicAdd(&acc_s[k * MID + lane], wave_transpose_reduce64(v));
   }
-  // g_bn = (W2^T go) * [a > 0]
 #pragma unroll
-  for (int i = 0; i < MID; ++i) {
-    const float xh = (h[i] - mu[i]) * is[i];
-    float s = 0.f;
+  for (int e = 0; e < 8; ++e) {
+    agb[e] = sum_pixels(agb[e]);
+    agx[e] = sum_pixels(agx[e]);
 #pragma unroll
-    for (int k = 0; k < K; ++k) s = fmaf(w2s[k * MID + i], go[k], s);
-    v[i] = (fmaf(ga[i], xh, be[i]) > 0.f) ? s : 0.f;
+    for (int k = 0; k < K; ++k) aw2[k][e] = sum_pixels(aw2[k][e]);
   }
-  // keep g_bn in h (h no longer needed after computing xhat * g_bn)
 #pragma unroll
-  for (int i = 0; i < MID; ++i) {
-    const float xh = (h[i] - mu[i]) * is[i];
-    h[i] = v[i] * xh;
-  }
-  atomicAdd(&acc_s[K * MID + lane], wave_transpose_reduce64(v));
-  atomicAdd(&acc_s[(K + 1) * MID + lane], wave_transpose_reduce64(h));
+  for (int k = 0; k < K; ++k) ab2[k] = sum_pixels(ab2[k]);
+  if (lane < 8) {
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const float s = wave_sum(go[k]);
-    if (lane == 0) atomicAdd(&acc_s[(K + 2) * MID + k], s);
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[wv][k * MID + 8 * g + e] = aw2[k][e];
+      red[wv][K * MID + 8 * g + e] = agb[e];
+      red[wv][(K + 1) * MID + 8 * g + e] = agx[e];
+    }
+    if (g == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) red[wv][(K + 2) * MID + k] = ab2[k];
   }
   __syncthreads();
-  const int stride = (K + 2) * MID + K;
-  for (int i = tid; i < stride; i += NT) a.part[(long long)blockIdx.x * stride + i] = acc_s[i];
+  for (int i = tid; i < STRIDE; i += NT)
+    a.part[(long long)blockIdx.x * STRIDE + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
-// pass 2: g_h on the tile + 1-px halo -> gW1/gb1 partials and g_u (written to a.gu)
-template <int K>
-__global__ __launch_bounds__(NT) void head_bwd2_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float dyn[];
-  float* sgh = dyn;                  // [324][65]
-  float* su = sgh + 324 * 65;        // [400][3]
-  float* w1s = su + 400 * 3;         // [64*K*9]
-  float* b1s = w1s + MID * K * 9;    // [64]
-  float* prm = b1s + MID;            // ga, be, mu, is, dbeta, dgamma [6][64]
-  float* w2s = prm + 6 * MID;        // [K*64]
-  const int tid = threadIdx.x;
-  int n, oy0, ox0;
-  tile_coords(a, blockIdx.x, n, oy0, ox0);
-  for (int i = tid; i < MID * K * 9; i += NT) w1s[i] = a.w1[i];
-  for (int i = tid; i < K * MID; i += NT) w2s[i] = a.w2[i];
-  if (tid < MID) {
-    b1s[tid] = a.b1[tid];
-    prm[0 * MID + tid] = a.gamma[tid];
-    prm[1 * MID + tid] = a.beta[tid];
-    prm[2 * MID + tid] = a.mean[tid];
-    prm[3 * MID + tid] = a.istd[tid];
-    prm[4 * MID + tid] = a.dbeta[tid];
-    prm[5 * MID + tid] = a.dgamma[tid];
-  }
-  fill_u(a, su, n, oy0, ox0, 20, 2);
-  __syncthreads();
+// ---------------------------------------------------------------------------
+// backward: g_h (stored, dtype T) and the per-tap products v[p][k*9+t]
+// ---------------------------------------------------------------------------
+template <int K, typename T>
+__global__ __launch_bounds__(NT) void head_bwd_gh_kernel(HeadArgs a) {
+  constexpr int GLD = MID + 4;  // padded row of the per-pass g_h staging tile
+  __shared__ __attribute__((aligned(16))) float w1t[K * 9 * MID];
+  __shared__ __attribute__((aligned(16))) float b1s[MID], ga[MID], be[MID], mu[MID], is[MID], c1[MID], c2[MID];
+  __shared__ __attribute__((aligned(16))) float w2s[K * MID];
+  __shared__ __attribute__((aligned(16))) float gls[32 * GLD];
+  __shared__ float su[18 * 18 * 3];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane & 7, ps = tid >> 3;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const float inv_cnt = 1.f / ((float)a.N * (float)H2 * (float)W2);
-  for (int i = tid; i < 18 * 18; i += NT) {
-    const int gy = i / 18, gx = i - gy * 18;
-    const int oy = oy0 + gy - 1, ox = ox0 + gx - 1;
-    float* dst = sgh + i * 65;
-    if (oy < 0 || oy >= H2 || ox < 0 || ox >= W2) {
-      for (int ch = 0; ch < MID; ++ch) dst[ch] = 0.f;
-      continue;
-    }
-    float h[MID];
-    conv_h<K>(su, w1s, b1s, gy, gx, 20, h);
-    float go[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) go[k] = g_out(a, K, n, k, oy, ox);
-#pragma unroll
-    for (int ch = 0; ch < MID; ++ch) {
-      const float xh = (h[ch] - prm[2 * MID + ch]) * prm[3 * MID + ch];
-      float s = 0.f;
-#pragma unroll
-      for (int k = 0; k < K; ++k) s = fmaf(w2s[k * MID + ch], go[k], s);
-      const float gbn = (fmaf(prm[ch], xh, prm[MID + ch]) > 0.f) ? s : 0.f;
-      dst[ch] = prm[ch] * prm[3 * MID + ch] *
-                (gbn - prm[4 * MID + ch] * inv_cnt - xh * prm[5 * MID + ch] * inv_cnt);
-    }
+  load_w1t<K>(a, w1t, b1s);
+  for (int i = tid; i < K * MID; i += NT) w2s[i] = a.w2[i];
+  if (tid < MID) {
+    ga[tid] = a.gamma[tid];
+    be[tid] = a.beta[tid];
+    mu[tid] = a.mean[tid];
+    is[tid] = a.istd[tid];
+    c1[tid] = a.dbeta[tid] * inv_cnt;
+    c2[tid] = a.dgamma[tid] * inv_cnt;
   }
   __syncthreads();
-  // g_u for the interior pixel of this thread
-  {
-    const int r = tid / T2, c = tid % T2;
-    const int oy = oy0 + r, ox = ox0 + c;
-    if (oy < H2 && ox < W2) {
-      float acc[K];
+  float ga8[8], be8[8], mu8[8], is8[8], c18[8], c28[8];
+  load8(ga + 8 * g, ga8);
+  load8(be + 8 * g, be8);
+  load8(mu + 8 * g, mu8);
+  load8(is + 8 * g, is8);
+  load8(c1 + 8 * g, c18);
+  load8(c2 + 8 * g, c28);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+    for (int pass = 0; pass < 8; ++pass) {
+      int r, c;
+      pass_pixel(pass, tid, r, c);
+      const int oy = oy0 + r, ox = ox0 + c;
+      const bool pv = oy < H2 && ox < W2;
+      float h[8];
+      conv_h8<K>(su, w1t, b1s, r, c, g, h);
+      float go[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] = g_out(a, K, n, k, oy, ox);
+      for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (h[e] - mu8[e]) * is8[e];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) s = fmaf(w2s[k * MID + 8 * g + e], go[k], s);
+        const float gbn = (fmaf(ga8[e], xh, be8[e]) > 0.f) ? s : 0.f;
+        h[e] = ga8[e] * is8[e] * (gbn - c18[e] - xh * c28[e]);  // g_h
+      }
+      const long long p = ((long long)n * H2 + oy) * W2 + ox;
+      if (pv) {
+        T* ghp = (T*)a.gh + p * MID + 8 * g;
+        *(uint4*)ghp = Vec16<T>::pack(h);
+        if constexpr (sizeof(T) == 4) *(uint4*)(ghp + 4) = Vec16<T>::pack(h + 4);
+      }
+      *(float4*)(gls + ps * GLD + 8 * g) = make_float4(h[0], h[1], h[2], h[3]);
+      *(float4*)(gls + ps * GLD + 8 * g + 4) = make_float4(h[4], h[5], h[6], h[7]);
+      __syncthreads();
+      // per-tap products v[j] = sum_c W1[c][j] g_h[c], lane g takes j = 4g..4g+3
+      float vj[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int c4 = 0; c4 < MID; c4 += 4) {
+        const float4 gv = *(const float4*)(gls + ps * GLD + c4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int j = 4 * g + i;
+          if (j < K * 9) {
+            const float4 wv = *(const float4*)(w1t + j * MID + c4);
+            vj[i] = fmaf(wv.x, gv.x, fmaf(wv.y, gv.y, fmaf(wv.z, gv.z, fmaf(wv.w, gv.w, vj[i]))));
+          }
+        }
+      }
+      if (pv) {
+        float* vp = a.v + p * (K * 9);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * g + i < K * 9) vp[4 * g + i] = vj[i];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// g_u[q][k] = g_o[q][k] + sum_t v[q - d_t][k*9+t]   (d_t = (ky-1, kx-1))
+template <int K>
+__global__ void head_bwd_gu_kernel(HeadArgs a) {
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)a.N * H2 * W2) return;
+  const int ox = (int)(id % W2);
+  const int oy = (int)((id / W2) % H2);
+  const int n = (int)(id / ((long long)W2 * H2));
+  float acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = g_out(a, K, n, k, oy, ox);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ky = t / 3, kx = t - ky * 3;
+    const int py = oy - ky + 1, px = ox - kx + 1;
+    if (py < 0 || py >= H2 || px < 0 || px >= W2) continue;
+    const float* vp = a.v + (((long long)n * H2 + py) * W2 + px) * (K * 9);
+#pragma unroll
+    for (int k = 0; k < K; ++k) acc[k] += vp[k * 9 + t];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) a.gu[id * K + k] = acc[k];
+}
+
+// ---------------------------------------------------------------------------
+// gW1[c][k][t] = sum_p g_h[p][c] u[p + d_t][k],  gb1[c] = sum_p g_h[p][c]
+// MFMA with the pixels as the reduction dimension; im2col(u) [256 px][32] in LDS
+// ---------------------------------------------------------------------------
+template <int K, typename T>
+__global__ __launch_bounds__(NT) void head_wgrad_kernel(HeadArgs a) {
+  constexpr int E = Vec16<T>::N;
+  constexpr int STRIDE = MID * K * 9 + MID;
+  __shared__ __attribute__((aligned(16))) T gs[T2 * T2 * MID];  // g_h tile [256 px][64]
+  __shared__ __attribute__((aligned(16))) T cs[T2 * T2 * 32];   // im2col [256 px][32]
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float dbs[4][MID];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  f32x4 acc[2];
+  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  acc[1] = acc[0];
+  float dbacc = 0.f;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    for (int id = tid; id < T2 * T2 * MID / E; id += NT) {  // stage g_h (zero outside the image)
+      const int px = id / (MID / E), u = id - px * (MID / E);
+      const int oy = oy0 + px / T2, ox = ox0 + px % T2;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (oy < H2 && ox < W2)
+        val = *(const uint4*)((const T*)a.gh + (((long long)n * H2 + oy) * W2 + ox) * MID + u * E);
+      *(uint4*)(gs + px * MID + u * E) = val;
+    }
+    __syncthreads();
+    for (int id = tid; id < T2 * T2 * 32; id += NT) {  // im2col of u
+      const int px = id >> 5, j = id & 31;
+      float val = 0.f;
+      if (j < K * 9) {
+        const int k = j / 9, t = j - k * 9;
         const int ky = t / 3, kx = t - ky * 3;
-        const float* gp = sgh + ((r - ky + 2) * 18 + (c - kx + 2)) * 65;
-        for (int ch = 0; ch < MID; ++ch) {
-          const float g = gp[ch];
+        val = su[((px / T2 + ky) * 18 + (px % T2) + kx) * 3 + k];
+      }
+      Elem<T>::st(cs + id, val);
+    }
+    __syncthreads();
+    for (int px = wv; px < T2 * T2; px += 4) dbacc += Elem<T>::ld(gs + px * MID + lane);
+    const int cw = wv * 16;
+    if constexpr (sizeof(T) == 2) {
+      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
+#pragma unroll 2
+      for (int ks = 0; ks < T2 * T2 / 32; ++ks) {
+        const int pxa = ks * 32 + 8 * g + q4;
+        const s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, (char*)gs + (pxa * MID + cw + 4 * p4) * 2));
+        const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, (char*)gs + ((pxa + 4) * MID + cw + 4 * p4) * 2));
+        const bf16x8 af = cat_bf16x4(alo, ahi);
 #pragma unroll
-          for (int k = 0; k < K; ++k) acc[k] = fmaf(w1s[ch * K * 9 + k * 9 + t], g, acc[k]);
+        for (int jt = 0; jt < 2; ++jt) {
+          const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              LDS_PTR(s16x4, (char*)cs + (pxa * 32 + jt * 16 + 4 * p4) * 2));
+          const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              LDS_PTR(s16x4, (char*)cs + ((pxa + 4) * 32 + jt * 16 + 4 * p4) * 2));
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, cat_bf16x4(blo, bhi), acc[jt], 0, 0, 0);
         }
       }
+    } else {
+      const int kq = lane >> 4, i = lane & 15;
+#pragma unroll 4
+      for (int ks = 0; ks < T2 * T2 / 4; ++ks) {
+        const int px = ks * 4 + kq;
+        const float av = ((const float*)gs)[px * MID + cw + i];
 #pragma unroll
-      for (int k = 0; k < K; ++k) a.gu[(((long long)n * H2 + oy) * W2 + ox) * K + k] = acc[k];
-    }
-  }
-  // gW1 / gb1 partials
-  {
-    const int ch = tid & 63, tg = tid >> 6;
-    float acc[3][K];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-#pragma unroll
-      for (int k = 0; k < K; ++k) acc[j][k] = 0.f;
-    float gb = 0.f;
-    for (int p = 0; p < T2 * T2; ++p) {
-      const int r = p / T2, c = p - r * T2;
-      const float g = sgh[((r + 1) * 18 + c + 1) * 65 + ch];
-      gb += g;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int t = tg + 4 * j;
-        if (t < 9) {
-          const int ky = t / 3, kx = t - ky * 3;
-          const float* up = su + ((r + ky + 1) * 20 + c + kx + 1) * 3;
-#pragma unroll
-          for (int k = 0; k < K; ++k) acc[j][k] = fmaf(g, up[k], acc[j][k]);
-        }
+        for (int jt = 0; jt < 2; ++jt)
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ((const float*)cs)[px * 32 + jt * 16 + i], acc[jt],
+                                                          0, 0, 0);
       }
     }
-    const int stride = MID * K * 9 + MID;
-    float* out = a.part + (long long)blockIdx.x * stride;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int t = tg + 4 * j;
-      if (t < 9)
-#pragma unroll
-        for (int k = 0; k < K; ++k) out[(ch * K + k) * 9 + t] = acc[j][k];
-    }
-    if (tg == 0) out[MID * K * 9 + ch] = gb;
   }
+  float* out = a.part + (long long)blockIdx.x * STRIDE;
+  const int g = lane >> 4, li = lane & 15;
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = wv * 16 + g * 4 + e, j = jt * 16 + li;
+      if (j < K * 9) out[c * K * 9 + j] = acc[jt][e];
+    }
+  __syncthreads();
+  dbs[wv][lane] = dbacc;
+  __syncthreads();
+  if (tid < MID) out[MID * K * 9 + tid] = dbs[0][tid] + dbs[1][tid] + dbs[2][tid] + dbs[3][tid];
 }
 
 struct WsLayout {
-  size_t stats, part1, part2, gu, scale, shift, total;
+  size_t stats, part1, partw, gh, v, gu, scale, shift, cws, total;
+  int grid;
 };
 WsLayout ws_layout(int N, int h, int w, int K) {
   const int tiles = N * cdiv(2 * w, T2) * cdiv(2 * h, T2);
+  const int grid = tiles < HEAD_BLOCKS ? tiles : HEAD_BLOCKS;
+  const size_t P2 = (size_t)N * 4 * h * w;
   WsLayout L;
+  L.grid = grid;
   size_t off = 0;
   auto take = [&](size_t floats) {
     size_t o = off;
     off += (floats + 63) / 64 * 64;
     return o;
   };
-  L.stats = take((size_t)tiles * (2 * MID + 1));
-  L.part1 = take((size_t)tiles * ((K + 2) * MID + K));
-  L.part2 = take((size_t)tiles * (MID * K * 9 + MID));
-  L.gu = take((size_t)N * 4 * h * w * K);
+  L.stats = take((size_t)grid * (2 * MID + 1));
+  L.part1 = take((size_t)grid * ((K + 2) * MID + K));
+  L.partw = take((size_t)grid * (MID * K * 9 + MID));
+  L.gh = take(P2 * MID);  // sized for fp32
+  L.v = take(P2 * K * 9);
+  L.gu = take(P2 * K);
   L.scale = take(MID);
   L.shift = take(MID);
+  L.cws = take((size_t)2 * 16 * (MID * K * 9 + MID));  // fp64 colsum stage-1 rows (<= 16 for <= 1024 rows)
   L.total = off * sizeof(float);
   return L;
 }
@@ -383,8 +600,21 @@ extern "C" int eunet_bn_finalize(const float*, int, int, const float*, const flo
                                  float*, float*, float*, float*, void*);
 extern "C" int eunet_bn_eval_affine(int, const float*, const float*, const float*, const float*, float, float*,
                                     float*, void*);
-int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, hipStream_t s);
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s);
 extern "C" int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream);
+
+#define HEAD_DISPATCH(KERNEL, ...)                  \
+  do {                                              \
+    if (k == 1) KERNEL<1><<<__VA_ARGS__>>>(a);      \
+    else if (k == 2) KERNEL<2><<<__VA_ARGS__>>>(a); \
+    else KERNEL<3><<<__VA_ARGS__>>>(a);             \
+  } while (0)
+#define HEAD_DISPATCH_T(KERNEL, T, ...)                \
+  do {                                                 \
+    if (k == 1) KERNEL<1, T><<<__VA_ARGS__>>>(a);      \
+    else if (k == 2) KERNEL<2, T><<<__VA_ARGS__>>>(a); \
+    else KERNEL<3, T><<<__VA_ARGS__>>>(a);             \
+  } while (0)
 
 extern "C" {
 
@@ -411,11 +641,9 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
   a.scale = wsf + L.scale; a.shift = wsf + L.shift;
   hipStream_t s = (hipStream_t)stream;
   if (training) {
-    if (k == 1) head_stats_kernel<1><<<a.ntiles, NT, 0, s>>>(a);
-    else if (k == 2) head_stats_kernel<2><<<a.ntiles, NT, 0, s>>>(a);
-    else head_stats_kernel<3><<<a.ntiles, NT, 0, s>>>(a);
+    HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_stats");
-    int rc = eunet_bn_finalize(a.stats, a.ntiles, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
+    int rc = eunet_bn_finalize(a.stats, L.grid, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
                                wsf + L.scale, wsf + L.shift, stream);
     if (rc) return rc;
   } else {
@@ -423,9 +651,7 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     int rc = eunet_bn_eval_affine(MID, gamma, beta, run_mean, run_var, eps, wsf + L.scale, wsf + L.shift, stream);
     if (rc) return rc;
   }
-  if (k == 1) head_out_kernel<1><<<a.ntiles, NT, 0, s>>>(a);
-  else if (k == 2) head_out_kernel<2><<<a.ntiles, NT, 0, s>>>(a);
-  else head_out_kernel<3><<<a.ntiles, NT, 0, s>>>(a);
+  HEAD_DISPATCH(head_out_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_out");
   return EUNET_OK;
 }
@@ -433,44 +659,45 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
 int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1, const float* gamma,
                    const float* beta, const float* w2, const float* mean, const float* invstd, const float* g_logits,
                    const float* g_out2h, float* gz, float* gw1, float* gb1, float* ggamma, float* gbeta, float* gw2,
-                   float* gb2, void* ws, void* stream) {
+                   float* gb2, int dtype, void* ws, void* stream) {
   EUNET_REQUIRE(z && w1 && b1 && gamma && beta && w2 && mean && invstd && gz && gw1 && gb1 && ggamma && gbeta &&
                     gw2 && gb2 && ws && k >= 1 && k <= 3,
                 "head_bwd: bad args");
   EUNET_REQUIRE((g_logits != nullptr) != (g_out2h != nullptr), "head_bwd: exactly one of g_logits/g_out2h");
+  EUNET_REQUIRE(dtype == EUNET_F32 || dtype == EUNET_BF16, "head_bwd: dtype");
   const WsLayout L = ws_layout(n, h, w, k);
   float* wsf = (float*)ws;
+  void* cws = wsf + L.cws;
   HeadArgs a = {};
   a.z = z; a.N = n; a.h = h; a.w = w; a.K = k;
   a.w1 = w1; a.b1 = b1; a.gamma = gamma; a.beta = beta; a.w2 = w2;
   a.mean = mean; a.istd = invstd; a.glog = g_logits; a.gout2h = g_out2h;
   a.tx = cdiv(2 * w, T2); a.ty = cdiv(2 * h, T2); a.ntiles = n * a.tx * a.ty;
+  a.gh = wsf + L.gh; a.v = wsf + L.v; a.gu = wsf + L.gu;
   hipStream_t s = (hipStream_t)stream;
+  int rc;
   a.part = wsf + L.part1;
-  if (k == 1) head_bwd1_kernel<1><<<a.ntiles, NT, 0, s>>>(a);
-  else if (k == 2) head_bwd1_kernel<2><<<a.ntiles, NT, 0, s>>>(a);
-  else head_bwd1_kernel<3><<<a.ntiles, NT, 0, s>>>(a);
+  HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_bwd1");
   const int ld1 = (k + 2) * MID + k;
-  int rc;
-  if ((rc = eunet_colsum_ld(a.part, a.ntiles, k * MID, ld1, gw2, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + k * MID, a.ntiles, MID, ld1, gbeta, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + (k + 1) * MID, a.ntiles, MID, ld1, ggamma, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + (k + 2) * MID, a.ntiles, k, ld1, gb2, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part, L.grid, k * MID, ld1, gw2, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part + k * MID, L.grid, MID, ld1, gbeta, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part + (k + 1) * MID, L.grid, MID, ld1, ggamma, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part + (k + 2) * MID, L.grid, k, ld1, gb2, cws, s))) return rc;
   a.dbeta = gbeta; a.dgamma = ggamma;
-  a.part = wsf + L.part2;
-  a.gu = wsf + L.gu;
-  const size_t lds = (324 * 65 + 400 * 3 + MID * k * 9 + MID + 6 * MID + k * MID) * sizeof(float);
-  allow_lds(head_bwd2_kernel<1>, lds);
-  allow_lds(head_bwd2_kernel<2>, lds);
-  allow_lds(head_bwd2_kernel<3>, lds);
-  if (k == 1) head_bwd2_kernel<1><<<a.ntiles, NT, lds, s>>>(a);
-  else if (k == 2) head_bwd2_kernel<2><<<a.ntiles, NT, lds, s>>>(a);
-  else head_bwd2_kernel<3><<<a.ntiles, NT, lds, s>>>(a);
-  EUNET_LAUNCH_CHECK("head_bwd2");
-  const int ld2 = MID * k * 9 + MID;
-  if ((rc = eunet_colsum_ld(a.part, a.ntiles, MID * k * 9, ld2, gw1, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + MID * k * 9, a.ntiles, MID, ld2, gb1, s))) return rc;
+  if (dtype == EUNET_BF16) HEAD_DISPATCH_T(head_bwd_gh_kernel, bf16_t, L.grid, NT, 0, s);
+  else HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
+  EUNET_LAUNCH_CHECK("head_bwd_gh");
+  const long long P2 = (long long)n * 4 * h * w;
+  HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
+  EUNET_LAUNCH_CHECK("head_bwd_gu");
+  a.part = wsf + L.partw;
+  if (dtype == EUNET_BF16) HEAD_DISPATCH_T(head_wgrad_kernel, bf16_t, L.grid, NT, 0, s);
+  else HEAD_DISPATCH_T(head_wgrad_kernel, float, L.grid, NT, 0, s);
+  EUNET_LAUNCH_CHECK("head_wgrad");
+  const int ldw = MID * k * 9 + MID;
+  if ((rc = eunet_colsum_ld(a.part, L.grid, MID * k * 9, ldw, gw1, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part + MID * k * 9, L.grid, MID, ldw, gb1, cws, s))) return rc;
   eunet_act ghi = {a.gu, n, 2 * h, 2 * w, k, k, 0, EUNET_F32};
   eunet_act glo = {gz, n, h, w, k, k, 0, EUNET_F32};
   return eunet_upsample_bwd(&ghi, &glo, stream);

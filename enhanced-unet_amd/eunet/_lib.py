@@ -46,13 +46,14 @@ SIGNATURES = {
     "eunet_head_fwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, c_int, c_float, c_float,
                        _f, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_head_bwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
-                       _f, _f, _f, _f, _f, _f, _f, c_void_p],
+                       _f, _f, _f, _f, _f, _f, c_int, _f, c_void_p],
     "eunet_loss_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_loss_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, c_void_p],
     "eunet_loss_bwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, c_void_p],
     "eunet_bn_bwd_tiles": [_P, POINTER(c_int)],
     "eunet_bn_bwd_reduce": [_P, _P, _f, _f, _f, _f, _f, c_void_p],
-    "eunet_colsum": [_f, c_int, c_int, _f, c_void_p],
+    "eunet_colsum_ws_bytes": [c_int, c_int, POINTER(c_size_t)],
+    "eunet_colsum": [_f, c_int, c_int, _f, _f, c_void_p],
     "eunet_bn_bwd_apply": [_P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
     "eunet_pool_bwd_add": [_P, _P, _P, _P, c_void_p],
     "eunet_upsample_bwd": [_P, _P, c_void_p],

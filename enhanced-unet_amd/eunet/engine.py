@@ -252,7 +252,7 @@ class UNetEngine:
         gout2h = g_out if S["want"] == "out2h" else None
         ops.head_bwd(S["z"], N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
                      P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), S["hmean"], S["hinv"],
-                     glog, gout2h, gz, gw1, gb1, gg, gbt, gw2, gb2, hws)
+                     glog, gout2h, gz, gw1, gb1, gg, gbt, gw2, gb2, hws, dtype=dt)
         sink.ready(["enhance.0.weight", "enhance.0.bias", "enhance.1.weight", "enhance.1.bias",
                     "enhance.3.weight", "enhance.3.bias"])
         # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))

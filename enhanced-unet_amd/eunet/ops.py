@@ -35,7 +35,9 @@ def act(t: torch.Tensor, coff: int = 0, c: int | None = None) -> Act:
     if not t.is_cuda:
         raise _lib.EunetError("act(): tensor must live on the GPU")
     n, h, w, ct = t.shape
-    return Act(t.data_ptr(), n, h, w, ct - coff if c is None else c, ct, coff, DTYPES[t.dtype])
+    a = Act(t.data_ptr(), n, h, w, ct - coff if c is None else c, ct, coff, DTYPES[t.dtype])
+    a._keep = t  # the view keeps its tensor (and device memory) alive
+    return a
 
 
 def _ref(a):
@@ -144,10 +146,10 @@ def head_fwd(z, n, h, w, k, w1, b1, gamma, beta, w2, b2, training, eps, momentum
 
 
 def head_bwd(z, n, h, w, k, w1, b1, gamma, beta, w2, mean, invstd, g_logits, g_out2h, gz, gw1, gb1, ggamma,
-             gbeta, gw2, gb2, ws):
+             gbeta, gw2, gb2, ws, dtype=torch.float32):
     call("eunet_head_bwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2),
          _ptr(mean), _ptr(invstd), _ptr(g_logits), _ptr(g_out2h), _ptr(gz), _ptr(gw1), _ptr(gb1), _ptr(ggamma),
-         _ptr(gbeta), _ptr(gw2), _ptr(gb2), _ptr(ws), _stream())
+         _ptr(gbeta), _ptr(gw2), _ptr(gb2), DTYPES[dtype], _ptr(ws), _stream())
 
 
 def loss_workspace_bytes(n, k, h, w):
@@ -180,7 +182,10 @@ def bn_bwd_reduce(g: Act, y: Act, mean, invstd, gamma, beta, part):
 
 
 def colsum(part, rows, cols, out):
-    call("eunet_colsum", _ptr(part), rows, cols, _ptr(out), _stream())
+    b = c_size_t()
+    call("eunet_colsum_ws_bytes", rows, cols, ctypes.byref(b))
+    ws = torch.empty(b.value, dtype=torch.uint8, device=part.device)
+    call("eunet_colsum", _ptr(part), rows, cols, _ptr(out), _ptr(ws), _stream())
 
 
 def bn_bwd_apply(g: Act, y: Act, mean, invstd, gamma, beta, dbeta, dgamma, gy: Act):

@@ -119,12 +119,13 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
                    float* mean, float* invstd, float* out2h, float* logits, void* ws,
                    void* stream);
 /* backward from g_logits (or g_out2h when g_logits == NULL).  Writes gz and the
- * head parameter gradients gw1 [64][K][3][3], gb1, ggamma, gbeta, gw2 [K][64], gb2. */
+ * head parameter gradients gw1 [64][K][3][3], gb1, ggamma, gbeta, gw2 [K][64], gb2.
+ * dtype selects the storage of the one materialised 2H tensor (g_h, 64 ch). */
 int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1,
                    const float* gamma, const float* beta, const float* w2, const float* mean,
                    const float* invstd, const float* g_logits, const float* g_out2h, float* gz,
                    float* gw1, float* gb1, float* ggamma, float* gbeta, float* gw2, float* gb2,
-                   void* ws, void* stream);
+                   int dtype, void* ws, void* stream);
 
 /* ---- combined loss (train_eval.py:28-60, 134-197, 262-337) ----------------
  * logits [N,K,H,W] fp32 NCHW, target [N,H,W] int64; K <= 3.
@@ -146,7 +147,9 @@ int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles);
 int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mean,
                         const float* invstd, const float* gamma, const float* beta, float* part,
                         void* stream);
-int eunet_colsum(const float* part, int rows, int cols, float* out, void* stream);
+/* deterministic column sum of a [rows][cols] fp32 partial matrix (fp64 two-stage) */
+int eunet_colsum_ws_bytes(int rows, int cols, size_t* bytes);
+int eunet_colsum(const float* part, int rows, int cols, float* out, void* ws, void* stream);
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean,
                        const float* invstd, const float* gamma, const float* beta,
                        const float* dbeta, const float* dgamma, const eunet_act* gy,

@@ -1,0 +1,53 @@
+"""Per-parameter gradient error of the fp32 HIP path vs the fp64 oracle, next to the
+fp32 oracle's own error (diagnostic for parity tolerances).
+
+    python tools/grad_diag.py [--base 64] [--cin 1] [--K 2] [--H 64]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "enhanced-unet_amd")]
+
+import torch  # noqa: E402
+
+from oracle import eunet_ref as R  # noqa: E402
+
+
+def oracle(base, cin, K, x, m, dt):
+    S = R.formula_weights(base, cin, K, dtype=dt)
+    for k in S:
+        if S[k].is_floating_point() and "running" not in k:
+            S[k].requires_grad_(True)
+    R.batch_loss(R.forward(S, x.to(dt), training=True), m).backward()
+    return S
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--base", type=int, default=64)
+    ap.add_argument("--cin", type=int, default=1)
+    ap.add_argument("--K", type=int, default=2)
+    ap.add_argument("--H", type=int, default=64)
+    a = ap.parse_args()
+    from eunet import synth
+    from eunet.losses import combined_loss
+    from eunet.models import EnhancedUNet
+    x, m = synth.batch(2, a.H, a.H, start_index=7, num_classes=a.K, in_channels=a.cin)
+    S64 = oracle(a.base, a.cin, a.K, x, m, torch.float64)
+    S32 = oracle(a.base, a.cin, a.K, x, m, torch.float32)
+    model = EnhancedUNet(num_classes=a.K, in_channels=a.cin, base_ch=a.base)
+    model.load_state_dict({k: v.detach().float() if v.is_floating_point() else v for k, v in S64.items()})
+    model = model.cuda().train()
+    combined_loss(model.forward_lowres(x.cuda()), m.cuda()).backward()
+    rl2 = lambda p, q: float((p.double().cpu() - q).norm() / q.norm().clamp_min(1e-30))
+    rows = []
+    for k, p in model.named_parameters():
+        rows.append((rl2(p.grad, S64[k].grad), rl2(S32[k].grad, S64[k].grad), k))
+    for ours, o32, k in sorted(rows, reverse=True)[:20]:
+        print(f"{k:32s} ours {ours:.2e}   oracle32 {o32:.2e}   ratio {ours / max(o32, 1e-30):.1f}")
+
+
+if __name__ == "__main__":
+    main()
