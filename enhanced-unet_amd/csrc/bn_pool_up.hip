@@ -31,13 +31,15 @@ struct SmallArgs {
   float* stats; int tx, ty, ntiles;
 };
 
+// 8 lanes per pixel (lane group g = lane & 7 owns output channels co0+8g..+7),
+// 32 pixels per pass = one output row of the 8x32 tile; per-thread Welford over
+// its 8 pixels, Chan-combined across lanes and waves (no transposes)
 template <typename T>
 __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
   __shared__ float xs[(STH + 2) * (STW + 2) * 4];
-  __shared__ float ws[64 * 4 * 9];
-  __shared__ float red[4][64];
-  __shared__ float meanb[64], sums[64];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ __attribute__((aligned(16))) float wsm[4 * 9 * 64];  // [ci*9+t][64 co]
+  __shared__ float wn_s[4], wm_s[4][64], wq_s[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int tile = blockIdx.x, tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
   const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
@@ -54,62 +56,93 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
   }
   for (int i = tid; i < 64 * cin * 9; i += NT) {
     const int co = i / (cin * 9), r = i - co * cin * 9;
-    ws[co * 36 + r] = (co0 + co < a.cout) ? a.w[(long long)(co0 + co) * cin * 9 + r] : 0.f;
+    wsm[r * 64 + co] = (co0 + co < a.cout) ? a.w[(long long)(co0 + co) * cin * 9 + r] : 0.f;
   }
   __syncthreads();
-  const int r = tid / STW, c = tid - r * STW;
-  const int yy = y0 + r, xx = x0 + c;
-  const bool pv = yy < a.H && xx < a.W;
-  float acc[64];
+  float bias[8];
 #pragma unroll
-  for (int co = 0; co < 64; ++co) acc[co] = (a.b != nullptr && co0 + co < a.cout) ? a.b[co0 + co] : 0.f;
-  for (int ci = 0; ci < cin; ++ci) {
+  for (int e = 0; e < 8; ++e) bias[e] = (a.b != nullptr && co0 + 8 * g + e < a.cout) ? a.b[co0 + 8 * g + e] : 0.f;
+  float cnt = 0.f, mean[8], m2[8];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = t / 3, kx = t - ky * 3;
-      const float v = xs[((r + ky) * (STW + 2) + c + kx) * 4 + ci];
+  for (int e = 0; e < 8; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  constexpr int E = Vec16<T>::N;
+  const bool full = (co0 + 64 <= a.cout) && ((a.yct | a.yco) % E) == 0;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int px = pass * 32 + ps;
+    const int r = px / STW, c = px - r * STW;
+    const int yy = y0 + r, xx = x0 + c;
+    if (yy >= a.H || xx >= a.W) continue;
+    float acc[8];
 #pragma unroll
-      for (int co = 0; co < 64; ++co) acc[co] = fmaf(ws[co * 36 + ci * 9 + t], v, acc[co]);
+    for (int e = 0; e < 8; ++e) acc[e] = bias[e];
+    for (int ci = 0; ci < cin; ++ci) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t - ky * 3;
+        const float v = xs[((r + ky) * (STW + 2) + c + kx) * 4 + ci];
+        const float4 w0 = *(const float4*)(wsm + (ci * 9 + t) * 64 + 8 * g);
+        const float4 w1 = *(const float4*)(wsm + (ci * 9 + t) * 64 + 8 * g + 4);
+        acc[0] = fmaf(w0.x, v, acc[0]); acc[1] = fmaf(w0.y, v, acc[1]);
+        acc[2] = fmaf(w0.z, v, acc[2]); acc[3] = fmaf(w0.w, v, acc[3]);
+        acc[4] = fmaf(w1.x, v, acc[4]); acc[5] = fmaf(w1.y, v, acc[5]);
+        acc[6] = fmaf(w1.z, v, acc[6]); acc[7] = fmaf(w1.w, v, acc[7]);
+      }
     }
-  }
-  if (pv) {
-    T* yp = (T*)a.y + ((long long)(n * a.H + yy) * a.W + xx) * a.yct + a.yco + co0;
-    const int nco = min(64, a.cout - co0);
-    constexpr int E = Vec16<T>::N;
-    if (nco == 64 && ((a.yct | a.yco) % E) == 0) {
-#pragma unroll
-      for (int u = 0; u < 64 / E; ++u) *(uint4*)(yp + u * E) = Vec16<T>::pack(acc + u * E);
+    T* yp = (T*)a.y + ((long long)(n * a.H + yy) * a.W + xx) * a.yct + a.yco + co0 + 8 * g;
+    if (full) {
+      *(uint4*)yp = Vec16<T>::pack(acc);
+      if constexpr (E == 4) *(uint4*)(yp + 4) = Vec16<T>::pack(acc + 4);
     } else {
-      for (int co = 0; co < nco; ++co) Elem<T>::st(yp + co, acc[co]);
+      for (int e = 0; e < 8; ++e)
+        if (co0 + 8 * g + e < a.cout) Elem<T>::st(yp + e, acc[e]);
+    }
+    cnt += 1.f;
+    const float inv = 1.f / cnt;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = acc[e] - mean[e];
+      mean[e] = fmaf(d, inv, mean[e]);
+      m2[e] = fmaf(d, acc[e] - mean[e], m2[e]);
     }
   }
   if (a.stats == nullptr) return;
-  float v[64];
 #pragma unroll
-  for (int co = 0; co < 64; ++co) v[co] = pv ? acc[co] : 0.f;
-  float s = wave_transpose_reduce64(v);
-  red[wv][lane] = s;
-  __syncthreads();
-  const float cnt = (float)(min(STH, a.H - y0) * min(STW, a.W - x0));
-  if (tid < 64) {
-    sums[tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    meanb[tid] = sums[tid] / cnt;
-  }
-  __syncthreads();
-  const float sum_tile = sums[lane];
+  for (int off = 8; off <= 32; off <<= 1) {
+    const float nb = __shfl_xor(cnt, off, 64);
+    const float nt = cnt + nb;
 #pragma unroll
-  for (int co = 0; co < 64; ++co) {
-    const float d = acc[co] - meanb[co];
-    v[co] = pv ? d * d : 0.f;
+    for (int e = 0; e < 8; ++e) {
+      const float mb = __shfl_xor(mean[e], off, 64), qb = __shfl_xor(m2[e], off, 64);
+      const float d = mb - mean[e];
+      if (nt > 0.f) {
+        mean[e] += d * nb / nt;
+        m2[e] += qb + d * d * cnt * nb / nt;
+      }
+    }
+    cnt = nt;
   }
-  s = wave_transpose_reduce64(v);
-  __syncthreads();
-  red[wv][lane] = s;
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      wm_s[wv][8 * g + e] = mean[e];
+      wq_s[wv][8 * g + e] = m2[e];
+    }
+    if (lane == 0) wn_s[wv] = cnt;
+  }
   __syncthreads();
   if (tid < 64 && co0 + tid < a.cout) {
-    a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum_tile;
-    a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-    if (blockIdx.y == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
+    double bn = 0.0, bm = 0.0, bq = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      const double nb = wn_s[w];
+      if (nb <= 0.0) continue;
+      const double d = (double)wm_s[w][tid] - bm, nt = bn + nb;
+      bm += d * nb / nt;
+      bq += (double)wq_s[w][tid] + d * d * bn * nb / nt;
+      bn = nt;
+    }
+    a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = (float)(bm * bn);
+    a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = (float)bq;
+    if (blockIdx.y == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = (float)bn;
   }
 }
 
@@ -120,19 +153,22 @@ struct SmallWgArgs {
   int tx, ty, ntiles, per_split;
 };
 
+// first-conv wgrad as MFMA: dW[co][ci*9+t] = sum_p dY[p][co] im2col(x)[p][ci*9+t];
+// im2col (<= 27 of 32 columns) and the dY tile are staged in LDS per 8x32 tile
 template <typename T>
 __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
+  constexpr int E = Vec16<T>::N;
   __shared__ float xs[(STH + 2) * (STW + 2) * 4];
-  __shared__ float ds[STH * STW][65];
-  const int tid = threadIdx.x, co = tid & 63, tg = tid >> 6;
+  __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];  // dY tile [256 px][64 co]
+  __shared__ __attribute__((aligned(16))) T cs[STH * STW * 32];  // im2col [256 px][32]
+  __shared__ float dbs[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int split = blockIdx.x, co0 = blockIdx.y * 64;
   const int t_begin = split * a.per_split, t_end = min(a.ntiles, t_begin + a.per_split);
   const int tpi = a.tx * a.ty, cin = a.cin;
-  float acc[3][4];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  f32x4 acc[2];
+  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  acc[1] = acc[0];
   float dbacc = 0.f;
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
@@ -147,42 +183,71 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
         v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
       xs[hp * 4 + ci] = v;
     }
-    for (int i = tid; i < STH * STW * 64; i += NT) {
-      const int px = i >> 6, cc = i & 63;
+    for (int id = tid; id < STH * STW * 64 / E; id += NT) {
+      const int px = id / (64 / E), u = id - px * (64 / E);
       const int r = px / STW, c = px - r * STW;
-      const int yy = y0 + r, xx = x0 + c;
-      float v = 0.f;
-      if (yy < a.H && xx < a.W && co0 + cc < a.cout)
-        v = Elem<T>::ld((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co0 + cc);
-      ds[px][cc] = v;
+      const int yy = y0 + r, xx = x0 + c, co = co0 + u * E;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (yy < a.H && xx < a.W && co < a.cout)
+        v = *(const uint4*)((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
+      *(uint4*)(gs + px * 64 + u * E) = v;
     }
     __syncthreads();
-    for (int px = 0; px < STH * STW; ++px) {
-      const float g = ds[px][co];
-      const int r = px / STW, c = px - r * STW;
-      if (tg == 0) dbacc += g;
+    for (int id = tid; id < STH * STW * 32; id += NT) {
+      const int px = id >> 5, j = id & 31;
+      float v = 0.f;
+      if (j < cin * 9) {
+        const int ci = j / 9, t = j - ci * 9;
+        const int ky = t / 3, kx = t - ky * 3;
+        v = xs[((px / STW + ky) * (STW + 2) + (px % STW) + kx) * 4 + ci];
+      }
+      Elem<T>::st(cs + id, v);
+    }
+    __syncthreads();
+    for (int px = wv; px < STH * STW; px += 4) dbacc += Elem<T>::ld(gs + px * 64 + lane);
+    const int cw = wv * 16;
+    if constexpr (sizeof(T) == 2) {
+      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
+      for (int ks = 0; ks < STH * STW / 32; ++ks) {
+        const int pxa = ks * 32 + 8 * g + q4;
+        const s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)gs + (pxa * 64 + cw + 4 * p4) * 2));
+        const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)gs + ((pxa + 4) * 64 + cw + 4 * p4) * 2));
+        const bf16x8 af = cat_bf16x4(alo, ahi);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int t = tg + 4 * k;
-        if (t < 9) {
-          const int ky = t / 3, kx = t - ky * 3;
-          const float* xp = xs + ((r + ky) * (STW + 2) + c + kx) * 4;
-#pragma unroll
-          for (int ci = 0; ci < 4; ++ci)
-            if (ci < cin) acc[k][ci] = fmaf(g, xp[ci], acc[k][ci]);
+        for (int jt = 0; jt < 2; ++jt) {
+          const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + (pxa * 32 + jt * 16 + 4 * p4) * 2));
+          const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + ((pxa + 4) * 32 + jt * 16 + 4 * p4) * 2));
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, cat_bf16x4(blo, bhi), acc[jt], 0, 0, 0);
         }
+      }
+    } else {
+      const int kq = lane >> 4, i = lane & 15;
+      for (int ks = 0; ks < STH * STW / 4; ++ks) {
+        const int px = ks * 4 + kq;
+        const float av = ((const float*)gs)[px * 64 + cw + i];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ((const float*)cs)[px * 32 + jt * 16 + i], acc[jt], 0, 0, 0);
       }
     }
   }
-  if (co0 + co >= a.cout) return;
   float* out = a.dw + (long long)split * a.cout * 9 * cin;
+  const int g = lane >> 4, li = lane & 15;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int t = tg + 4 * k;
-    if (t < 9)
-      for (int ci = 0; ci < cin; ++ci) out[((long long)(co0 + co) * 9 + t) * cin + ci] = acc[k][ci];
-  }
-  if (a.db != nullptr && tg == 0) a.db[(long long)split * a.cout + co0 + co] = dbacc;
+  for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = co0 + wv * 16 + g * 4 + e, j = jt * 16 + li;
+      if (co < a.cout && j < cin * 9) {
+        const int ci = j / 9, t = j - ci * 9;
+        out[((long long)co * 9 + t) * cin + ci] = acc[jt][e];
+      }
+    }
+  __syncthreads();
+  dbs[wv][lane] = dbacc;
+  __syncthreads();
+  if (a.db != nullptr && tid < 64 && co0 + tid < a.cout)
+    a.db[(long long)split * a.cout + co0 + tid] = dbs[0][tid] + dbs[1][tid] + dbs[2][tid] + dbs[3][tid];
 }
 
 // ---------------------------------------------------------------------------
@@ -572,60 +637,93 @@ __global__ void up_bwd_small_kernel(const float* g, float* o, int N, int h, int 
   for (int k = 0; k < K; ++k) o[id * K + k] = acc[k];
 }
 
-// dec1 backward: gact = W^T gz; per-tile partials of gW [K][C] and gb [K]
+// dec1 backward: gact = W^T gz; per-block partials of gW [K][C] and gb [K].
+// 8 lanes per pixel, lane group g owns channels 8g+64j (C <= 128); partial
+// sums stay in registers over the block's C1X_PIX pixels.
+constexpr int C1X_PIX = 1024;
 template <typename T>
 __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P, int C, int yct, int yco,
                                                          const float* sc, const float* sh, const float* w, int K,
                                                          const float* gz, T* ga, int gct, int gco, float* part) {
   constexpr int E = Vec16<T>::N;
-  __shared__ float acc_s[3 * 256 + 3];
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ float red[4][3 * 128 + 3];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int stride = K * C + K;
-  for (int i = tid; i < stride; i += NT) acc_s[i] = 0.f;
-  __syncthreads();
-  const long long p = (long long)blockIdx.x * NT + tid;
-  const bool pv = p < P;
-  float g[3] = {0.f, 0.f, 0.f};
-  if (pv)
-    for (int k = 0; k < K; ++k) g[k] = gz[p * K + k];
-  for (int c0 = 0; c0 < C; c0 += 64) {
-    float a[64];
+  float aw[2][3][8], ab[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 64 / E; ++u) {
-      const int c = c0 + u * E;
-      float f[E];
-      if (pv && c < C) {
-        Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
-      } else {
+    for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int j = 0; j < E; ++j) f[j] = 0.f;
-      }
-      float go[E];
+      for (int e = 0; e < 8; ++e) aw[j][k][e] = 0.f;
+  const long long p0 = (long long)blockIdx.x * C1X_PIX;
+  const long long p1 = min(P, p0 + C1X_PIX);
+  for (long long p = p0 + ps; p < p1; p += 32) {
+    float gk[3] = {0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) gk[k] = gz[p * K + k];
+    if (g == 0)
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        a[u * E + j] = f[j];
+      for (int k = 0; k < 3; ++k) ab[k] += gk[k];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = 64 * j + 8 * g;
+      if (c >= C) continue;
+      float f[8], go[8];
+      Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+      if constexpr (E == 4) Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c + 4), f + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float act = fmaxf(fmaf(f[e], sc[c + e], sh[c + e]), 0.f);
         float s = 0.f;
-        for (int k = 0; k < K; ++k) s = fmaf(w[k * C + c + j], g[k], s);
-        go[j] = s;
-      }
-      if (pv && c < C) *(uint4*)(ga + p * gct + gco + c) = Vec16<T>::pack(go);
-    }
-    for (int k = 0; k < K; ++k) {
-      float v[64];
 #pragma unroll
-      for (int j = 0; j < 64; ++j) v[j] = a[j] * g[k];
-      const float s = wave_transpose_reduce64(v);
-      if (c0 + lane < C) atomicAdd(&acc_s[k * C + c0 + lane], s);
+        for (int k = 0; k < 3; ++k)
+          if (k < K) {
+            s = fmaf(w[k * C + c + e], gk[k], s);
+            aw[j][k][e] = fmaf(gk[k], act, aw[j][k][e]);
+          }
+        go[e] = s;
+      }
+      *(uint4*)(ga + p * gct + gco + c) = Vec16<T>::pack(go);
+      if constexpr (E == 4) *(uint4*)(ga + p * gct + gco + c + 4) = Vec16<T>::pack(go + 4);
     }
   }
-  for (int k = 0; k < K; ++k) {
-    const float s = wave_sum(g[k]);
-    if (lane == 0) atomicAdd(&acc_s[K * C + k], s);
+  // reduce over the 8 pixel slots of each wave (xor 8, 16, 32), then across waves
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = aw[j][k][e];
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        aw[j][k][e] = v;
+      }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float v = ab[k];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    ab[k] = v;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = 64 * j + 8 * g + e;
+          if (k < K && c < C) red[wv][k * C + c] = aw[j][k][e];
+        }
+    if (lane == 0)
+      for (int k = 0; k < K; ++k) red[wv][K * C + k] = ab[k];
   }
   __syncthreads();
-  for (int i = tid; i < stride; i += NT) part[(long long)blockIdx.x * stride + i] = acc_s[i];
+  for (int i = tid; i < stride; i += NT)
+    part[(long long)blockIdx.x * stride + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
 }
 
 }  // namespace
@@ -674,7 +772,7 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, 
 int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit, "conv_small_wgrad_splits: bad args");
   const int ntiles = dy->n * cdiv(dy->h, STH) * cdiv(dy->w, STW);
-  int s = cdiv(1024, cdiv(dy->c, 64));
+  int s = cdiv(512, cdiv(dy->c, 64));
   s = s > ntiles ? ntiles : (s < 1 ? 1 : s);
   const int per = cdiv(ntiles, s);
   *nsplit = cdiv(ntiles, per);
@@ -897,7 +995,7 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
 
 int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles) {
   EUNET_REQUIRE(act_ok(y) && tiles, "conv1x1_bwd_tiles: bad args");
-  *tiles = (int)(((long long)y->n * y->h * y->w + NT - 1) / NT);
+  *tiles = (int)(((long long)y->n * y->h * y->w + C1X_PIX - 1) / C1X_PIX);
   return EUNET_OK;
 }
 
@@ -905,10 +1003,10 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
                       const float* gz, const eunet_act* gact, float* part, void* stream) {
   EUNET_REQUIRE(act_ok(y) && act_ok(gact) && vec_ok(y) && vec_ok(gact) && scale && shift && w && gz && part,
                 "conv1x1_bwd: bad args");
-  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 256 && gact->c == y->c && gact->dtype == y->dtype,
-                "conv1x1_bwd: K<=3, C<=256");
+  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 128 && y->c % 8 == 0 && gact->c == y->c && gact->dtype == y->dtype,
+                "conv1x1_bwd: K<=3, C<=128, C%8==0");
   const long long P = (long long)y->n * y->h * y->w;
-  const unsigned tiles = (unsigned)((P + NT - 1) / NT);
+  const unsigned tiles = (unsigned)((P + C1X_PIX - 1) / C1X_PIX);
   if (y->dtype == EUNET_BF16)
     conv1x1_bwd_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
                                                                         y->coff, scale, shift, w, k, gz,

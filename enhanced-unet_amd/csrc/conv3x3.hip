@@ -440,6 +440,116 @@ __global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
   }
 }
 
+// bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
+// w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
+// 32-pixel k-step costs 8 + 18 transposed fragment reads for 36 MFMAs.
+constexpr int KCW = 64;                       // ci channels per wgrad block (bf16)
+constexpr int WX_LDS = 8 * HPXP * 16;         // X halo [8 octants][HPXP][16 B]
+constexpr int WD_LDS = TH * TW * 64 * 2;      // dY tile [256 px][64 co] bf16
+constexpr int WG_LDS = WX_LDS + WD_LDS + 4 * 64 * 4;
+
+__global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Xs = smem;
+  char* Ds = smem + WX_LDS;
+  float* dbred = (float*)(Ds + WD_LDS);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int split = blockIdx.x, co0 = blockIdx.y * 64, kc = blockIdx.z;
+  const int t_begin = split * a.per_split;
+  const int t_end = min(a.ntiles, t_begin + a.per_split);
+  const int tpi = a.tx * a.ty;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+    __syncthreads();
+    // X halo, 64 channels: unit id -> (pixel id>>3, octant id&7), BN+ReLU applied here
+    for (int id = tid; id < 8 * HPX; id += NTHR) {
+      const int hp = id >> 3, oc = id & 7;
+      const int hy = hp / HW_, hx = hp - hy * HW_;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const int c = kc * KCW + oc * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
+        v = *(const uint4*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
+        if (a.isc != nullptr) {
+          float f[8];
+          Vec16<bf16_t>::unpack(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
+          v = Vec16<bf16_t>::pack(f);
+        }
+      }
+      *(uint4*)(Xs + (oc * HPXP + hp) * 16) = v;
+    }
+    // dY tile
+    for (int id = tid; id < TH * TW * 8; id += NTHR) {
+      const int px = id >> 3, u = id & 7;
+      const int r = px / TW, c = px - r * TW;
+      const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (yy < a.H && xx < a.W && co < a.cout)
+        v = *(const uint4*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
+      *(uint4*)(Ds + id * 16) = v;
+    }
+    __syncthreads();
+    if (a.db != nullptr && kc == 0) {
+      const bf16_t* d = (const bf16_t*)Ds;
+      for (int px = wv; px < TH * TW; px += 4) dbacc += bf2f(d[px * 64 + lane]);
+    }
+    for (int ks = 0; ks < TH; ++ks) {
+      const int pxa = ks * TW + 8 * g + q4;
+      bf16x8 af[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa * 64 + ct * 16 + 4 * p4) * 2));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, Ds + ((pxa + 4) * 64 + ct * 16 + 4 * p4) * 2));
+        af[ct] = cat_bf16x4(lo, hi);
+      }
+      const int oc = 2 * wv + (p4 >> 1);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t - ky * 3;
+        const int hp = (ks + ky) * HW_ + 8 * g + q4 + kx;
+        const char* base = Xs + (oc * HPXP + hp) * 16 + (p4 & 1) * 8;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
+        const bf16x8 bfr = cat_bf16x4(lo, hi);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
+      }
+    }
+  }
+  float* out = a.dw + (long long)split * a.cout * 9 * a.cin;
+  const int ci = kc * KCW + wv * 16 + i16;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = co0 + ct * 16 + g * 4 + e;
+        if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[t][ct][e];
+      }
+  if (a.db != nullptr && kc == 0) {
+    __syncthreads();
+    dbred[wv * 64 + lane] = dbacc;
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.cout)
+      a.db[(long long)split * a.cout + co0 + tid] = dbred[tid] + dbred[64 + tid] + dbred[128 + tid] + dbred[192 + tid];
+  }
+}
+
 __global__ void wgrad_reduce_kernel(const float* part, const float* dbp, int nsplit, int cout, int cin, int taps,
                                     float* dw, float* db) {
   const long long per = (long long)cout * taps * cin;
@@ -532,8 +642,8 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
   const int ntiles = dy->n * cdiv(dy->h, TH) * cdiv(dy->w, TW);
-  const int blocks = cdiv(dy->c, 64) * cdiv(cin, kchunk(dtype));
-  int s = cdiv(2048, blocks);
+  const int blocks = cdiv(dy->c, 64) * cdiv(cin, dtype == EUNET_BF16 ? KCW : kchunk(dtype));
+  int s = cdiv(dtype == EUNET_BF16 ? 512 : 2048, blocks);
   s = s < 1 ? 1 : s;
   s = s > ntiles ? ntiles : s;
   // keep partials <= 256 MiB
@@ -561,11 +671,12 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
-  dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
   if (x->dtype == EUNET_BF16) {
-    const size_t lds = A_LDS_BYTES + TH * TW * 64 * 2 + 4 * 64 * 4;
-    conv3x3_wgrad_kernel<bf16_t><<<grid, NTHR, lds, (hipStream_t)stream>>>(a);
+    dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, KCW));
+    allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
+    conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
   } else {
+    dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
     const size_t lds = A_LDS_BYTES + TH * TW * 64 * 4 + 4 * 64 * 4;
     allow_lds(conv3x3_wgrad_kernel<float>, lds);
     conv3x3_wgrad_kernel<float><<<grid, NTHR, lds, (hipStream_t)stream>>>(a);

@@ -45,7 +45,8 @@ def main():
     rows = []
     for k, p in model.named_parameters():
         rows.append((rl2(p.grad, S64[k].grad), rl2(S32[k].grad, S64[k].grad), k))
-    for ours, o32, k in sorted(rows, reverse=True)[:20]:
+    rows = [r for r in rows if not (r[2].endswith((".0.bias", ".3.bias")) and not r[2].startswith("enhance.3"))]
+    for ours, o32, k in sorted(rows, reverse=True)[:12]:
         print(f"{k:32s} ours {ours:.2e}   oracle32 {o32:.2e}   ratio {ours / max(o32, 1e-30):.1f}")
 
 
