@@ -57,7 +57,8 @@ def cpu_baseline(args):
     """Oracle train step on the host CPU: one image, B=1 (bounded ~10-30 s)."""
     from oracle import eunet_ref as R
     from eunet import synth
-    threads = os.cpu_count() or 1
+    # the box exports OMP_NUM_THREADS = this job's CPU share; os.cpu_count() is the whole host
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     torch.set_num_threads(threads)
     S = R.formula_weights(args.base, 1, 2, dtype=torch.float32)
     tr = R.OracleTrainer(S, total_epochs=50)
@@ -71,6 +72,26 @@ def cpu_baseline(args):
     return {"value": round(scale / dt, 5), "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"1 oracle train step (PyTorch CPU fp32 restatement of Trainer.train_epoch), B=1, "
                       f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s"}
+
+
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
+    (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes) of this same
+    bench command; None when no summary for this workload exists."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != [args.base, args.size, args.batch, args.dtype]:
+        return None
+    k = d["kernels"].get(kernel)
+    if not k:
+        return None
+    return round(k["hbm_bytes_per_launch"]), f"profiles/{os.path.basename(PMC_SUMMARY)} ({d['correction']})"
 
 
 def main():
@@ -127,7 +148,11 @@ def main():
             "achieved": round(achieved, 2) if achieved else None, "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
             "launches_per_step": fam["launches"] // max(1, args.steps),
-            "kernel_ms_per_step": round(fam["ms"] / args.steps, 3)}
+            "kernel_ms_per_step": round(fam["ms"] / args.steps, 3),
+            "algorithmic_bytes_per_launch": round(fam["bytes"] / max(1, fam["launches"]))}
+    pmc = pmc_traffic(args, "conv3x3_fwd_kernel")
+    if pmc is not None:
+        roof["traffic"], roof["traffic_source"] = pmc
     if "conv3x3_wgrad" in ks:
         wg = ks["conv3x3_wgrad"]
         roof["wgrad_tflops"] = round(wg["flops"] / (wg["ms"] * 1e-3) / 1e12, 2)

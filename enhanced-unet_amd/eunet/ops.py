@@ -70,7 +70,10 @@ def conv3x3_tiles(y_act: Act) -> int:
 
 def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None):
     flops = 2.0 * 9 * x.c * y.c * x.n * x.h * x.w
-    with kprof.timed("conv3x3_fwd", flops):
+    esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
+    # algorithmic HBM bytes: read x once, write y once, read the packed weights once
+    nbytes = float(esz * x.n * x.h * x.w * (x.c + y.c) + wp.numel() * wp.element_size())
+    with kprof.timed("conv3x3_fwd", flops, nbytes):
         call("eunet_conv3x3_fwd", ctypes.byref(x), _ptr(scale), _ptr(shift), _ptr(wp), _ptr(bias),
              ctypes.byref(y), _ptr(stats), _stream())
 
