@@ -438,7 +438,7 @@ __global__ __launch_bounds__(NT) void head_bwd_gh_kernel(HeadArgs a) {
         }
       }
       if (pv) {
-        float* vp = a.v + p * (K * 9);
+        float* vp = a.v + p * ((K * 9 + 3) & ~3);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (4 * g + i < K * 9) vp[4 * g + i] = vj[i];
@@ -465,7 +465,7 @@ __global__ void head_bwd_gu_kernel(HeadArgs a) {
     const int ky = t / 3, kx = t - ky * 3;
     const int py = oy - ky + 1, px = ox - kx + 1;
     if (py < 0 || py >= H2 || px < 0 || px >= W2) continue;
-    const float* vp = a.v + (((long long)n * H2 + py) * W2 + px) * (K * 9);
+    const float* vp = a.v + (((long long)n * H2 + py) * W2 + px) * ((K * 9 + 3) & ~3);
 #pragma unroll
     for (int k = 0; k < K; ++k) acc[k] += vp[k * 9 + t];
   }
@@ -565,11 +565,528 @@ __global__ __launch_bounds__(NT) void head_wgrad_kernel(HeadArgs a) {
   if (tid < MID) out[MID * K * 9 + tid] = dbs[0][tid] + dbs[1][tid] + dbs[2][tid] + dbs[3][tid];
 }
 
+// ===========================================================================
+// bf16 MFMA head (dtype EUNET_BF16; the reference's autocast runs these convs in
+// bf16).  Per 16-pixel row segment the 64-channel conv is one GEMM,
+//   h^T[c][px] = W1[c][j] * im2col^T[j][px]    (v_mfma_f32_16x16x32_bf16,
+//   4 channel blocks, j = k*9+t zero-padded to 32),
+// leaving lane l with channels c = 16cb + 4q + i (q = l>>4, i = 0..3) of pixel
+// x = l&15.  Those 16 values, converted to bf16 in the order (cb = 2ch, i),
+// (cb = 2ch+1, i), ARE the B operand of the next GEMM over channels when its A
+// operand is loaded with the same channel permutation (perm_c) -- the 1x1 conv,
+// the per-tap products v and the backward g_a all chain without transposes.
+// Wave w of a 256-thread block owns rows 4w..4w+3 of the 16x16 tile.
+// ===========================================================================
+__device__ __forceinline__ int perm_c(int q, int ch, int jj) { return 16 * (2 * ch + (jj >> 2)) + 4 * q + (jj & 3); }
+
+// C-layout values v[cb][i] -> B fragment over channel chunk ch
+__device__ __forceinline__ bf16x8 cfrag(const f32x4 (&v)[4], int ch) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    b[i] = (__bf16)v[2 * ch][i];
+    b[4 + i] = (__bf16)v[2 * ch + 1][i];
+  }
+  return b;
+}
+
+// A operand of h^T: row c = 16cb + (l&15), k = j = 8q + jj
+template <int K>
+__device__ __forceinline__ void load_a_w1(const float* w1, int lane, bf16x8 (&A)[4]) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = 8 * q + jj;
+      A[cb][jj] = (__bf16)(j < K * 9 ? w1[(16 * cb + r) * K * 9 + j] : 0.f);
+    }
+}
+
+// per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner
+template <int K>
+__device__ __forceinline__ void im2col_offsets(int q, int (&off)[8]) {
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int j = 8 * q + jj;
+    if (j < K * 9) {
+      const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
+      off[jj] = (ky * 18 + kx) * 3 + k;
+    } else {
+      off[jj] = -1;
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 im2col_frag(const float* su, int base, const int (&off)[8]) {
+  bf16x8 b;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const float v = su[base + (off[jj] < 0 ? 0 : off[jj])];
+    b[jj] = (__bf16)(off[jj] < 0 ? 0.f : v);
+  }
+  return b;
+}
+
+// h^T (bias excluded) for the pixel row segment whose window corner is su[base]
+__device__ __forceinline__ void conv_h_mfma(const float* su, int base, const int (&off)[8], const bf16x8 (&Ah)[4],
+                                            f32x4 (&acc)[4]) {
+  const bf16x8 b = im2col_frag(su, base, off);
+  const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ah[cb], b, z, 0, 0, 0);
+}
+
+// A operand of s^T[c][px] = sum_k W2[k][c] g_o[k][px]: row c = 16cb + (l&15), k = class 8q + jj
+template <int K>
+__device__ __forceinline__ void load_a_w2t(const float* w2, int lane, bf16x8 (&A)[4]) {
+  const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int kk = 8 * q + jj;
+      A[cb][jj] = (__bf16)(kk < K ? w2[kk * MID + 16 * cb + r] : 0.f);
+    }
+}
+
+template <int K>
+__device__ __forceinline__ bf16x8 go_frag(int q, const float (&go)[K]) {
+  bf16x8 b;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) b[jj] = (__bf16)0.f;
+  if (q == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) b[k] = (__bf16)go[k];
+  }
+  return b;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// sum over the 16 pixel lanes of a row (lanes with equal q)
+__device__ __forceinline__ float sum_x16(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+template <int K>
+__global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float wn_s[4], wm_s[4][MID], wq_s[4][MID];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  bf16x8 Ah[4];
+  load_a_w1<K>(a.w1, lane, Ah);
+  int off[8];
+  im2col_offsets<K>(q, off);
+  float n = 0.f, mean[16], m2[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int nn, oy0, ox0;
+    tile_coords(a, tile, nn, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, nn, oy0, ox0);
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = 4 * wv + rr;
+      f32x4 acc[4];
+      conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+      if (oy0 + r < 2 * a.h && ox0 + x < 2 * a.w) {
+        n += 1.f;
+        const float inv = 1.f / n;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int e = 4 * cb + i;
+            const float d = acc[cb][i] - mean[e];
+            mean[e] = fmaf(d, inv, mean[e]);
+            m2[e] = fmaf(d, acc[cb][i] - mean[e], m2[e]);
+          }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 1; o <= 8; o <<= 1) {
+    const float nb = __shfl_xor(n, o, 64);
+    const float nt = n + nb;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float mb = __shfl_xor(mean[e], o, 64), qb = __shfl_xor(m2[e], o, 64);
+      const float d = mb - mean[e];
+      if (nt > 0.f) {
+        mean[e] += d * nb / nt;
+        m2[e] += qb + d * d * n * nb / nt;
+      }
+    }
+    n = nt;
+  }
+  if (x == 0) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 16 * cb + 4 * q + i;
+        wm_s[wv][c] = mean[4 * cb + i] + a.b1[c];
+        wq_s[wv][c] = m2[4 * cb + i];
+      }
+    if (q == 0) wn_s[wv] = n;
+  }
+  __syncthreads();
+  if (tid < MID) {
+    double bn = 0.0, bm = 0.0, bq = 0.0;
+    for (int w = 0; w < 4; ++w) {
+      const double nb = wn_s[w];
+      if (nb <= 0.0) continue;
+      const double d = (double)wm_s[w][tid] - bm, nt = bn + nb;
+      bm += d * nb / nt;
+      bq += (double)wq_s[w][tid] + d * d * bn * nb / nt;
+      bn = nt;
+    }
+    a.stats[((long long)blockIdx.x * 2 + 0) * MID + tid] = (float)(bm * bn);
+    a.stats[((long long)blockIdx.x * 2 + 1) * MID + tid] = (float)bq;
+    if (tid == 0) a.stats[(long long)2 * MID * gridDim.x + blockIdx.x] = (float)bn;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(NT) void head_out_mfma_kernel(HeadArgs a) {
+  __shared__ float su[18 * 18 * 3];
+  __shared__ __attribute__((aligned(16))) float scs[MID], shs[MID];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  if (tid < MID) {
+    scs[tid] = a.scale[tid];
+    shs[tid] = fmaf(a.b1[tid], a.scale[tid], a.shift[tid]);  // b1 folded into the shift
+  }
+  bf16x8 Ah[4], Ao[2];
+  load_a_w1<K>(a.w1, lane, Ah);
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj)
+      Ao[ch][jj] = (__bf16)(x < K ? a.w2[x * MID + perm_c(q, ch, jj)] : 0.f);
+  int off[8];
+  im2col_offsets<K>(q, off);
+  float b2k[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) b2k[k] = a.b2[k];
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+      float lsum[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) lsum[k] = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 4 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + x;
+        f32x4 acc[4];
+        conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const float4 s4 = ld4(scs + 16 * cb + 4 * q), t4 = ld4(shs + 16 * cb + 4 * q);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[cb][i] = fmaxf(fmaf(acc[cb][i], f4(s4, i), f4(t4, i)), 0.f);
+        }
+        f32x4 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[0], cfrag(acc, 0), z4, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[1], cfrag(acc, 1), o, 0, 0, 0);
+        // lanes q == 0 hold o[k = i][pixel x]
+        const bool pv = q == 0 && oy < H2 && ox < W2;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float val = o[k] + b2k[k] + su[((r + 1) * 18 + x + 1) * 3 + k];
+          if (pv && a.out2h) a.out2h[(((long long)n * K + k) * H2 + oy) * W2 + ox] = val;
+          lsum[k] += val;
+        }
+      }
+      const int oy = oy0 + 4 * wv + 2 * rp, ox = ox0 + x;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float t = lsum[k] + __shfl_xor(lsum[k], 1, 64);
+        if (q == 0 && (x & 1) == 0 && oy < H2 && ox < W2 && a.logits)
+          a.logits[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)] = 0.25f * t;
+      }
+    }
+  }
+}
+
+// BN backward parameters, per channel: xhat = h*is + off, pre = h*P + Q (h without b1)
+__device__ __forceinline__ void bwd_params(const HeadArgs& a, int c, float& is, float& off, float& P, float& Q) {
+  is = a.istd[c];
+  off = (a.b1[c] - a.mean[c]) * is;
+  P = a.gamma[c] * is;
+  Q = fmaf(a.gamma[c], off, a.beta[c]);
+}
+
+template <int K>
+__global__ __launch_bounds__(NT) void head_bwd1_mfma_kernel(HeadArgs a) {
+  constexpr int STRIDE = (K + 2) * MID + K;
+  __shared__ float su[18 * 18 * 3];
+  __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID];
+  __shared__ float red[STRIDE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  if (tid < MID) bwd_params(a, tid, pis[tid], poff[tid], pP[tid], pQ[tid]);
+  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
+  bf16x8 Ah[4], As[4];
+  load_a_w1<K>(a.w1, lane, Ah);
+  load_a_w2t<K>(a.w2, lane, As);
+  int off[8];
+  im2col_offsets<K>(q, off);
+  float agb[16], agx[16], aw2[K][16], ab2[K];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    agb[e] = 0.f;
+    agx[e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) aw2[k][e] = 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) ab2[k] = 0.f;
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+#pragma unroll 1
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = 4 * wv + rr, oy = oy0 + r, ox = ox0 + x;
+      const bool pv = oy < H2 && ox < W2;
+      f32x4 acc[4], sv[4];
+      conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+      float go[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
+      const bf16x8 gb = go_frag<K>(q, go);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(As[cb], gb, z4, 0, 0, 0);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int c0 = 16 * cb + 4 * q;
+        const float4 i4 = ld4(pis + c0), o4 = ld4(poff + c0), p4 = ld4(pP + c0), q4 = ld4(pQ + c0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * cb + i;
+          const float xh = fmaf(acc[cb][i], f4(i4, i), f4(o4, i));
+          const float pre = fmaf(acc[cb][i], f4(p4, i), f4(q4, i));
+          const float act = fmaxf(pre, 0.f);
+          const float gbn = pre > 0.f ? sv[cb][i] : 0.f;
+          agb[e] += gbn;
+          agx[e] = fmaf(gbn, xh, agx[e]);
+#pragma unroll
+          for (int k = 0; k < K; ++k) aw2[k][e] = fmaf(go[k], act, aw2[k][e]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) ab2[k] += (q == 0) ? go[k] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    agb[e] = sum_x16(agb[e]);
+    agx[e] = sum_x16(agx[e]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) aw2[k][e] = sum_x16(aw2[k][e]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) ab2[k] = sum_x16(ab2[k]);
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w && x == 0) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * cb + 4 * q + i, e = 4 * cb + i;
+#pragma unroll
+          for (int k = 0; k < K; ++k) red[k * MID + c] += aw2[k][e];
+          red[K * MID + c] += agb[e];
+          red[(K + 1) * MID + c] += agx[e];
+        }
+      if (q == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[(K + 2) * MID + k] += ab2[k];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
+}
+
+// g_h (never stored), the per-tap products v = g_h * W1 (stored, fp32) and the
+// W1/b1 gradients (MFMA over pixels from a wave-private bf16 g_h tile in LDS).
+template <int K>
+__global__ __launch_bounds__(NT) void head_gh_mfma_kernel(HeadArgs a) {
+  constexpr int STRIDE = MID * K * 9 + MID;
+  constexpr int KJ = K * 9;
+  __shared__ float su[18 * 18 * 3];
+  __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID], pB[MID], pC[MID];
+  constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
+  __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
+  __shared__ float red[STRIDE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  if (tid < MID) {
+    float is, of, P, Q;
+    bwd_params(a, tid, is, of, P, Q);
+    const float inv_cnt = 1.f / ((float)a.N * (float)H2 * (float)W2);
+    pis[tid] = is; poff[tid] = of; pP[tid] = P; pQ[tid] = Q;
+    pB[tid] = -P * a.dgamma[tid] * inv_cnt;  // g_h = P*gbn + B*xhat + C
+    pC[tid] = -P * a.dbeta[tid] * inv_cnt;
+  }
+  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
+  bf16x8 Ah[4], As[4], Av[2][2];
+  load_a_w1<K>(a.w1, lane, Ah);
+  load_a_w2t<K>(a.w2, lane, As);
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 16 * jb + x;
+        Av[jb][ch][jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
+      }
+  int off[8];
+  im2col_offsets<K>(q, off);
+  // wgrad B operand: im2col[px slot 8q + jj][j = 16jb + x]; slot -> (row q>>1, col 8(q&1) + jj)
+  int boff[2];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int j = 16 * jb + x;
+    if (j < KJ) {
+      const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
+      boff[jb] = (((q >> 1) + ky) * 18 + 8 * (q & 1) + kx) * 3 + k;
+    } else {
+      boff[jb] = -1;
+    }
+  }
+  f32x4 accW[4][2];
+  float agb1[16];
+#pragma unroll
+  for (int pb = 0; pb < 4; ++pb) accW[pb][0] = accW[pb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) agb1[e] = 0.f;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  constexpr int VLD = (KJ + 3) & ~3;
+  bf16_t* gw = gsw[wv];
+  const int q4 = x >> 2, p4 = x & 3;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    fill_u(a, su, n, oy0, ox0);
+    __syncthreads();
+    for (int rp = 0; rp < 2; ++rp) {
+#pragma unroll 1
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 4 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + x;
+        const bool pv = oy < H2 && ox < W2;
+        f32x4 acc[4], sv[4];
+        conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+        float go[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
+        const bf16x8 gb = go_frag<K>(q, go);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(As[cb], gb, z4, 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int c0 = 16 * cb + 4 * q;
+          const float4 i4 = ld4(pis + c0), o4 = ld4(poff + c0), p4v = ld4(pP + c0), q4v = ld4(pQ + c0);
+          const float4 b4 = ld4(pB + c0), cc4 = ld4(pC + c0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float xh = fmaf(acc[cb][i], f4(i4, i), f4(o4, i));
+            const float pre = fmaf(acc[cb][i], f4(p4v, i), f4(q4v, i));
+            const float gbn = pre > 0.f ? sv[cb][i] : 0.f;
+            const float g = pv ? fmaf(f4(p4v, i), gbn, fmaf(f4(b4, i), xh, f4(cc4, i))) : 0.f;
+            acc[cb][i] = g;
+            agb1[4 * cb + i] += g;
+          }
+        }
+        const bf16x8 g0 = cfrag(acc, 0), g1 = cfrag(acc, 1);
+        f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[0][0], g0, z4, 0, 0, 0);
+        v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[0][1], g1, v0, 0, 0, 0);
+        f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[1][0], g0, z4, 0, 0, 0);
+        v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[1][1], g1, v1, 0, 0, 0);
+        if (pv) {
+          float* vp = a.v + (((long long)n * H2 + oy) * W2 + ox) * VLD;
+          if (4 * q < KJ) *(f32x4*)(vp + 4 * q) = v0;
+          if (16 + 4 * q < KJ) *(f32x4*)(vp + 16 + 4 * q) = v1;
+        }
+        // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
+        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
+        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
+      }
+      __syncthreads();
+      const int r0 = 4 * wv + 2 * rp;
+      bf16x8 Bw[2];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const float v = su[r0 * 54 + (boff[jb] < 0 ? 0 : boff[jb]) + 3 * jj];
+          Bw[jb][jj] = (__bf16)(boff[jb] < 0 ? 0.f : v);
+        }
+      const int pxa = 8 * q + q4;
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, (char*)gw + (pxa * GLD + 16 * pb + 4 * p4) * 2));
+        const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            LDS_PTR(s16x4, (char*)gw + ((pxa + 4) * GLD + 16 * pb + 4 * p4) * 2));
+        const bf16x8 af = cat_bf16x4(alo, ahi);
+        accW[pb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, Bw[0], accW[pb][0], 0, 0, 0);
+        accW[pb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, Bw[1], accW[pb][1], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) agb1[e] = sum_x16(agb1[e]);
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w) {
+      // accW[pb][jb][i]: row = position 16pb + 4q + i -> channel 16q + 4pb + i; col j = 16jb + x
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int c = 16 * q + 4 * pb + i, j = 16 * jb + x;
+            if (j < KJ) red[c * KJ + j] += accW[pb][jb][i];
+          }
+      if (x == 0)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[MID * KJ + 16 * cb + 4 * q + i] += agb1[4 * cb + i];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
+}
+
 struct WsLayout {
   size_t stats, part1, partw, gh, v, gu, scale, shift, cws, total;
   int grid;
 };
-WsLayout ws_layout(int N, int h, int w, int K) {
+WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   const int tiles = N * cdiv(2 * w, T2) * cdiv(2 * h, T2);
   const int grid = tiles < HEAD_BLOCKS ? tiles : HEAD_BLOCKS;
   const size_t P2 = (size_t)N * 4 * h * w;
@@ -584,8 +1101,8 @@ WsLayout ws_layout(int N, int h, int w, int K) {
   L.stats = take((size_t)grid * (2 * MID + 1));
   L.part1 = take((size_t)grid * ((K + 2) * MID + K));
   L.partw = take((size_t)grid * (MID * K * 9 + MID));
-  L.gh = take(P2 * MID);  // sized for fp32
-  L.v = take(P2 * K * 9);
+  L.gh = take(dtype == EUNET_F32 ? P2 * MID : 0);  // the bf16 path never stores g_h
+  L.v = take(P2 * ((K * 9 + 3) & ~3));
   L.gu = take(P2 * K);
   L.scale = take(MID);
   L.shift = take(MID);
@@ -618,20 +1135,23 @@ extern "C" int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, vo
 
 extern "C" {
 
-int eunet_head_workspace_bytes(int n, int h, int w, int k, size_t* bytes) {
+int eunet_head_workspace_bytes(int n, int h, int w, int k, int dtype, size_t* bytes) {
   EUNET_REQUIRE(bytes && n > 0 && h > 0 && w > 0 && k >= 1 && k <= 3, "head_workspace_bytes: bad args");
-  *bytes = ws_layout(n, h, w, k).total;
+  EUNET_REQUIRE(dtype == EUNET_F32 || dtype == EUNET_BF16, "head_workspace_bytes: dtype");
+  *bytes = ws_layout(n, h, w, k, dtype).total;
   return EUNET_OK;
 }
 
 int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1, const float* gamma,
                    const float* beta, const float* w2, const float* b2, int training, float eps, float momentum,
                    float* run_mean, float* run_var, float* mean, float* invstd, float* out2h, float* logits,
-                   void* ws, void* stream) {
+                   int dtype, void* ws, void* stream) {
   EUNET_REQUIRE(z && w1 && b1 && gamma && beta && w2 && b2 && ws && k >= 1 && k <= 3, "head_fwd: bad args");
   EUNET_REQUIRE(out2h || logits, "head_fwd: nothing to write");
   EUNET_REQUIRE(!training || (mean && invstd), "head_fwd: training needs mean/invstd outputs");
-  const WsLayout L = ws_layout(n, h, w, k);
+  EUNET_REQUIRE(dtype == EUNET_F32 || dtype == EUNET_BF16, "head_fwd: dtype");
+  const bool mf = dtype == EUNET_BF16;
+  const WsLayout L = ws_layout(n, h, w, k, dtype);
   float* wsf = (float*)ws;
   HeadArgs a = {};
   a.z = z; a.N = n; a.h = h; a.w = w; a.K = k;
@@ -641,7 +1161,8 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
   a.scale = wsf + L.scale; a.shift = wsf + L.shift;
   hipStream_t s = (hipStream_t)stream;
   if (training) {
-    HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
+    if (mf) HEAD_DISPATCH(head_stats_mfma_kernel, L.grid, NT, 0, s);
+    else HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_stats");
     int rc = eunet_bn_finalize(a.stats, L.grid, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
                                wsf + L.scale, wsf + L.shift, stream);
@@ -651,7 +1172,8 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     int rc = eunet_bn_eval_affine(MID, gamma, beta, run_mean, run_var, eps, wsf + L.scale, wsf + L.shift, stream);
     if (rc) return rc;
   }
-  HEAD_DISPATCH(head_out_kernel, L.grid, NT, 0, s);
+  if (mf) HEAD_DISPATCH(head_out_mfma_kernel, L.grid, NT, 0, s);
+  else HEAD_DISPATCH(head_out_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_out");
   return EUNET_OK;
 }
@@ -665,7 +1187,8 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
                 "head_bwd: bad args");
   EUNET_REQUIRE((g_logits != nullptr) != (g_out2h != nullptr), "head_bwd: exactly one of g_logits/g_out2h");
   EUNET_REQUIRE(dtype == EUNET_F32 || dtype == EUNET_BF16, "head_bwd: dtype");
-  const WsLayout L = ws_layout(n, h, w, k);
+  const bool mf = dtype == EUNET_BF16;
+  const WsLayout L = ws_layout(n, h, w, k, dtype);
   float* wsf = (float*)ws;
   void* cws = wsf + L.cws;
   HeadArgs a = {};
@@ -677,7 +1200,8 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   hipStream_t s = (hipStream_t)stream;
   int rc;
   a.part = wsf + L.part1;
-  HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
+  if (mf) HEAD_DISPATCH(head_bwd1_mfma_kernel, L.grid, NT, 0, s);
+  else HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_bwd1");
   const int ld1 = (k + 2) * MID + k;
   if ((rc = eunet_colsum_ld(a.part, L.grid, k * MID, ld1, gw2, cws, s))) return rc;
@@ -685,16 +1209,22 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   if ((rc = eunet_colsum_ld(a.part + (k + 1) * MID, L.grid, MID, ld1, ggamma, cws, s))) return rc;
   if ((rc = eunet_colsum_ld(a.part + (k + 2) * MID, L.grid, k, ld1, gb2, cws, s))) return rc;
   a.dbeta = gbeta; a.dgamma = ggamma;
-  if (dtype == EUNET_BF16) HEAD_DISPATCH_T(head_bwd_gh_kernel, bf16_t, L.grid, NT, 0, s);
-  else HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
-  EUNET_LAUNCH_CHECK("head_bwd_gh");
   const long long P2 = (long long)n * 4 * h * w;
-  HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
-  EUNET_LAUNCH_CHECK("head_bwd_gu");
-  a.part = wsf + L.partw;
-  if (dtype == EUNET_BF16) HEAD_DISPATCH_T(head_wgrad_kernel, bf16_t, L.grid, NT, 0, s);
-  else HEAD_DISPATCH_T(head_wgrad_kernel, float, L.grid, NT, 0, s);
-  EUNET_LAUNCH_CHECK("head_wgrad");
+  if (mf) {
+    a.part = wsf + L.partw;  // g_h, v and the W1/b1 partials in one pass
+    HEAD_DISPATCH(head_gh_mfma_kernel, L.grid, NT, 0, s);
+    EUNET_LAUNCH_CHECK("head_gh_mfma");
+    HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
+    EUNET_LAUNCH_CHECK("head_bwd_gu");
+  } else {
+    HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
+    EUNET_LAUNCH_CHECK("head_bwd_gh");
+    HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
+    EUNET_LAUNCH_CHECK("head_bwd_gu");
+    a.part = wsf + L.partw;
+    HEAD_DISPATCH_T(head_wgrad_kernel, float, L.grid, NT, 0, s);
+    EUNET_LAUNCH_CHECK("head_wgrad");
+  }
   const int ldw = MID * k * 9 + MID;
   if ((rc = eunet_colsum_ld(a.part, L.grid, MID * k * 9, ldw, gw1, cws, s))) return rc;
   if ((rc = eunet_colsum_ld(a.part + MID * k * 9, L.grid, MID, ldw, gb1, cws, s))) return rc;

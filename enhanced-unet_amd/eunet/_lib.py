@@ -42,9 +42,9 @@ SIGNATURES = {
     "eunet_bnrelu_pool": [_P, _f, _f, _P, _P, c_void_p],
     "eunet_bnrelu_upsample": [_P, _f, _f, _P, c_void_p],
     "eunet_bnrelu_conv1x1": [_P, _f, _f, _f, _f, c_int, _f, c_void_p],
-    "eunet_head_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],
+    "eunet_head_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_head_fwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, c_int, c_float, c_float,
-                       _f, _f, _f, _f, _f, _f, _f, c_void_p],
+                       _f, _f, _f, _f, _f, _f, c_int, _f, c_void_p],
     "eunet_head_bwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
                        _f, _f, _f, _f, _f, _f, c_int, _f, c_void_p],
     "eunet_loss_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],

@@ -162,7 +162,7 @@ class UNetEngine:
         ops.bnrelu_conv1x1(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
                            P["model.dec1.weight"].reshape(K, b).contiguous(), P["model.dec1.bias"], K, z)
         S["z"] = z
-        hws = _e(ops.head_workspace_bytes(N, H, W, K), torch.uint8, dev)
+        hws = _e(ops.head_workspace_bytes(N, H, W, K, self.dtype), torch.uint8, dev)
         hmean = _e(64, torch.float32, dev) if training else None
         hinv = _e(64, torch.float32, dev) if training else None
         out2h = _e((N, K, 2 * H, 2 * W), torch.float32, dev) if want == "out2h" else None
@@ -170,7 +170,7 @@ class UNetEngine:
         ops.head_fwd(z, N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
                      P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), P["enhance.3.bias"],
                      training, BN_EPS, BN_MOMENTUM, B["enhance.1.running_mean"], B["enhance.1.running_var"],
-                     hmean, hinv, out2h, logits, hws)
+                     hmean, hinv, out2h, logits, hws, dtype=self.dtype)
         if training:
             B["enhance.1.num_batches_tracked"].add_(1)
         S.update(hmean=hmean, hinv=hinv, N=N, H=H, W=W, want=want)
@@ -241,7 +241,7 @@ class UNetEngine:
         g_out = g_out.contiguous().float()
         # ---- 2H head -> gz
         gz = _e((N, H, W, K), torch.float32, dev)
-        hws = _e(ops.head_workspace_bytes(N, H, W, K), torch.uint8, dev)
+        hws = _e(ops.head_workspace_bytes(N, H, W, K, dt), torch.uint8, dev)
         gw1 = sink.slot("enhance.0.weight", (64, K, 3, 3))
         gb1 = sink.slot("enhance.0.bias", (64,))
         gg = sink.slot("enhance.1.weight", (64,))

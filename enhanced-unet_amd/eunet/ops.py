@@ -135,17 +135,17 @@ def bnrelu_conv1x1(y: Act, scale, shift, w, b, k, z):
          _stream())
 
 
-def head_workspace_bytes(n, h, w, k):
+def head_workspace_bytes(n, h, w, k, dtype=torch.float32):
     b = c_size_t()
-    call("eunet_head_workspace_bytes", n, h, w, k, ctypes.byref(b))
+    call("eunet_head_workspace_bytes", n, h, w, k, DTYPES[dtype], ctypes.byref(b))
     return b.value
 
 
 def head_fwd(z, n, h, w, k, w1, b1, gamma, beta, w2, b2, training, eps, momentum, run_mean, run_var, mean,
-             invstd, out2h, logits, ws):
+             invstd, out2h, logits, ws, dtype=torch.float32):
     call("eunet_head_fwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2), _ptr(b2),
          int(training), float(eps), float(momentum), _ptr(run_mean), _ptr(run_var), _ptr(mean), _ptr(invstd),
-         _ptr(out2h), _ptr(logits), _ptr(ws), _stream())
+         _ptr(out2h), _ptr(logits), DTYPES[dtype], _ptr(ws), _stream())
 
 
 def head_bwd(z, n, h, w, k, w1, b1, gamma, beta, w2, mean, invstd, g_logits, g_out2h, gz, gw1, gb1, ggamma,

@@ -111,16 +111,19 @@ int eunet_bnrelu_conv1x1(const eunet_act* y, const float* scale, const float* sh
 /* ---- enhance head at 2H + residual + 2x2 mean (models.py:308-313,336-337;
  *      train_eval.py:306-310 resize == 2x2 mean) ------------------------------
  * z: [N,H,W,K] fp32. out2h (nullable) [N,K,2H,2W] fp32 NCHW, logits
- * (nullable) [N,K,H,W] fp32 NCHW.  Head BN stats saved in mean/invstd (64). */
-int eunet_head_workspace_bytes(int n, int h, int w, int k, size_t* bytes);
+ * (nullable) [N,K,H,W] fp32 NCHW.  Head BN stats saved in mean/invstd (64).
+ * dtype: EUNET_F32 = fp32 FMA path; EUNET_BF16 = bf16 MFMA GEMMs with fp32
+ * accumulation (the reference's autocast precision for these convs). */
+int eunet_head_workspace_bytes(int n, int h, int w, int k, int dtype, size_t* bytes);
 int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1,
                    const float* gamma, const float* beta, const float* w2, const float* b2,
                    int training, float eps, float momentum, float* run_mean, float* run_var,
-                   float* mean, float* invstd, float* out2h, float* logits, void* ws,
-                   void* stream);
+                   float* mean, float* invstd, float* out2h, float* logits, int dtype,
+                   void* ws, void* stream);
 /* backward from g_logits (or g_out2h when g_logits == NULL).  Writes gz and the
  * head parameter gradients gw1 [64][K][3][3], gb1, ggamma, gbeta, gw2 [K][64], gb2.
- * dtype selects the storage of the one materialised 2H tensor (g_h, 64 ch). */
+ * dtype as for head_fwd (EUNET_BF16: g_h never leaves the chip; the W1 gradient
+ * is fused into the g_h pass). */
 int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, const float* b1,
                    const float* gamma, const float* beta, const float* w2, const float* mean,
                    const float* invstd, const float* g_logits, const float* g_out2h, float* gz,

@@ -148,13 +148,17 @@ def test_trainer_step_matches_reference_fixture(golden_dir):
             assert float((post - ref).abs().max()) < 2.0 * lr, k
             continue
         # AdamW's first step is lr * g / (|g| + eps): parameters agree to a small fraction
-        # of lr, except where |g| is within a few hundred eps (d/dg = lr*eps/(|g|+eps)^2),
-        # where a gradient difference of 1e-4 of the tensor's scale is amplified.
+        # of lr.  With dg = the fp32 gradient accuracy (2e-3 of the tensor's scale, a
+        # cancelling sum over ~10^6 pixels), elements whose reference |g| <= dg may take
+        # either sign (any update in [-lr, lr]); above that the update moves by at most
+        # lr*eps*dg/(|g|-dg+eps)^2.
         tol = 0.05 * lr + 1e-6 * ref.abs().max()
         if gref is not None:
             eps = 1e-8
-            dg = 1e-4 * float(gref.abs().max())
-            tol = tol + lr * eps * dg / (gref.double().abs() + eps) ** 2
+            ga = gref.double().abs()
+            dg = 2e-3 * float(ga.max())
+            lin = lr * eps * dg / ((ga - dg).clamp_min(0) + eps) ** 2
+            tol = tol + torch.where(ga <= dg, torch.full_like(ga, 2.0 * lr), lin)
         assert bool(((post - ref).abs() < tol).all()), (k, float((post - ref).abs().max()))
 
 

@@ -277,8 +277,14 @@ def _head_ref(z, w1, b1, gamma, beta, w2, b2):
     return u + F.conv2d(a, w2, b2)
 
 
-@pytest.mark.parametrize("K", [2, 3])
-def test_head_fwd_bwd(K):
+@pytest.mark.parametrize("K,dt", [(2, torch.float32), (3, torch.float32), (1, torch.bfloat16),
+                                  (2, torch.bfloat16), (3, torch.bfloat16)])
+def test_head_fwd_bwd(K, dt):
+    """fp32: FMA path, 1e-4 of the fp64 reference.  bf16: MFMA path (bf16 operands,
+    fp32 accumulation = the reference's autocast precision): each quantity within
+    max(1e-2, 1.5x) the error that CPU bf16 autocast of the same head makes vs fp64
+    (g_z and g_W1 pass through sums of bf16 g_h that cancel: autocast itself is
+    off by 2-9% there)."""
     ops = _ops()
     g = torch.Generator().manual_seed(7)
     N, H, W = 2, 12, 20
@@ -296,28 +302,37 @@ def test_head_fwd_bwd(K):
     logit_ref.backward(glog)
     f = lambda t: t.float().contiguous().to(DEV)
     zd = f(nhwc(z))
-    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K), dtype=torch.uint8, device=DEV)
+    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K, dt), dtype=torch.uint8, device=DEV)
     rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
     mean, inv = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
     out2h = torch.empty(N, K, 2 * H, 2 * W, device=DEV)
     logits = torch.empty(N, K, H, W, device=DEV)
     ops.head_fwd(zd, N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2.reshape(K, 64)), f(b2), True, 1e-5, 0.1,
-                 rm, rv, mean, inv, out2h, logits, ws)
+                 rm, rv, mean, inv, out2h, logits, ws, dtype=dt)
     gz = torch.empty(N, H, W, K, device=DEV)
     gw1, gb1 = torch.empty(64, K, 3, 3, device=DEV), torch.empty(64, device=DEV)
     gg, gbt = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
     gw2, gb2 = torch.empty(K, 64, device=DEV), torch.empty(K, device=DEV)
     ops.head_bwd(zd, N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2.reshape(K, 64)), mean, inv, f(glog), None,
-                 gz, gw1, gb1, gg, gbt, gw2, gb2, ws)
+                 gz, gw1, gb1, gg, gbt, gw2, gb2, ws, dtype=dt)
     torch.cuda.synchronize()
-    assert rel(out2h, out) < 1e-4
-    assert rel(logits, logit_ref) < 1e-4
-    assert rel(gz, nhwc(leaves[0].grad)) < 1e-4
-    assert rel(gw1, leaves[1].grad) < 1e-4
-    assert rel(gg, leaves[3].grad) < 1e-4
-    assert rel(gbt, leaves[4].grad) < 1e-4
-    assert rel(gw2, leaves[5].grad.reshape(K, 64)) < 1e-4
-    assert rel(gb2, leaves[6].grad) < 1e-4
+    names = ["out2h", "logits", "gz", "gw1", "gg", "gbt", "gw2", "gb2"]
+    ours = [out2h, logits, gz, gw1, gg, gbt, gw2, gb2]
+    refs = [out, logit_ref, nhwc(leaves[0].grad), leaves[1].grad, leaves[3].grad, leaves[4].grad,
+            leaves[5].grad.reshape(K, 64), leaves[6].grad]
+    if dt == torch.float32:
+        tols = [1e-4] * len(names)
+    else:
+        ac = [t.float().clone().requires_grad_(True) for t in (z, w1, b1, gamma, beta, w2, b2)]
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ao = _head_ref(*ac)
+            al = F.avg_pool2d(ao, 2)
+        al.float().backward(glog.float())
+        acv = [ao.detach(), al.detach(), nhwc(ac[0].grad), ac[1].grad, ac[3].grad, ac[4].grad,
+               ac[5].grad.reshape(K, 64), ac[6].grad]
+        tols = [max(1e-2, 1.5 * rel(a, r)) for a, r in zip(acv, refs)]
+    for nm, o, r, t in zip(names, ours, refs, tols):
+        assert rel(o, r) < t, (nm, rel(o, r), t)
     assert float(gb1.abs().max()) < 1e-3 * float(gw1.abs().max()) + 1e-5  # pre-BN bias: ~0
 
 
