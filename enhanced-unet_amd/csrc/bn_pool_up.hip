@@ -9,7 +9,8 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int STH = 8, STW = 32;  // same pixel tiling as conv3x3 (stats rows agree)
+constexpr int STH = 8, STW = 32;  // wgrad tile of conv_small
+constexpr int SFH = 16;           // forward tile SFH x STW = conv3x3 forward tiling (BN stats rows agree)
 
 bool act_ok(const eunet_act* a) {
   return a && a->ptr && a->n > 0 && a->h > 0 && a->w > 0 && a->c > 0 && a->coff >= 0 &&
@@ -32,20 +33,20 @@ struct SmallArgs {
 };
 
 // 8 lanes per pixel (lane group g = lane & 7 owns output channels co0+8g..+7),
-// 32 pixels per pass = one output row of the 8x32 tile; per-thread Welford over
+// 32 pixels per pass = one output row of the 16x32 tile; per-thread Welford over
 // its 8 pixels, Chan-combined across lanes and waves (no transposes)
 template <typename T>
 __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
-  __shared__ float xs[(STH + 2) * (STW + 2) * 4];
+  __shared__ float xs[(SFH + 2) * (STW + 2) * 4];
   __shared__ __attribute__((aligned(16))) float wsm[4 * 9 * 64];  // [ci*9+t][64 co]
   __shared__ float wn_s[4], wm_s[4][64], wq_s[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int tile = blockIdx.x, tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
-  const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
+  const int y0 = (trem / a.tx) * SFH, x0 = (trem % a.tx) * STW;
   const int co0 = blockIdx.y * 64;
   const int cin = a.cin;
-  for (int i = tid; i < (STH + 2) * (STW + 2) * cin; i += NT) {
+  for (int i = tid; i < (SFH + 2) * (STW + 2) * cin; i += NT) {
     const int hp = i / cin, ci = i - hp * cin;
     const int hy = hp / (STW + 2), hx = hp - hy * (STW + 2);
     const int yy = y0 + hy - 1, xx = x0 + hx - 1;
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
   for (int e = 0; e < 8; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
   constexpr int E = Vec16<T>::N;
   const bool full = (co0 + 64 <= a.cout) && ((a.yct | a.yco) % E) == 0;
-  for (int pass = 0; pass < 8; ++pass) {
+  for (int pass = 0; pass < SFH; ++pass) {
     const int px = pass * 32 + ps;
     const int r = px / STW, c = px - r * STW;
     const int yy = y0 + r, xx = x0 + c;
@@ -759,7 +760,7 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, 
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
   a.w = w; a.b = bias;
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
-  a.stats = stats; a.tx = cdiv(x->w, STW); a.ty = cdiv(x->h, STH); a.ntiles = x->n * a.tx * a.ty;
+  a.stats = stats; a.tx = cdiv(x->w, STW); a.ty = cdiv(x->h, SFH); a.ntiles = x->n * a.tx * a.ty;
   dim3 grid(a.ntiles, cdiv(y->c, 64));
   if (x->dtype == EUNET_BF16)
     conv_small_fwd_kernel<bf16_t><<<grid, NT, 0, (hipStream_t)stream>>>(a);

@@ -80,136 +80,254 @@ __device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int
   *(uint4*)(lds + (q * HPXP + hp) * 16) = v;
 }
 
-// v2: 512 threads = 8 waves (2 per SIMD); wave w computes output row w of the
-// 8x32 tile (32 px x 64 co = 2x4 MFMA tiles).  LDS is double-buffered: the next
-// chunk's global loads go to registers before the MFMAs of the current chunk
-// and are written (with the BN+ReLU transform) into the other buffer right
-// after them, so there is ONE barrier per K-chunk.  The epilogue stages the
-// tile through LDS and stores whole 16-byte vectors.
-constexpr int FT = 512;
-constexpr int FA_ITERS = (A_UNITS + FT - 1) / FT;  // 3
-constexpr int FB_ITERS = B_UNITS / FT;             // 4 full rounds ...
-constexpr int FB_TAIL = B_UNITS - FB_ITERS * FT;   // ... + 256 units for threads 0..255
-constexpr int STAGE_BYTES = A_LDS_BYTES + B_LDS_BYTES;  // 59392
-constexpr int OUT_LD = 68;                              // fp32 row stride of the output staging tile
-constexpr int FWD_LDS = 2 * STAGE_BYTES;                // 118784 (>= 256*68*4 + 2*8*64*4)
+// Forward v3: 256 threads = 4 waves (one per SIMD), output tile 16 x 32 px x 64 co;
+// wave w computes rows 4w..4w+3 (128 px = 8 m-tiles) x 64 co = 32 accumulators,
+// so each tap issues 8 A + 4 B 16-byte LDS reads for 32 MFMAs (LDS well below
+// its 256 B/clk).  LDS is double-buffered (2 x 75 KB): the next chunk's global
+// loads go to registers before the current chunk's MFMAs and are written (with
+// the BN+ReLU transform) into the other buffer after them -> one barrier per
+// K-chunk.  Halo units are loaded 8 pixels x 4 quarters per 32 lanes so the
+// LDS writes are conflict-free.  The epilogue stages the tile through LDS and
+// stores whole 16-byte vectors.
+constexpr int FTH = 16, FTW = 32;            // output tile
+constexpr int FHW = FTW + 2;                 // 34
+constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
+constexpr int FHPXP = 624;                   // plane stride (multiple of 16 units)
+constexpr int FT = 256;
+constexpr int FA_UNITS = 4 * FHPX;           // 2448
+constexpr int FA_ITERS = (FA_UNITS + FT - 1) / FT;  // 10
+constexpr int FB_ITERS = B_UNITS / FT;       // 9
+constexpr int FA_BYTES = 4 * FHPXP * 16;     // 39936
+constexpr int STAGE_BYTES = FA_BYTES + B_LDS_BYTES;  // 76800
+constexpr int OUT_LD = 68;                   // fp32 row stride of the output staging tile
+constexpr int FWD_LDS_DB = 2 * STAGE_BYTES;  // 153600: one block / CU, double-buffered
+constexpr int FWD_LDS = STAGE_BYTES;         // 76800: two blocks / CU
+static_assert(FTH * FTW / 2 * OUT_LD * 4 + 2 * 4 * 64 * 4 <= FWD_LDS, "epilogue staging must fit");
+
+// XCD-aware block order: hardware block b runs on XCD b % 8.  Logical block L =
+// (tile, co-block) with the co-block fastest; each XCD gets a contiguous range of L,
+// so the co-blocks that re-read one input tile (and its halo neighbours) share
+// that XCD's L2 and run at the same time.
+__device__ __forceinline__ void xcd_map(int b, int ntiles, int ncob, int& tile, int& cob) {
+  const int total = ntiles * ncob, full = total & ~7;
+  const int L = b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+  tile = L / ncob;
+  cob = L - tile * ncob;
+}
+
+// unit id -> (halo pixel, quarter): 32 consecutive ids = 8 pixels x 4 quarters
+__device__ __forceinline__ void fwd_unit(int id, int& hp, int& q) {
+  hp = (id >> 5) * 8 + (id & 7);
+  q = (id >> 3) & 3;
+}
 
 template <typename T>
-__global__ __launch_bounds__(FT, 1) void conv3x3_fwd_kernel(FwdArgs a) {
+__device__ __forceinline__ u32x4 fwd_load_unit(const FwdArgs& a, int n, int y0, int x0, int id, int kc, bool& ok) {
+  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
+  int hp, q;
+  fwd_unit(id, hp, q);
+  const int hy = hp / FHW, hx = hp - hy * FHW;
+  const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+  const int c = kc * KC + q * E;
+  ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin;
+  if (!ok) return (u32x4){0u, 0u, 0u, 0u};
+  const T* p = (const T*)a.x + (((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
+  return *(const u32x4*)p;
+}
+
+template <typename T>
+__device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int id, int kc, u32x4 v, bool ok) {
+  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
+  int hp, q;
+  fwd_unit(id, hp, q);
+  if (hp >= FHPX) return;
+  if (ok && a.isc != nullptr) {
+    const int c = kc * KC + q * E;
+    float f[E];
+    Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
+    v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
+  }
+  *(u32x4*)(lds + (q * FHPXP + hp) * 16) = v;
+}
+
+// MODE: 0 = production.  Diagnostic builds only (tools/conv_ablate.hip):
+//   1 = no global loads / LDS writes inside the K loop, 2 = no MFMAs (VALU keeps the
+//   LDS reads alive), 4 = LDS fragments read once before the loop (MFMA-only loop),
+//   8 = plain tile-fastest block order instead of xcd_map.
+// DB: true = one block per CU, double-buffered LDS (next chunk prefetched into
+//   registers during the MFMAs); false = two blocks per CU, one LDS stage each
+//   (a block's staging overlaps the other block's MFMAs).
+template <typename T, int MODE = 0, bool DB = false>
+__global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int tile = blockIdx.x;
+  int tile, cob;
+  if constexpr ((MODE & 8) != 0) {  // diagnostic: plain tile-fastest order
+    tile = blockIdx.x % a.ntiles;
+    cob = blockIdx.x / a.ntiles;
+  } else {  // XCD-grouped (conv_bench: +5-15% on the 256^2-512^2 layers, +-3% elsewhere)
+    xcd_map(blockIdx.x, a.ntiles, a.cout_pad / BN, tile, cob);
+  }
   const int tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
-  const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-  const int co0 = blockIdx.y * BN;
+  const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
+  const int co0 = cob * BN;
   const int q = lane >> 4, li = lane & 15;
 
-  f32x4 acc[2][4];
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[FA_ITERS];
+  u32x4 ra[FA_ITERS];
   bool rok[FA_ITERS];
   u32x4 rb[FB_ITERS];
-  u32x4 rbt = (u32x4){0u, 0u, 0u, 0u};
   const u32x4* wp = (const u32x4*)a.wp;
-  const bool tail = tid < FB_TAIL;
 
 #define CONV_BUNIT(ID_, KC_) \
   wp[((long long)((KC_) * 4 + (ID_) / (BN * 9)) * a.cout_pad + co0) * 9 + (ID_) % (BN * 9)]
-#define CONV_GLOAD(KC_)                                                                       \
+#define CONV_GLOAD_A(KC_, I0_, I1_)                                                           \
   do {                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < FA_ITERS; ++i)                                      \
-        ra[i] = load_halo_unit<T>(a, n, y0, x0, tid + i * FT, (KC_), rok[i]);                 \
-    _Pragma("unroll") for (int i = 0; i < FB_ITERS; ++i) rb[i] = CONV_BUNIT(tid + i * FT, KC_); \
-    if (tail) rbt = CONV_BUNIT(tid + FB_ITERS * FT, KC_);                                     \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
+        ra[i] = fwd_load_unit<T>(a, n, y0, x0, tid + i * FT, (KC_), rok[i]);                  \
   } while (0)
-#define CONV_LWRITE(KC_, BUF_)                                                                \
+#define CONV_GLOAD_B(KC_, I0_, I1_)                                                           \
+  do {                                                                                        \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) rb[i] = CONV_BUNIT(tid + i * FT, KC_); \
+  } while (0)
+#define CONV_LWRITE_A(KC_, BUF_, I0_, I1_)                                                    \
   do {                                                                                        \
     char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
-    char* Bs_ = As_ + A_LDS_BYTES;                                                            \
-    _Pragma("unroll") for (int i = 0; i < FA_ITERS; ++i)                                      \
-        store_halo_unit<T>(a, As_, tid + i * FT, (KC_), ra[i], rok[i]);                       \
-    _Pragma("unroll") for (int i = 0; i < FB_ITERS; ++i) *(u32x4*)(Bs_ + (tid + i * FT) * 16) = rb[i]; \
-    if (tail) *(u32x4*)(Bs_ + (tid + FB_ITERS * FT) * 16) = rbt;                              \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
+        fwd_store_unit<T>(a, As_, tid + i * FT, (KC_), ra[i], rok[i]);                        \
+  } while (0)
+#define CONV_LWRITE_B(BUF_, I0_, I1_)                                                         \
+  do {                                                                                        \
+    char* Bs_ = smem + (BUF_) * STAGE_BYTES + FA_BYTES;                                       \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) *(u32x4*)(Bs_ + (tid + i * FT) * 16) = rb[i]; \
   } while (0)
 
-  CONV_GLOAD(0);
-  CONV_LWRITE(0, 0);
-  __syncthreads();
-  for (int kc = 0; kc < a.nkc; ++kc) {
-    const int cur = kc & 1;
-    if (kc + 1 < a.nkc) CONV_GLOAD(kc + 1);
-    const char* As = smem + cur * STAGE_BYTES;
-    const char* Bs = As + A_LDS_BYTES;
+  constexpr int AH = FA_ITERS / 2, BH = FB_ITERS / 2;
+  auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
+    CONV_GLOAD_A(kc, 0, AH);
+    CONV_LWRITE_A(kc, buf, 0, AH);
+    CONV_GLOAD_A(kc, AH, FA_ITERS);
+    CONV_LWRITE_A(kc, buf, AH, FA_ITERS);
+    CONV_GLOAD_B(kc, 0, BH);
+    CONV_LWRITE_B(buf, 0, BH);
+    CONV_GLOAD_B(kc, BH, FB_ITERS);
+    CONV_LWRITE_B(buf, BH, FB_ITERS);
+  };
+  auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[8], const uint4 (&fb0)[4]) {
+#pragma unroll 1
+    for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int ky = t / 3, kx = t - ky * 3;
-      uint4 fa[2], fb[4];
+    for (int kx = 0; kx < 3; ++kx) {
+      const int t = ky * 3 + kx;
+      uint4 fb[4];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int hp = (wv + ky) * HW_ + mt * 16 + li + kx;
-        fa[mt] = *(const uint4*)(As + (q * HPXP + hp) * 16);
-      }
+      for (int nt = 0; nt < 4; ++nt)
+        fb[nt] = (MODE & 4) ? fb0[nt] : *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 8; ++mt) {
+        const int hp = (4 * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
+        const uint4 fa = (MODE & 4) ? fa0[mt] : *(const uint4*)(As + (q * FHPXP + hp) * 16);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          if constexpr (sizeof(T) == 2) {
+          if constexpr ((MODE & 2) != 0) {
+            acc[mt][nt][0] += __uint_as_float((fa.x ^ fb[nt].x) & 0x3f000000u);
+          } else if constexpr (sizeof(T) == 2) {
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, fa[mt]), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
+                __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
           } else {
-            const uint4 A_ = fa[mt], B_ = fb[nt];
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
+            const uint4 B_ = fb[nt];
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
           }
         }
+      }
     }
-    if (kc + 1 < a.nkc) CONV_LWRITE(kc + 1, cur ^ 1);
-    __syncthreads();
+  };
+
+  uint4 fa0[8], fb0[4];
+  if constexpr (DB) {
+    CONV_GLOAD_A(0, 0, FA_ITERS);
+    CONV_GLOAD_B(0, 0, FB_ITERS);
+    CONV_LWRITE_A(0, 0, 0, FA_ITERS);
+    CONV_LWRITE_B(0, 0, FB_ITERS);
+  } else {
+    stage(0, 0);
   }
-#undef CONV_GLOAD
-#undef CONV_LWRITE
+  __syncthreads();
+  if constexpr ((MODE & 4) != 0) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) fb0[nt] = *(const uint4*)(smem + FA_BYTES + (q * (BN * 9) + (nt * 16 + li) * 9) * 16);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt)
+      fa0[mt] = *(const uint4*)(smem + (q * FHPXP + (4 * wv + (mt >> 1)) * FHW + (mt & 1) * 16 + li) * 16);
+  }
+  for (int kc = 0; kc < a.nkc; ++kc) {
+    if constexpr (DB) {
+      const int cur = kc & 1;
+      if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
+        CONV_GLOAD_A(kc + 1, 0, FA_ITERS);
+        CONV_GLOAD_B(kc + 1, 0, FB_ITERS);
+      }
+      chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
+      if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
+        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, FA_ITERS);
+        CONV_LWRITE_B(cur ^ 1, 0, FB_ITERS);
+      }
+      __syncthreads();
+    } else {
+      if (kc > 0) {
+        if ((MODE & 1) == 0) {
+          __syncthreads();  // every wave is done reading the stage
+          stage(kc, 0);
+        }
+        __syncthreads();
+      }
+      chunk(smem, smem + FA_BYTES, fa0, fb0);
+    }
+  }
+#undef CONV_GLOAD_A
+#undef CONV_GLOAD_B
+#undef CONV_LWRITE_A
+#undef CONV_LWRITE_B
 #undef CONV_BUNIT
 
-  // ---- epilogue: bias, BN partials, LDS-staged vector stores ---------------
-  const int vh = min(TH, a.H - y0), vw = min(TW, a.W - x0);
-  const bool rv = wv < vh;
+  // ---- epilogue: bias, BN partials, LDS-staged vector stores (two half tiles) ----
+  const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int co = co0 + nt * 16 + li;
     const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[mt][nt][i] += bv;
   }
-  float* stage = (float*)smem;                              // [256 px][OUT_LD]
-  float* red = (float*)(smem + TH * TW * OUT_LD * 4);       // [8][64] x 2
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int px = wv * TW + mt * 16 + q * 4 + i;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) stage[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
-    }
+  constexpr int HALF_PX = FTH * FTW / 2;                        // 256 px per half tile
+  float* stg = (float*)smem;                                    // [256 px][OUT_LD]
+  float* red = (float*)(smem + HALF_PX * OUT_LD * 4);           // [4][64] x 2
+  __syncthreads();  // all waves are done with the K loop's LDS
   if (a.stats != nullptr) {
     float s[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v += (rv && mt * 16 + q * 4 + i < vw) ? acc[mt][nt][i] : 0.f;
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = 4 * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
+          v += ok ? acc[mt][nt][i] : 0.f;
+        }
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       s[nt] = v;
@@ -224,18 +342,19 @@ __global__ __launch_bounds__(FT, 1) void conv3x3_fwd_kernel(FwdArgs a) {
     for (int nt = 0; nt < 4; ++nt) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) t += red[w * 64 + nt * 16 + li];
+      for (int w = 0; w < 4; ++w) t += red[w * 64 + nt * 16 + li];
       mb[nt] = t / cnt;
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+          const bool ok = 4 * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
           const float d = acc[mt][nt][i] - mb[nt];
-          v += (rv && mt * 16 + q * 4 + i < vw) ? d * d : 0.f;
+          v += ok ? d * d : 0.f;
         }
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
@@ -243,39 +362,52 @@ __global__ __launch_bounds__(FT, 1) void conv3x3_fwd_kernel(FwdArgs a) {
     }
     if (q == 0)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) red[512 + wv * 64 + nt * 16 + li] = s[nt];
+      for (int nt = 0; nt < 4; ++nt) red[256 + wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
     if (tid < 64 && co0 + tid < a.cout) {
       float sum = 0.f, m2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) {
+      for (int w = 0; w < 4; ++w) {
         sum += red[w * 64 + tid];
-        m2 += red[512 + w * 64 + tid];
+        m2 += red[256 + w * 64 + tid];
       }
       a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
       a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
     }
-    if (blockIdx.y == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
-  } else {
-    __syncthreads();
+    if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
   }
   constexpr int E = Vec16<T>::N;
   constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
   T* yp = (T*)a.y;
 #pragma unroll
-  for (int j = 0; j < TH * TW * UPX / FT; ++j) {
-    const int id = tid + j * FT;
-    const int px = id / UPX, u = id - px * UPX;
-    const int r = px / TW, c = px - r * TW;
-    const int co = co0 + u * E;
-    if (r < vh && c < vw && co < a.cout) {
-      const float* sp = stage + px * OUT_LD + u * E;
-      float f[E];
+  for (int half = 0; half < 2; ++half) {
+    if ((wv >> 1) == half) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) f[e] = sp[e];
-      const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
-      *(uint4*)(yp + pix * a.yct + a.yco + co) = Vec16<T>::pack(f);
+      for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int px = ((wv & 1) * 4 + (mt >> 1)) * FTW + (mt & 1) * 16 + q * 4 + i;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) stg[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
+        }
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < HALF_PX * UPX / FT; ++j) {
+      const int id = tid + j * FT;
+      const int px = id / UPX, u = id - px * UPX;
+      const int r = half * (FTH / 2) + px / FTW, c = px % FTW;
+      const int co = co0 + u * E;
+      if (r < vh && c < vw && co < a.cout) {
+        const float* sp = stg + px * OUT_LD + u * E;
+        float f[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) f[e] = sp[e];
+        const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
+        *(uint4*)(yp + pix * a.yct + a.yco + co) = Vec16<T>::pack(f);
+      }
+    }
+    if (half == 0) __syncthreads();
   }
 }
 
@@ -316,7 +448,7 @@ struct WgArgs {
   const float* isc; const float* ish;
   const void* dy; int dct, dco, cout;
   float* dw; float* db;
-  int tx, ty, ntiles, per_split;
+  int tx, ty, ntiles, per_split, nsplit;
 };
 
 template <typename T>
@@ -443,18 +575,39 @@ __global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
 // w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
 // 32-pixel k-step costs 8 + 18 transposed fragment reads for 36 MFMAs.
-constexpr int KCW = 64;                       // ci channels per wgrad block (bf16)
-constexpr int WX_LDS = 8 * HPXP * 16;         // X halo [8 octants][HPXP][16 B]
-constexpr int WD_LDS = TH * TW * 64 * 2;      // dY tile [256 px][64 co] bf16
-constexpr int WG_LDS = WX_LDS + WD_LDS + 4 * 64 * 4;
+constexpr int KCW = 64;                        // ci channels per wgrad block (bf16)
+constexpr int WX_LDS = 8 * HPXP * 16;          // X halo [8 octants][HPXP][16 B]
+constexpr int WD_LDS = TH * TW * 64 * 2;       // dY tile [256 px][64 co] bf16
+constexpr int WSTAGE = WX_LDS + WD_LDS;        // 77824
+constexpr int WG_LDS = WSTAGE + 4 * 64 * 4;      // one stage + db reduction (2 blocks / CU)
+constexpr int WX_IDS = ((HPX + 7) / 8) * 64;   // 2752: X unit ids (8 pixels x 8 octants per 64)
+constexpr int WX_ITERS = (WX_IDS + NTHR - 1) / NTHR;  // 11
+constexpr int WD_ITERS = TH * TW * 8 / NTHR;   // 8
+static_assert(WG_LDS <= 160 * 1024, "wgrad LDS");
 
+// Block order: logical L = (split, co-block, ci-block), ci fastest, XCD-contiguous
+// (see xcd_map): the blocks sharing a split's X / dY tiles share one L2.
+__device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, int& split, int& cob, int& cib) {
+  const int total = nsplit * ncob * ncib, full = total & ~7;
+  const int L = b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+  cib = L % ncib;
+  const int r = L / ncib;
+  cob = r % ncob;
+  split = r / ncob;
+}
+
+// Pixels are the GEMM K: dW[co][t][ci] += dY^T[co][px] * X~[px + d_t][ci].
+// 4 waves, wave w owns ci 16w..16w+15 of the block's 64, all 64 co and 9 taps
+// (36 accumulators).  Two blocks per CU: a tile's X halo / dY loads are all
+// issued before the barrier that ends the previous tile's MFMAs, then written
+// to LDS (BN+ReLU applied to X there); the other block computes meanwhile.
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Xs = smem;
-  char* Ds = smem + WX_LDS;
-  float* dbred = (float*)(Ds + WD_LDS);
+  float* dbred = (float*)(smem + WSTAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int split = blockIdx.x, co0 = blockIdx.y * 64, kc = blockIdx.z;
+  int split, cob, kc;
+  wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
+  const int co0 = cob * 64;
   const int t_begin = split * a.per_split;
   const int t_end = min(a.ntiles, t_begin + a.per_split);
   const int tpi = a.tx * a.ty;
@@ -466,45 +619,85 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
+  u32x4 rx[WX_ITERS], rd[WD_ITERS];
 
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  auto gload_x = [&](int tile, int i0, int i1) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-    __syncthreads();
-    // X halo, 64 channels: unit id -> (pixel id>>3, octant id&7), BN+ReLU applied here
-    for (int id = tid; id < 8 * HPX; id += NTHR) {
-      const int hp = id >> 3, oc = id & 7;
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int id = tid + i * NTHR;
+      const int hp = (id >> 6) * 8 + (id & 7), oc = (id >> 3) & 7;
       const int hy = hp / HW_, hx = hp - hy * HW_;
       const int yy = y0 + hy - 1, xx = x0 + hx - 1;
       const int c = kc * KCW + oc * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
-        v = *(const uint4*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
-        if (a.isc != nullptr) {
-          float f[8];
-          Vec16<bf16_t>::unpack(v, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
-          v = Vec16<bf16_t>::pack(f);
-        }
-      }
-      *(uint4*)(Xs + (oc * HPXP + hp) * 16) = v;
+      rx[i] = (u32x4){0u, 0u, 0u, 0u};
+      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
+        rx[i] = *(const u32x4*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
     }
-    // dY tile
-    for (int id = tid; id < TH * TW * 8; id += NTHR) {
+  };
+  auto gload_d = [&](int tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+#pragma unroll
+    for (int i = 0; i < WD_ITERS; ++i) {
+      const int id = tid + i * NTHR;
       const int px = id >> 3, u = id & 7;
       const int r = px / TW, c = px - r * TW;
       const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
-      uint4 v = make_uint4(0, 0, 0, 0);
+      rd[i] = (u32x4){0u, 0u, 0u, 0u};
       if (yy < a.H && xx < a.W && co < a.cout)
-        v = *(const uint4*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
-      *(uint4*)(Ds + id * 16) = v;
+        rd[i] = *(const u32x4*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
     }
+  };
+  auto lwrite_x = [&](int tile, int i0, int i1) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+    char* Xs = smem;
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int id = tid + i * NTHR;
+      const int hp = (id >> 6) * 8 + (id & 7), oc = (id >> 3) & 7;
+      if (hp >= HPX) continue;
+      u32x4 v = rx[i];
+      if (a.isc != nullptr) {
+        const int hy = hp / HW_, hx = hp - hy * HW_;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        const int c = kc * KCW + oc * 8;
+        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {  // padding stays 0
+          float f[8];
+          Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
+          v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
+        }
+      }
+      *(u32x4*)(Xs + (oc * HPXP + hp) * 16) = v;
+    }
+  };
+  auto lwrite_d = [&]() {
+    char* Ds = smem + WX_LDS;
+#pragma unroll
+    for (int i = 0; i < WD_ITERS; ++i) *(u32x4*)(Ds + (tid + i * NTHR) * 16) = rd[i];
+  };
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    constexpr int XH = WX_ITERS / 2;
+    gload_x(tile, 0, XH);
+    __syncthreads();  // previous tile's LDS reads are done
+    lwrite_x(tile, 0, XH);
+    gload_x(tile, XH, WX_ITERS);
+    lwrite_x(tile, XH, WX_ITERS);
+    gload_d(tile);
+    lwrite_d();
     __syncthreads();
+    const char* Xs = smem;
+    const char* Ds = Xs + WX_LDS;
     if (a.db != nullptr && kc == 0) {
       const bf16_t* d = (const bf16_t*)Ds;
       for (int px = wv; px < TH * TW; px += 4) dbacc += bf2f(d[px * 64 + lane]);
     }
+#pragma unroll 1
     for (int ks = 0; ks < TH; ++ks) {
       const int pxa = ks * TW + 8 * g + q4;
       bf16x8 af[4];
@@ -542,31 +735,43 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[t][ct][e];
       }
   if (a.db != nullptr && kc == 0) {
-    __syncthreads();
-    dbred[wv * 64 + lane] = dbacc;
+    dbred[wv * 64 + lane] = dbacc;  // dbred lies outside the tile stage
     __syncthreads();
     if (tid < 64 && co0 + tid < a.cout)
       a.db[(long long)split * a.cout + co0 + tid] = dbred[tid] + dbred[64 + tid] + dbred[128 + tid] + dbred[192 + tid];
   }
 }
 
-__global__ void wgrad_reduce_kernel(const float* part, const float* dbp, int nsplit, int cout, int cin, int taps,
-                                    float* dw, float* db) {
+// Deterministic split reduction: 64 consecutive elements x 4 split groups per block
+// (fixed-order fp64 sums); blocks past the dW range reduce the bias partials.
+constexpr int RSG = 4;
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, const float* dbp, int nsplit, int cout,
+                                                           int cin, int taps, float* dw, float* db) {
+  __shared__ double red[RSG][64];
+  const int tx = threadIdx.x & 63, sg = threadIdx.x >> 6;
   const long long per = (long long)cout * taps * cin;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id < per) {
-    double s = 0.0;
-    for (int k = 0; k < nsplit; ++k) s += (double)part[(long long)k * per + id];
-    const int ci = (int)(id % cin);
-    const long long r = id / cin;
-    const int t = (int)(r % taps);
-    const int co = (int)(r / taps);
-    dw[((long long)co * cin + ci) * taps + t] = (float)s;
+  const long long nbw = (per + 63) / 64;
+  const bool isdw = blockIdx.x < nbw;
+  const long long e = (isdw ? (long long)blockIdx.x : (long long)blockIdx.x - nbw) * 64 + tx;
+  const long long cnt = isdw ? per : cout;
+  const float* src = isdw ? part : dbp;
+  double s = 0.0;
+  if (e < cnt) {
+#pragma unroll 4
+    for (int k = sg; k < nsplit; k += RSG) s += (double)src[(long long)k * cnt + e];
   }
-  if (db != nullptr && id < cout) {
-    double s = 0.0;
-    for (int k = 0; k < nsplit; ++k) s += (double)dbp[(long long)k * cout + id];
-    db[id] = (float)s;
+  red[sg][tx] = s;
+  __syncthreads();
+  if (sg != 0 || e >= cnt) return;
+  const double t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+  if (isdw) {
+    const int ci = (int)(e % cin);
+    const long long r = e / cin;
+    const int tp = (int)(r % taps);
+    const int co = (int)(r / taps);
+    dw[((long long)co * cin + ci) * taps + tp] = (float)t;
+  } else {
+    db[e] = (float)t;
   }
 }
 
@@ -605,7 +810,7 @@ int eunet_conv3x3_pack(const float* w, int cout, int cin, int flip, void* wp, in
 
 int eunet_conv3x3_tiles(const eunet_act* y, int* tiles) {
   EUNET_REQUIRE(act_ok(y) && tiles, "conv3x3_tiles: bad args");
-  *tiles = y->n * cdiv(y->h, TH) * cdiv(y->w, TW);
+  *tiles = y->n * cdiv(y->h, FTH) * cdiv(y->w, FTW);
   return EUNET_OK;
 }
 
@@ -624,10 +829,10 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.wp = wp; a.cout_pad = cdiv(y->c, BN) * BN; a.nkc = cdiv(x->c, kchunk(x->dtype));
   a.bias = bias;
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
-  a.stats = stats; a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
+  a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
-  dim3 grid(a.ntiles, a.cout_pad / BN);
+  dim3 grid(a.ntiles * (a.cout_pad / BN));
   if (x->dtype == EUNET_BF16) {
     allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
@@ -670,9 +875,10 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.dw = dw_part; a.db = db_part;
   a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
+  a.nsplit = nsplit;
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
-    dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, KCW));
+    dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));
     allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
     conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
   } else {
@@ -691,8 +897,8 @@ int eunet_wgrad_reduce(const float* dw_part, const float* db_part, int nsplit, i
   EUNET_REQUIRE((db_part == nullptr) == (db == nullptr), "wgrad_reduce: db pair");
   long long per = (long long)cout * taps * cin;
   if (per < cout) per = cout;
-  wgrad_reduce_kernel<<<(unsigned)((per + 255) / 256), 256, 0, (hipStream_t)stream>>>(dw_part, db_part, nsplit,
-                                                                                      cout, cin, taps, dw, db);
+  const unsigned nb = (unsigned)((per + 63) / 64 + (db != nullptr ? (cout + 63) / 64 : 0));
+  wgrad_reduce_kernel<<<nb, 256, 0, (hipStream_t)stream>>>(dw_part, db_part, nsplit, cout, cin, taps, dw, db);
   EUNET_LAUNCH_CHECK("wgrad_reduce");
   return EUNET_OK;
 }

@@ -9,7 +9,8 @@ import ctypes
 import os
 from ctypes import POINTER, c_float, c_int, c_size_t, c_void_p, c_char_p, c_int64
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeunet_hip.so")
+# EUNET_LIB overrides the in-tree library (A/B of two builds); the default is the in-tree build
+LIB_PATH = os.environ.get("EUNET_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeunet_hip.so")
 
 EUNET_F32 = 0
 EUNET_BF16 = 1

@@ -78,10 +78,13 @@ def _pre_bn_bias(k):
     return k.endswith((".0.bias", ".3.bias")) and not k.startswith("enhance.3")
 
 
-def _oracle_grads(base, cin, K, x, msk, dtype):
+def _oracle_grads(base, cin, K, x, msk, dtype, noise=0.0, seed=0):
     S = R.formula_weights(base, cin, K, dtype=dtype)
+    g = torch.Generator().manual_seed(seed)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:
+            if noise:
+                S[k] = S[k] * (1 + noise * torch.randn(S[k].shape, generator=g, dtype=dtype))
             S[k].requires_grad_(True)
     loss = R.batch_loss(R.forward(S, x.to(dtype), training=True), msk)
     loss.backward()
@@ -92,14 +95,24 @@ def _oracle_grads(base, cin, K, x, msk, dtype):
 def test_train_grads_match_oracle(base, cin, K, H):
     """Loss + every parameter gradient of one train step vs the fp64 oracle.
 
-    Tolerance per tensor: max(1e-3, 3x the error of the fp32 oracle itself vs fp64)
-    -- the deepest gradients (enc1) accumulate fp32 rounding through 14 conv layers
-    in ANY fp32 implementation, the reference's included."""
+    The step is discontinuous at ReLU kinks and max-pool ties, and with ~10^6
+    activations some always sit within 1e-6 of a kink: an activation moved by fp32
+    rounding (~1e-6 relative, the measured conv error) can take the other branch
+    and shift a BN-beta gradient, and through it every gradient below, by ~1e-3.
+    Tolerance per tensor is therefore max(1e-3, 3x the fp32 oracle's error,
+    1.5x the spread of the fp64 oracle itself under 1e-6 relative weight
+    perturbations) -- the last term measures that kink noise for this input."""
     from eunet.losses import combined_loss
     from eunet import synth
     x, msk = synth.batch(2, H, H, start_index=7, num_classes=K, in_channels=cin)
     S, loss_ref = _oracle_grads(base, cin, K, x, msk, torch.float64)
     S32, _ = _oracle_grads(base, cin, K, x, msk, torch.float32)
+    spread = {}
+    for seed in (1, 2):
+        Sp, _ = _oracle_grads(base, cin, K, x, msk, torch.float64, noise=1e-6, seed=seed)
+        for k in S:
+            if S[k].grad is not None:
+                spread[k] = max(spread.get(k, 0.0), _rel_l2(Sp[k].grad, S[k].grad))
     m = _model(base, cin, K)
     m.train()
     logits = m.forward_lowres(x.to(DEV))
@@ -115,7 +128,7 @@ def test_train_grads_match_oracle(base, cin, K, H):
             continue
         # relative L2: a few max-pool argmax flips at ReLU ties (a discontinuity every
         # fp32 implementation hits) move single elements but not the tensor
-        tol = max(1e-3, 3.0 * _rel_l2(S32[k].grad, ref))
+        tol = max(1e-3, 3.0 * _rel_l2(S32[k].grad, ref), 1.5 * spread[k])
         assert _rel_l2(p.grad, ref) < tol, (k, _rel_l2(p.grad, ref), tol, _rel(p.grad, ref))
     for k, v in m.state_dict().items():
         if "running" in k:

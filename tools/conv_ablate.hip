@@ -1,0 +1,90 @@
+// Diagnostic: time the conv3x3 forward kernel with parts of its K loop removed
+// (MODE bits, see conv3x3.hip) on one layer shape.  Build:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/conv_ablate.hip -o tools/conv_ablate
+// Run: tools/conv_ablate N H W CIN COUT [reps]
+// Prints per-mode ms and TFLOP/s.  Not part of the product; outputs of modes != 0 are garbage.
+#include "../enhanced-unet_amd/csrc/conv3x3.hip"
+#include "../enhanced-unet_amd/csrc/capi.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+template <int MODE, bool DB = false>
+static float run(const FwdArgs& a, dim3 grid, int reps) {
+  const int lds = DB ? FWD_LDS_DB : FWD_LDS;
+  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB>, lds);
+  conv3x3_fwd_kernel<bf16_t, MODE, DB><<<grid, FT, lds>>>(a);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB><<<grid, FT, lds>>>(a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 6) {
+    fprintf(stderr, "usage: %s N H W CIN COUT [reps]\n", argv[0]);
+    return 2;
+  }
+  const int N = atoi(argv[1]), H = atoi(argv[2]), W = atoi(argv[3]), cin = atoi(argv[4]), cout = atoi(argv[5]);
+  const int reps = argc > 6 ? atoi(argv[6]) : 10;
+  if (N <= 0 || H <= 0 || W <= 0 || cin % 32 || cout % 64 || (long long)N * H * W * (cin + cout) > (1ll << 31)) {
+    fprintf(stderr, "bad shape\n");
+    return 2;
+  }
+  const size_t nx = (size_t)N * H * W * cin, ny = (size_t)N * H * W * cout;
+  std::vector<uint16_t> hx(nx);
+  for (size_t i = 0; i < nx; ++i) hx[i] = 0x3c00 + (uint16_t)((i * 2654435761u) >> 24 & 0x7f);  // ~[1,2)
+  std::vector<float> hw((size_t)cout * cin * 9);
+  for (size_t i = 0; i < hw.size(); ++i) hw[i] = ((int)((i * 40503u) & 255) - 128) / 4096.f;
+  void *x, *y, *wp;
+  float *w, *stats;
+  CK(hipMalloc(&x, nx * 2));
+  CK(hipMalloc(&y, ny * 2));
+  CK(hipMalloc(&w, hw.size() * 4));
+  size_t wpb = 0;
+  eunet_conv3x3_packed_bytes(cout, cin, EUNET_BF16, &wpb);
+  CK(hipMalloc(&wp, wpb));
+  CK(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+  if (eunet_conv3x3_pack(w, cout, cin, 0, wp, EUNET_BF16, nullptr)) {
+    fprintf(stderr, "pack: %s\n", eunet_last_error());
+    return 1;
+  }
+  FwdArgs a;
+  a.x = x; a.N = N; a.H = H; a.W = W; a.xct = cin; a.xco = 0; a.cin = cin;
+  a.isc = nullptr; a.ish = nullptr;
+  a.wp = wp; a.cout_pad = cout; a.nkc = cin / 32;
+  a.bias = nullptr;
+  a.y = y; a.yct = cout; a.yco = 0; a.cout = cout;
+  a.tx = cdiv(W, FTW); a.ty = cdiv(H, FTH); a.ntiles = N * a.tx * a.ty;
+  CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
+  a.stats = stats;
+  dim3 grid(a.ntiles * (cout / BN));
+  const double flop = 2.0 * 9 * cin * cout * (double)N * H * W;
+  const float t0 = run<0>(a, grid, reps), t1 = run<1>(a, grid, reps), t2 = run<2>(a, grid, reps);
+  const float t4 = run<4>(a, grid, reps), t5 = run<5>(a, grid, reps), t8 = run<8>(a, grid, reps);
+  const float tdb = run<0, true>(a, grid, reps), tdb5 = run<5, true>(a, grid, reps);
+  printf("{\"shape\": [%d, %d, %d, %d, %d], \"blocks\": %d", N, H, W, cin, cout, a.ntiles * cout / BN);
+  const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db_full", "db_mfma_only"};
+  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5};
+  for (int i = 0; i < 8; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+  printf("}\n");
+  return 0;
+}
