@@ -352,70 +352,109 @@ __global__ void bnrelu_pool_kernel(const T* y, int N, int H, int W, int C, int y
   *(uint4*)(pool + po * pct + pco + c) = Vec16<T>::pack(m);
 }
 
-// BN+ReLU -> bilinear x2 upsample (align_corners=False)
+// BN+ReLU -> bilinear x2 upsample (align_corners=False).  One thread per low-res pixel
+// and 16-byte channel unit: the 3x3 clamped neighbourhood is transformed once and
+// gives the 2x2 outputs 2i+a, 2j+b with PyTorch's weights (0.25/0.75, edge rows
+// weighted 1/0 exactly as upsample_bilinear2d's clamped source index).
 template <typename T>
-__global__ void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco, const float* sc,
-                                 const float* sh, T* out, int oct, int oco) {
+__global__ __launch_bounds__(256) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
+                                                        const float* sc, const float* sh, T* out, int oct, int oco) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E, H2 = 2 * h, W2 = 2 * w;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)N * H2 * W2 * U;
+  const long long total = (long long)N * h * w * U;
   if (id >= total) return;
   const int u = (int)(id % U);
   long long p = id / U;
-  const int ox = (int)(p % W2); p /= W2;
-  const int oy = (int)(p % H2);
-  const int n = (int)(p / H2);
+  const int j = (int)(p % w); p /= w;
+  const int i = (int)(p % h);
+  const int n = (int)(p / h);
   const int c = u * E;
-  int y0, y1, x0, x1;
-  float ly, lx;
-  up2_src(oy, h, y0, y1, ly);
-  up2_src(ox, w, x0, x1, lx);
-  const int ys[2] = {y0, y1}, xs[2] = {x0, x1};
-  const float wy[2] = {1.f - ly, ly}, wx[2] = {1.f - lx, lx};
-  float s[E], t[E], acc[E];
+  float s[E], t[E];
 #pragma unroll
-  for (int j = 0; j < E; ++j) { s[j] = sc[c + j]; t[j] = sh[c + j]; acc[j] = 0.f; }
+  for (int e = 0; e < E; ++e) { s[e] = sc[c + e]; t[e] = sh[c + e]; }
+  const int rs[3] = {max(i - 1, 0), i, min(i + 1, h - 1)}, cs[3] = {max(j - 1, 0), j, min(j + 1, w - 1)};
+  float v[3][3][E];
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    float row[E];
+  for (int a = 0; a < 3; ++a)
 #pragma unroll
-    for (int j = 0; j < E; ++j) row[j] = 0.f;
+    for (int b = 0; b < 3; ++b) {
+      const long long pix = (long long)(n * h + rs[a]) * w + cs[b];
+      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), v[a][b]);
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      float f[E];
-      const long long pix = (long long)(n * h + ys[a]) * w + xs[b];
-      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), f);
-#pragma unroll
-      for (int j = 0; j < E; ++j) row[j] = fmaf(wx[b], fmaxf(fmaf(f[j], s[j], t[j]), 0.f), row[j]);
+      for (int e = 0; e < E; ++e) v[a][b][e] = fmaxf(fmaf(v[a][b][e], s[e], t[e]), 0.f);
     }
+  // output 2i: rows (i-1, i) weights (0.25, 0.75), or row i with weights (1, 0) at i = 0;
+  // output 2i+1: rows (i, i+1) weights (0.75, 0.25) (i+1 clamped).  Same along x; x first.
+  const float wya = i > 0 ? 0.25f : 1.f, wyb = i > 0 ? 0.75f : 0.f;
+  const float wxa = j > 0 ? 0.25f : 1.f, wxb = j > 0 ? 0.75f : 0.f;
 #pragma unroll
-    for (int j = 0; j < E; ++j) acc[j] = fmaf(wy[a], row[j], acc[j]);
+  for (int b = 0; b < 2; ++b) {
+    float o0[E], o1[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float x[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        x[r] = b == 0 ? fmaf(wxb, v[r][1][e], wxa * (j > 0 ? v[r][0][e] : v[r][1][e]))
+                      : fmaf(0.25f, v[r][2][e], 0.75f * v[r][1][e]);
+      o0[e] = fmaf(wyb, x[1], wya * (i > 0 ? x[0] : x[1]));
+      o1[e] = fmaf(0.25f, x[2], 0.75f * x[1]);
+    }
+    const long long po = (long long)(n * H2 + 2 * i) * W2 + 2 * j + b;
+    *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(o0);
+    *(uint4*)(out + (po + W2) * oct + oco + c) = Vec16<T>::pack(o1);
   }
-  const long long po = (long long)(n * H2 + oy) * W2 + ox;
-  *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(acc);
 }
 
 // BN+ReLU -> 1x1 conv (C -> K <= 3), fp32 NHWC output
+// 8 lanes per pixel: lane g reads the 16-byte channel groups 8g (+64) of its pixel, so a
+// wave reads 8 whole pixel rows (coalesced); BN scale/shift and W live in registers.
+// C <= 128, C % 8 == 0 (host-checked).
 template <typename T>
-__global__ void bnrelu_conv1x1_kernel(const T* y, long long P, int C, int yct, int yco, const float* sc,
-                                      const float* sh, const float* w, const float* b, int K, float* z) {
+__global__ __launch_bounds__(256) void bnrelu_conv1x1_kernel(const T* y, long long P, int C, int yct, int yco,
+                                                             const float* sc, const float* sh, const float* w,
+                                                             const float* b, int K, float* z) {
   constexpr int E = Vec16<T>::N;
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float acc[3] = {0.f, 0.f, 0.f};
-  for (int c = 0; c < C; c += E) {
-    float f[E];
-    Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+  const int g = threadIdx.x & 7;
+  float s8[2][8], t8[2][8], w8[2][3][8];
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      const float a = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
-        if (k < K) acc[k] = fmaf(w[k * C + c + j], a, acc[k]);
+    for (int e = 0; e < 8; ++e) {
+      const int c = 64 * j + 8 * g + e;
+      const bool ok = c < C;
+      s8[j][e] = ok ? sc[c] : 0.f;
+      t8[j][e] = ok ? sh[c] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w8[j][k][e] = (ok && k < K) ? w[k * C + c] : 0.f;
     }
+  const long long step = (long long)gridDim.x * 32;
+  for (long long p = (long long)blockIdx.x * 32 + (threadIdx.x >> 3); p < P; p += step) {
+    float acc[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = 64 * j + 8 * g;
+      if (c >= C) continue;
+      float f[8];
+      Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+      if constexpr (E == 4) Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c + 4), f + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = fmaxf(fmaf(f[e], s8[j][e], t8[j][e]), 0.f);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc[k] = fmaf(w8[j][k][e], a, acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      acc[k] += __shfl_xor(acc[k], 1, 64);
+      acc[k] += __shfl_xor(acc[k], 2, 64);
+      acc[k] += __shfl_xor(acc[k], 4, 64);
+    }
+    if (g == 0)
+      for (int k = 0; k < K; ++k) z[p * K + k] = acc[k] + b[k];
   }
-  for (int k = 0; k < K; ++k) z[p * K + k] = acc[k] + b[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -657,6 +696,18 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
     for (int k = 0; k < 3; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) aw[j][k][e] = 0.f;
+  float s8[2][8], t8[2][8], w8[2][3][8];  // this lane's channels 64j + 8g + e
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = 64 * j + 8 * g + e;
+      const bool ok = c < C;
+      s8[j][e] = ok ? sc[c] : 0.f;
+      t8[j][e] = ok ? sh[c] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w8[j][k][e] = (ok && k < K) ? w[k * C + c] : 0.f;
+    }
   const long long p0 = (long long)blockIdx.x * C1X_PIX;
   const long long p1 = min(P, p0 + C1X_PIX);
   for (long long p = p0 + ps; p < p1; p += 32) {
@@ -674,14 +725,13 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
       if constexpr (E == 4) Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c + 4), f + 4);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float act = fmaxf(fmaf(f[e], sc[c + e], sh[c + e]), 0.f);
+        const float act = fmaxf(fmaf(f[e], s8[j][e], t8[j][e]), 0.f);
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-          if (k < K) {
-            s = fmaf(w[k * C + c + e], gk[k], s);
-            aw[j][k][e] = fmaf(gk[k], act, aw[j][k][e]);
-          }
+        for (int k = 0; k < 3; ++k) {
+          s = fmaf(w8[j][k][e], gk[k], s);
+          aw[j][k][e] = fmaf(gk[k], act, aw[j][k][e]);
+        }
         go[e] = s;
       }
       *(uint4*)(ga + p * gct + gco + c) = Vec16<T>::pack(go);
@@ -852,7 +902,7 @@ int eunet_bnrelu_upsample(const eunet_act* y, const float* scale, const float* s
                     out->dtype == y->dtype,
                 "bnrelu_upsample: shape");
   const int E = e16(y->dtype);
-  const long long total = (long long)out->n * out->h * out->w * (y->c / E);
+  const long long total = (long long)y->n * y->h * y->w * (y->c / E);
   const unsigned g = (unsigned)((total + 255) / 256);
   if (y->dtype == EUNET_BF16)
     bnrelu_up_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, y->n, y->h, y->w, y->c,
@@ -870,8 +920,10 @@ int eunet_bnrelu_conv1x1(const eunet_act* y, const float* scale, const float* sh
                          int k, float* z, void* stream) {
   EUNET_REQUIRE(act_ok(y) && vec_ok(y) && scale && shift && w && b && z && k >= 1 && k <= 3,
                 "bnrelu_conv1x1: bad args");
+  EUNET_REQUIRE(y->c <= 128 && y->c % 8 == 0, "bnrelu_conv1x1: needs C <= 128, C %% 8 == 0");
   const long long P = (long long)y->n * y->h * y->w;
-  const unsigned g = (unsigned)((P + 255) / 256);
+  const long long nb = (P + 31) / 32;
+  const unsigned g = (unsigned)(nb < 8192 ? nb : 8192);
   if (y->dtype == EUNET_BF16)
     bnrelu_conv1x1_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
                                                                         y->coff, scale, shift, w, b, k, z);

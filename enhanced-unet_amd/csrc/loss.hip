@@ -86,40 +86,58 @@ __global__ __launch_bounds__(NT) void loss_fwd_kernel(const float* logits, const
     part[((long long)n * gridDim.x + blockIdx.x) * NV + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
 
+// One 256-thread block: per sample, the threads stride over the tile partials (fp64),
+// a fixed-order LDS tree combines them (deterministic), thread 0 forms the sample's
+// loss; the batch mean is summed in sample order.
 template <int K>
-__global__ void loss_finalize_kernel(const float* part, int tiles, int N, int HW, float* sums, float* loss,
-                                     float* parts) {
+__global__ __launch_bounds__(256) void loss_finalize_kernel(const float* part, int tiles, int N, int HW, float* sums,
+                                                            float* loss, float* parts) {
   constexpr int NV = 1 + 3 * K;
-  // one thread per sample, fp64 combine; thread 0 reduces the batch
+  __shared__ double red[256][NV];
   __shared__ double per[64];
-  const int n = threadIdx.x;
-  double tot = 0.0;
-  if (n < N) {
+  const int tid = threadIdx.x;
+  for (int n = 0; n < N; ++n) {
     double v[NV];
+#pragma unroll
     for (int i = 0; i < NV; ++i) v[i] = 0.0;
-    for (int t = 0; t < tiles; ++t)
+    for (int t = tid; t < tiles; t += 256)
+#pragma unroll
       for (int i = 0; i < NV; ++i) v[i] += (double)part[((long long)n * tiles + t) * NV + i];
-    for (int i = 0; i < NV; ++i) sums[n * NV + i] = (float)v[i];
-    const double focal = v[0] / (double)HW;
-    double dice = 0.0, tv = 0.0;
-    for (int k = 0; k < K; ++k) {
-      const double I = v[1 + k], S = v[1 + K + k], T = v[1 + 2 * K + k];
-      dice += kDW[k] * (1.0 - (2.0 * I + EPS) / (S + T + EPS));
-      const double fp = S - I, fn = T - I;
-      tv += kTW[k] * (1.0 - (I + EPS) / (I + TVA * fp + (1.0 - TVA) * fn + EPS));
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[tid][i] = v[i];
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (tid < off)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[tid][i] += red[tid + off][i];
+      __syncthreads();
     }
-    dice /= 3.0;
-    tv /= 3.0;
-    if (parts) {
-      parts[n * 3 + 0] = (float)focal;
-      parts[n * 3 + 1] = (float)dice;
-      parts[n * 3 + 2] = (float)tv;
+    if (tid == 0) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        v[i] = red[0][i];
+        sums[n * NV + i] = (float)v[i];
+      }
+      const double focal = v[0] / (double)HW;
+      double dice = 0.0, tv = 0.0;
+      for (int k = 0; k < K; ++k) {
+        const double I = v[1 + k], S = v[1 + K + k], T = v[1 + 2 * K + k];
+        dice += kDW[k] * (1.0 - (2.0 * I + EPS) / (S + T + EPS));
+        const double fp = S - I, fn = T - I;
+        tv += kTW[k] * (1.0 - (I + EPS) / (I + TVA * fp + (1.0 - TVA) * fn + EPS));
+      }
+      dice /= 3.0;
+      tv /= 3.0;
+      if (parts) {
+        parts[n * 3 + 0] = (float)focal;
+        parts[n * 3 + 1] = (float)dice;
+        parts[n * 3 + 2] = (float)tv;
+      }
+      per[n] = W_FOCAL * focal + W_DICE * dice + W_TV * tv;
     }
-    tot = W_FOCAL * focal + W_DICE * dice + W_TV * tv;
+    __syncthreads();
   }
-  if (n < 64) per[n] = tot;
-  __syncthreads();
-  if (n == 0) {
+  if (tid == 0) {
     double s = 0.0;
     for (int i = 0; i < N; ++i) s += per[i];
     loss[0] = (float)(s / (double)N);
@@ -190,7 +208,7 @@ int eunet_loss_fwd(const float* logits, const int64_t* target, int n, int k, int
   dim3 grid(tiles, n);
 #define LF(KK)                                                                                        \
   loss_fwd_kernel<KK><<<grid, NT, 0, s>>>(logits, target, HW, (float*)ws);                            \
-  loss_finalize_kernel<KK><<<1, 64, 0, s>>>((const float*)ws, tiles, n, HW, sums, loss, parts);
+  loss_finalize_kernel<KK><<<1, 256, 0, s>>>((const float*)ws, tiles, n, HW, sums, loss, parts);
   if (k == 1) { LF(1) } else if (k == 2) { LF(2) } else { LF(3) }
 #undef LF
   EUNET_LAUNCH_CHECK("loss_fwd");
