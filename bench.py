@@ -100,7 +100,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        # nccl == RCCL over xGMI; EUNET_DIST_BACKEND=gloo only to rehearse N ranks on one GPU
+        dist.init_process_group(os.environ.get("EUNET_DIST_BACKEND", "nccl"), init_method="env://")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

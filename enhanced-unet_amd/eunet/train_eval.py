@@ -18,6 +18,7 @@ Differences that are implementation, not semantics:
 from __future__ import annotations
 
 import math
+import warnings
 from typing import Dict
 
 import torch
@@ -130,9 +131,13 @@ class Trainer:
         return total / max(1, n)
 
     def epoch_lr_step(self, epoch: int) -> float:
-        """train_model's per-epoch stepping (train_eval.py:1104-1111)."""
-        if epoch < self.warmup_epochs:
-            self.warmup_scheduler.step()
-        else:
-            self.scheduler.step()
+        """train_model's per-epoch stepping (train_eval.py:1104-1111).  The reference steps the
+        scheduler at the start of the epoch, before any optimizer.step(); torch warns about
+        that order, the LR trajectory is the reference's (pinned by lr_traj.npz)."""
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message="Detected call of `lr_scheduler.step\\(\\)` before")
+            if epoch < self.warmup_epochs:
+                self.warmup_scheduler.step()
+            else:
+                self.scheduler.step()
         return self.optimizer.param_groups[0]["lr"]
