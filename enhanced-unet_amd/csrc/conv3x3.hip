@@ -47,6 +47,12 @@ struct FwdArgs {
   const float* bias;
   void* y; int yct, yco, cout;
   float* stats; int tx, ty, ntiles;
+  // optional fused BN-backward reduction over the produced gradient (dgrad only):
+  // part[tile][2][cout] = (sum g', sum g' xhat), g' = g [gamma xhat + beta > 0],
+  // xhat = (by - mean) istd, g = the stored (rounded) output
+  const void* by; int byct, byco;
+  const float* bmean; const float* bistd; const float* bgam; const float* bbet;
+  float* bpart;
 };
 
 // stage one halo unit (pixel hp, quarter q) of chunk kc into registers
@@ -102,7 +108,7 @@ constexpr int STAGE_BYTES = FA_BYTES + B_LDS_BYTES;  // 76800
 constexpr int OUT_LD = 68;                   // fp32 row stride of the output staging tile
 constexpr int FWD_LDS_DB = 2 * STAGE_BYTES;  // 153600: one block / CU, double-buffered
 constexpr int FWD_LDS = STAGE_BYTES;         // 76800: two blocks / CU
-static_assert(FTH * FTW / 2 * OUT_LD * 4 + 2 * 4 * 64 * 4 <= FWD_LDS, "epilogue staging must fit");
+static_assert(FTH * FTW / 2 * OUT_LD * 4 + 2 * 4 * 64 * 4 + 4 * 64 * 4 <= FWD_LDS, "epilogue staging must fit");
 
 // XCD-aware block order: hardware block b runs on XCD b % 8.  Logical block L =
 // (tile, co-block) with the co-block fastest; each XCD gets a contiguous range of L,
@@ -378,7 +384,22 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
   }
   constexpr int E = Vec16<T>::N;
   constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
+  static_assert(FT % UPX == 0, "a thread's channel unit must be fixed across store iterations");
   T* yp = (T*)a.y;
+  const bool bnb = a.bpart != nullptr;
+  const int ucol = tid % UPX;
+  // BN-backward constants of the block's 64 channels live in LDS (registers are full of acc)
+  float* bprm = (float*)(smem + HALF_PX * OUT_LD * 4 + 2 * 4 * 64 * 4);  // [4][64]: mean, istd, gamma, beta
+  float bs1[E], bs2[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { bs1[e] = 0.f; bs2[e] = 0.f; }
+  if (bnb && tid < BN) {
+    const bool ok = co0 + tid < a.cout;
+    bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
+    bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
+    bprm[2 * BN + tid] = ok ? a.bgam[co0 + tid] : 0.f;
+    bprm[3 * BN + tid] = ok ? a.bbet[co0 + tid] : 0.f;
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if ((wv >> 1) == half) {
@@ -404,10 +425,40 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
 #pragma unroll
         for (int e = 0; e < E; ++e) f[e] = sp[e];
         const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
-        *(uint4*)(yp + pix * a.yct + a.yco + co) = Vec16<T>::pack(f);
+        const uint4 packed = Vec16<T>::pack(f);
+        *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
+        if (bnb) {
+          float gr[E], yv[E];
+          Vec16<T>::unpack(packed, gr);
+          Vec16<T>::unpack(*(const uint4*)((const T*)a.by + pix * a.byct + a.byco + co), yv);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int cc = ucol * E + e;
+            const float xh = (yv[e] - bprm[cc]) * bprm[BN + cc];
+            const float gp = fmaf(bprm[2 * BN + cc], xh, bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
+            bs1[e] += gp;
+            bs2[e] = fmaf(gp, xh, bs2[e]);
+          }
+        }
       }
     }
     if (half == 0) __syncthreads();
+  }
+  if (bnb) {  // fixed-order block reduction of the per-thread channel sums
+    __syncthreads();
+    float* r2 = (float*)smem;  // [FT][2E]
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      r2[tid * 2 * E + e] = bs1[e];
+      r2[tid * 2 * E + E + e] = bs2[e];
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int which = tid / BN, cc = tid % BN, u = cc / E, e = cc % E;
+      float t = 0.f;
+      for (int k = u; k < FT; k += UPX) t += r2[k * 2 * E + which * E + e];
+      if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
+    }
   }
 }
 
@@ -783,6 +834,19 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
+int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
+  dim3 grid(a.ntiles * (a.cout_pad / BN));
+  if (dtype == EUNET_BF16) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else {
+    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
+    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  }
+  EUNET_LAUNCH_CHECK("conv3x3_fwd");
+  return EUNET_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -830,19 +894,38 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.bias = bias;
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
+  a.by = nullptr; a.byct = 0; a.byco = 0;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
-  dim3 grid(a.ntiles * (a.cout_pad / BN));
-  if (x->dtype == EUNET_BF16) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
-  } else {
-    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
-    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
-  }
-  EUNET_LAUNCH_CHECK("conv3x3_fwd");
-  return EUNET_OK;
+  return launch_fwd(a, x->dtype, stream);
 }
+
+int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const eunet_act* y,
+                              const float* mean, const float* invstd, const float* gamma, const float* beta,
+                              float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && act_ok(y) && wp_t && mean && invstd && gamma && beta && part,
+                "conv3x3_dgrad_bnbwd: bad args");
+  EUNET_REQUIRE(dy->dtype == gx->dtype && y->dtype == gx->dtype, "conv3x3_dgrad_bnbwd: dtype mismatch");
+  EUNET_REQUIRE(dy->n == gx->n && dy->h == gx->h && dy->w == gx->w && y->n == gx->n && y->h == gx->h &&
+                    y->w == gx->w && y->c == gx->c,
+                "conv3x3_dgrad_bnbwd: shape mismatch");
+  const int E = elems16(dy->dtype);
+  EUNET_REQUIRE(dy->c % E == 0 && dy->ctot % E == 0 && dy->coff % E == 0 && gx->c % E == 0 && gx->ctot % E == 0 &&
+                    gx->coff % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
+                "conv3x3_dgrad_bnbwd: channels/strides must be multiples of %d", E);
+  FwdArgs a;
+  a.x = dy->ptr; a.N = dy->n; a.H = dy->h; a.W = dy->w; a.xct = dy->ctot; a.xco = dy->coff; a.cin = dy->c;
+  a.isc = nullptr; a.ish = nullptr;
+  a.wp = wp_t; a.cout_pad = cdiv(gx->c, BN) * BN; a.nkc = cdiv(dy->c, kchunk(dy->dtype));
+  a.bias = nullptr;
+  a.y = gx->ptr; a.yct = gx->ctot; a.yco = gx->coff; a.cout = gx->c;
+  a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
+  a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
+  a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part;
+  return launch_fwd(a, dy->dtype, stream);
+}
+
 
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");

@@ -22,7 +22,7 @@ namespace {
 constexpr int NT = 256;
 constexpr int T2 = 16;  // tile side at 2H
 constexpr int MID = 64;
-constexpr int HEAD_BLOCKS = 1024;
+constexpr int HEAD_BLOCKS = 768;  // persistent grid: 3 resident blocks x 256 CUs (no second round)
 
 struct HeadArgs {
   const float* z; int N, h, w, K;
@@ -831,7 +831,7 @@ __device__ __forceinline__ void bwd_params(const HeadArgs& a, int c, float& is, 
 }
 
 template <int K>
-__global__ __launch_bounds__(NT) void head_bwd1_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = (K + 2) * MID + K;
   __shared__ float su[18 * 18 * 3];
   __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID];
@@ -839,9 +839,16 @@ __global__ __launch_bounds__(NT) void head_bwd1_mfma_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   if (tid < MID) bwd_params(a, tid, pis[tid], poff[tid], pP[tid], pQ[tid]);
   for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
-  bf16x8 Ah[4], As[4];
-  load_a_w1<K>(a.w1, lane, Ah);
-  load_a_w2t<K>(a.w2, lane, As);
+  __shared__ __attribute__((aligned(16))) bf16x8 fr[8][64];  // Ah[4], As[4] per lane
+  if (wv == 0) {
+    bf16x8 A4[4];
+    load_a_w1<K>(a.w1, lane, A4);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fr[f][lane] = A4[f];
+    load_a_w2t<K>(a.w2, lane, A4);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
+  }
   int off[8];
   im2col_offsets<K>(q, off);
   float agb[16], agx[16], aw2[K][16], ab2[K];
@@ -866,14 +873,20 @@ __global__ __launch_bounds__(NT) void head_bwd1_mfma_kernel(HeadArgs a) {
     for (int rr = 0; rr < 4; ++rr) {
       const int r = 4 * wv + rr, oy = oy0 + r, ox = ox0 + x;
       const bool pv = oy < H2 && ox < W2;
+      int fl = lane;
+      asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
       f32x4 acc[4], sv[4];
-      conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+      {
+        const bf16x8 b = im2col_frag(su, (r * 18 + x) * 3, off);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[cb][fl], b, z4, 0, 0, 0);
+      }
       float go[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
       const bf16x8 gb = go_frag<K>(q, go);
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(As[cb], gb, z4, 0, 0, 0);
+      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int c0 = 16 * cb + 4 * q;
@@ -928,12 +941,17 @@ __global__ __launch_bounds__(NT) void head_bwd1_mfma_kernel(HeadArgs a) {
 
 // g_h (never stored), the per-tap products v = g_h * W1 (stored, fp32) and the
 // W1/b1 gradients (MFMA over pixels from a wave-private bf16 g_h tile in LDS).
+// Register budget (<= 128 VGPRs -> 4 waves/SIMD to overlap the dependent MFMA -> VALU
+// chains): the BN-backward algebra is folded into 4 per-channel constants,
+//   pre = h P + Q,   g_h = P gbn + h D + E   (D = -P c2 is, E = -P (c2 off + c1)),
+// and the constant A fragments (W1 for h, W2^T for s, W1^T for v) are read from LDS.
 template <int K>
-__global__ __launch_bounds__(NT) void head_gh_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = MID * K * 9 + MID;
   constexpr int KJ = K * 9;
   __shared__ float su[18 * 18 * 3];
-  __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID], pB[MID], pC[MID];
+  __shared__ __attribute__((aligned(16))) float pP[MID], pQ[MID], pD[MID], pE[MID];
+  __shared__ __attribute__((aligned(16))) bf16x8 fr[12][64];  // Ah[4], As[4], Av[jb][ch] per lane
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
   __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
   __shared__ float red[STRIDE];
@@ -943,23 +961,33 @@ __global__ __launch_bounds__(NT) void head_gh_mfma_kernel(HeadArgs a) {
     float is, of, P, Q;
     bwd_params(a, tid, is, of, P, Q);
     const float inv_cnt = 1.f / ((float)a.N * (float)H2 * (float)W2);
-    pis[tid] = is; poff[tid] = of; pP[tid] = P; pQ[tid] = Q;
-    pB[tid] = -P * a.dgamma[tid] * inv_cnt;  // g_h = P*gbn + B*xhat + C
-    pC[tid] = -P * a.dbeta[tid] * inv_cnt;
+    const float c1 = a.dbeta[tid] * inv_cnt, c2 = a.dgamma[tid] * inv_cnt;
+    pP[tid] = P; pQ[tid] = Q;
+    pD[tid] = -P * c2 * is;
+    pE[tid] = -P * fmaf(c2, of, c1);
   }
   for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
-  bf16x8 Ah[4], As[4], Av[2][2];
-  load_a_w1<K>(a.w1, lane, Ah);
-  load_a_w2t<K>(a.w2, lane, As);
+  if (wv == 0) {
+    bf16x8 A4[4];
+    load_a_w1<K>(a.w1, lane, A4);
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb)
+    for (int f = 0; f < 4; ++f) fr[f][lane] = A4[f];
+    load_a_w2t<K>(a.w2, lane, A4);
 #pragma unroll
-    for (int ch = 0; ch < 2; ++ch)
+    for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int j = 16 * jb + x;
-        Av[jb][ch][jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch) {
+        bf16x8 v;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int j = 16 * jb + x;
+          v[jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
+        }
+        fr[8 + 2 * jb + ch][lane] = v;
       }
+  }
   int off[8];
   im2col_offsets<K>(q, off);
   // wgrad B operand: im2col[px slot 8q + jj][j = 16jb + x]; slot -> (row q>>1, col 8(q&1) + jj)
@@ -990,39 +1018,44 @@ __global__ __launch_bounds__(NT) void head_gh_mfma_kernel(HeadArgs a) {
     __syncthreads();
     fill_u(a, su, n, oy0, ox0);
     __syncthreads();
+#pragma unroll 1
     for (int rp = 0; rp < 2; ++rp) {
 #pragma unroll 1
       for (int rr = 0; rr < 2; ++rr) {
         const int r = 4 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + x;
         const bool pv = oy < H2 && ox < W2;
-        f32x4 acc[4], sv[4];
-        conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+        int fl = lane;
+        asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
+        f32x4 acc[4];
+        {
+          const bf16x8 b = im2col_frag(su, (r * 18 + x) * 3, off);
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[cb][fl], b, z4, 0, 0, 0);
+        }
         float go[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
         const bf16x8 gb = go_frag<K>(q, go);
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(As[cb], gb, z4, 0, 0, 0);
-#pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
           const int c0 = 16 * cb + 4 * q;
-          const float4 i4 = ld4(pis + c0), o4 = ld4(poff + c0), p4v = ld4(pP + c0), q4v = ld4(pQ + c0);
-          const float4 b4 = ld4(pB + c0), cc4 = ld4(pC + c0);
+          const float4 P4 = ld4(pP + c0), Q4 = ld4(pQ + c0), D4 = ld4(pD + c0), E4 = ld4(pE + c0);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float xh = fmaf(acc[cb][i], f4(i4, i), f4(o4, i));
-            const float pre = fmaf(acc[cb][i], f4(p4v, i), f4(q4v, i));
-            const float gbn = pre > 0.f ? sv[cb][i] : 0.f;
-            const float g = pv ? fmaf(f4(p4v, i), gbn, fmaf(f4(b4, i), xh, f4(cc4, i))) : 0.f;
+            const float h = acc[cb][i];
+            const float pre = fmaf(h, f4(P4, i), f4(Q4, i));
+            const float gbn = pre > 0.f ? sv[i] : 0.f;
+            const float g = pv ? fmaf(f4(P4, i), gbn, fmaf(h, f4(D4, i), f4(E4, i))) : 0.f;
             acc[cb][i] = g;
             agb1[4 * cb + i] += g;
           }
         }
         const bf16x8 g0 = cfrag(acc, 0), g1 = cfrag(acc, 1);
-        f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[0][0], g0, z4, 0, 0, 0);
-        v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[0][1], g1, v0, 0, 0, 0);
-        f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[1][0], g0, z4, 0, 0, 0);
-        v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Av[1][1], g1, v1, 0, 0, 0);
+        f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8][fl], g0, z4, 0, 0, 0);
+        v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
+        f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
+        v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
         if (pv) {
           float* vp = a.v + (((long long)n * H2 + oy) * W2 + ox) * VLD;
           if (4 * q < KJ) *(f32x4*)(vp + 4 * q) = v0;

@@ -185,11 +185,12 @@ class UNetEngine:
         dev, dt = yb.device, self.dtype
         red = _e(2 * C, torch.float32, dev)
 
-        def bn_back(prefix, g, y, bn):
-            tiles = ops.bn_bwd_tiles(ops.act(y))
-            part = _e(tiles * 2 * C, torch.float32, dev)
-            ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                              P[prefix + ".bias"], part)
+        def bn_back(prefix, g, y, bn, part=None, tiles=0):
+            if part is None:  # reduction not fused into the producer of g
+                tiles = ops.bn_bwd_tiles(ops.act(y))
+                part = _e(tiles * 2 * C, torch.float32, dev)
+                ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
+                                  P[prefix + ".bias"], part)
             ops.colsum(part, tiles, 2 * C, red)
             sink.slot(prefix + ".bias", (C,)).copy_(red[:C])
             sink.slot(prefix + ".weight", (C,)).copy_(red[C:])
@@ -219,9 +220,12 @@ class UNetEngine:
         wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
         wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
         gaa = torch.empty_like(ya)
-        ops.conv3x3_fwd(ops.act(gyb), wpt, ops.act(gaa))
+        ctiles = ops.conv3x3_tiles(ops.act(gaa))
+        cpart = _e(ctiles * 2 * C, torch.float32, dev)
+        ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
+                                P[p + ".1.weight"], P[p + ".1.bias"], cpart)
         del gyb
-        gya = bn_back(p + ".1", gaa, ya, bna)
+        gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
         del gaa
         wgrad(p + ".0", X, gya, small_conv=small)
         sink.ready([f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")])

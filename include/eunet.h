@@ -66,6 +66,15 @@ int eunet_conv3x3_tiles(const eunet_act* y, int* tiles);
 int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in_shift,
                       const void* wp, const float* bias, const eunet_act* y, float* stats,
                       void* stream);
+/* dgrad (wp_t packed with transpose_flip) fused with the reduction half of the
+ * BatchNorm backward of the layer whose output gradient it produces (autograd of
+ * models.py:220-221, BN+ReLU after the conv): y = that layer's pre-BN output,
+ * part [tiles][2][gx.c] = per-tile (sum g', sum g' xhat), g' = gx [gamma xhat +
+ * beta > 0], xhat = (y - mean) invstd, gx as stored (rounded).  Replaces
+ * conv3x3_fwd(dgrad) + bn_bwd_reduce; colsum(part, tiles, 2C) -> (dbeta, dgamma). */
+int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx,
+                              const eunet_act* y, const float* mean, const float* invstd,
+                              const float* gamma, const float* beta, float* part, void* stream);
 /* wgrad (split over pixel tiles): dw_part [nsplit][cout][9][cin] and
  * db_part [nsplit][cout] (db only when db_part != NULL) */
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit);

@@ -356,3 +356,37 @@ def test_loss_fwd_bwd(K):
     assert rel(ld.grad, lt.grad) < 1e-4
     p0 = R.combined_loss(logits[0], target[0], parts=True)[1]
     assert abs(parts[0, 0].item() - p0["focal"].item()) < 1e-5 * abs(p0["focal"].item()) + 1e-7
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_dgrad_bnbwd_fused(dt):
+    """dgrad with the BN-backward reduction fused into its epilogue: gx identical to the
+    plain dgrad, partial sums equal to (sum g', sum g' xhat) of the stored gx."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(11)
+    N, H, W, Cin, Cout, YT, YO = 2, 20, 44, 64, 128, 144, 16  # gx has Cout channels, y a channel slice
+    gy = torch.randn(N, H, W, Cin, generator=g).to(DEV, dt)
+    w = (torch.randn(Cin, Cout, 3, 3, generator=g) / 20).to(DEV)  # conv weight [Cin_out][Cout_in]
+    ybuf = torch.randn(N, H, W, YT, generator=g).to(DEV, dt)
+    mean = torch.randn(Cout, generator=g).to(DEV) * 0.1
+    istd = (torch.rand(Cout, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(Cout, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(Cout, generator=g) * 0.2).to(DEV)
+    wpt = ops.conv3x3_pack(w, dt, flip=True)
+    gx_ref = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    ops.conv3x3_fwd(ops.act(gy), wpt, ops.act(gx_ref))
+    gx = torch.empty_like(gx_ref)
+    tiles = ops.conv3x3_tiles(ops.act(gx))
+    part = torch.empty(tiles * 2 * Cout, device=DEV)
+    ops.conv3x3_dgrad_bnbwd(ops.act(gy), wpt, ops.act(gx), ops.act(ybuf, YO, Cout), mean, istd, gamma, beta, part)
+    red = torch.empty(2 * Cout, device=DEV)
+    ops.colsum(part, tiles, 2 * Cout, red)
+    torch.cuda.synchronize()
+    assert torch.equal(gx, gx_ref)
+    y = ybuf[..., YO:YO + Cout].double()
+    xh = (y - mean.double()) * istd.double()
+    gp = torch.where(gamma.double() * xh + beta.double() > 0, gx.double(), torch.zeros_like(xh))
+    s1 = gp.sum(dim=(0, 1, 2))
+    s2 = (gp * xh).sum(dim=(0, 1, 2))
+    assert rel(red[:Cout], s1) < 1e-5
+    assert rel(red[Cout:], s2) < 1e-5
