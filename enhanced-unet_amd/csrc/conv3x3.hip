@@ -99,16 +99,13 @@ constexpr int FTH = 16, FTW = 32;            // output tile
 constexpr int FHW = FTW + 2;                 // 34
 constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
 constexpr int FHPXP = 624;                   // plane stride (multiple of 16 units)
-constexpr int FT = 256;
+constexpr int FT = 256;                      // threads of the production (NW = 4) forward block
 constexpr int FA_UNITS = 4 * FHPX;           // 2448
-constexpr int FA_ITERS = (FA_UNITS + FT - 1) / FT;  // 10
-constexpr int FB_ITERS = B_UNITS / FT;       // 9
 constexpr int FA_BYTES = 4 * FHPXP * 16;     // 39936
 constexpr int STAGE_BYTES = FA_BYTES + B_LDS_BYTES;  // 76800
 constexpr int OUT_LD = 68;                   // fp32 row stride of the output staging tile
 constexpr int FWD_LDS_DB = 2 * STAGE_BYTES;  // 153600: one block / CU, double-buffered
 constexpr int FWD_LDS = STAGE_BYTES;         // 76800: two blocks / CU
-static_assert(FTH * FTW / 2 * OUT_LD * 4 + 2 * 4 * 64 * 4 + 4 * 64 * 4 <= FWD_LDS, "epilogue staging must fit");
 
 // XCD-aware block order: hardware block b runs on XCD b % 8.  Logical block L =
 // (tile, co-block) with the co-block fastest; each XCD gets a contiguous range of L,
@@ -162,11 +159,20 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 //   1 = no global loads / LDS writes inside the K loop, 2 = no MFMAs (VALU keeps the
 //   LDS reads alive), 4 = LDS fragments read once before the loop (MFMA-only loop),
 //   8 = plain tile-fastest block order instead of xcd_map.
+// NW = waves per block (4: 128 px x 64 co per wave; 8: 64 px x 64 co per wave).
 // DB: true = one block per CU, double-buffered LDS (next chunk prefetched into
-//   registers during the MFMAs); false = two blocks per CU, one LDS stage each
-//   (a block's staging overlaps the other block's MFMAs).
-template <typename T, int MODE = 0, bool DB = false>
-__global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
+//   registers during the MFMAs, one barrier per chunk); false = two blocks per CU,
+//   one LDS stage each (a block's staging overlaps the other block's MFMAs).
+template <typename T, int MODE = 0, bool DB = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
+  constexpr int NTH = 64 * NW;
+  constexpr int RPW = FTH / NW;               // output rows per wave
+  constexpr int MT = 2 * RPW;                 // 16-px m-tiles per wave
+  constexpr int A_IT = (FA_UNITS + NTH - 1) / NTH;
+  constexpr int B_IT = (B_UNITS + NTH - 1) / NTH;
+  constexpr bool B_TAIL = B_UNITS % NTH != 0;
+  constexpr int NPASS = DB ? 1 : 2;           // epilogue staging passes (LDS budget)
+  constexpr int PROWS = FTH / NPASS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int tile, cob;
@@ -182,15 +188,15 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
   const int co0 = cob * BN;
   const int q = lane >> 4, li = lane & 15;
 
-  f32x4 acc[8][4];
+  f32x4 acc[MT][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  u32x4 ra[FA_ITERS];
-  bool rok[FA_ITERS];
-  u32x4 rb[FB_ITERS];
+  u32x4 ra[A_IT];
+  bool rok[A_IT];
+  u32x4 rb[B_IT];
   const u32x4* wp = (const u32x4*)a.wp;
 
 #define CONV_BUNIT(ID_, KC_) \
@@ -198,36 +204,42 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
 #define CONV_GLOAD_A(KC_, I0_, I1_)                                                           \
   do {                                                                                        \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        ra[i] = fwd_load_unit<T>(a, n, y0, x0, tid + i * FT, (KC_), rok[i]);                  \
+        ra[i] = fwd_load_unit<T>(a, n, y0, x0, tid + i * NTH, (KC_), rok[i]);                 \
   } while (0)
 #define CONV_GLOAD_B(KC_, I0_, I1_)                                                           \
   do {                                                                                        \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) rb[i] = CONV_BUNIT(tid + i * FT, KC_); \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
+      const int id_ = tid + i * NTH;                                                          \
+      if (!B_TAIL || id_ < B_UNITS) rb[i] = CONV_BUNIT(id_, KC_);                             \
+    }                                                                                         \
   } while (0)
 #define CONV_LWRITE_A(KC_, BUF_, I0_, I1_)                                                    \
   do {                                                                                        \
     char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        fwd_store_unit<T>(a, As_, tid + i * FT, (KC_), ra[i], rok[i]);                        \
+        fwd_store_unit<T>(a, As_, tid + i * NTH, (KC_), ra[i], rok[i]);                       \
   } while (0)
 #define CONV_LWRITE_B(BUF_, I0_, I1_)                                                         \
   do {                                                                                        \
     char* Bs_ = smem + (BUF_) * STAGE_BYTES + FA_BYTES;                                       \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) *(u32x4*)(Bs_ + (tid + i * FT) * 16) = rb[i]; \
+    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
+      const int id_ = tid + i * NTH;                                                          \
+      if (!B_TAIL || id_ < B_UNITS) *(u32x4*)(Bs_ + id_ * 16) = rb[i];                        \
+    }                                                                                         \
   } while (0)
 
-  constexpr int AH = FA_ITERS / 2, BH = FB_ITERS / 2;
+  constexpr int AH = A_IT / 2, BH = B_IT / 2;
   auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
     CONV_GLOAD_A(kc, 0, AH);
     CONV_LWRITE_A(kc, buf, 0, AH);
-    CONV_GLOAD_A(kc, AH, FA_ITERS);
-    CONV_LWRITE_A(kc, buf, AH, FA_ITERS);
+    CONV_GLOAD_A(kc, AH, A_IT);
+    CONV_LWRITE_A(kc, buf, AH, A_IT);
     CONV_GLOAD_B(kc, 0, BH);
     CONV_LWRITE_B(buf, 0, BH);
-    CONV_GLOAD_B(kc, BH, FB_ITERS);
-    CONV_LWRITE_B(buf, BH, FB_ITERS);
+    CONV_GLOAD_B(kc, BH, B_IT);
+    CONV_LWRITE_B(buf, BH, B_IT);
   };
-  auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[8], const uint4 (&fb0)[4]) {
+  auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[MT], const uint4 (&fb0)[4]) {
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -238,8 +250,8 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
       for (int nt = 0; nt < 4; ++nt)
         fb[nt] = (MODE & 4) ? fb0[nt] : *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const int hp = (4 * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
+      for (int mt = 0; mt < MT; ++mt) {
+        const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
         const uint4 fa = (MODE & 4) ? fa0[mt] : *(const uint4*)(As + (q * FHPXP + hp) * 16);
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
@@ -260,12 +272,12 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     }
   };
 
-  uint4 fa0[8], fb0[4];
+  uint4 fa0[MT], fb0[4];
   if constexpr (DB) {
-    CONV_GLOAD_A(0, 0, FA_ITERS);
-    CONV_GLOAD_B(0, 0, FB_ITERS);
-    CONV_LWRITE_A(0, 0, 0, FA_ITERS);
-    CONV_LWRITE_B(0, 0, FB_ITERS);
+    CONV_GLOAD_A(0, 0, A_IT);
+    CONV_GLOAD_B(0, 0, B_IT);
+    CONV_LWRITE_A(0, 0, 0, A_IT);
+    CONV_LWRITE_B(0, 0, B_IT);
   } else {
     stage(0, 0);
   }
@@ -274,20 +286,20 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) fb0[nt] = *(const uint4*)(smem + FA_BYTES + (q * (BN * 9) + (nt * 16 + li) * 9) * 16);
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-      fa0[mt] = *(const uint4*)(smem + (q * FHPXP + (4 * wv + (mt >> 1)) * FHW + (mt & 1) * 16 + li) * 16);
+    for (int mt = 0; mt < MT; ++mt)
+      fa0[mt] = *(const uint4*)(smem + (q * FHPXP + (RPW * wv + (mt >> 1)) * FHW + (mt & 1) * 16 + li) * 16);
   }
   for (int kc = 0; kc < a.nkc; ++kc) {
     if constexpr (DB) {
       const int cur = kc & 1;
       if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
-        CONV_GLOAD_A(kc + 1, 0, FA_ITERS);
-        CONV_GLOAD_B(kc + 1, 0, FB_ITERS);
+        CONV_GLOAD_A(kc + 1, 0, A_IT);
+        CONV_GLOAD_B(kc + 1, 0, B_IT);
       }
       chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
       if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
-        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, FA_ITERS);
-        CONV_LWRITE_B(cur ^ 1, 0, FB_ITERS);
+        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, A_IT);
+        CONV_LWRITE_B(cur ^ 1, 0, B_IT);
       }
       __syncthreads();
     } else {
@@ -307,20 +319,22 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
 #undef CONV_LWRITE_B
 #undef CONV_BUNIT
 
-  // ---- epilogue: bias, BN partials, LDS-staged vector stores (two half tiles) ----
+  // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
   const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int co = co0 + nt * 16 + li;
     const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[mt][nt][i] += bv;
   }
-  constexpr int HALF_PX = FTH * FTW / 2;                        // 256 px per half tile
-  float* stg = (float*)smem;                                    // [256 px][OUT_LD]
-  float* red = (float*)(smem + HALF_PX * OUT_LD * 4);           // [4][64] x 2
+  constexpr int PASS_PX = PROWS * FTW;
+  float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
+  float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NW][64] x 2
+  float* bprm = red + 2 * NW * 64;                              // [4][64] BN-backward constants
+  static_assert(PASS_PX * OUT_LD * 4 + (2 * NW + 4) * 64 * 4 <= (DB ? FWD_LDS_DB : FWD_LDS), "epilogue LDS");
   __syncthreads();  // all waves are done with the K loop's LDS
   if (a.stats != nullptr) {
     float s[4];
@@ -328,10 +342,10 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     for (int nt = 0; nt < 4; ++nt) {
       float v = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool ok = 4 * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
+          const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
           v += ok ? acc[mt][nt][i] : 0.f;
         }
       v += __shfl_xor(v, 16, 64);
@@ -348,17 +362,17 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     for (int nt = 0; nt < 4; ++nt) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) t += red[w * 64 + nt * 16 + li];
+      for (int w = 0; w < NW; ++w) t += red[w * 64 + nt * 16 + li];
       mb[nt] = t / cnt;
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v = 0.f;
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool ok = 4 * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
+          const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
           const float d = acc[mt][nt][i] - mb[nt];
           v += ok ? d * d : 0.f;
         }
@@ -368,14 +382,14 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     }
     if (q == 0)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) red[256 + wv * 64 + nt * 16 + li] = s[nt];
+      for (int nt = 0; nt < 4; ++nt) red[NW * 64 + wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
     if (tid < 64 && co0 + tid < a.cout) {
       float sum = 0.f, m2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NW; ++w) {
         sum += red[w * 64 + tid];
-        m2 += red[256 + w * 64 + tid];
+        m2 += red[NW * 64 + w * 64 + tid];
       }
       a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
       a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
@@ -384,12 +398,10 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
   }
   constexpr int E = Vec16<T>::N;
   constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
-  static_assert(FT % UPX == 0, "a thread's channel unit must be fixed across store iterations");
+  static_assert(NTH % UPX == 0, "a thread's channel unit must be fixed across store iterations");
   T* yp = (T*)a.y;
   const bool bnb = a.bpart != nullptr;
   const int ucol = tid % UPX;
-  // BN-backward constants of the block's 64 channels live in LDS (registers are full of acc)
-  float* bprm = (float*)(smem + HALF_PX * OUT_LD * 4 + 2 * 4 * 64 * 4);  // [4][64]: mean, istd, gamma, beta
   float bs1[E], bs2[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) { bs1[e] = 0.f; bs2[e] = 0.f; }
@@ -401,23 +413,23 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     bprm[3 * BN + tid] = ok ? a.bbet[co0 + tid] : 0.f;
   }
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if ((wv >> 1) == half) {
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int px = ((wv & 1) * 4 + (mt >> 1)) * FTW + (mt & 1) * 16 + q * 4 + i;
+          const int px = (RPW * wv - pass * PROWS + (mt >> 1)) * FTW + (mt & 1) * 16 + q * 4 + i;
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) stg[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < HALF_PX * UPX / FT; ++j) {
-      const int id = tid + j * FT;
+    for (int j = 0; j < PASS_PX * UPX / NTH; ++j) {
+      const int id = tid + j * NTH;
       const int px = id / UPX, u = id - px * UPX;
-      const int r = half * (FTH / 2) + px / FTW, c = px % FTW;
+      const int r = pass * PROWS + px / FTW, c = px % FTW;
       const int co = co0 + u * E;
       if (r < vh && c < vw && co < a.cout) {
         const float* sp = stg + px * OUT_LD + u * E;
@@ -442,11 +454,11 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
         }
       }
     }
-    if (half == 0) __syncthreads();
+    if (pass + 1 < NPASS) __syncthreads();
   }
   if (bnb) {  // fixed-order block reduction of the per-thread channel sums
     __syncthreads();
-    float* r2 = (float*)smem;  // [FT][2E]
+    float* r2 = (float*)smem;  // [NTH][2E]
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       r2[tid * 2 * E + e] = bs1[e];
@@ -456,7 +468,7 @@ __global__ __launch_bounds__(FT, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) 
     if (tid < 2 * BN) {
       const int which = tid / BN, cc = tid % BN, u = cc / E, e = cc % E;
       float t = 0.f;
-      for (int k = u; k < FT; k += UPX) t += r2[k * 2 * E + which * E + e];
+      for (int k = u; k < NTH; k += UPX) t += r2[k * 2 * E + which * E + e];
       if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
     }
   }
@@ -652,6 +664,9 @@ __device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, in
 // (36 accumulators).  Two blocks per CU: a tile's X halo / dY loads are all
 // issued before the barrier that ends the previous tile's MFMAs, then written
 // to LDS (BN+ReLU applied to X there); the other block computes meanwhile.
+// MODE (diagnostic builds only, tools/conv_ablate.hip): 1 = stage only the first tile,
+// 2 = no MFMAs (VALU keeps the LDS reads alive).
+template <int MODE = 0>
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* dbred = (float*)(smem + WSTAGE);
@@ -734,14 +749,16 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     constexpr int XH = WX_ITERS / 2;
-    gload_x(tile, 0, XH);
-    __syncthreads();  // previous tile's LDS reads are done
-    lwrite_x(tile, 0, XH);
-    gload_x(tile, XH, WX_ITERS);
-    lwrite_x(tile, XH, WX_ITERS);
-    gload_d(tile);
-    lwrite_d();
-    __syncthreads();
+    if ((MODE & 1) == 0 || tile == t_begin) {
+      gload_x(tile, 0, XH);
+      __syncthreads();  // previous tile's LDS reads are done
+      lwrite_x(tile, 0, XH);
+      gload_x(tile, XH, WX_ITERS);
+      lwrite_x(tile, XH, WX_ITERS);
+      gload_d(tile);
+      lwrite_d();
+      __syncthreads();
+    }
     const char* Xs = smem;
     const char* Ds = Xs + WX_LDS;
     if (a.db != nullptr && kc == 0) {
@@ -769,8 +786,12 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
         const bf16x8 bfr = cat_bf16x4(lo, hi);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
+        for (int ct = 0; ct < 4; ++ct) {
+          if constexpr ((MODE & 2) != 0)
+            acc[t][ct][0] += __uint_as_float((__builtin_bit_cast(u32x4, af[ct]).x ^ __builtin_bit_cast(u32x4, bfr).x) & 0x3f000000u);
+          else
+            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
+        }
       }
     }
   }
@@ -962,8 +983,8 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));
-    allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
-    conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+    allow_lds(conv3x3_wgrad_bf16_kernel<0>, WG_LDS);
+    conv3x3_wgrad_bf16_kernel<0><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
   } else {
     dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
     const size_t lds = A_LDS_BYTES + TH * TW * 64 * 4 + 4 * 64 * 4;

@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                              \
@@ -19,17 +20,17 @@
     }                                                                      \
   } while (0)
 
-template <int MODE, bool DB = false>
+template <int MODE, bool DB = false, int NW = 4>
 static float run(const FwdArgs& a, dim3 grid, int reps) {
   const int lds = DB ? FWD_LDS_DB : FWD_LDS;
-  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB>, lds);
-  conv3x3_fwd_kernel<bf16_t, MODE, DB><<<grid, FT, lds>>>(a);
+  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB, NW>, lds);
+  conv3x3_fwd_kernel<bf16_t, MODE, DB, NW><<<grid, 64 * NW, lds>>>(a);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB><<<grid, FT, lds>>>(a);
+  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB, NW><<<grid, 64 * NW, lds>>>(a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -37,7 +38,63 @@ static float run(const FwdArgs& a, dim3 grid, int reps) {
   return ms / reps;
 }
 
+template <int MODE>
+static float run_wg(const WgArgs& a, dim3 grid, int reps) {
+  allow_lds(conv3x3_wgrad_bf16_kernel<MODE>, WG_LDS);
+  conv3x3_wgrad_bf16_kernel<MODE><<<grid, NTHR, WG_LDS>>>(a);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) conv3x3_wgrad_bf16_kernel<MODE><<<grid, NTHR, WG_LDS>>>(a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
+static int wgrad_main(int N, int H, int W, int cin, int cout, int reps) {
+  const size_t nx = (size_t)N * H * W * cin, nd = (size_t)N * H * W * cout;
+  std::vector<uint16_t> hx(nx), hd(nd);
+  for (size_t i = 0; i < nx; ++i) hx[i] = 0x3c00 + (uint16_t)((i * 2654435761u) >> 24 & 0x7f);
+  for (size_t i = 0; i < nd; ++i) hd[i] = 0x3c00 + (uint16_t)((i * 40503u) >> 8 & 0x7f);
+  void *x, *dy;
+  CK(hipMalloc(&x, nx * 2));
+  CK(hipMalloc(&dy, nd * 2));
+  CK(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dy, hd.data(), nd * 2, hipMemcpyHostToDevice));
+  eunet_act dya = {dy, N, H, W, cout, cout, 0, EUNET_BF16};
+  int ns = 0;
+  eunet_conv3x3_wgrad_splits(&dya, cin, EUNET_BF16, &ns);
+  float *dwp, *dbp;
+  CK(hipMalloc(&dwp, (size_t)ns * cout * 9 * cin * 4));
+  CK(hipMalloc(&dbp, (size_t)ns * cout * 4));
+  WgArgs a;
+  a.x = x; a.N = N; a.H = H; a.W = W; a.xct = cin; a.xco = 0; a.cin = cin;
+  a.isc = nullptr; a.ish = nullptr;
+  a.dy = dy; a.dct = cout; a.dco = 0; a.cout = cout;
+  a.dw = dwp; a.db = dbp;
+  a.tx = cdiv(W, TW); a.ty = cdiv(H, TH); a.ntiles = N * a.tx * a.ty;
+  a.per_split = cdiv(a.ntiles, ns);
+  a.nsplit = ns;
+  dim3 grid(ns * cdiv(cout, 64) * cdiv(cin, KCW));
+  const double flop = 2.0 * 9 * cin * cout * (double)N * H * W;
+  const float t0 = run_wg<0>(a, grid, reps), t1 = run_wg<1>(a, grid, reps), t2 = run_wg<2>(a, grid, reps),
+              t3 = run_wg<3>(a, grid, reps);
+  printf("{\"wgrad_shape\": [%d, %d, %d, %d, %d], \"blocks\": %u, \"splits\": %d", N, H, W, cin, cout, grid.x, ns);
+  const char* nm[] = {"full", "stage_once", "no_mfma", "lds_only"};
+  const float ts[] = {t0, t1, t2, t3};
+  for (int i = 0; i < 4; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+  printf("}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 7 && std::string(argv[1]) == "wgrad")
+    return wgrad_main(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
+                      argc > 7 ? atoi(argv[7]) : 10);
   if (argc < 6) {
     fprintf(stderr, "usage: %s N H W CIN COUT [reps]\n", argv[0]);
     return 2;
@@ -74,17 +131,21 @@ int main(int argc, char** argv) {
   a.bias = nullptr;
   a.y = y; a.yct = cout; a.yco = 0; a.cout = cout;
   a.tx = cdiv(W, FTW); a.ty = cdiv(H, FTH); a.ntiles = N * a.tx * a.ty;
+  a.by = nullptr; a.byct = 0; a.byco = 0;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr;
   CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
   a.stats = stats;
   dim3 grid(a.ntiles * (cout / BN));
   const double flop = 2.0 * 9 * cin * cout * (double)N * H * W;
   const float t0 = run<0>(a, grid, reps), t1 = run<1>(a, grid, reps), t2 = run<2>(a, grid, reps);
   const float t4 = run<4>(a, grid, reps), t5 = run<5>(a, grid, reps), t8 = run<8>(a, grid, reps);
-  const float tdb = run<0, true>(a, grid, reps), tdb5 = run<5, true>(a, grid, reps);
+  const float tdb = run<0, true, 8>(a, grid, reps), tdb5 = run<5, true, 8>(a, grid, reps);
+  const float t8w = run<0, false, 8>(a, grid, reps);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"blocks\": %d", N, H, W, cin, cout, a.ntiles * cout / BN);
-  const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db_full", "db_mfma_only"};
-  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5};
-  for (int i = 0; i < 8; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+  const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db8_full",
+                      "db8_mfma_only", "w8_2blk_full"};
+  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w};
+  for (int i = 0; i < 9; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
   printf("}\n");
   return 0;
 }
