@@ -540,28 +540,41 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
   if (rg == 0 && col < cols) out[col] = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
 }
 
+// gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [gamma xhat + beta > 0], folded per
+// channel into pre = y P + Q and gy = K1 g' + y K2 + K3.  A thread keeps one 16-byte channel
+// unit (256 % U == 0) with its coefficients in registers and strides over pixels.
 template <typename T, typename TO>
-__global__ void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco, long long P, int C,
-                                    const float* mean, const float* istd, const float* gamma, const float* beta,
-                                    const float* dbeta, const float* dgamma, TO* gy, int oct, int oco) {
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
+                                                           long long P, int C, const float* mean, const float* istd,
+                                                           const float* gamma, const float* beta, const float* dbeta,
+                                                           const float* dgamma, TO* gy, int oct, int oco) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= P * U) return;
-  const int u = (int)(id % U);
-  const long long p = id / U;
-  const int c = u * E;
+  const int u = threadIdx.x % U, c = u * E;
   const float inv_n = 1.f / (float)P;
-  float gf[E], yf[E], o[E];
-  Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
-  Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), yf);
+  float kP[E], kQ[E], k1[E], k2[E], k3[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
-    const float xh = (yf[j] - mean[c + j]) * istd[c + j];
-    const float gg = (fmaf(gamma[c + j], xh, beta[c + j]) > 0.f) ? gf[j] : 0.f;
-    o[j] = gamma[c + j] * istd[c + j] * (gg - dbeta[c + j] * inv_n - xh * dgamma[c + j] * inv_n);
+    const float is = istd[c + j], ga = gamma[c + j], off = -mean[c + j] * is;
+    kP[j] = ga * is;
+    kQ[j] = fmaf(ga, off, beta[c + j]);
+    k1[j] = ga * is;
+    const float dg = dgamma[c + j] * inv_n;
+    k2[j] = -k1[j] * is * dg;
+    k3[j] = -k1[j] * fmaf(off, dg, dbeta[c + j] * inv_n);
   }
-  *(uint4*)(gy + p * oct + oco + c) = Vec16<T>::pack(o);
+  const int ppb = 256 / U;  // pixels per block per step
+  for (long long p = (long long)blockIdx.x * ppb + threadIdx.x / U; p < P; p += (long long)gridDim.x * ppb) {
+    float gf[E], yf[E], o[E];
+    Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
+    Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), yf);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float gg = fmaf(yf[j], kP[j], kQ[j]) > 0.f ? gf[j] : 0.f;
+      o[j] = fmaf(k1[j], gg, fmaf(yf[j], k2[j], k3[j]));
+    }
+    *(uint4*)(gy + p * oct + oco + c) = Vec16<TO>::pack(o);
+  }
 }
 
 template <typename T>
@@ -981,8 +994,10 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
   EUNET_REQUIRE(g->dtype == y->dtype && gy->dtype == y->dtype && g->c == y->c && gy->c == y->c,
                 "bn_bwd_apply: mismatch");
   const long long P = (long long)y->n * y->h * y->w;
-  const long long total = P * (y->c / e16(y->dtype));
-  const unsigned gr = (unsigned)((total + 255) / 256);
+  const int U = y->c / e16(y->dtype);
+  EUNET_REQUIRE(256 % U == 0, "bn_bwd_apply: 256 must be a multiple of C/%d", e16(y->dtype));
+  const long long nb = (P * U + 255) / 256;
+  const unsigned gr = (unsigned)(nb < 4096 ? nb : 4096);
   if (y->dtype == EUNET_BF16)
     bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
