@@ -163,14 +163,19 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 // DB: true = one block per CU, double-buffered LDS (next chunk prefetched into
 //   registers during the MFMAs, one barrier per chunk); false = two blocks per CU,
 //   one LDS stage each (a block's staging overlaps the other block's MFMAs).
-template <typename T, int MODE = 0, bool DB = false, int NW = 4>
+// SPEC (with DB, NW = 8): waves 0-3 only compute (128 px x 64 co each), waves 4-7 only
+//   stage the next chunk (global -> registers -> BN+ReLU -> LDS) into the other buffer.
+template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false>
 __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
+  static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
   constexpr int NTH = 64 * NW;
-  constexpr int RPW = FTH / NW;               // output rows per wave
+  constexpr int NCW = SPEC ? 4 : NW;          // computing waves
+  constexpr int NLT = SPEC ? 256 : NTH;       // staging threads
+  constexpr int RPW = FTH / NCW;              // output rows per computing wave
   constexpr int MT = 2 * RPW;                 // 16-px m-tiles per wave
-  constexpr int A_IT = (FA_UNITS + NTH - 1) / NTH;
-  constexpr int B_IT = (B_UNITS + NTH - 1) / NTH;
-  constexpr bool B_TAIL = B_UNITS % NTH != 0;
+  constexpr int A_IT = (FA_UNITS + NLT - 1) / NLT;
+  constexpr int B_IT = (B_UNITS + NLT - 1) / NLT;
+  constexpr bool B_TAIL = B_UNITS % NLT != 0;
   constexpr int NPASS = DB ? 1 : 2;           // epilogue staging passes (LDS budget)
   constexpr int PROWS = FTH / NPASS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -187,6 +192,8 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
   const int co0 = cob * BN;
   const int q = lane >> 4, li = lane & 15;
+  const int lt = SPEC ? tid - 256 : tid;  // staging thread index
+  const bool computes = !SPEC || wv < NCW;
 
   f32x4 acc[MT][4];
 #pragma unroll
@@ -204,12 +211,12 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
 #define CONV_GLOAD_A(KC_, I0_, I1_)                                                           \
   do {                                                                                        \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        ra[i] = fwd_load_unit<T>(a, n, y0, x0, tid + i * NTH, (KC_), rok[i]);                 \
+        ra[i] = fwd_load_unit<T>(a, n, y0, x0, lt + i * NLT, (KC_), rok[i]);                  \
   } while (0)
 #define CONV_GLOAD_B(KC_, I0_, I1_)                                                           \
   do {                                                                                        \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
-      const int id_ = tid + i * NTH;                                                          \
+      const int id_ = lt + i * NLT;                                                           \
       if (!B_TAIL || id_ < B_UNITS) rb[i] = CONV_BUNIT(id_, KC_);                             \
     }                                                                                         \
   } while (0)
@@ -217,13 +224,13 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   do {                                                                                        \
     char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        fwd_store_unit<T>(a, As_, tid + i * NTH, (KC_), ra[i], rok[i]);                       \
+        fwd_store_unit<T>(a, As_, lt + i * NLT, (KC_), ra[i], rok[i]);                        \
   } while (0)
 #define CONV_LWRITE_B(BUF_, I0_, I1_)                                                         \
   do {                                                                                        \
     char* Bs_ = smem + (BUF_) * STAGE_BYTES + FA_BYTES;                                       \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
-      const int id_ = tid + i * NTH;                                                          \
+      const int id_ = lt + i * NLT;                                                           \
       if (!B_TAIL || id_ < B_UNITS) *(u32x4*)(Bs_ + id_ * 16) = rb[i];                        \
     }                                                                                         \
   } while (0)
@@ -273,7 +280,14 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   };
 
   uint4 fa0[MT], fb0[4];
-  if constexpr (DB) {
+  if constexpr (SPEC) {
+    if (!computes) {
+      CONV_GLOAD_A(0, 0, A_IT);
+      CONV_GLOAD_B(0, 0, B_IT);
+      CONV_LWRITE_A(0, 0, 0, A_IT);
+      CONV_LWRITE_B(0, 0, B_IT);
+    }
+  } else if constexpr (DB) {
     CONV_GLOAD_A(0, 0, A_IT);
     CONV_GLOAD_B(0, 0, B_IT);
     CONV_LWRITE_A(0, 0, 0, A_IT);
@@ -290,7 +304,18 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
       fa0[mt] = *(const uint4*)(smem + (q * FHPXP + (RPW * wv + (mt >> 1)) * FHW + (mt & 1) * 16 + li) * 16);
   }
   for (int kc = 0; kc < a.nkc; ++kc) {
-    if constexpr (DB) {
+    if constexpr (SPEC) {
+      const int cur = kc & 1;
+      if (computes) {
+        chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
+      } else if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
+        CONV_GLOAD_A(kc + 1, 0, A_IT);
+        CONV_GLOAD_B(kc + 1, 0, B_IT);
+        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, A_IT);
+        CONV_LWRITE_B(cur ^ 1, 0, B_IT);
+      }
+      __syncthreads();
+    } else if constexpr (DB) {
       const int cur = kc & 1;
       if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
         CONV_GLOAD_A(kc + 1, 0, A_IT);
@@ -332,9 +357,9 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   }
   constexpr int PASS_PX = PROWS * FTW;
   float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
-  float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NW][64] x 2
-  float* bprm = red + 2 * NW * 64;                              // [4][64] BN-backward constants
-  static_assert(PASS_PX * OUT_LD * 4 + (2 * NW + 4) * 64 * 4 <= (DB ? FWD_LDS_DB : FWD_LDS), "epilogue LDS");
+  float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NCW][64] x 2
+  float* bprm = red + 2 * NCW * 64;                             // [4][64] BN-backward constants
+  static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= (DB ? FWD_LDS_DB : FWD_LDS), "epilogue LDS");
   __syncthreads();  // all waves are done with the K loop's LDS
   if (a.stats != nullptr) {
     float s[4];
@@ -352,7 +377,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
       v += __shfl_xor(v, 32, 64);
       s[nt] = v;
     }
-    if (q == 0)
+    if (q == 0 && computes)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) red[wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
@@ -362,7 +387,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     for (int nt = 0; nt < 4; ++nt) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) t += red[w * 64 + nt * 16 + li];
+      for (int w = 0; w < NCW; ++w) t += red[w * 64 + nt * 16 + li];
       mb[nt] = t / cnt;
     }
 #pragma unroll
@@ -380,16 +405,16 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
       v += __shfl_xor(v, 32, 64);
       s[nt] = v;
     }
-    if (q == 0)
+    if (q == 0 && computes)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) red[NW * 64 + wv * 64 + nt * 16 + li] = s[nt];
+      for (int nt = 0; nt < 4; ++nt) red[NCW * 64 + wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
     if (tid < 64 && co0 + tid < a.cout) {
       float sum = 0.f, m2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
+      for (int w = 0; w < NCW; ++w) {
         sum += red[w * 64 + tid];
-        m2 += red[NW * 64 + w * 64 + tid];
+        m2 += red[NCW * 64 + w * 64 + tid];
       }
       a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
       a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
@@ -414,7 +439,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   }
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
+    if (computes && RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll

@@ -20,17 +20,17 @@
     }                                                                      \
   } while (0)
 
-template <int MODE, bool DB = false, int NW = 4>
+template <int MODE, bool DB = false, int NW = 4, bool SPEC = false>
 static float run(const FwdArgs& a, dim3 grid, int reps) {
   const int lds = DB ? FWD_LDS_DB : FWD_LDS;
-  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB, NW>, lds);
-  conv3x3_fwd_kernel<bf16_t, MODE, DB, NW><<<grid, 64 * NW, lds>>>(a);
+  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC>, lds);
+  conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC><<<grid, 64 * NW, lds>>>(a);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB, NW><<<grid, 64 * NW, lds>>>(a);
+  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC><<<grid, 64 * NW, lds>>>(a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -141,11 +141,12 @@ int main(int argc, char** argv) {
   const float t4 = run<4>(a, grid, reps), t5 = run<5>(a, grid, reps), t8 = run<8>(a, grid, reps);
   const float tdb = run<0, true, 8>(a, grid, reps), tdb5 = run<5, true, 8>(a, grid, reps);
   const float t8w = run<0, false, 8>(a, grid, reps);
+  const float tsp = run<0, true, 8, true>(a, grid, reps), tsp5 = run<5, true, 8, true>(a, grid, reps);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"blocks\": %d", N, H, W, cin, cout, a.ntiles * cout / BN);
   const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db8_full",
-                      "db8_mfma_only", "w8_2blk_full"};
-  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w};
-  for (int i = 0; i < 9; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+                      "db8_mfma_only", "w8_2blk_full", "spec_full", "spec_mfma_only"};
+  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w, tsp, tsp5};
+  for (int i = 0; i < 11; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
   printf("}\n");
   return 0;
 }
