@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=1024, help="CPU baseline sample: one B=1 step at this size")
+    ap.add_argument("--dice-size", type=int, default=1024, help="Dice-vs-CPU-reference image side (0 = skip)")
     return ap.parse_args()
 
 
@@ -72,6 +73,44 @@ def cpu_baseline(args):
     return {"value": round(scale / dt, 5), "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"1 oracle train step (PyTorch CPU fp32 restatement of Trainer.train_epoch), B=1, "
                       f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s"}
+
+
+def dice_vs_cpu_ref(model, args, dev):
+    """The metric's "Dice vs CPU ref": the trained model (its compute dtype) predicts a held-out
+    synthetic tile on the GPU (eval mode, Evaluator._run_model_single + the reference's
+    probability->mask rules, all HIP); the oracle runs the same weights in fp32 on the CPU
+    (reference path: full 2H forward, bilinear resize, softmax, mask rules).  Reported:
+    calculate_semantic_metrics(gpu_mask, cpu_mask) (GPU-counted), pixel agreement, max |dprob|."""
+    from eunet import metrics, ops, synth
+    from eunet.evaluator import Evaluator
+    from oracle import evalpath_ref as E
+    n = args.dice_size
+    x, gt = synth.batch(1, n, n, start_index=100000, num_classes=2, in_channels=1)
+    ev = Evaluator(model, dev, "enhanced_unet")
+    model.eval()
+    with torch.no_grad():
+        probs = ev._run_model_single(x[0].to(dev))
+        gpu_mask = ops.probs_to_mask(probs)
+    model.train()
+    S = {k: (v.detach().float().cpu() if v.is_floating_point() else v.cpu()) for k, v in model.state_dict().items()}
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref_probs = E.run_model_single(S, x[0])
+    cpu_mask = E.convert_probs_to_mask(ref_probs.numpy())
+    dt = time.perf_counter() - t0
+    m = metrics.calculate_semantic_metrics(gpu_mask, cpu_mask)
+    m_gt = metrics.calculate_semantic_metrics(gpu_mask, gt[0])
+    agree = float((gpu_mask.cpu().numpy() == cpu_mask).mean())
+    pg, pc = probs[1].double().cpu(), ref_probs[1].double()  # live-class probabilities
+    soft = float(2 * (pg * pc).sum() / ((pg * pg).sum() + (pc * pc).sum()))
+    return {"sem_mean_dice": round(m["sem_mean_dice"], 6), "sem_live_dice": round(m["sem_live_dice"], 6),
+            "sem_background_dice": round(m["sem_background_dice"], 6), "pixel_agreement": round(agree, 7),
+            "max_abs_prob_diff": round(float((probs.cpu() - ref_probs).abs().max()), 6),
+            "live_soft_dice": round(soft, 7),
+            "live_pixels_gpu": int((gpu_mask == 1).sum()), "live_pixels_cpu": int((cpu_mask == 1).sum()),
+            "gpu_vs_synthetic_gt_live_dice": round(m_gt["sem_live_dice"], 6),
+            "sample": f"1 held-out {n}x{n} synthetic tile after the timed steps; GPU {args.dtype} vs CPU fp32 "
+                      f"oracle ({dt:.1f} s)"}
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
@@ -162,6 +201,7 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+    dice = dice_vs_cpu_ref(model, args, dev) if args.dice_size > 0 else None
     from oracle.eunet_ref import flops_per_pixel
     step_flops = flops_per_pixel(args.base, 1, 2) * args.size * args.size * args.batch
     line = {
@@ -183,6 +223,7 @@ def main():
         "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
         "roofline": roof,
         "cpu_baseline": cpu,
+        "dice_vs_cpu_ref": dice,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -224,3 +224,57 @@ def conv1x1_bwd_tiles(y: Act) -> int:
 def conv1x1_bwd(y: Act, scale, shift, w, k, gz, gact: Act, part):
     call("eunet_conv1x1_bwd", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),
          ctypes.byref(gact), _ptr(part), _stream())
+
+
+# ---- evaluation path (evalpath.hip) ------------------------------------------------
+def semantic_counts(pred, gt):
+    """pred, gt int64 [n, ...] -> counts int64 [n, 3, 3] = (#pred==c, #gt==c, #both==c)."""
+    n = pred.shape[0]
+    hw = pred[0].numel()
+    counts = torch.empty(n, 3, 3, dtype=torch.int64, device=pred.device)
+    call("eunet_semantic_counts", _ptr(pred.contiguous()), _ptr(gt.contiguous()), n, hw, _ptr(counts), _stream())
+    return counts
+
+
+def binary_overlap(a, b):
+    """int64 masks -> (inter, union, sum a, sum b) as python ints (nonzero = foreground)."""
+    out = torch.empty(4, dtype=torch.int64, device=a.device)
+    call("eunet_binary_overlap", _ptr(a.contiguous()), _ptr(b.contiguous()), a.numel(), _ptr(out), _stream())
+    return tuple(int(v) for v in out.tolist())
+
+
+def resize_bilinear(x, hout, wout, scale_h=None, scale_w=None, flip_h=False, flip_w=False, out=None):
+    """x [..., H, W] fp32 -> [..., hout, wout]; scale_* = 1/scale_factor (F.interpolate with
+    scale_factor) or None for in/out (F.interpolate with size)."""
+    x = x.contiguous()
+    hin, win = x.shape[-2:]
+    planes = x.numel() // (hin * win)
+    sh = float(scale_h) if scale_h is not None else hin / hout
+    sw = float(scale_w) if scale_w is not None else win / wout
+    y = out if out is not None else torch.empty(*x.shape[:-2], hout, wout, dtype=torch.float32, device=x.device)
+    call("eunet_resize_bilinear", _ptr(x), planes, hin, win, _ptr(y), hout, wout, sh, sw, int(flip_h), int(flip_w),
+         _stream())
+    return y
+
+
+def softmax_crop(logits, h, w, flip_h=False, flip_w=False, out=None):
+    """logits [K, hp, wp] fp32 -> probs [K, h, w] (crop to the top-left h x w, optional flips)."""
+    logits = logits.contiguous().float()
+    k, hp, wp = logits.shape
+    y = out if out is not None else torch.empty(k, h, w, dtype=torch.float32, device=logits.device)
+    call("eunet_softmax_crop", _ptr(logits), k, hp, wp, h, w, int(flip_h), int(flip_w), _ptr(y), _stream())
+    return y
+
+
+def accumulate(acc, p, mode: int, count: float = 1.0):
+    call("eunet_accumulate", _ptr(acc), _ptr(p.contiguous()), acc.numel(), int(mode), float(count), _stream())
+
+
+def probs_to_mask(probs):
+    """probs [K, h, w] fp32 -> int64 mask [h, w] (the reference's thresholded conversion)."""
+    probs = probs.contiguous().float()
+    k, h, w = probs.shape
+    mask = torch.empty(h, w, dtype=torch.int64, device=probs.device)
+    ws = torch.empty(2, dtype=torch.int64, device=probs.device)
+    call("eunet_probs_to_mask", _ptr(probs), k, h, w, _ptr(mask), _ptr(ws), _stream())
+    return mask

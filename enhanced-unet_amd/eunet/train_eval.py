@@ -141,3 +141,6 @@ class Trainer:
             else:
                 self.scheduler.step()
         return self.optimizer.param_groups[0]["lr"]
+
+
+from .evaluator import Evaluator  # noqa: E402,F401  (train_eval.Evaluator, train_eval.py:356-904)

@@ -179,6 +179,35 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
                       const float* w, int k, const float* gz, const eunet_act* gact, float* part,
                       void* stream);
 
+/* ---- evaluation path (evalpath.hip) ---------------------------------------
+ * Semantic metric counts (metrics.py:29-58, calculate_semantic_metrics): pred, gt
+ * int64 [n][hw]; counts int64 [n][3 classes][3] = (#pred==c, #gt==c, #both==c),
+ * zeroed by the call.  IoU / Dice follow from the counts on the host. */
+int eunet_semantic_counts(const int64_t* pred, const int64_t* gt, int n, long long hw,
+                          int64_t* counts, void* stream);
+/* calculate_iou / calculate_dice (metrics.py:12-26) of two int64 masks of n elements:
+ * out int64[4] = (#(a!=0 & b!=0), #(a!=0 | b!=0), sum a, sum b), zeroed by the call */
+int eunet_binary_overlap(const int64_t* a, const int64_t* b, long long n, int64_t* out,
+                         void* stream);
+/* Bilinear resample, align_corners=False, PyTorch upsample_bilinear2d index math
+ * (F.interpolate in train_eval.py:413, 441-449): x [planes][hin][win] ->
+ * y [planes][hout][wout]; scale_* = 1/scale_factor or hin/hout; flip_* mirror the
+ * destination index (torch.flip, train_eval.py:427-437). */
+int eunet_resize_bilinear(const float* x, int planes, int hin, int win, float* y, int hout,
+                          int wout, float scale_h, float scale_w, int flip_h, int flip_w,
+                          void* stream);
+/* softmax over K (2 or 3) of logits [K][hp][wp], cropped to [h][w] and optionally
+ * flipped (F.softmax + crop, train_eval.py:414-417) -> probs [K][h][w] */
+int eunet_softmax_crop(const float* logits, int k, int hp, int wp, int h, int w, int flip_h,
+                       int flip_w, float* probs, void* stream);
+/* TTA mean (train_eval.py:453): mode 0 acc = p, 1 acc += p, 2 acc = (acc + p) / count */
+int eunet_accumulate(float* acc, const float* p, long long n, int mode, float count,
+                     void* stream);
+/* _convert_probs_to_mask (train_eval.py:455-568): probs [K][h][w] (K = 3; K = 2 with a
+ * zero dead-cell probability) -> mask int64 [h][w]; counts: 2 int64 of workspace. */
+int eunet_probs_to_mask(const float* probs, int k, int h, int w, int64_t* mask,
+                        int64_t* counts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,13 @@ Fixtures (all with formula weights, oracle/weights.py):
   loss_k2.npz      K=2 via a -inf third logit fed to the reference loss
   step_c3k3.npz    one Trainer.train_epoch (warmup-stepped LR, clip, AdamW) on a B=2 batch
   lr_traj.npz      train_model's per-epoch LR for E in {6, 50}
+  metrics.npz      metrics.calculate_semantic_metrics / calculate_iou / calculate_dice on
+                   mask pairs incl. empty classes and out-of-range labels
+  probs_mask.npz   Evaluator._convert_probs_to_mask on probability maps that reach every
+                   branch (argmax filters, background promotions, all pixel-ratio regimes)
+  tta_c3k3.npz     Evaluator._run_model_single / _run_tta_inference (flips + 0.75/1.25
+                   rescales) of the reference model (eval mode, BN stats from one train
+                   forward) on a 40x56 image (reflect pad to /32 and crop exercised)
 """
 from __future__ import annotations
 
@@ -204,18 +211,90 @@ def gen_lr(ref_te):
     np.savez_compressed(os.path.join(HERE, "lr_traj.npz"), **out)
 
 
-def main():
+def gen_metrics():
+    import metrics as ref_metrics  # /root/reference/metrics.py (imported after the stubs)
+    g = np.random.default_rng(51)
+    cases = [
+        (g.integers(0, 3, (37, 53)), g.integers(0, 3, (37, 53))),
+        (np.zeros((16, 16), np.int64), g.integers(0, 3, (16, 16))),
+        (g.integers(0, 2, (20, 24)), g.integers(0, 2, (20, 24))),          # class 2 absent in both
+        (g.integers(0, 4, (19, 23)), g.integers(0, 4, (19, 23))),          # label 3 is ignored
+        (np.full((1, 1), 2, np.int64), np.full((1, 1), 2, np.int64)),
+        (np.zeros((8, 8), np.int64), np.zeros((8, 8), np.int64)),
+    ]
+    out = {}
+    for i, (p, t) in enumerate(cases):
+        p, t = p.astype(np.int64), t.astype(np.int64)
+        out[f"pred{i}"], out[f"gt{i}"] = p, t
+        m = ref_metrics.calculate_semantic_metrics(p, t)
+        out[f"keys{i}"] = np.array(sorted(m))
+        out[f"vals{i}"] = np.array([float(m[k]) for k in sorted(m)])
+        out[f"iou{i}"] = float(ref_metrics.calculate_iou(p, t))
+        out[f"dice{i}"] = float(ref_metrics.calculate_dice(p, t))
+    np.savez_compressed(os.path.join(HERE, "metrics.npz"), n=len(cases), **out)
+
+
+def _probs(g, h, w, bias, spread):
+    lg = torch.from_numpy(g.normal(0.0, spread, (3, h, w))) + torch.tensor(bias).view(3, 1, 1)
+    return F.softmax(lg.float(), dim=0)
+
+
+def gen_probs_mask(ref_te):
+    ev = ref_te.Evaluator(torch.nn.Identity(), "cpu", "enhanced_unet")
+    g = np.random.default_rng(61)
+    biases = [(0.0, 0.0, 0.0), (0.0, 1.5, -1.0), (-1.0, 2.5, 0.0), (0.0, -1.0, 1.2),
+              (-0.5, -0.5, 1.6), (-1.5, -1.0, 2.0), (-2.5, -1.5, 2.8), (-3.0, -1.0, 3.5),
+              (0.5, 0.0, 0.5), (-2.0, 1.0, 1.0)]
+    out = {}
+    for i, b in enumerate(biases):
+        probs = _probs(g, 48, 56, b, 1.5)
+        mask = ev._convert_probs_to_mask(probs)
+        out[f"probs{i}"], out[f"mask{i}"] = probs.numpy(), np.asarray(mask, np.int64)
+    np.savez_compressed(os.path.join(HERE, "probs_mask.npz"), n=len(biases), **out)
+
+
+def gen_tta(ref_models, ref_te):
+    model = ref_models.get_model("enhanced_unet", num_classes=3, device="cpu")
+    _load_formula(model, 64, 3, 3)
+    g = torch.Generator().manual_seed(71)
+    xw = torch.rand(2, 3, 64, 64, generator=g)
+    model.train()
+    with torch.no_grad():
+        model(xw)  # one train forward: BN running stats away from (0, 1)
+    stats = _bn_stats(model)
+    model.eval()
+    img = torch.rand(3, 40, 56, generator=g)
+    ev = ref_te.Evaluator(model, "cpu", "enhanced_unet")
+    with torch.no_grad():
+        single = ev._run_model_single(img)
+        tta = ev._run_tta_inference(img)
+    mask = ev._convert_probs_to_mask(tta)
+    np.savez_compressed(os.path.join(HERE, "tta_c3k3.npz"), xw=xw.numpy(), img=img.numpy(),
+                        single=single.numpy(), tta=tta.numpy(), mask=np.asarray(mask, np.int64),
+                        **{"bn:" + k: v for k, v in stats.items()})
+
+
+def main(only=()):
+    """python gen_golden.py [name ...]: regenerate all fixtures, or only the named ones."""
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref_models, ref_te = _import_reference()
-    gen_forward(ref_models, 3, "fwd_c3k3.npz")
-    gen_forward(ref_models, 2, "fwd_c3k2.npz")
-    gen_in1(ref_models)
-    gen_loss(ref_te, 3, "loss_k3.npz")
-    gen_loss(ref_te, 2, "loss_k2.npz")
-    gen_step(ref_models, ref_te)
-    gen_lr(ref_te)
+    jobs = {
+        "fwd_c3k3": lambda: gen_forward(ref_models, 3, "fwd_c3k3.npz"),
+        "fwd_c3k2": lambda: gen_forward(ref_models, 2, "fwd_c3k2.npz"),
+        "in1_equiv": lambda: gen_in1(ref_models),
+        "loss_k3": lambda: gen_loss(ref_te, 3, "loss_k3.npz"),
+        "loss_k2": lambda: gen_loss(ref_te, 2, "loss_k2.npz"),
+        "step_c3k3": lambda: gen_step(ref_models, ref_te),
+        "lr_traj": lambda: gen_lr(ref_te),
+        "metrics": gen_metrics,
+        "probs_mask": lambda: gen_probs_mask(ref_te),
+        "tta_c3k3": lambda: gen_tta(ref_models, ref_te),
+    }
+    for name, job in jobs.items():
+        if not only or name in only:
+            job()
     print("fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -128,3 +128,42 @@ def test_formula_weights_deterministic():
     assert np.array_equal(a, b) and (a >= 0).all() and (a < 1).all()
     spec = R.state_spec(64, 3, 3)
     assert len(spec) == 109
+
+
+# ---- evaluation path (oracle/evalpath_ref.py) vs the reference's own outputs ----------
+def test_semantic_metrics_match_reference(golden_dir):
+    from oracle import evalpath_ref as E
+    g = _load(golden_dir, "metrics.npz")
+    for i in range(int(g["n"])):
+        m = E.calculate_semantic_metrics(g[f"pred{i}"], g[f"gt{i}"])
+        for k, v in zip(g[f"keys{i}"], g[f"vals{i}"]):
+            assert m[str(k)] == v, (i, k)
+        assert E.calculate_iou(g[f"pred{i}"], g[f"gt{i}"]) == g[f"iou{i}"]
+        assert E.calculate_dice(g[f"pred{i}"], g[f"gt{i}"]) == g[f"dice{i}"]
+
+
+def test_probs_to_mask_matches_reference_all_regimes(golden_dir):
+    from oracle import evalpath_ref as E
+    g = _load(golden_dir, "probs_mask.npz")
+    regimes = set()
+    for i in range(int(g["n"])):
+        assert np.array_equal(E.convert_probs_to_mask(g[f"probs{i}"]), g[f"mask{i}"]), i
+        lr, dr = E.mask_regime(g[f"probs{i}"])
+        regimes.add(("live" if lr > 0.5 else "-", 3 if dr > 0.4 else 2 if dr > 0.25 else 1 if dr > 0.15 else 0))
+    # every refinement branch of train_eval.py:533-563 is reached by some case
+    assert {r[1] for r in regimes} >= {1, 2, 3} and any(r[0] == "live" for r in regimes)
+
+
+def test_tta_matches_reference(golden_dir):
+    from oracle import evalpath_ref as E
+    g = _load(golden_dir, "tta_c3k3.npz")
+    S = R.formula_weights(64, 3, 3, dtype=torch.float32)
+    for k in g.files:
+        if k.startswith("bn:"):
+            S[k[3:]] = torch.from_numpy(g[k])
+    img = torch.from_numpy(g["img"])
+    with torch.no_grad():
+        assert _rel(E.run_model_single(S, img).numpy(), g["single"]) < 1e-5
+        p = E.run_tta(S, img)
+    assert _rel(p.numpy(), g["tta"]) < 1e-5
+    assert np.array_equal(E.convert_probs_to_mask(g["tta"]), g["mask"])
