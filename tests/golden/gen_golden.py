@@ -21,6 +21,8 @@ Fixtures (all with formula weights, oracle/weights.py):
                    mask pairs incl. empty classes and out-of-range labels
   probs_mask.npz   Evaluator._convert_probs_to_mask on probability maps that reach every
                    branch (argmax filters, background promotions, all pixel-ratio regimes)
+  dual_c3k3.npz    SMP-path EnhancedUNet (attention gate, fusion head, residual, aux outputs)
+                   with stand-in branches + one train_epoch with auxiliary supervision
   tta_c3k3.npz     Evaluator._run_model_single / _run_tta_inference (flips + 0.75/1.25
                    rescales) of the reference model (eval mode, BN stats from one train
                    forward) on a 40x56 image (reflect pad to /32 and crop exercised)
@@ -274,6 +276,96 @@ def gen_tta(ref_models, ref_te):
                         **{"bn:" + k: v for k, v in stats.items()})
 
 
+def _fake_smp(ref_models):
+    """Stand-in for segmentation_models_pytorch (absent here, and its backbones need ImageNet
+    weights): UnetPlusPlus / DeepLabV3Plus return the reference's own BasicUNet trunk ending at
+    input resolution (dec1 on d2, no final upsample), the build's branch definition."""
+    def trunk_forward(self, x):
+        e1 = self.enc1(x)
+        e2 = self.enc2(self.pool(e1))
+        e3 = self.enc3(self.pool(e2))
+        e4 = self.enc4(self.pool(e3))
+        d4 = self.dec4(torch.cat([self.upsample(e4), e3], dim=1))
+        d3 = self.dec3(torch.cat([self.upsample(d4), e2], dim=1))
+        d2 = self.dec2(torch.cat([self.upsample(d3), e1], dim=1))
+        return self.dec1(d2)
+
+    def branch(**kw):
+        prev, ref_models.SMP_AVAILABLE = ref_models.SMP_AVAILABLE, False  # -> BasicUNet
+        try:
+            net = ref_models.UNet(kw["classes"]).model
+        finally:
+            ref_models.SMP_AVAILABLE = prev
+        net.forward = types.MethodType(trunk_forward, net)
+        return net
+
+    return types.SimpleNamespace(UnetPlusPlus=branch, DeepLabV3Plus=branch)
+
+
+def gen_dual(ref_models, ref_te, K=3):
+    """dual_c3k3.npz: the reference SMP-path EnhancedUNet (models.py:253-339) with stand-in
+    branches: train forward (fused + aux outputs, gate/fusion BN stats), eval forward and one
+    Trainer.train_epoch with auxiliary supervision (train_eval.py:199-234).  The two Dropout2d
+    use seeded keep-masks that are saved with the fixture."""
+    from oracle.dual_ref import dual_state_spec
+    smp = _fake_smp(ref_models)
+    g = torch.Generator().manual_seed(81)
+    B, H = 2, 32
+    masks = [(torch.rand(B, 256, generator=g) > 0.2).float(), (torch.rand(B, 128, generator=g) > 0.15).float()]
+
+    def build():
+        ref_models.smp, ref_models.SMP_AVAILABLE = smp, True
+        try:
+            model = ref_models.EnhancedUNet(num_classes=K)
+        finally:
+            ref_models.SMP_AVAILABLE = False
+        sd = formula_state_dict(dual_state_spec(64, 3, K))
+        ref_sd = model.state_dict()
+        assert list(ref_sd.keys()) == list(sd.keys()), "dual state_dict schema mismatch"
+        model.load_state_dict({k: (torch.tensor(0, dtype=torch.long) if k.endswith("num_batches_tracked") else
+                                   torch.from_numpy(np.asarray(v)).float().reshape(ref_sd[k].shape))
+                               for k, v in sd.items()})
+        for idx, (mi, p) in zip((3, 7), zip(masks, (0.2, 0.15))):
+            mod = model.fusion_head[idx]
+            mod.forward = (lambda mod_, m_, p_: (lambda h: h * m_[:, :, None, None] / (1 - p_) if mod_.training
+                                                 else h))(mod, mi, p)
+        return model
+
+    def run(model, x, training):
+        ref_models.SMP_AVAILABLE = True
+        try:
+            model.train(training)
+            with torch.no_grad():
+                out = model(x)
+            aux = model.get_aux_outputs()
+        finally:
+            ref_models.SMP_AVAILABLE = False
+        return out, aux
+
+    x, m = _inputs(B, 3, H, H, K, seed=83)
+    model = build()
+    out, aux = run(model, x, True)
+    stats = _bn_stats(model)
+    out_eval, _ = run(model, x, False)
+    model = build()
+    tr = ref_te.Trainer(model, "cpu", "enhanced_unet", total_epochs=50)
+    tr.warmup_scheduler.step()
+    batch = {"images": x, "batch_items": [{"semantic_mask": m[i]} for i in range(B)]}
+    ref_models.SMP_AVAILABLE = True
+    try:
+        loss = tr.train_epoch([batch])
+    finally:
+        ref_models.SMP_AVAILABLE = False
+    sd = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    grads = {k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
+    np.savez_compressed(os.path.join(HERE, f"dual_c3k{K}.npz"), x=x.numpy(), m=m.numpy(),
+                        drop0=masks[0].numpy(), drop1=masks[1].numpy(), out_train=out.numpy(),
+                        aux_unetpp=aux["unetpp"].numpy(), aux_deeplab=aux["deeplab"].numpy(),
+                        out_eval=out_eval.numpy(), loss=loss, lr=tr.optimizer.param_groups[0]["lr"],
+                        **{"bn:" + k: v for k, v in stats.items() if not k.startswith(("unetpp", "deeplab"))},
+                        **_summaries("post", sd), **_summaries("grad", grads))
+
+
 def main(only=()):
     """python gen_golden.py [name ...]: regenerate all fixtures, or only the named ones."""
     torch.set_num_threads(min(8, os.cpu_count() or 1))
@@ -289,6 +381,7 @@ def main(only=()):
         "metrics": gen_metrics,
         "probs_mask": lambda: gen_probs_mask(ref_te),
         "tta_c3k3": lambda: gen_tta(ref_models, ref_te),
+        "dual_c3k3": lambda: gen_dual(ref_models, ref_te, 3),
     }
     for name, job in jobs.items():
         if not only or name in only:

@@ -167,3 +167,48 @@ def test_tta_matches_reference(golden_dir):
         p = E.run_tta(S, img)
     assert _rel(p.numpy(), g["tta"]) < 1e-5
     assert np.array_equal(E.convert_probs_to_mask(g["tta"]), g["mask"])
+
+
+# ---- dual-branch (SMP-path) EnhancedUNet: oracle/dual_ref.py vs the reference module ----
+def _dual_setup(golden_dir):
+    from oracle import dual_ref as D
+    g = _load(golden_dir, "dual_c3k3.npz")
+    S = D.dual_formula_weights(64, 3, 3, dtype=torch.float32)
+    masks = (torch.from_numpy(g["drop0"]), torch.from_numpy(g["drop1"]))
+    return D, g, S, masks
+
+
+def test_dual_forward_matches_reference(golden_dir):
+    D, g, S, masks = _dual_setup(golden_dir)
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        fused, aux = D.dual_forward(S, x, training=True, drop_masks=masks)
+    assert _rel(fused.numpy(), g["out_train"]) < 1e-5
+    assert _rel(aux["unetpp"].numpy(), g["aux_unetpp"]) < 1e-5
+    assert _rel(aux["deeplab"].numpy(), g["aux_deeplab"]) < 1e-5
+    for k in g.files:
+        if k.startswith("bn:"):
+            assert _rel(S[k[3:]].numpy(), g[k]) < 1e-4, k
+    with torch.no_grad():
+        out_e, _ = D.dual_forward(S, x, training=False)
+    assert _rel(out_e.numpy(), g["out_eval"]) < 1e-5
+
+
+def test_dual_train_step_matches_reference(golden_dir):
+    D, g, S, masks = _dual_setup(golden_dir)
+    tr = D.DualOracleTrainer(S, total_epochs=50, drop_masks=masks)
+    lr = tr.epoch_lr_step(0)
+    loss = tr.step(torch.from_numpy(g["x"]), torch.from_numpy(g["m"]))
+    assert abs(loss - float(g["loss"])) < 1e-5 * abs(float(g["loss"]))
+    for k in tr.keys:
+        for tag, arr in (("grad", S[k].grad.detach().numpy().astype(np.float64)),
+                         ("post", S[k].detach().numpy().astype(np.float64))):
+            if f"{tag}:{k}" in g.files:
+                ref = g[f"{tag}:{k}"]
+                floor = 2.0 * lr if (tag == "post" and k.endswith((".0.bias", ".3.bias"))) else 1e-6
+                assert np.abs(arr.reshape(ref.shape) - ref).max() < 2e-3 * max(np.abs(ref).max(), 1e-12) + floor, \
+                    (tag, k)
+            else:
+                flat = arr.reshape(-1)
+                ref_norm = float(g[f"{tag}_norm:{k}"])
+                assert abs(np.sqrt((flat ** 2).sum()) - ref_norm) < 1e-3 * ref_norm, (tag, k)
