@@ -11,6 +11,8 @@ namespace {
 constexpr int NT = 256;
 constexpr int STH = 8, STW = 32;  // wgrad tile of conv_small
 constexpr int SFH = 16;           // forward tile SFH x STW = conv3x3 forward tiling (BN stats rows agree)
+constexpr int SCI = 8;            // max input channels of the direct conv (enc1.0: in_ch; fusion_head.0: 2K)
+constexpr int SJT = (SCI * 9 + 15) / 16;  // 16-column im2col MFMA tiles of its wgrad (5)
 
 bool act_ok(const eunet_act* a) {
   return a && a->ptr && a->n > 0 && a->h > 0 && a->w > 0 && a->c > 0 && a->coff >= 0 &&
@@ -23,7 +25,7 @@ bool vec_ok(const eunet_act* a) {
 }
 
 // ---------------------------------------------------------------------------
-// enc1.0: direct 3x3 conv for Cin <= 4, 64 output channels per block.y
+// enc1.0 / fusion_head.0: direct 3x3 conv for Cin <= 8, 64 output channels per block.y
 // ---------------------------------------------------------------------------
 struct SmallArgs {
   const void* x; int N, H, W, xct, xco, cin;
@@ -37,8 +39,8 @@ struct SmallArgs {
 // its 8 pixels, Chan-combined across lanes and waves (no transposes)
 template <typename T>
 __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
-  __shared__ float xs[(SFH + 2) * (STW + 2) * 4];
-  __shared__ __attribute__((aligned(16))) float wsm[4 * 9 * 64];  // [ci*9+t][64 co]
+  __shared__ float xs[(SFH + 2) * (STW + 2) * SCI];
+  __shared__ __attribute__((aligned(16))) float wsm[SCI * 9 * 64];  // [ci*9+t][64 co]
   __shared__ float wn_s[4], wm_s[4][64], wq_s[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int tile = blockIdx.x, tpi = a.tx * a.ty;
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
     float v = 0.f;
     if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
       v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
-    xs[hp * 4 + ci] = v;
+    xs[hp * SCI + ci] = v;
   }
   for (int i = tid; i < 64 * cin * 9; i += NT) {
     const int co = i / (cin * 9), r = i - co * cin * 9;
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
-        const float v = xs[((r + ky) * (STW + 2) + c + kx) * 4 + ci];
+        const float v = xs[((r + ky) * (STW + 2) + c + kx) * SCI + ci];
         const float4 w0 = *(const float4*)(wsm + (ci * 9 + t) * 64 + 8 * g);
         const float4 w1 = *(const float4*)(wsm + (ci * 9 + t) * 64 + 8 * g + 4);
         acc[0] = fmaf(w0.x, v, acc[0]); acc[1] = fmaf(w0.y, v, acc[1]);
@@ -154,22 +156,23 @@ struct SmallWgArgs {
   int tx, ty, ntiles, per_split;
 };
 
-// first-conv wgrad as MFMA: dW[co][ci*9+t] = sum_p dY[p][co] im2col(x)[p][ci*9+t];
-// im2col (<= 27 of 32 columns) and the dY tile are staged in LDS per 8x32 tile
+// direct-conv wgrad as MFMA: dW[co][ci*9+t] = sum_p dY[p][co] im2col(x)[p][ci*9+t];
+// im2col (cin*9 columns padded to njt*16 <= 80) and the dY tile are staged in LDS per 8x32 tile
 template <typename T>
 __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   constexpr int E = Vec16<T>::N;
-  __shared__ float xs[(STH + 2) * (STW + 2) * 4];
-  __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];  // dY tile [256 px][64 co]
-  __shared__ __attribute__((aligned(16))) T cs[STH * STW * 32];  // im2col [256 px][32]
+  __shared__ float xs[(STH + 2) * (STW + 2) * SCI];
+  __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];         // dY tile [256 px][64 co]
+  __shared__ __attribute__((aligned(16))) T cs[STH * STW * SJT * 16];  // im2col [256 px][icw]
   __shared__ float dbs[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int split = blockIdx.x, co0 = blockIdx.y * 64;
   const int t_begin = split * a.per_split, t_end = min(a.ntiles, t_begin + a.per_split);
   const int tpi = a.tx * a.ty, cin = a.cin;
-  f32x4 acc[2];
-  acc[0] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  acc[1] = acc[0];
+  const int njt = (cin * 9 + 15) / 16, icw = njt * 16;  // im2col columns (LDS row stride)
+  f32x4 acc[SJT];
+#pragma unroll
+  for (int j = 0; j < SJT; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       float v = 0.f;
       if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
         v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
-      xs[hp * 4 + ci] = v;
+      xs[hp * SCI + ci] = v;
     }
     for (int id = tid; id < STH * STW * 64 / E; id += NT) {
       const int px = id / (64 / E), u = id - px * (64 / E);
@@ -194,13 +197,13 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       *(uint4*)(gs + px * 64 + u * E) = v;
     }
     __syncthreads();
-    for (int id = tid; id < STH * STW * 32; id += NT) {
-      const int px = id >> 5, j = id & 31;
+    for (int id = tid; id < STH * STW * icw; id += NT) {
+      const int px = id / icw, j = id - px * icw;
       float v = 0.f;
       if (j < cin * 9) {
         const int ci = j / 9, t = j - ci * 9;
         const int ky = t / 3, kx = t - ky * 3;
-        v = xs[((px / STW + ky) * (STW + 2) + (px % STW) + kx) * 4 + ci];
+        v = xs[((px / STW + ky) * (STW + 2) + (px % STW) + kx) * SCI + ci];
       }
       Elem<T>::st(cs + id, v);
     }
@@ -215,9 +218,10 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
         const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)gs + ((pxa + 4) * 64 + cw + 4 * p4) * 2));
         const bf16x8 af = cat_bf16x4(alo, ahi);
 #pragma unroll
-        for (int jt = 0; jt < 2; ++jt) {
-          const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + (pxa * 32 + jt * 16 + 4 * p4) * 2));
-          const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + ((pxa + 4) * 32 + jt * 16 + 4 * p4) * 2));
+        for (int jt = 0; jt < SJT; ++jt) {
+          if (jt >= njt) break;
+          const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + (pxa * icw + jt * 16 + 4 * p4) * 2));
+          const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, (char*)cs + ((pxa + 4) * icw + jt * 16 + 4 * p4) * 2));
           acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, cat_bf16x4(blo, bhi), acc[jt], 0, 0, 0);
         }
       }
@@ -227,15 +231,17 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
         const int px = ks * 4 + kq;
         const float av = ((const float*)gs)[px * 64 + cw + i];
 #pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ((const float*)cs)[px * 32 + jt * 16 + i], acc[jt], 0, 0, 0);
+        for (int jt = 0; jt < SJT; ++jt) {
+          if (jt >= njt) break;
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ((const float*)cs)[px * icw + jt * 16 + i], acc[jt], 0, 0, 0);
+        }
       }
     }
   }
   float* out = a.dw + (long long)split * a.cout * 9 * cin;
   const int g = lane >> 4, li = lane & 15;
 #pragma unroll
-  for (int jt = 0; jt < 2; ++jt)
+  for (int jt = 0; jt < SJT; ++jt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int co = co0 + wv * 16 + g * 4 + e, j = jt * 16 + li;
@@ -542,7 +548,8 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
 
 // gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [gamma xhat + beta > 0], folded per
 // channel into pre = y P + Q and gy = K1 g' + y K2 + K3.  A thread keeps one 16-byte channel
-// unit (256 % U == 0) with its coefficients in registers and strides over pixels.
+// unit with its coefficients in registers and strides over pixels; the block holds
+// floor(256 / U) pixels x U units (base_ch 96 -> U = 12, 21 pixels per step).
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
     k2[j] = -k1[j] * is * dg;
     k3[j] = -k1[j] * fmaf(off, dg, dbeta[c + j] * inv_n);
   }
-  const int ppb = 256 / U;  // pixels per block per step
+  const int ppb = blockDim.x / U;  // pixels per block per step (blockDim.x = ppb * U)
   for (long long p = (long long)blockIdx.x * ppb + threadIdx.x / U; p < P; p += (long long)gridDim.x * ppb) {
     float gf[E], yf[E], o[E];
     Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
@@ -817,7 +824,7 @@ int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
 int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, const eunet_act* y, float* stats,
                          void* stream) {
   EUNET_REQUIRE(act_ok(x) && act_ok(y) && w, "conv_small_fwd: bad args");
-  EUNET_REQUIRE(x->c <= 4 && x->dtype == y->dtype, "conv_small_fwd: Cin <= 4 and equal dtypes required");
+  EUNET_REQUIRE(x->c <= SCI && x->dtype == y->dtype, "conv_small_fwd: Cin <= 8 and equal dtypes required");
   EUNET_REQUIRE(x->n == y->n && x->h == y->h && x->w == y->w, "conv_small_fwd: spatial mismatch");
   SmallArgs a;
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
@@ -846,7 +853,7 @@ int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
 int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
                            void* stream) {
   EUNET_REQUIRE(act_ok(x) && act_ok(dy) && dw_part && nsplit > 0, "conv_small_wgrad: bad args");
-  EUNET_REQUIRE(x->c <= 4 && x->dtype == dy->dtype, "conv_small_wgrad: Cin <= 4, equal dtypes");
+  EUNET_REQUIRE(x->c <= SCI && x->dtype == dy->dtype, "conv_small_wgrad: Cin <= 8, equal dtypes");
   SmallWgArgs a;
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
   a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
@@ -995,15 +1002,16 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
                 "bn_bwd_apply: mismatch");
   const long long P = (long long)y->n * y->h * y->w;
   const int U = y->c / e16(y->dtype);
-  EUNET_REQUIRE(256 % U == 0, "bn_bwd_apply: 256 must be a multiple of C/%d", e16(y->dtype));
-  const long long nb = (P * U + 255) / 256;
+  EUNET_REQUIRE(U <= 256, "bn_bwd_apply: at most 256 channel units (C <= 256 x %d)", e16(y->dtype));
+  const int bs = (256 / U) * U;
+  const long long nb = (P * U + bs - 1) / bs;
   const unsigned gr = (unsigned)(nb < 4096 ? nb : 4096);
   if (y->dtype == EUNET_BF16)
-    bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
+    bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
         gamma, beta, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff);
   else
-    bn_bwd_apply_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
+    bn_bwd_apply_kernel<float, float><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
         gamma, beta, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff);
   EUNET_LAUNCH_CHECK("bn_bwd_apply");

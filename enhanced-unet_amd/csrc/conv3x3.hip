@@ -42,7 +42,7 @@ template <typename T> struct KCh { static constexpr int v = 4 * Vec16<T>::N; }; 
 
 struct FwdArgs {
   const void* x; int N, H, W, xct, xco, cin;
-  const float* isc; const float* ish;
+  const float* isc; const float* ish; int iss;  // operand transform; iss = per-sample stride (0: shared)
   const void* wp; int cout_pad, nkc;
   const float* bias;
   void* y; int yct, yco, cout;
@@ -53,6 +53,7 @@ struct FwdArgs {
   const void* by; int byct, byco;
   const float* bmean; const float* bistd; const float* bgam; const float* bbet;
   float* bpart;
+  const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
 };
 
 // stage one halo unit (pixel hp, quarter q) of chunk kc into registers
@@ -71,12 +72,13 @@ __device__ __forceinline__ uint4 load_halo_unit(const FwdArgs& a, int n, int y0,
 }
 
 template <typename T>
-__device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int id, int kc, uint4 v, bool ok) {
+__device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int n, int id, int kc, uint4 v,
+                                                bool ok) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   if (id >= A_UNITS) return;
   const int hp = id >> 2, q = id & 3;
   if (ok && a.isc != nullptr) {
-    const int c = kc * KC + q * E;
+    const int c = kc * KC + q * E + n * a.iss;
     float f[E];
     Vec16<T>::unpack(v, f);
 #pragma unroll
@@ -139,13 +141,13 @@ __device__ __forceinline__ u32x4 fwd_load_unit(const FwdArgs& a, int n, int y0, 
 }
 
 template <typename T>
-__device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int id, int kc, u32x4 v, bool ok) {
+__device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int n, int id, int kc, u32x4 v, bool ok) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   int hp, q;
   fwd_unit(id, hp, q);
   if (hp >= FHPX) return;
   if (ok && a.isc != nullptr) {
-    const int c = kc * KC + q * E;
+    const int c = kc * KC + q * E + n * a.iss;
     float f[E];
     Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
 #pragma unroll
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   do {                                                                                        \
     char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
     _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        fwd_store_unit<T>(a, As_, lt + i * NLT, (KC_), ra[i], rok[i]);                        \
+        fwd_store_unit<T>(a, As_, n, lt + i * NLT, (KC_), ra[i], rok[i]);                     \
   } while (0)
 #define CONV_LWRITE_B(BUF_, I0_, I1_)                                                         \
   do {                                                                                        \
@@ -350,10 +352,11 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   for (int nt = 0; nt < 4; ++nt) {
     const int co = co0 + nt * 16 + li;
     const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
+    const float gv = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[mt][nt][i] += bv;
+      for (int i = 0; i < 4; ++i) acc[mt][nt][i] = (acc[mt][nt][i] + bv) * gv;
   }
   constexpr int PASS_PX = PROWS * FTW;
   float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
@@ -533,7 +536,7 @@ __global__ void pack_kernel(const float* w, int cout, int cin, int flip, T* wp, 
 // ---------------------------------------------------------------------------
 struct WgArgs {
   const void* x; int N, H, W, xct, xco, cin;
-  const float* isc; const float* ish;
+  const float* isc; const float* ish; int iss;
   const void* dy; int dct, dco, cout;
   float* dw; float* db;
   int tx, ty, ntiles, per_split, nsplit;
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
 
   FwdArgs fa;
   fa.x = a.x; fa.N = a.N; fa.H = a.H; fa.W = a.W; fa.xct = a.xct; fa.xco = a.xco; fa.cin = a.cin;
-  fa.isc = a.isc; fa.ish = a.ish;
+  fa.isc = a.isc; fa.ish = a.ish; fa.iss = a.iss;
 
   constexpr int NACC = (sizeof(T) == 2) ? 18 : 9;
   f32x4 acc[NACC];
@@ -575,7 +578,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
       bool ok;
       const int id = tid + i * NTHR;
       uint4 v = load_halo_unit<T>(fa, n, y0, x0, id, kc, ok);
-      store_halo_unit<T>(fa, As, id, kc, v, ok);
+      store_halo_unit<T>(fa, As, n, id, kc, v, ok);
     }
     // stage dY tile
     for (int id = tid; id < DY_UNITS; id += NTHR) {
@@ -757,9 +760,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         const int c = kc * KCW + oc * 8;
         if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {  // padding stays 0
           float f[8];
+          const int cs = c + n * a.iss;
           Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[cs + j], a.ish[cs + j]), 0.f);
           v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
         }
       }
@@ -924,8 +928,8 @@ int eunet_conv3x3_tiles(const eunet_act* y, int* tiles) {
   return EUNET_OK;
 }
 
-int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in_shift, const void* wp,
-                      const float* bias, const eunet_act* y, float* stats, void* stream) {
+int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in_shift, int in_nstride,
+                      const void* wp, const float* bias, const eunet_act* y, float* stats, void* stream) {
   EUNET_REQUIRE(act_ok(x) && act_ok(y) && wp, "conv3x3_fwd: bad tensors");
   EUNET_REQUIRE(x->dtype == y->dtype, "conv3x3_fwd: dtype mismatch");
   EUNET_REQUIRE(x->n == y->n && x->h == y->h && x->w == y->w, "conv3x3_fwd: spatial mismatch");
@@ -935,13 +939,14 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   EUNET_REQUIRE((in_scale == nullptr) == (in_shift == nullptr), "conv3x3_fwd: scale/shift pair");
   FwdArgs a;
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
-  a.isc = in_scale; a.ish = in_shift;
+  EUNET_REQUIRE(in_nstride == 0 || (in_scale && in_nstride >= x->c), "conv3x3_fwd: in_nstride");
+  a.isc = in_scale; a.ish = in_shift; a.iss = in_nstride;
   a.wp = wp; a.cout_pad = cdiv(y->c, BN) * BN; a.nkc = cdiv(x->c, kchunk(x->dtype));
   a.bias = bias;
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
-  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   return launch_fwd(a, x->dtype, stream);
@@ -949,7 +954,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
 
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const eunet_act* y,
                               const float* mean, const float* invstd, const float* gamma, const float* beta,
-                              float* part, void* stream) {
+                              const float* gscale, float* part, void* stream) {
   EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && act_ok(y) && wp_t && mean && invstd && gamma && beta && part,
                 "conv3x3_dgrad_bnbwd: bad args");
   EUNET_REQUIRE(dy->dtype == gx->dtype && y->dtype == gx->dtype, "conv3x3_dgrad_bnbwd: dtype mismatch");
@@ -962,13 +967,13 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
                 "conv3x3_dgrad_bnbwd: channels/strides must be multiples of %d", E);
   FwdArgs a;
   a.x = dy->ptr; a.N = dy->n; a.H = dy->h; a.W = dy->w; a.xct = dy->ctot; a.xco = dy->coff; a.cin = dy->c;
-  a.isc = nullptr; a.ish = nullptr;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0;
   a.wp = wp_t; a.cout_pad = cdiv(gx->c, BN) * BN; a.nkc = cdiv(dy->c, kchunk(dy->dtype));
   a.bias = nullptr;
   a.y = gx->ptr; a.yct = gx->ctot; a.yco = gx->coff; a.cout = gx->c;
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
-  a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part;
+  a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
   return launch_fwd(a, dy->dtype, stream);
 }
 
@@ -988,8 +993,8 @@ int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsp
   return EUNET_OK;
 }
 
-int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* in_shift, const eunet_act* dy,
-                        float* dw_part, float* db_part, int nsplit, void* stream) {
+int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* in_shift, int in_nstride,
+                        const eunet_act* dy, float* dw_part, float* db_part, int nsplit, void* stream) {
   EUNET_REQUIRE(act_ok(x) && act_ok(dy) && dw_part && nsplit > 0, "conv3x3_wgrad: bad args");
   EUNET_REQUIRE(x->dtype == dy->dtype, "conv3x3_wgrad: dtype mismatch");
   EUNET_REQUIRE(x->n == dy->n && x->h == dy->h && x->w == dy->w, "conv3x3_wgrad: spatial mismatch");
@@ -999,7 +1004,8 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
                 "conv3x3_wgrad: channels/strides must be multiples of %d", E);
   WgArgs a;
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
-  a.isc = in_scale; a.ish = in_shift;
+  EUNET_REQUIRE(in_nstride == 0 || (in_scale && in_nstride >= x->c), "conv3x3_wgrad: in_nstride");
+  a.isc = in_scale; a.ish = in_shift; a.iss = in_nstride;
   a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
   a.dw = dw_part; a.db = db_part;
   a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;

@@ -31,10 +31,10 @@ SIGNATURES = {
     "eunet_conv3x3_packed_bytes": [c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_conv3x3_pack": [_f, c_int, c_int, c_int, _f, c_int, c_void_p],
     "eunet_conv3x3_tiles": [_P, POINTER(c_int)],
-    "eunet_conv3x3_fwd": [_P, _f, _f, _f, _f, _P, _f, c_void_p],
-    "eunet_conv3x3_dgrad_bnbwd": [_P, _f, _P, _P, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_conv3x3_fwd": [_P, _f, _f, c_int, _f, _f, _P, _f, c_void_p],
+    "eunet_conv3x3_dgrad_bnbwd": [_P, _f, _P, _P, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_conv3x3_wgrad_splits": [_P, c_int, c_int, POINTER(c_int)],
-    "eunet_conv3x3_wgrad": [_P, _f, _f, _P, _f, _f, c_int, c_void_p],
+    "eunet_conv3x3_wgrad": [_P, _f, _f, c_int, _P, _f, _f, c_int, c_void_p],
     "eunet_wgrad_reduce": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, c_void_p],
     "eunet_conv_small_fwd": [_P, _f, _f, _P, _f, c_void_p],
     "eunet_conv_small_wgrad_splits": [_P, POINTER(c_int)],
@@ -68,6 +68,22 @@ SIGNATURES = {
     "eunet_softmax_crop": [_f, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _f, c_void_p],
     "eunet_accumulate": [_f, _f, c_int64, c_int, c_float, c_void_p],
     "eunet_probs_to_mask": [_f, c_int, c_int, c_int, _f, _f, c_void_p],
+    "eunet_fusion_tiles": [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)],
+    "eunet_gate_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_gate_mid_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_gate_out_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _P, c_void_p],
+    "eunet_fusion_out_fwd": [_f, _f, c_int, _P, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_fusion_out_bwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_gate_bwd1": [_f, _f, c_int, _P, _f, _f, _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_gate_bwd2": [c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
+                        _f, c_void_p],
+    "eunet_gate_bwd3": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
+                        _f, _f, c_void_p],
+    "eunet_dropout_affine": [_f, _f, _f, c_int, c_int, c_float, _f, _f, _f, c_void_p],
+    "eunet_consistency_tiles": [c_int, c_int, POINTER(c_int)],
+    "eunet_consistency_fwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, c_void_p],
+    "eunet_consistency_bwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, _f, _f,
+                              c_void_p],
 }
 STRING_FNS = ("eunet_version", "eunet_last_error")
 

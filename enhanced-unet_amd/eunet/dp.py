@@ -26,6 +26,9 @@ from .engine import BLOCKS
 
 
 def backward_order(model) -> List[str]:
+    custom = getattr(model, "backward_param_order", None)
+    if custom is not None and custom() is not None:  # dual-branch model (eunet.dual)
+        return custom()
     names = [n for n, _ in model.named_parameters()]
     order = [n for n in names if n.startswith("enhance.")]
     order += [n for n in names if n.startswith("model.dec1.")]

@@ -56,8 +56,13 @@ def _e(shape, dtype, device):
 
 
 class UNetEngine:
-    def __init__(self, model):
+    """One BasicUNet trunk (+ the enhance head for the single-branch model).  prefix names the
+    trunk's parameters in the owning module ('model.' for EnhancedUNet, 'unetpp.' / 'deeplab.'
+    for the branches of the dual-branch model)."""
+
+    def __init__(self, model, prefix: str = "model."):
         self.m = model
+        self.prefix = prefix
         self.base = model.base_ch
         self.K = model.num_classes
         self.cin = model.in_channels
@@ -89,7 +94,7 @@ class UNetEngine:
         return _e(tiles * (2 * C + 1), torch.float32, y.device), tiles
 
     def _block_fwd(self, nm, X: ops.Act, training, P, B, small: bool):
-        p = f"model.{nm}"
+        p = f"{self.prefix}{nm}"
         N, H, W = X.n, X.h, X.w
         C = P[p + ".0.weight"].shape[0]
         dev = P[p + ".0.weight"].device
@@ -112,6 +117,27 @@ class UNetEngine:
     def forward(self, x: torch.Tensor, training: bool, want: str = "logits"):
         """x [N,Cin,H,W] fp32 -> logits [N,K,H,W] ('logits', the 2x2 mean of the
         2H output) or out2h [N,K,2H,2W] ('out2h', the reference forward)."""
+        S = self.forward_trunk(x, training)
+        P, B = self._P(), self._B()
+        N, H, W, K, dev = S["N"], S["H"], S["W"], self.K, x.device
+        z = S["z"]
+        hws = _e(ops.head_workspace_bytes(N, H, W, K, self.dtype), torch.uint8, dev)
+        hmean = _e(64, torch.float32, dev) if training else None
+        hinv = _e(64, torch.float32, dev) if training else None
+        out2h = _e((N, K, 2 * H, 2 * W), torch.float32, dev) if want == "out2h" else None
+        logits = _e((N, K, H, W), torch.float32, dev) if want == "logits" else None
+        ops.head_fwd(z, N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
+                     P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), P["enhance.3.bias"],
+                     training, BN_EPS, BN_MOMENTUM, B["enhance.1.running_mean"], B["enhance.1.running_var"],
+                     hmean, hinv, out2h, logits, hws, dtype=self.dtype)
+        if training:
+            B["enhance.1.num_batches_tracked"].add_(1)
+        S.update(hmean=hmean, hinv=hinv, want=want)
+        return (logits if want == "logits" else out2h), S
+
+    def forward_trunk(self, x: torch.Tensor, training: bool):
+        """BasicUNet trunk up to z = dec1(d2) at input resolution, NHWC fp32 [N,H,W,K]
+        (models.py:227-237 with dec1 commuted before the final upsample)."""
         if not x.is_cuda:
             raise EunetError("EnhancedUNet (eunet) runs on the GPU only; no CPU fallback")
         N, Cin, H, W = x.shape
@@ -160,25 +186,13 @@ class UNetEngine:
         s = S["dec2"]
         z = _e((N, H, W, K), torch.float32, dev)
         ops.bnrelu_conv1x1(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
-                           P["model.dec1.weight"].reshape(K, b).contiguous(), P["model.dec1.bias"], K, z)
-        S["z"] = z
-        hws = _e(ops.head_workspace_bytes(N, H, W, K, self.dtype), torch.uint8, dev)
-        hmean = _e(64, torch.float32, dev) if training else None
-        hinv = _e(64, torch.float32, dev) if training else None
-        out2h = _e((N, K, 2 * H, 2 * W), torch.float32, dev) if want == "out2h" else None
-        logits = _e((N, K, H, W), torch.float32, dev) if want == "logits" else None
-        ops.head_fwd(z, N, H, W, K, P["enhance.0.weight"], P["enhance.0.bias"], P["enhance.1.weight"],
-                     P["enhance.1.bias"], P["enhance.3.weight"].reshape(K, 64).contiguous(), P["enhance.3.bias"],
-                     training, BN_EPS, BN_MOMENTUM, B["enhance.1.running_mean"], B["enhance.1.running_var"],
-                     hmean, hinv, out2h, logits, hws, dtype=self.dtype)
-        if training:
-            B["enhance.1.num_batches_tracked"].add_(1)
-        S.update(hmean=hmean, hinv=hinv, N=N, H=H, W=W, want=want)
-        return (logits if want == "logits" else out2h), S
+                           P[self.prefix + "dec1.weight"].reshape(K, b).contiguous(), P[self.prefix + "dec1.bias"], K, z)
+        S.update(z=z, N=N, H=H, W=W)
+        return S
 
     # --------------------------------------------------------------- backward
     def _block_bwd(self, nm, G: torch.Tensor, S, P, sink: GradSink, need_gx: bool, small: bool):
-        p = f"model.{nm}"
+        p = f"{self.prefix}{nm}"
         s = S[nm]
         ya, yb, bna, bnb, X = s["ya"], s["yb"], s["bna"], s["bnb"], s["X"]
         N, H, W, C = yb.shape
@@ -259,19 +273,28 @@ class UNetEngine:
                      glog, gout2h, gz, gw1, gb1, gg, gbt, gw2, gb2, hws, dtype=dt)
         sink.ready(["enhance.0.weight", "enhance.0.bias", "enhance.1.weight", "enhance.1.bias",
                     "enhance.3.weight", "enhance.3.bias"])
+        return self.backward_trunk(S, gz, sink)
+
+    def backward_trunk(self, S, gz: torch.Tensor, sink: GradSink):
+        """Backward of forward_trunk from gz = d loss / d z (NHWC fp32 [N,H,W,K])."""
+        P = self._P()
+        N, H, W, K, b = S["N"], S["H"], S["W"], self.K, self.base
+        dev, dt = gz.device, self.dtype
+        ch = [b, 2 * b, 4 * b, 8 * b]
+        pre = self.prefix
         # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))
         s2 = S["dec2"]
         gd2 = torch.empty_like(s2["yb"])
         yb_act = ops.act(s2["yb"])
         tiles = ops.conv1x1_bwd_tiles(yb_act)
         part = _e(tiles * (K * b + K), torch.float32, dev)
-        ops.conv1x1_bwd(yb_act, s2["bnb"]["scale"], s2["bnb"]["shift"], P["model.dec1.weight"].reshape(K, b).contiguous(),
+        ops.conv1x1_bwd(yb_act, s2["bnb"]["scale"], s2["bnb"]["shift"], P[pre + "dec1.weight"].reshape(K, b).contiguous(),
                         K, gz, ops.act(gd2), part)
         red = _e(K * b + K, torch.float32, dev)
         ops.colsum(part, tiles, K * b + K, red)
-        sink.slot("model.dec1.weight", (K, b, 1, 1)).copy_(red[:K * b].view(K, b, 1, 1))
-        sink.slot("model.dec1.bias", (K,)).copy_(red[K * b:])
-        sink.ready(["model.dec1.weight", "model.dec1.bias"])
+        sink.slot(pre + "dec1.weight", (K, b, 1, 1)).copy_(red[:K * b].view(K, b, 1, 1))
+        sink.slot(pre + "dec1.bias", (K,)).copy_(red[K * b:])
+        sink.ready([pre + "dec1.weight", pre + "dec1.bias"])
         # ---- decoder
         g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False)
         del gd2

@@ -23,6 +23,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from .dual import DualEngine, DualFunction, dual_backward_order
 from .engine import UNetEngine, UNetFunction
 
 _DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
@@ -62,7 +63,8 @@ class UNet(nn.Module):
 class EnhancedUNet(nn.Module):
     """Enhanced U-Net (reference fallback definition) on the MI355X engine."""
 
-    def __init__(self, num_classes: int = 3, *, in_channels: int = 3, base_ch: int = 64, dtype: str = "fp32"):
+    def __init__(self, num_classes: int = 3, *, in_channels: int = 3, base_ch: int = 64, dtype: str = "fp32",
+                 dual_branch: bool = False):
         super().__init__()
         if not 1 <= num_classes <= 3:
             raise ValueError("num_classes must be 1..3 (the reference loss tables have 3 classes)")
@@ -74,19 +76,54 @@ class EnhancedUNet(nn.Module):
         self.in_channels = in_channels
         self.base_ch = base_ch
         self.compute_dtype = _DTYPES[dtype]
-        self.model = UNet(num_classes, in_channels=in_channels, base_ch=base_ch).model
-        self.enhance = nn.Sequential(nn.Conv2d(num_classes, 64, 3, padding=1), nn.BatchNorm2d(64),
-                                     nn.ReLU(inplace=True), nn.Conv2d(64, num_classes, 1))
+        self.dual_branch = dual_branch
         self._aux_outputs = None
-        self._engine = UNetEngine(self)
         self.grad_sink_factory = None  # set by eunet.dp for bucketed all-reduce overlap
+        if dual_branch:  # the reference's SMP path (models.py:253-302), build-defined branches
+            k2 = 2 * num_classes
+            self.unetpp = _UNetParams(in_channels, base_ch, num_classes)
+            self.deeplab = _UNetParams(in_channels, base_ch, num_classes)
+            self.attention_gate = nn.Sequential(
+                nn.Conv2d(k2, k2 // 2, 3, padding=1, bias=False), nn.BatchNorm2d(k2 // 2), nn.GELU(),
+                nn.Conv2d(k2 // 2, k2, 1, bias=False), nn.BatchNorm2d(k2), nn.Sigmoid())
+            self.fusion_head = nn.Sequential(
+                nn.Conv2d(k2, 256, 3, padding=1, bias=False), nn.BatchNorm2d(256), nn.ReLU(inplace=True),
+                nn.Dropout2d(0.2),
+                nn.Conv2d(256, 128, 3, padding=1, bias=False), nn.BatchNorm2d(128), nn.ReLU(inplace=True),
+                nn.Dropout2d(0.15),
+                nn.Conv2d(128, 64, 3, padding=1, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True),
+                nn.Conv2d(64, num_classes, 1))
+            self.fusion_residual = nn.Conv2d(k2, num_classes, 1)
+            self._engine = DualEngine(self)
+        else:  # SMP-absent fallback (models.py:304-314)
+            self.model = UNet(num_classes, in_channels=in_channels, base_ch=base_ch).model
+            self.enhance = nn.Sequential(nn.Conv2d(num_classes, 64, 3, padding=1), nn.BatchNorm2d(64),
+                                         nn.ReLU(inplace=True), nn.Conv2d(64, num_classes, 1))
+            self._engine = UNetEngine(self)
 
     def set_dtype(self, dtype: str):
         self.compute_dtype = _DTYPES[dtype]
         self._engine.dtype = self.compute_dtype
         return self
 
+    def backward_param_order(self):
+        """Parameter names in gradient-production order (eunet.dp buckets)."""
+        return dual_backward_order(self) if self.dual_branch else None
+
+    def _run_dual(self, x: torch.Tensor) -> torch.Tensor:
+        """models.py:317-333: fused logits [B,K,H,W]; _aux_outputs = branch logits."""
+        if self.training and torch.is_grad_enabled():
+            out, aux_a, aux_b = DualFunction.apply(x, self._engine, self.grad_sink_factory,
+                                                   *[p for _, p in self.named_parameters()])
+        else:
+            with torch.no_grad():
+                out, aux_a, aux_b, _ = self._engine.forward(x, training=self.training)
+        self._aux_outputs = {"unetpp": aux_a, "deeplab": aux_b}
+        return out
+
     def _run(self, x: torch.Tensor, want: str) -> torch.Tensor:
+        if self.dual_branch:
+            return self._run_dual(x)
         self._aux_outputs = None
         if self.training:
             if torch.is_grad_enabled():

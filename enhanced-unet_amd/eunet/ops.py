@@ -68,24 +68,25 @@ def conv3x3_tiles(y_act: Act) -> int:
     return t.value
 
 
-def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None):
+def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None, nstride=0):
+    """nstride > 0: scale/shift are per-sample [N][nstride] (BN+ReLU+Dropout2d folded)."""
     flops = 2.0 * 9 * x.c * y.c * x.n * x.h * x.w
     esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
     # algorithmic HBM bytes: read x once, write y once, read the packed weights once
     nbytes = float(esz * x.n * x.h * x.w * (x.c + y.c) + wp.numel() * wp.element_size())
     with kprof.timed("conv3x3_fwd", flops, nbytes):
-        call("eunet_conv3x3_fwd", ctypes.byref(x), _ptr(scale), _ptr(shift), _ptr(wp), _ptr(bias),
+        call("eunet_conv3x3_fwd", ctypes.byref(x), _ptr(scale), _ptr(shift), int(nstride), _ptr(wp), _ptr(bias),
              ctypes.byref(y), _ptr(stats), _stream())
 
 
-def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, gamma, beta, part):
+def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, gamma, beta, part, gscale=None):
     """dgrad + the BN-backward partial sums of the layer it feeds (see eunet.h)."""
     flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
     esz = 2 if dy.dtype == _lib.EUNET_BF16 else 4
     nbytes = float(esz * dy.n * dy.h * dy.w * (dy.c + 2 * gx.c) + wp_t.numel() * wp_t.element_size())
     with kprof.timed("conv3x3_fwd", flops, nbytes):
         call("eunet_conv3x3_dgrad_bnbwd", ctypes.byref(dy), _ptr(wp_t), ctypes.byref(gx), ctypes.byref(y), _ptr(mean),
-             _ptr(invstd), _ptr(gamma), _ptr(beta), _ptr(part), _stream())
+             _ptr(invstd), _ptr(gamma), _ptr(beta), _ptr(gscale), _ptr(part), _stream())
 
 
 def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
@@ -94,10 +95,11 @@ def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
     return s.value
 
 
-def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=None):
+def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=None, nstride=0):
     flops = 2.0 * 9 * x.c * dy.c * x.n * x.h * x.w
     with kprof.timed("conv3x3_wgrad", flops):
-        call("eunet_conv3x3_wgrad", ctypes.byref(x), _ptr(scale), _ptr(shift), ctypes.byref(dy), _ptr(dw_part),
+        call("eunet_conv3x3_wgrad", ctypes.byref(x), _ptr(scale), _ptr(shift), int(nstride), ctypes.byref(dy),
+             _ptr(dw_part),
              _ptr(db_part), nsplit, _stream())
 
 
@@ -278,3 +280,81 @@ def probs_to_mask(probs):
     ws = torch.empty(2, dtype=torch.int64, device=probs.device)
     call("eunet_probs_to_mask", _ptr(probs), k, h, w, _ptr(mask), _ptr(ws), _stream())
     return mask
+
+
+# ---- dual-branch fusion (fusion.hip) -------------------------------------------------
+def fusion_tiles(n, h, w):
+    t, gt = c_int(), c_int()
+    call("eunet_fusion_tiles", n, h, w, ctypes.byref(t), ctypes.byref(gt))
+    return t.value, gt.value
+
+
+def gate_fwd(za, zb, k, w1, a, st1, aux_a, aux_b):
+    n, h, w, _ = za.shape
+    call("eunet_gate_fwd", _ptr(za), _ptr(zb), n, h, w, k, _ptr(w1), _ptr(a), _ptr(st1), _ptr(aux_a), _ptr(aux_b),
+         _stream())
+
+
+def gate_mid_fwd(za, zb, k, a, sc1, sh1, w2, b, st2):
+    n, h, w, _ = za.shape
+    call("eunet_gate_mid_fwd", _ptr(za), _ptr(zb), n, h, w, k, _ptr(a), _ptr(sc1), _ptr(sh1), _ptr(w2), _ptr(b),
+         _ptr(st2), _stream())
+
+
+def gate_out_fwd(za, zb, k, b, sc2, sh2, f2: Act):
+    n, h, w, _ = za.shape
+    call("eunet_gate_out_fwd", _ptr(za), _ptr(zb), n, h, w, k, _ptr(b), _ptr(sc2), _ptr(sh2), ctypes.byref(f2),
+         _stream())
+
+
+def fusion_out_fwd(za, zb, k, y3: Act, sc3, sh3, w11, b11, b, sc2, sh2, wr, br, out):
+    call("eunet_fusion_out_fwd", _ptr(za), _ptr(zb), k, ctypes.byref(y3), _ptr(sc3), _ptr(sh3), _ptr(w11), _ptr(b11),
+         _ptr(b), _ptr(sc2), _ptr(sh2), _ptr(wr), _ptr(br), _ptr(out), _stream())
+
+
+def fusion_out_bwd(za, zb, k, gout, b, sc2, sh2, wr, gz, gf2res, part):
+    n, h, w, _ = za.shape
+    call("eunet_fusion_out_bwd", _ptr(za), _ptr(zb), n, h, w, k, _ptr(gout), _ptr(b), _ptr(sc2), _ptr(sh2),
+         _ptr(wr), _ptr(gz), _ptr(gf2res), _ptr(part), _stream())
+
+
+def gate_bwd1(za, zb, k, gf2conv: Act, gf2res, b, mean2, istd2, gam2, bet2, gffd, gbhat, part):
+    call("eunet_gate_bwd1", _ptr(za), _ptr(zb), k, ctypes.byref(gf2conv), _ptr(gf2res), _ptr(b), _ptr(mean2),
+         _ptr(istd2), _ptr(gam2), _ptr(bet2), _ptr(gffd), _ptr(gbhat), _ptr(part), _stream())
+
+
+def gate_bwd2(n, h, w, k, gbhat, b, mean2, istd2, gam2, dbet2, dgam2, a, mean1, istd1, gam1, bet1, w2, gabn, part):
+    call("eunet_gate_bwd2", n, h, w, k, _ptr(gbhat), _ptr(b), _ptr(mean2), _ptr(istd2), _ptr(gam2), _ptr(dbet2),
+         _ptr(dgam2), _ptr(a), _ptr(mean1), _ptr(istd1), _ptr(gam1), _ptr(bet1), _ptr(w2), _ptr(gabn), _ptr(part),
+         _stream())
+
+
+def gate_bwd3(za, zb, k, gabn, a, mean1, istd1, gam1, dbet1, dgam1, w1, gffd, gaux_a, gaux_b, gz_a, gz_b, part):
+    n, h, w, _ = za.shape
+    call("eunet_gate_bwd3", _ptr(za), _ptr(zb), n, h, w, k, _ptr(gabn), _ptr(a), _ptr(mean1), _ptr(istd1),
+         _ptr(gam1), _ptr(dbet1), _ptr(dgam1), _ptr(w1), _ptr(gffd), _ptr(gaux_a), _ptr(gaux_b), _ptr(gz_a),
+         _ptr(gz_b), _ptr(part), _stream())
+
+
+def dropout_affine(scale, shift, keep, p, nscale, nshift, gscale=None):
+    n, c = keep.shape
+    call("eunet_dropout_affine", _ptr(scale), _ptr(shift), _ptr(keep), n, c, float(p), _ptr(nscale), _ptr(nshift),
+         _ptr(gscale), _stream())
+
+
+def consistency_tiles(h, w):
+    t = c_int()
+    call("eunet_consistency_tiles", h, w, ctypes.byref(t))
+    return t.value
+
+
+def consistency_fwd(fused, b0, b1, c0, c1, part, loss):
+    n, k, h, w = fused.shape
+    call("eunet_consistency_fwd", _ptr(fused), _ptr(b0), _ptr(b1), n, k, h, w, float(c0), float(c1), _ptr(part),
+         _ptr(loss), _stream())
+
+
+def consistency_bwd(fused, b0, b1, c0, c1, gloss, gfused, g0, g1):
+    n, k, h, w = fused.shape
+    call("eunet_consistency_bwd", _ptr(fused), _ptr(b0), _ptr(b1), n, k, h, w, float(c0), float(c1), _ptr(gloss),
+         _ptr(gfused), _ptr(g0), _ptr(g1), _stream())

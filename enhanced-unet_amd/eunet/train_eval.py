@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .losses import combined_loss
+from .losses import combined_loss, consistency_loss
 from .models import EnhancedUNet
 
 
@@ -77,6 +77,20 @@ class Trainer:
     def tversky_loss(self, pred, target, num_classes=3, alpha=0.7):
         return combined_loss(pred, target, return_parts=True)[1][:, 2].mean()
 
+    def aux_loss(self, fused, aux_outputs, masks):
+        """Batched train_eval.py:326-337 with _apply_auxiliary_supervision (:199-234):
+        (1/B) sum_i [CL(fused_i) + sum_b w_b (CL(branch_b,i) + consistency_weight MSE(p_b,i, p_f,i))]."""
+        loss = combined_loss(fused, masks)
+        if not aux_outputs or not self.aux_branch_weights:
+            return loss
+        for name, w in self.aux_branch_weights.items():
+            loss = loss + w * combined_loss(aux_outputs[name], masks)
+        if self.consistency_weight > 0:
+            (n0, w0), (n1, w1) = list(self.aux_branch_weights.items())
+            loss = loss + consistency_loss(fused, aux_outputs[n0], aux_outputs[n1], self.consistency_weight * w0,
+                                           self.consistency_weight * w1)
+        return loss
+
     # ---- the hot loop ----------------------------------------------------------
     @staticmethod
     def _masks(batch, device, h_pad, w_pad):
@@ -104,12 +118,17 @@ class Trainer:
         self.optimizer.zero_grad(set_to_none=True)
         if self.dp is not None:
             self.dp.before_forward()
-        if isinstance(self.model, EnhancedUNet):
-            logits = self.model.forward_lowres(images)
+        if isinstance(self.model, EnhancedUNet) and self.model.dual_branch:
+            # SMP-path model: fused + branch outputs at mask size (train_eval.py:255-257, 326-335)
+            fused = self.model(images)
+            loss = self.aux_loss(fused, self.model.get_aux_outputs(), masks)
         else:
-            out = self.model(images)
-            logits = F.interpolate(out, size=masks.shape[-2:], mode="bilinear", align_corners=False)
-        loss = combined_loss(logits, masks)
+            if isinstance(self.model, EnhancedUNet):
+                logits = self.model.forward_lowres(images)
+            else:
+                out = self.model(images)
+                logits = F.interpolate(out, size=masks.shape[-2:], mode="bilinear", align_corners=False)
+            loss = combined_loss(logits, masks)
         loss.backward()
         if self.dp is not None:
             self.dp.after_backward()

@@ -61,31 +61,37 @@ int eunet_conv3x3_pack(const float* w, int cout, int cin, int transpose_flip, vo
 int eunet_conv3x3_tiles(const eunet_act* y, int* tiles);
 /* y = conv(t(x)) + bias, t = relu(x*in_scale+in_shift) per input channel when
  * in_scale != NULL (the preceding BN+ReLU fused into the operand load, zero
- * padding applied after the transform).  stats (nullable): [tiles][2][cout]
+ * padding applied after the transform).  in_nstride = 0: one [cin] scale/shift
+ * pair; > 0: per-sample pairs at in_scale + n*in_nstride (a BN+ReLU followed by a
+ * Dropout2d keep-mask/(1-p), models.py:287,291, folded into the affine).  stats (nullable): [tiles][2][cout]
  * per-tile (sum, M2) plus [tiles] counts appended after 2*cout*tiles floats. */
 int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in_shift,
-                      const void* wp, const float* bias, const eunet_act* y, float* stats,
+                      int in_nstride, const void* wp, const float* bias, const eunet_act* y, float* stats,
                       void* stream);
 /* dgrad (wp_t packed with transpose_flip) fused with the reduction half of the
  * BatchNorm backward of the layer whose output gradient it produces (autograd of
  * models.py:220-221, BN+ReLU after the conv): y = that layer's pre-BN output,
  * part [tiles][2][gx.c] = per-tile (sum g', sum g' xhat), g' = gx [gamma xhat +
  * beta > 0], xhat = (y - mean) invstd, gx as stored (rounded).  Replaces
- * conv3x3_fwd(dgrad) + bn_bwd_reduce; colsum(part, tiles, 2C) -> (dbeta, dgamma). */
+ * conv3x3_fwd(dgrad) + bn_bwd_reduce; colsum(part, tiles, 2C) -> (dbeta, dgamma).
+ * gscale (nullable) [N][gx.c]: gx is scaled per sample and channel before the store
+ * and the reduction (the backward of a Dropout2d between the BN+ReLU and this conv). */
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx,
                               const eunet_act* y, const float* mean, const float* invstd,
-                              const float* gamma, const float* beta, float* part, void* stream);
+                              const float* gamma, const float* beta, const float* gscale,
+                              float* part, void* stream);
 /* wgrad (split over pixel tiles): dw_part [nsplit][cout][9][cin] and
  * db_part [nsplit][cout] (db only when db_part != NULL) */
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit);
 int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* in_shift,
-                        const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
+                        int in_nstride, const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
                         void* stream);
 /* reduce split partials -> torch layout dw [cout][cin][taps], db [cout] (fp64 combine) */
 int eunet_wgrad_reduce(const float* dw_part, const float* db_part, int nsplit, int cout, int cin,
                        int taps, float* dw, float* db, void* stream);
 
-/* ---- first conv (models.py:203 enc1.0, Cin = in_channels <= 4): direct ---- */
+/* ---- direct 3x3 conv for Cin <= 8: enc1.0 (models.py:203, Cin = in_channels) and the
+ *      dual-branch fusion_head.0 (models.py:285, Cin = 2K); no bias when bias == NULL */
 int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias,
                          const eunet_act* y, float* stats, void* stream);
 int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit);
@@ -207,6 +213,71 @@ int eunet_accumulate(float* acc, const float* p, long long n, int mode, float co
  * zero dead-cell probability) -> mask int64 [h][w]; counts: 2 int64 of workspace. */
 int eunet_probs_to_mask(const float* probs, int k, int h, int w, int64_t* mask,
                         int64_t* counts, void* stream);
+
+/* ---- dual-branch fusion (fusion.hip) -----------------------------------------
+ * SMP-path EnhancedUNet (models.py:253-302, 316-333): ff = cat(unetpp, deeplab) with the
+ * branch outputs za, zb NHWC fp32 [n,h,w,K]; all gate tensors fp32 NHWC.  Per-tile
+ * partials: BN statistics in the eunet_bn_finalize layout ([tiles][2][C] + counts),
+ * gradient partials [tiles][cols] reduced with eunet_colsum.  K <= 3.
+ * tiles: pixel tiles of the per-pixel kernels; gate_tiles: 16x32 tiles of gate_bwd3. */
+int eunet_fusion_tiles(int n, int h, int w, int* tiles, int* gate_tiles);
+/* attention_gate.0 (3x3, 2K->K, no bias; models.py:280): a [P][K] + BN1 stats; also
+ * copies za, zb to the NCHW aux outputs (_aux_outputs, models.py:329-332) */
+int eunet_gate_fwd(const float* za, const float* zb, int n, int h, int w, int k, const float* w1,
+                   float* a, float* st1, float* aux_a, float* aux_b, void* stream);
+/* GELU(BN1) + attention_gate.3 (1x1 K->2K, models.py:282-283): b [P][2K] + BN2 stats */
+int eunet_gate_mid_fwd(const float* za, const float* zb, int n, int h, int w, int k, const float* a,
+                       const float* sc1, const float* sh1, const float* w2, float* b, float* st2,
+                       void* stream);
+/* Sigmoid(BN2) * ff (models.py:284, 322-323) -> f2 [n,h,w,8] view c = 2K, compute dtype */
+int eunet_gate_out_fwd(const float* za, const float* zb, int n, int h, int w, int k, const float* b,
+                       const float* sc2, const float* sh2, const eunet_act* f2, void* stream);
+/* fusion_head.11 on relu(bn3(y3)) + fusion_residual on f2 (models.py:294, 296, 325-328)
+ * -> out NCHW fp32 [n,K,h,w] */
+int eunet_fusion_out_fwd(const float* za, const float* zb, int k, const eunet_act* y3,
+                         const float* sc3, const float* sh3, const float* w11, const float* b11,
+                         const float* b, const float* sc2, const float* sh2, const float* wr,
+                         const float* br, float* out, void* stream);
+/* backward of the residual + output layout: gz [P][K] (NHWC, for eunet_conv1x1_bwd),
+ * gf2res [P][2K] = Wr^T gout, part [tiles][K*2K + K] = (dWr, dbr) partials */
+int eunet_fusion_out_bwd(const float* za, const float* zb, int n, int h, int w, int k,
+                         const float* gout, const float* b, const float* sc2, const float* sh2,
+                         const float* wr, float* gz, float* gf2res, float* part, void* stream);
+/* gate backward: (1) sigmoid/product: gffd [P][2K], gbhat [P][2K], BN2 partials [tiles][2][2K];
+ * (2) BN2 apply, 1x1, GELU': gabn [P][K], partials [tiles][2K*K + 2K] = (dWg2, BN1 sums);
+ * (3) BN1 apply + transposed 3x3 + aux-output gradients (nullable, NCHW) -> branch gradients
+ *     gz_a, gz_b [P][K]; partials [gate_tiles][K*2K*9] of dWg1 */
+int eunet_gate_bwd1(const float* za, const float* zb, int k, const eunet_act* gf2conv,
+                    const float* gf2res, const float* b, const float* mean2, const float* istd2,
+                    const float* gam2, const float* bet2, float* gffd, float* gbhat, float* part,
+                    void* stream);
+int eunet_gate_bwd2(int n, int h, int w, int k, const float* gbhat, const float* b,
+                    const float* mean2, const float* istd2, const float* gam2, const float* dbet2,
+                    const float* dgam2, const float* a, const float* mean1, const float* istd1,
+                    const float* gam1, const float* bet1, const float* w2, float* gabn, float* part,
+                    void* stream);
+int eunet_gate_bwd3(const float* za, const float* zb, int n, int h, int w, int k,
+                    const float* gabn, const float* a, const float* mean1, const float* istd1,
+                    const float* gam1, const float* dbet1, const float* dgam1, const float* w1,
+                    const float* gffd, const float* gaux_a, const float* gaux_b, float* gz_a,
+                    float* gz_b, float* part, void* stream);
+/* Dropout2d(p) after a BN+ReLU (models.py:287, 291) folded into per-sample affines:
+ * keep [n][c] in {0,1} -> nscale/nshift [n][c] = scale/shift * keep/(1-p) (for the
+ * in_nstride operand transform of eunet_conv3x3_fwd / _wgrad) and gscale (nullable)
+ * [n][c] = keep/(1-p) (for eunet_conv3x3_dgrad_bnbwd) */
+int eunet_dropout_affine(const float* scale, const float* shift, const float* keep, int n, int c,
+                         float p, float* nscale, float* nshift, float* gscale, void* stream);
+/* consistency term of the auxiliary supervision (train_eval.py:207-232): loss =
+ * sum_b c_b (1/n) sum_i MSE(softmax(branch_b[i]), softmax(fused[i])), c_b = 0.4 w_b;
+ * part: [n][tiles][2] workspace (eunet_consistency_tiles).  bwd ACCUMULATES into the
+ * three NCHW gradients, scaled by the device scalar gloss. */
+int eunet_consistency_tiles(int h, int w, int* tiles);
+int eunet_consistency_fwd(const float* fused, const float* br0, const float* br1, int n, int k,
+                          int h, int w, float c0, float c1, float* part, float* loss,
+                          void* stream);
+int eunet_consistency_bwd(const float* fused, const float* br0, const float* br1, int n, int k,
+                          int h, int w, float c0, float c1, const float* gloss, float* gfused,
+                          float* g0, float* g1, void* stream);
 
 #ifdef __cplusplus
 }

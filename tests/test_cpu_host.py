@@ -73,3 +73,15 @@ def test_header_declares_reference_citations():
     src = open(os.path.join(ROOT, "include", "eunet.h")).read()
     for cite in ("models.py:219", "models.py:214", "train_eval.py:28-60", "models.py:308-313"):
         assert cite in src, cite
+
+
+def test_dual_branch_schema_matches_reference():
+    """SMP-path EnhancedUNet parameter tree (models.py:253-302): keys and order of the
+    reference module with stand-in branches (oracle/dual_ref.dual_state_spec)."""
+    from eunet.dp import backward_order
+    from eunet.models import EnhancedUNet
+    from oracle.dual_ref import dual_state_spec
+    m = EnhancedUNet(num_classes=3, dual_branch=True)
+    assert list(m.state_dict().keys()) == [k for k, _, _ in dual_state_spec(64, 3, 3)]
+    assert sorted(backward_order(m)) == sorted(n for n, _ in m.named_parameters())
+    assert m.get_aux_outputs() is None

@@ -1,0 +1,168 @@
+"""Dual-branch (SMP-path) Enhanced-UNet on the GPU vs the reference fixture and the oracle.
+
+dual_c3k3.npz was produced by the reference EnhancedUNet (models.py:253-339) built
+with stand-in branches (tests/golden/gen_golden.py gen_dual); the Dropout2d keep
+masks are part of the fixture and injected here.  fp32 gates: fused / aux outputs
+and BN running statistics within 1e-3 relative; gradients within
+max(1e-3, 3x the fp32 oracle's own error) relative L2 of the fp64 oracle.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import dual_ref as D
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def _rel(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _rel_l2(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _model(base, cin, K, dtype="fp32", keep=None):
+    from eunet.models import EnhancedUNet
+    m = EnhancedUNet(num_classes=K, in_channels=cin, base_ch=base, dtype=dtype, dual_branch=True)
+    sd = {k: (v.float() if v.is_floating_point() else v) for k, v in D.dual_formula_weights(base, cin, K).items()}
+    m.load_state_dict(sd)
+    m = m.to(DEV)
+    if keep is not None:
+        m._engine.drop_keep = keep
+    return m
+
+
+def test_dual_forward_matches_reference_fixture(golden_dir):
+    g = _load(golden_dir, "dual_c3k3.npz")
+    keep = (torch.from_numpy(g["drop0"]), torch.from_numpy(g["drop1"]))
+    m = _model(64, 3, 3, keep=keep).train()
+    x = torch.from_numpy(g["x"]).to(DEV)
+    with torch.no_grad():
+        out = m(x)
+    aux = m.get_aux_outputs()
+    assert out.shape == g["out_train"].shape
+    assert _rel(out, g["out_train"]) < 1e-3
+    assert _rel(aux["unetpp"], g["aux_unetpp"]) < 1e-3
+    assert _rel(aux["deeplab"], g["aux_deeplab"]) < 1e-3
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("bn:"):
+            assert _rel(sd[k[3:]], g[k]) < 1e-3, k
+    m.eval()
+    with torch.no_grad():
+        out_e = m(x)
+    assert _rel(out_e, g["out_eval"]) < 1e-3
+
+
+def _oracle(base, cin, K, x, msk, keep, dtype):
+    S = D.dual_formula_weights(base, cin, K, dtype=dtype)
+    for k in S:
+        if S[k].is_floating_point() and "running" not in k:
+            S[k].requires_grad_(True)
+    fused, aux = D.dual_forward(S, x.to(dtype), training=True, drop_masks=keep)
+    loss = D.dual_batch_loss(fused, aux, msk)
+    loss.backward()
+    return S, loss
+
+
+@pytest.mark.parametrize("base,cin,K,H", [(64, 3, 3, 32), (16, 1, 2, 64)])
+def test_dual_train_grads_match_oracle(golden_dir, base, cin, K, H):
+    from eunet.train_eval import Trainer
+    if base == 64:
+        g = _load(golden_dir, "dual_c3k3.npz")
+        x, msk = torch.from_numpy(g["x"]), torch.from_numpy(g["m"])
+        keep = (torch.from_numpy(g["drop0"]), torch.from_numpy(g["drop1"]))
+    else:
+        from eunet import synth
+        x, msk = synth.batch(2, H, H, start_index=11, num_classes=K, in_channels=cin)
+        gen = torch.Generator().manual_seed(5)
+        keep = ((torch.rand(2, 256, generator=gen) > 0.2).float(), (torch.rand(2, 128, generator=gen) > 0.15).float())
+    S, loss_ref = _oracle(base, cin, K, x, msk, keep, torch.float64)
+    S32, _ = _oracle(base, cin, K, x, msk, keep, torch.float32)
+    m = _model(base, cin, K, keep=keep).train()
+    tr = Trainer(m, DEV, "enhanced_unet")
+    out = m(x.to(DEV))
+    loss = tr.aux_loss(out, m.get_aux_outputs(), msk.to(DEV))
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) < 1e-4 * abs(loss_ref.item())
+
+    for k, p in m.named_parameters():
+        ref = S[k].grad
+        err32 = _rel_l2(S32[k].grad, ref)
+        e = _rel_l2(p.grad, ref)
+
+        assert e < max(1e-3, 3 * err32), (k, e, err32)
+
+
+def test_dual_trainer_step_matches_reference_fixture(golden_dir):
+    """One Trainer.step (aux supervision, clip, AdamW) vs the reference train_epoch."""
+    from eunet.train_eval import Trainer
+    g = _load(golden_dir, "dual_c3k3.npz")
+    keep = (torch.from_numpy(g["drop0"]), torch.from_numpy(g["drop1"]))
+    m = _model(64, 3, 3, keep=keep)
+    tr = Trainer(m, DEV, "enhanced_unet", total_epochs=50)
+    lr = tr.epoch_lr_step(0)
+    loss = tr.step(torch.from_numpy(g["x"]).to(DEV), torch.from_numpy(g["m"]).to(DEV))
+    assert abs(loss - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    sd = m.state_dict()
+    for k, p in m.named_parameters():
+        post = p.detach().double().cpu().numpy()
+        if f"post:{k}" in g.files:
+            ref = g[f"post:{k}"]
+            floor = 2.0 * lr if k.endswith((".0.bias", ".3.bias")) else 1e-6
+            # AdamW's first step is ~lr * sign(g): a gradient within noise of 0 may flip it
+            assert np.abs(post.reshape(ref.shape) - ref).max() < 2e-3 * np.abs(ref).max() + max(floor, 2.0 * lr), k
+        else:
+            flat = post.reshape(-1)
+            assert abs(np.sqrt((flat ** 2).sum()) - float(g[f"post_norm:{k}"])) < 1e-3 * float(g[f"post_norm:{k}"]), k
+    for k in g.files:
+        if k.startswith("post:") and ("running" in k):
+            assert _rel(sd[k[5:]], g[k]) < 1e-3, k
+
+
+def test_consistency_loss_matches_torch():
+    from eunet.losses import consistency_loss
+    gen = torch.Generator().manual_seed(3)
+    f, a, b = (torch.randn(2, 3, 17, 23, generator=gen, dtype=torch.float64) * 2 for _ in range(3))
+    ts = [t.clone().requires_grad_(True) for t in (f, a, b)]
+    pf = F.softmax(ts[0], 1)
+    ref = 0.24 * F.mse_loss(F.softmax(ts[1], 1), pf) + 0.2 * F.mse_loss(F.softmax(ts[2], 1), pf)
+    ref.backward()
+    gs = [t.float().to(DEV).requires_grad_(True) for t in (f, a, b)]
+    out = consistency_loss(gs[0], gs[1], gs[2], 0.24, 0.2)
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-5 * abs(ref.item())
+    for t, r in zip(gs, ts):
+        assert _rel(t.grad, r.grad) < 1e-4
+
+
+def test_dual_bf16_vs_autocast_reference(golden_dir):
+    """bf16 path vs the fp32 reference output, judged against bf16 autocast of the oracle
+    (the reference's own reduced-precision behaviour on the same input)."""
+    g = _load(golden_dir, "dual_c3k3.npz")
+    keep = (torch.from_numpy(g["drop0"]), torch.from_numpy(g["drop1"]))
+    x = torch.from_numpy(g["x"])
+    ref = torch.from_numpy(g["out_train"]).double()
+    with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+        ac = D.dual_forward(D.dual_formula_weights(64, 3, 3, dtype=torch.float32), x, True, keep)[0].float()
+    m = _model(64, 3, 3, dtype="bf16", keep=keep).train()
+    with torch.no_grad():
+        out = m(x.to(DEV)).double().cpu()
+    ours, auto = _rel_l2(out, ref), _rel_l2(ac, ref)
+    print("dual bf16 relL2 ours", ours, "autocast", auto)
+    assert torch.isfinite(out).all()
+    assert ours < max(2.0 * auto, 0.02), (ours, auto)

@@ -119,7 +119,7 @@ def test_conv3x3_dgrad_wgrad(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cin", [1, 3])
+@pytest.mark.parametrize("cin", [1, 3, 4, 6, 8])
 def test_conv_small(dt, cin):
     ops = _ops()
     g = torch.Generator().manual_seed(3)
@@ -390,3 +390,54 @@ def test_conv3x3_dgrad_bnbwd_fused(dt):
     s2 = (gp * xh).sum(dim=(0, 1, 2))
     assert rel(red[:Cout], s1) < 1e-5
     assert rel(red[Cout:], s2) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_per_sample_affine_and_gscale(dt):
+    """Dropout2d folded into the operand transform (in_nstride: per-sample scale/shift) for
+    the forward and the wgrad, and the per-sample output scale of the fused dgrad."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(12)
+    N, H, W, Cin, Cout = 3, 16, 36, 32, 64
+    x = torch.randn(N, H, W, Cin, generator=g).to(dt).double()
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 17
+    sc = torch.rand(N, Cin, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(N, Cin, generator=g, dtype=torch.float64) * 0.3
+    keep = (torch.rand(N, Cin, generator=g) > 0.3).double()
+    scn, shn = sc * keep / 0.7, sh * keep / 0.7
+    xt = torch.relu(x * scn[:, None, None, :] + shn[:, None, None, :])
+    if dt == torch.bfloat16:
+        xt = xt.to(torch.bfloat16).double()
+    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), None, padding=1))
+    y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
+    ops.conv3x3_fwd(ops.act(x.to(DEV, dt)), wp, ops.act(y), scale=scn.float().to(DEV), shift=shn.float().to(DEV),
+                    nstride=Cin)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < TOL[dt]
+    gy = torch.randn(N, H, W, Cout, generator=g).to(dt).double()
+    ns = ops.conv3x3_wgrad_splits(ops.act(gy.to(DEV, dt)), Cin, dt)
+    dwp = torch.empty(ns * Cout * 9 * Cin, device=DEV)
+    ops.conv3x3_wgrad(ops.act(x.to(DEV, dt)), ops.act(gy.to(DEV, dt)), dwp, None, ns, scale=scn.float().to(DEV),
+                      shift=shn.float().to(DEV), nstride=Cin)
+    dw = torch.empty(Cout, Cin, 3, 3, device=DEV)
+    ops.wgrad_reduce(dwp, None, ns, Cout, Cin, 9, dw, None)
+    wt = w.clone().requires_grad_(True)
+    F.conv2d(nchw(xt), wt, None, padding=1).backward(nchw(gy))
+    torch.cuda.synchronize()
+    assert rel(dw, wt.grad) < (1e-4 if dt == torch.float32 else 1e-2)
+    # dgrad with gscale: gx = conv_transpose(gy) * gs[n][c]
+    gs = (keep / 0.7).float().to(DEV)
+    wpt = ops.conv3x3_pack(w.float().to(DEV), dt, flip=True)
+    gx0 = torch.empty(N, H, W, Cin, dtype=dt, device=DEV)
+    ops.conv3x3_fwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx0))
+    gx = torch.empty_like(gx0)
+    yb = torch.randn(N, H, W, Cin, generator=g).to(DEV, dt)
+    ones, zeros = torch.ones(Cin, device=DEV), torch.zeros(Cin, device=DEV)
+    tiles = ops.conv3x3_tiles(ops.act(gx))
+    part = torch.empty(tiles * 2 * Cin, device=DEV)
+    ops.conv3x3_dgrad_bnbwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx), ops.act(yb), zeros, ones, ones, zeros, part,
+                            gscale=gs)
+    torch.cuda.synchronize()
+    exp = (gx0.double() * gs.double()[:, None, None, :]).to(dt).double()
+    assert rel(gx, exp) < (1e-6 if dt == torch.float32 else 1e-2)

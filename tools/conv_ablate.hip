@@ -73,7 +73,7 @@ static int wgrad_main(int N, int H, int W, int cin, int cout, int reps) {
   CK(hipMalloc(&dbp, (size_t)ns * cout * 4));
   WgArgs a;
   a.x = x; a.N = N; a.H = H; a.W = W; a.xct = cin; a.xco = 0; a.cin = cin;
-  a.isc = nullptr; a.ish = nullptr;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0;
   a.dy = dy; a.dct = cout; a.dco = 0; a.cout = cout;
   a.dw = dwp; a.db = dbp;
   a.tx = cdiv(W, TW); a.ty = cdiv(H, TH); a.ntiles = N * a.tx * a.ty;
@@ -126,13 +126,13 @@ int main(int argc, char** argv) {
   }
   FwdArgs a;
   a.x = x; a.N = N; a.H = H; a.W = W; a.xct = cin; a.xco = 0; a.cin = cin;
-  a.isc = nullptr; a.ish = nullptr;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0;
   a.wp = wp; a.cout_pad = cout; a.nkc = cin / 32;
   a.bias = nullptr;
   a.y = y; a.yct = cout; a.yco = 0; a.cout = cout;
   a.tx = cdiv(W, FTW); a.ty = cdiv(H, FTH); a.ntiles = N * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
-  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
   CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
   a.stats = stats;
   dim3 grid(a.ntiles * (cout / BN));
