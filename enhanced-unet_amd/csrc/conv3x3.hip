@@ -21,6 +21,8 @@
 // Wgrad: dW[co][t][ci] = sum_p dY[p][co] * X~[p+d_t][ci], pixels are the GEMM K.
 //   Block = (pixel-tile split, 64 co, KC ci); dY tile and X halo staged in LDS;
 //   bf16 fragments (8 consecutive pixels) come from ds_read_b64_tr_b16.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -54,7 +56,22 @@ struct FwdArgs {
   const float* bmean; const float* bistd; const float* bgam; const float* bbet;
   float* bpart;
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
+  int order;         // block -> (tile, co-block) order: 0 XCD-grouped, 1 tile-fastest, 2 co-block-fastest
 };
+
+// block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
+inline int env_order(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && v[0] >= '0' && v[0] <= '2') ? v[0] - '0' : dflt;
+}
+int conv_order() {
+  static const int o = env_order("EUNET_CONV_ORDER", 0);
+  return o;
+}
+int wgrad_order() {
+  static const int o = env_order("EUNET_WGRAD_ORDER", 0);
+  return o;
+}
 
 // stage one halo unit (pixel hp, quarter q) of chunk kc into registers
 template <typename T>
@@ -167,9 +184,12 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 //   one LDS stage each (a block's staging overlaps the other block's MFMAs).
 // SPEC (with DB, NW = 8): waves 0-3 only compute (128 px x 64 co each), waves 4-7 only
 //   stage the next chunk (global -> registers -> BN+ReLU -> LDS) into the other buffer.
-template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false>
+// BDMA (with DB): the weight tile is staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round
+//   trip); the packed layout makes every 64-unit wave-instruction one contiguous 1 KiB run.
+template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false>
 __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
   static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
+  static_assert(!BDMA || (DB && !SPEC), "BDMA needs the double-buffered block");
   constexpr int NTH = 64 * NW;
   constexpr int NCW = SPEC ? 4 : NW;          // computing waves
   constexpr int NLT = SPEC ? 256 : NTH;       // staging threads
@@ -183,10 +203,13 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int tile, cob;
-  if constexpr ((MODE & 8) != 0) {  // diagnostic: plain tile-fastest order
+  if ((MODE & 8) != 0 || a.order == 1) {  // tile-fastest: co-block-major
     tile = blockIdx.x % a.ntiles;
     cob = blockIdx.x / a.ntiles;
-  } else {  // XCD-grouped (conv_bench: +5-15% on the 256^2-512^2 layers, +-3% elsewhere)
+  } else if (a.order == 2) {  // co-block-fastest identity order
+    cob = blockIdx.x % (a.cout_pad / BN);
+    tile = blockIdx.x / (a.cout_pad / BN);
+  } else {  // XCD-grouped
     xcd_map(blockIdx.x, a.ntiles, a.cout_pad / BN, tile, cob);
   }
   const int tpi = a.tx * a.ty;
@@ -237,6 +260,15 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     }                                                                                         \
   } while (0)
 
+  auto dma_b = [&](int kc, int buf) {
+    char* Bs_ = smem + buf * STAGE_BYTES + FA_BYTES;
+// (wave-strided: not unrolled)
+    for (int j = wv; j < B_UNITS / 64; j += NW) {
+      const u32x4* src = &CONV_BUNIT(j * 64 + lane, kc);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Bs_ + j * 64 * 16), 16, 0, 0);
+    }
+  };
   constexpr int AH = A_IT / 2, BH = B_IT / 2;
   auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
     CONV_GLOAD_A(kc, 0, AH);
@@ -270,11 +302,11 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
           } else {
-            const uint4 B_ = fb[nt];
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
+            const uint4 A_ = fa, B_ = fb[nt];
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
           }
         }
       }
@@ -291,9 +323,13 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     }
   } else if constexpr (DB) {
     CONV_GLOAD_A(0, 0, A_IT);
-    CONV_GLOAD_B(0, 0, B_IT);
+    if constexpr (BDMA) {
+      dma_b(0, 0);
+    } else {
+      CONV_GLOAD_B(0, 0, B_IT);
+    }
     CONV_LWRITE_A(0, 0, 0, A_IT);
-    CONV_LWRITE_B(0, 0, B_IT);
+    if constexpr (!BDMA) CONV_LWRITE_B(0, 0, B_IT);
   } else {
     stage(0, 0);
   }
@@ -320,13 +356,17 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     } else if constexpr (DB) {
       const int cur = kc & 1;
       if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
+        if constexpr (BDMA) {
+          dma_b(kc + 1, cur ^ 1);
+        } else {
+          CONV_GLOAD_B(kc + 1, 0, B_IT);
+        }
         CONV_GLOAD_A(kc + 1, 0, A_IT);
-        CONV_GLOAD_B(kc + 1, 0, B_IT);
       }
       chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
       if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
         CONV_LWRITE_A(kc + 1, cur ^ 1, 0, A_IT);
-        CONV_LWRITE_B(cur ^ 1, 0, B_IT);
+        if constexpr (!BDMA) CONV_LWRITE_B(cur ^ 1, 0, B_IT);
       }
       __syncthreads();
     } else {
@@ -540,6 +580,7 @@ struct WgArgs {
   const void* dy; int dct, dco, cout;
   float* dw; float* db;
   int tx, ty, ntiles, per_split, nsplit;
+  int order;  // 0 XCD-grouped (wg_map), 1 identity
 };
 
 template <typename T>
@@ -700,7 +741,14 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   float* dbred = (float*)(smem + WSTAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int split, cob, kc;
-  wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
+  if (a.order == 1) {
+    const int ncib = cdiv(a.cin, KCW), ncob = cdiv(a.cout, 64);
+    kc = blockIdx.x % ncib;
+    cob = (blockIdx.x / ncib) % ncob;
+    split = blockIdx.x / (ncib * ncob);
+  } else {
+    wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
+  }
   const int co0 = cob * 64;
   const int t_begin = split * a.per_split;
   const int t_end = min(a.ntiles, t_begin + a.per_split);
@@ -947,6 +995,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
   a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
+  a.order = conv_order();
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   return launch_fwd(a, x->dtype, stream);
@@ -974,6 +1023,7 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
   a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
+  a.order = conv_order();
   return launch_fwd(a, dy->dtype, stream);
 }
 
@@ -1011,6 +1061,7 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;
+  a.order = wgrad_order();
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));

@@ -4,7 +4,8 @@ dual_c3k3.npz was produced by the reference EnhancedUNet (models.py:253-339) bui
 with stand-in branches (tests/golden/gen_golden.py gen_dual); the Dropout2d keep
 masks are part of the fixture and injected here.  fp32 gates: fused / aux outputs
 and BN running statistics within 1e-3 relative; gradients within
-max(1e-3, 3x the fp32 oracle's own error) relative L2 of the fp64 oracle.
+max(1e-3, 3x the fp32 oracle's own error, 1.5x the oracle's ReLU-kink spread) relative L2
+of the fp64 oracle.
 """
 import os
 
@@ -68,10 +69,13 @@ def test_dual_forward_matches_reference_fixture(golden_dir):
     assert _rel(out_e, g["out_eval"]) < 1e-3
 
 
-def _oracle(base, cin, K, x, msk, keep, dtype):
+def _oracle(base, cin, K, x, msk, keep, dtype, noise=0.0, seed=0):
     S = D.dual_formula_weights(base, cin, K, dtype=dtype)
+    gen = torch.Generator().manual_seed(seed)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:
+            if noise:
+                S[k] = S[k] * (1 + noise * torch.randn(S[k].shape, generator=gen, dtype=dtype))
             S[k].requires_grad_(True)
     fused, aux = D.dual_forward(S, x.to(dtype), training=True, drop_masks=keep)
     loss = D.dual_batch_loss(fused, aux, msk)
@@ -93,6 +97,14 @@ def test_dual_train_grads_match_oracle(golden_dir, base, cin, K, H):
         keep = ((torch.rand(2, 256, generator=gen) > 0.2).float(), (torch.rand(2, 128, generator=gen) > 0.15).float())
     S, loss_ref = _oracle(base, cin, K, x, msk, keep, torch.float64)
     S32, _ = _oracle(base, cin, K, x, msk, keep, torch.float32)
+    # ReLU-kink / max-pool-tie sensitivity of this input: spread of the fp64 oracle itself under
+    # 1e-6 relative weight perturbations (see test_gpu_model.test_train_grads_match_oracle)
+    spread = {}
+    for seed in (1, 2):
+        Sp, _ = _oracle(base, cin, K, x, msk, keep, torch.float64, noise=1e-6, seed=seed)
+        for k in S:
+            if S[k].grad is not None:
+                spread[k] = max(spread.get(k, 0.0), _rel_l2(Sp[k].grad, S[k].grad))
     m = _model(base, cin, K, keep=keep).train()
     tr = Trainer(m, DEV, "enhanced_unet")
     out = m(x.to(DEV))
@@ -100,12 +112,16 @@ def test_dual_train_grads_match_oracle(golden_dir, base, cin, K, H):
     loss.backward()
     assert abs(loss.item() - loss_ref.item()) < 1e-4 * abs(loss_ref.item())
 
+    rows = []
     for k, p in m.named_parameters():
         ref = S[k].grad
         err32 = _rel_l2(S32[k].grad, ref)
         e = _rel_l2(p.grad, ref)
-
-        assert e < max(1e-3, 3 * err32), (k, e, err32)
+        rows.append((e / max(1e-3, 3 * err32, 1.5 * spread[k]), k, e, err32, spread[k], float(ref.norm())))
+    for r in sorted(rows, reverse=True)[:6]:
+        print("dual grad (ratio, name, err, err32, spread, |g|):", r)
+    for r in rows:
+        assert r[0] < 1.0, r
 
 
 def test_dual_trainer_step_matches_reference_fixture(golden_dir):
