@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=1024, help="CPU baseline sample: one B=1 step at this size")
     ap.add_argument("--dice-size", type=int, default=1024, help="Dice-vs-CPU-reference image side (0 = skip)")
+    ap.add_argument("--dual", action="store_true",
+                    help="dual-branch model + deep supervision (BASELINE configs[4]: --dual --base 96 --size 2048)")
     return ap.parse_args()
 
 
@@ -150,7 +152,8 @@ def main():
     from eunet.train_eval import Trainer
 
     torch.manual_seed(0)
-    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=args.base, dtype=args.dtype).to(dev)
+    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=args.base, dtype=args.dtype,
+                         dual_branch=args.dual).to(dev)
     tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
     tr.epoch_lr_step(0)
     if world > 1:
@@ -201,9 +204,11 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
-    dice = dice_vs_cpu_ref(model, args, dev) if args.dice_size > 0 else None
+    dice = dice_vs_cpu_ref(model, args, dev) if args.dice_size > 0 and not args.dual else None
     from oracle.eunet_ref import flops_per_pixel
-    step_flops = flops_per_pixel(args.base, 1, 2) * args.size * args.size * args.batch
+    from oracle.dual_ref import dual_flops_per_pixel
+    fpp = dual_flops_per_pixel(args.base, 1, 2) if args.dual else flops_per_pixel(args.base, 1, 2)
+    step_flops = fpp * args.size * args.size * args.batch
     line = {
         "metric": METRIC,
         "value": round(imgs / elapsed, 3),
@@ -217,8 +222,10 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic bright-field tiles (eunet.synth, seeded), random-init weights",
-        "config": {"workload": f"base_ch={args.base}, 1x{args.size}x{args.size} 1-ch->2-cls, batch "
-                               f"{args.batch}/GPU, {args.dtype} (BASELINE configs[2]; configs[3] at N=8)",
+        "config": {"workload": (f"dual-branch + deep supervision, " if args.dual else "") +
+                               f"base_ch={args.base}, 1x{args.size}x{args.size} 1-ch->2-cls, batch "
+                               f"{args.batch}/GPU, {args.dtype} " +
+                               ("(BASELINE configs[4])" if args.dual else "(BASELINE configs[2]; configs[3] at N=8)"),
                    "global_batch": world * args.batch, "image_size": args.size, "parallelism": f"dp{world}"},
         "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
         "roofline": roof,

@@ -57,6 +57,7 @@ struct FwdArgs {
   float* bpart;
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
   int order;         // block -> (tile, co-block) order: 0 XCD-grouped, 1 tile-fastest, 2 co-block-fastest
+  int phase;         // 1: odd blocks start late (see conv3x3_fwd_kernel)
 };
 
 // block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
@@ -70,6 +71,14 @@ int conv_order() {
 }
 int wgrad_order() {
   static const int o = env_order("EUNET_WGRAD_ORDER", 0);
+  return o;
+}
+int conv_phase() {
+  static const int o = env_order("EUNET_CONV_PHASE", 1);
+  return o;
+}
+int wgrad_phase() {
+  static const int o = env_order("EUNET_WGRAD_PHASE", 1);
   return o;
 }
 
@@ -117,7 +126,7 @@ __device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int
 constexpr int FTH = 16, FTW = 32;            // output tile
 constexpr int FHW = FTW + 2;                 // 34
 constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
-constexpr int FHPXP = 624;                   // plane stride (multiple of 16 units)
+constexpr int FHPXP = 640;                   // plane stride (10 x 64 units: whole LDS-DMA wave-instructions)
 constexpr int FT = 256;                      // threads of the production (NW = 4) forward block
 constexpr int FA_UNITS = 4 * FHPX;           // 2448
 constexpr int FA_BYTES = 4 * FHPXP * 16;     // 39936
@@ -177,7 +186,8 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 // MODE: 0 = production.  Diagnostic builds only (tools/conv_ablate.hip):
 //   1 = no global loads / LDS writes inside the K loop, 2 = no MFMAs (VALU keeps the
 //   LDS reads alive), 4 = LDS fragments read once before the loop (MFMA-only loop),
-//   8 = plain tile-fastest block order instead of xcd_map.
+//   8 = plain tile-fastest block order instead of xcd_map, 16 / 32 = odd blocks start
+//   ~2.5k / ~5k clocks late (phase offset between the two blocks of a CU).
 // NW = waves per block (4: 128 px x 64 co per wave; 8: 64 px x 64 co per wave).
 // DB: true = one block per CU, double-buffered LDS (next chunk prefetched into
 //   registers during the MFMAs, one barrier per chunk); false = two blocks per CU,
@@ -186,7 +196,11 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 //   stage the next chunk (global -> registers -> BN+ReLU -> LDS) into the other buffer.
 // BDMA (with DB): the weight tile is staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round
 //   trip); the packed layout makes every 64-unit wave-instruction one contiguous 1 KiB run.
-template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false>
+// DMA (single-stage path): 1 = weights by LDS-DMA, 2 = also the input halo when it needs no
+//   BN+ReLU transform (out-of-image / padded-channel lanes read a global zero vector).
+__device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised)
+
+template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, int DMA = 0>
 __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
   static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
   static_assert(!BDMA || (DB && !SPEC), "BDMA needs the double-buffered block");
@@ -269,16 +283,39 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
                                        (__attribute__((address_space(3))) void*)(Bs_ + j * 64 * 16), 16, 0, 0);
     }
   };
+  auto dma_a = [&](int kc, int buf) {  // halo tile by LDS-DMA: wave-instruction j = quarter j/10, 64 pixels
+    constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
+    char* As_ = smem + buf * STAGE_BYTES;
+    for (int j = wv; j < 4 * (FHPXP / 64); j += NW) {
+      const int qq = j / (FHPXP / 64), hp0 = (j % (FHPXP / 64)) * 64, hp = hp0 + lane;
+      const int hy = hp / FHW, hx = hp - hy * FHW;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const int c = kc * KC + qq * E;
+      const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin;
+      const void* src = ok ? (const void*)((const T*)a.x + (((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c))
+                           : (const void*)&g_conv_zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(As_ + (qq * FHPXP + hp0) * 16), 16, 0,
+                                       0);
+    }
+  };
   constexpr int AH = A_IT / 2, BH = B_IT / 2;
   auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
-    CONV_GLOAD_A(kc, 0, AH);
-    CONV_LWRITE_A(kc, buf, 0, AH);
-    CONV_GLOAD_A(kc, AH, A_IT);
-    CONV_LWRITE_A(kc, buf, AH, A_IT);
-    CONV_GLOAD_B(kc, 0, BH);
-    CONV_LWRITE_B(buf, 0, BH);
-    CONV_GLOAD_B(kc, BH, B_IT);
-    CONV_LWRITE_B(buf, BH, B_IT);
+    if constexpr (DMA >= 1) dma_b(kc, buf);
+    if (DMA >= 2 && a.isc == nullptr) {
+      dma_a(kc, buf);
+    } else {
+      CONV_GLOAD_A(kc, 0, AH);
+      CONV_LWRITE_A(kc, buf, 0, AH);
+      CONV_GLOAD_A(kc, AH, A_IT);
+      CONV_LWRITE_A(kc, buf, AH, A_IT);
+    }
+    if constexpr (DMA == 0) {
+      CONV_GLOAD_B(kc, 0, BH);
+      CONV_LWRITE_B(buf, 0, BH);
+      CONV_GLOAD_B(kc, BH, B_IT);
+      CONV_LWRITE_B(buf, BH, B_IT);
+    }
   };
   auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[MT], const uint4 (&fb0)[4]) {
 #pragma unroll 1
@@ -314,6 +351,16 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   };
 
   uint4 fa0[MT], fb0[4];
+  // Phase offset: the two blocks sharing a CU start (and, with equal work, keep running) in
+  // lock-step, staging at the same time and leaving the MFMA pipes idle together.  Odd blocks
+  // start ~2.5k clocks late so one block's staging overlaps the other's MFMAs (ablation:
+  // +15-20 % on every layer shape).
+  if ((MODE & 48) != 0 || a.phase) {
+    if (blockIdx.x & 1) {
+#pragma unroll 1
+      for (int i = 0; i < ((MODE & 32) ? 2 : 1); ++i) __builtin_amdgcn_s_sleep(40);
+    }
+  }
   if constexpr (SPEC) {
     if (!computes) {
       CONV_GLOAD_A(0, 0, A_IT);
@@ -581,6 +628,7 @@ struct WgArgs {
   float* dw; float* db;
   int tx, ty, ntiles, per_split, nsplit;
   int order;  // 0 XCD-grouped (wg_map), 1 identity
+  int phase;  // 1: odd blocks start late (see conv3x3_fwd_kernel)
 };
 
 template <typename T>
@@ -762,6 +810,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   u32x4 rx[WX_ITERS], rd[WD_ITERS];
+  if (a.phase && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
   auto gload_x = [&](int tile, int i0, int i1) {
     const int n = tile / tpi, trem = tile - n * tpi;
@@ -932,14 +981,28 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
+int conv_dma() {
+  static const int o = env_order("EUNET_CONV_DMA", 0);
+  return o;
+}
+
+template <int DMA>
+void launch_fwd_dma(const FwdArgs& a, int dtype, dim3 grid, void* stream) {
+  if (dtype == EUNET_BF16) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, DMA>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, DMA><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else {
+    allow_lds(conv3x3_fwd_kernel<float, 0, false, 4, false, false, DMA>, FWD_LDS);
+    conv3x3_fwd_kernel<float, 0, false, 4, false, false, DMA><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  }
+}
+
 int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
   dim3 grid(a.ntiles * (a.cout_pad / BN));
-  if (dtype == EUNET_BF16) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
-  } else {
-    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
-    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  switch (conv_dma()) {
+    case 1: launch_fwd_dma<1>(a, dtype, grid, stream); break;
+    case 2: launch_fwd_dma<2>(a, dtype, grid, stream); break;
+    default: launch_fwd_dma<0>(a, dtype, grid, stream); break;
   }
   EUNET_LAUNCH_CHECK("conv3x3_fwd");
   return EUNET_OK;
@@ -996,6 +1059,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.by = nullptr; a.byct = 0; a.byco = 0;
   a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
   a.order = conv_order();
+  a.phase = conv_phase();
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   return launch_fwd(a, x->dtype, stream);
@@ -1024,6 +1088,7 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
   a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
   a.order = conv_order();
+  a.phase = conv_phase();
   return launch_fwd(a, dy->dtype, stream);
 }
 
@@ -1062,6 +1127,7 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;
   a.order = wgrad_order();
+  a.phase = wgrad_phase();
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));

@@ -50,3 +50,13 @@ def batch(n: int, h: int, w: int, start_index: int = 0, num_classes: int = 2, in
     x = torch.from_numpy(np.stack(xs)).to(device)
     m = torch.from_numpy(np.stack(ms)).to(device)
     return x, m
+
+
+def loader(n_batches: int, batch_size: int, h: int, w: int, start_index: int = 0, num_classes: int = 2,
+           in_channels: int = 1):
+    """A list of collate_fn-style batches (dataset.py:355-361) of synthetic tiles."""
+    out = []
+    for b in range(n_batches):
+        x, m = batch(batch_size, h, w, start_index + b * batch_size, num_classes, in_channels)
+        out.append({"images": x, "batch_items": [{"semantic_mask": m[i]} for i in range(batch_size)]})
+    return out

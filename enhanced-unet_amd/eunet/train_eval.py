@@ -163,3 +163,76 @@ class Trainer:
 
 
 from .evaluator import Evaluator  # noqa: E402,F401  (train_eval.Evaluator, train_eval.py:356-904)
+
+
+# ---- train_model driver + checkpoint interchange (train_eval.py:1036-1162, 1186-1202) -------
+CHECKPOINT_KEYS = ("epoch", "model_state_dict", "optimizer_state_dict", "scheduler_state_dict", "best_miou",
+                   "best_loss", "history")
+
+
+def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num_epochs: int = 50,
+                skip_training: bool = False, *, train_loader=None, val_loader=None, save_dir: str = None,
+                model=None, verbose: bool = True, **model_kwargs):
+    """train_eval.train_model: per-epoch LR stepping (warmup LinearLR, then cosine restarts) before
+    each train_epoch, semantic validation every 3 epochs, best-mIoU checkpoint in the reference's
+    dict format ('checkpoints/<model>/best_model.pth'), early stop after patience 10 (epoch > 25).
+
+    The reference builds its loaders from CellDataset (cv2 / PIL LabelMe pipeline, dataset.py),
+    which this build does not provide: pass train_loader / val_loader yielding the collate_fn batch
+    dict ({'images', 'batch_items': [{'semantic_mask'}]}), e.g. eunet.synth.loader."""
+    import os
+    from .models import get_model
+    save_dir = save_dir or os.path.join("checkpoints", model_name)
+    os.makedirs(save_dir, exist_ok=True)
+    checkpoint_path = os.path.join(save_dir, "best_model.pth")
+    if os.path.exists(checkpoint_path) and skip_training:
+        return checkpoint_path
+    if train_loader is None:
+        raise NotImplementedError("CellDataset (dataset.py, cv2/PIL LabelMe loader) is not part of this build: "
+                                  "pass train_loader/val_loader")
+    if model is None:
+        model = get_model(model_name, num_classes=3, device=device, **model_kwargs).to(device)
+    history = {"train_loss": [], "val_loss": [], "val_miou": [], "val_live_iou": [], "val_dead_iou": [],
+               "val_dice": [], "learning_rate": [], "epoch_axis": []}
+    train_epochs = num_epochs
+    trainer = Trainer(model, device, model_name, total_epochs=train_epochs)
+    best_loss, best_miou = float("inf"), 0.0
+    patience = 10 if model_name == "enhanced_unet" else 8
+    patience_counter = 0
+    for epoch in range(train_epochs):
+        current_lr = trainer.epoch_lr_step(epoch)
+        loss = trainer.train_epoch(train_loader)
+        history["train_loss"].append(loss)
+        history["learning_rate"].append(current_lr)
+        if verbose:
+            print(f"Epoch {epoch + 1}/{train_epochs}  lr {current_lr:.6f}  loss {loss:.4f}")
+        if (epoch + 1) % 3 == 0:
+            res = Evaluator(model, device, model_name).evaluate_semantic(val_loader or train_loader)
+            val_iou = res.get("sem_mean_iou", 0.0)
+            history["val_miou"].append(val_iou)
+            history["val_live_iou"].append(res.get("sem_live_iou", 0.0))
+            history["val_dead_iou"].append(res.get("sem_dead_iou", 0.0))
+            history["val_dice"].append([res.get("sem_live_dice", 0.0), res.get("sem_dead_dice", 0.0)])
+            history["val_loss"].append(loss)
+            history["epoch_axis"].append(epoch + 1)
+            if val_iou > best_miou:
+                best_miou, best_loss, patience_counter = val_iou, loss, 0
+                torch.save({"epoch": epoch + 1, "model_state_dict": model.state_dict(),
+                            "optimizer_state_dict": trainer.optimizer.state_dict(),
+                            "scheduler_state_dict": trainer.scheduler.state_dict(), "best_miou": best_miou,
+                            "best_loss": best_loss, "history": history}, checkpoint_path)
+            else:
+                patience_counter += 1
+        if patience_counter >= patience and epoch > 25:
+            break
+    return checkpoint_path
+
+
+def load_checkpoint(model, checkpoint_path: str, map_location=None):
+    """evaluate_model's checkpoint load (train_eval.py:1186-1202), safe loader: the file holds
+    only tensors and plain containers, so weights_only=True reads reference checkpoints too.
+    Also accepts a bare state_dict."""
+    ckpt = torch.load(checkpoint_path, map_location=map_location or "cpu", weights_only=True)
+    sd = ckpt["model_state_dict"] if isinstance(ckpt, dict) and "model_state_dict" in ckpt else ckpt
+    model.load_state_dict(sd)
+    return ckpt

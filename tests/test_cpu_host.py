@@ -85,3 +85,19 @@ def test_dual_branch_schema_matches_reference():
     assert list(m.state_dict().keys()) == [k for k, _, _ in dual_state_spec(64, 3, 3)]
     assert sorted(backward_order(m)) == sorted(n for n, _ in m.named_parameters())
     assert m.get_aux_outputs() is None
+
+
+def test_checkpoint_format_roundtrip_cpu(tmp_path):
+    """load_checkpoint reads the reference's best_model.pth dict (and bare state_dicts) with the
+    safe loader."""
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import load_checkpoint
+    a = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16)
+    b = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16)
+    p = tmp_path / "ck.pth"
+    torch.save({"epoch": 1, "model_state_dict": a.state_dict(), "best_miou": 0.1, "best_loss": 2.0,
+                "history": {"train_loss": [2.0]}}, p)
+    load_checkpoint(b, str(p))
+    assert all(torch.equal(x, y) for x, y in zip(a.state_dict().values(), b.state_dict().values()))
+    torch.save(a.state_dict(), tmp_path / "sd.pth")
+    load_checkpoint(b, str(tmp_path / "sd.pth"))

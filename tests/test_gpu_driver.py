@@ -1,0 +1,56 @@
+"""train_model driver and checkpoint interchange (train_eval.py:1036-1162, 1186-1202) on the GPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import eunet_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def test_train_model_checkpoint_roundtrip(tmp_path):
+    from eunet import synth
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import CHECKPOINT_KEYS, load_checkpoint, train_model
+    tl = synth.loader(2, 2, 64, 64, start_index=0, num_classes=3, in_channels=3)
+    vl = synth.loader(1, 1, 64, 64, start_index=50, num_classes=3, in_channels=3)
+    model = EnhancedUNet(num_classes=3, in_channels=3, base_ch=16).to(DEV)
+    path = train_model("enhanced_unet", device=DEV, num_epochs=4, train_loader=tl, val_loader=vl,
+                       save_dir=str(tmp_path), model=model, verbose=False)
+    assert os.path.basename(path) == "best_model.pth"
+    if not os.path.exists(path):  # mIoU stayed 0 at the epoch-3 validation: nothing to save
+        pytest.skip("no validation improvement in 4 epochs")
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(CHECKPOINT_KEYS) <= set(ck)
+    assert ck["epoch"] == 3
+    lrs = ck["history"]["learning_rate"]  # history as saved at the epoch-3 checkpoint
+    np.testing.assert_allclose(lrs, R.lr_trajectory(4)[:len(lrs)], rtol=1e-12)
+    fresh = EnhancedUNet(num_classes=3, in_channels=3, base_ch=16).to(DEV)
+    load_checkpoint(fresh, path)
+    for (k, a), (_, b) in zip(ck["model_state_dict"].items(), fresh.state_dict().items()):
+        assert torch.equal(a, b.cpu()), k
+
+
+def test_reference_format_checkpoint_loads(golden_dir, tmp_path):
+    """A checkpoint in the reference's dict format (model_state_dict with its 109 keys) loads
+    and reproduces the reference's eval-mode output."""
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import load_checkpoint
+    g = np.load(os.path.join(golden_dir, "fwd_c3k3.npz"), allow_pickle=False)
+    sd = {k: (v.float() if v.is_floating_point() else v) for k, v in R.formula_weights(64, 3, 3).items()}
+    for k in g.files:
+        if k.startswith("bn:"):
+            sd[k[3:]] = torch.from_numpy(g[k]).float()
+    path = tmp_path / "best_model.pth"
+    torch.save({"epoch": 3, "model_state_dict": sd, "best_miou": 0.5, "best_loss": 1.0, "history": {}}, path)
+    m = EnhancedUNet(num_classes=3)
+    ck = load_checkpoint(m, str(path))
+    assert ck["best_miou"] == 0.5
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        out = m(torch.from_numpy(g["x"]).to(DEV)).double().cpu()
+    ref = torch.from_numpy(g["out_eval"]).double()
+    assert float((out - ref).abs().max() / ref.abs().max()) < 1e-3

@@ -73,7 +73,7 @@ static int wgrad_main(int N, int H, int W, int cin, int cout, int reps) {
   CK(hipMalloc(&dbp, (size_t)ns * cout * 4));
   WgArgs a;
   a.x = x; a.N = N; a.H = H; a.W = W; a.xct = cin; a.xco = 0; a.cin = cin;
-  a.isc = nullptr; a.ish = nullptr; a.iss = 0; a.order = 0;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0; a.order = 0; a.phase = 0;
   a.dy = dy; a.dct = cout; a.dco = 0; a.cout = cout;
   a.dw = dwp; a.db = dbp;
   a.tx = cdiv(W, TW); a.ty = cdiv(H, TH); a.ntiles = N * a.tx * a.ty;
@@ -132,7 +132,7 @@ int main(int argc, char** argv) {
   a.y = y; a.yct = cout; a.yco = 0; a.cout = cout;
   a.tx = cdiv(W, FTW); a.ty = cdiv(H, FTH); a.ntiles = N * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
-  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr; a.order = 0;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr; a.order = 0; a.phase = 0;
   CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
   a.stats = stats;
   dim3 grid(a.ntiles * (cout / BN));
@@ -143,13 +143,14 @@ int main(int argc, char** argv) {
   const float t8w = run<0, false, 8>(a, grid, reps);
   const float tsp = run<0, true, 8, true>(a, grid, reps), tsp5 = run<5, true, 8, true>(a, grid, reps);
   const float tdb4 = run<0, true, 4>(a, grid, reps);
+  const float td16 = run<16>(a, grid, reps), td32 = run<32>(a, grid, reps);
   const float tbd8 = run<0, true, 8, false, true>(a, grid, reps), tbd4 = run<0, true, 4, false, true>(a, grid, reps);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"blocks\": %d", N, H, W, cin, cout, a.ntiles * cout / BN);
   const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db8_full",
                       "db8_mfma_only", "w8_2blk_full", "spec_full", "spec_mfma_only", "db4_full", "db8_bdma",
-                      "db4_bdma"};
-  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w, tsp, tsp5, tdb4, tbd8, tbd4};
-  for (int i = 0; i < 14; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+                      "db4_bdma", "delay2k", "delay5k"};
+  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w, tsp, tsp5, tdb4, tbd8, tbd4, td16, td32};
+  for (int i = 0; i < 16; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
   printf("}\n");
   return 0;
 }
