@@ -198,9 +198,13 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 //   trip); the packed layout makes every 64-unit wave-instruction one contiguous 1 KiB run.
 // DMA (single-stage path): 1 = weights by LDS-DMA, 2 = also the input halo when it needs no
 //   BN+ReLU transform (out-of-image / padded-channel lanes read a global zero vector).
+// PIPE: the 9 taps of a chunk are software-pipelined -- the fragments of tap t+1 are read
+//   from LDS into a second register set while tap t's MFMAs run (one wave per SIMD with DB,
+//   so no other wave hides the ds_read latency; 512 registers per lane leave room for it).
 __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised)
 
-template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, int DMA = 0>
+template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, int DMA = 0,
+          bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
   static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
   static_assert(!BDMA || (DB && !SPEC), "BDMA needs the double-buffered block");
@@ -317,7 +321,47 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
       CONV_LWRITE_B(buf, BH, B_IT);
     }
   };
+  auto ldfrag = [&](const char* As, const char* Bs, int t, uint4 (&fa)[MT], uint4 (&fb)[4]) {
+    const int ky = t / 3, kx = t - ky * 3;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
+      fa[mt] = *(const uint4*)(As + (q * FHPXP + hp) * 16);
+    }
+  };
+  auto mm = [&](const uint4 (&fa)[MT], const uint4 (&fb)[4]) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        if constexpr (sizeof(T) == 2) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[mt]),
+                                                                __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
+        } else {
+          const uint4 A_ = fa[mt], B_ = fb[nt];
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
+        }
+      }
+  };
+  auto chunk_pipe = [&](const char* As, const char* Bs) {
+    uint4 fa[2][MT], fb[2][4];
+    ldfrag(As, Bs, 0, fa[0], fb[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ldfrag(As, Bs, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+      mm(fa[t & 1], fb[t & 1]);
+    }
+  };
   auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[MT], const uint4 (&fb0)[4]) {
+    if constexpr (PIPE) {
+      chunk_pipe(As, Bs);
+      return;
+    }
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll

@@ -20,17 +20,17 @@
     }                                                                      \
   } while (0)
 
-template <int MODE, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false>
+template <int MODE, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, bool PIPE = false>
 static float run(const FwdArgs& a, dim3 grid, int reps) {
   const int lds = DB ? FWD_LDS_DB : FWD_LDS;
-  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA>, lds);
-  conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA><<<grid, 64 * NW, lds>>>(a);
+  allow_lds(conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA, 0, PIPE>, lds);
+  conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA, 0, PIPE><<<grid, 64 * NW, lds>>>(a);
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0));
-  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA><<<grid, 64 * NW, lds>>>(a);
+  for (int i = 0; i < reps; ++i) conv3x3_fwd_kernel<bf16_t, MODE, DB, NW, SPEC, BDMA, 0, PIPE><<<grid, 64 * NW, lds>>>(a);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -144,13 +144,17 @@ int main(int argc, char** argv) {
   const float tsp = run<0, true, 8, true>(a, grid, reps), tsp5 = run<5, true, 8, true>(a, grid, reps);
   const float tdb4 = run<0, true, 4>(a, grid, reps);
   const float td16 = run<16>(a, grid, reps), td32 = run<32>(a, grid, reps);
+  const float tp4 = run<0, true, 4, false, false, true>(a, grid, reps);
+  const float tp4m = run<5, true, 4, false, false, true>(a, grid, reps);
+  const float tp2 = run<0, false, 4, false, false, true>(a, grid, reps);
   const float tbd8 = run<0, true, 8, false, true>(a, grid, reps), tbd4 = run<0, true, 4, false, true>(a, grid, reps);
   printf("{\"shape\": [%d, %d, %d, %d, %d], \"blocks\": %d", N, H, W, cin, cout, a.ntiles * cout / BN);
   const char* nm[] = {"full", "no_gload", "no_mfma", "no_ldsread", "mfma_only", "tile_fastest", "db8_full",
                       "db8_mfma_only", "w8_2blk_full", "spec_full", "spec_mfma_only", "db4_full", "db8_bdma",
-                      "db4_bdma", "delay2k", "delay5k"};
-  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w, tsp, tsp5, tdb4, tbd8, tbd4, td16, td32};
-  for (int i = 0; i < 16; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+                      "db4_bdma", "delay2k", "delay5k", "db4_pipe",
+                      "db4_pipe_mfma_only", "pipe_2blk"};
+  const float ts[] = {t0, t1, t2, t4, t5, t8, tdb, tdb5, t8w, tsp, tsp5, tdb4, tbd8, tbd4, td16, td32, tp4, tp4m, tp2};
+  for (int i = 0; i < 19; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
   printf("}\n");
   return 0;
 }
