@@ -1,0 +1,180 @@
+// Device-side data path of the training loader.
+//
+// Reference: dataset.py:133-321 (CellDataset.__getitem__), 355-361 (collate_fn).
+// The reference runs all of it per sample on the host with cv2 / numpy /
+// PIL (num_workers=0); at the GPU's img/s that loader is the bottleneck.  Here
+// the decoded uint8 image and the LabelMe polygons go to the device once and
+// everything per-pixel runs in HIP:
+//   rasterize   LabelMe polygons -> semantic mask (instance order, last wins:
+//               dataset.py:197-201; fill rule documented at the kernel)
+//   flip        cv2.flip of image / mask (dataset.py:208-222)
+//   augment_u8  the reference's numpy pixel ops in its order -- brightness
+//               np.clip(img*alpha,0,255).astype(uint8) (:243), contrast
+//               np.clip(img+beta,...) (:251), additive noise (:268), gamma LUT
+//               (:273-276) -- each rounding to uint8 as numpy does (fp64 math)
+//   to_tensor   transforms.ToTensor: HWC uint8 -> CHW float / 255 (:302-305)
+//   resize_u8   cv2.resize INTER_LINEAR-style bilinear (half-pixel centres,
+//               round-half-up); cv2's fixed-point weights are not reproduced.
+// All are HBM-bound byte kernels: one thread per pixel, no reductions.
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+unsigned grid1(long long n) {
+  long long b = (n + NT - 1) / NT;
+  return (unsigned)(b > 65535 ? 65535 : (b < 1 ? 1 : b));
+}
+
+// Fill rule: pixel (x, y) (integer lattice, as cv2.fillPoly's int32 vertices) is inside when
+// the even-odd crossing test at (x + 0.5, y + 0.5) says so, or when it lies on an edge of the
+// polygon (cv2 always paints the outline).  pts: int32 (x, y) pairs; poly_off[i]..poly_off[i+1]
+// the vertices of polygon i; labels[i] in {1 live, 2 dead}.
+__device__ __forceinline__ bool on_segment(int x, int y, int x0, int y0, int x1, int y1) {
+  const long long cr = (long long)(x1 - x0) * (y - y0) - (long long)(y1 - y0) * (x - x0);
+  if (cr != 0) return false;
+  return x >= min(x0, x1) && x <= max(x0, x1) && y >= min(y0, y1) && y <= max(y0, y1);
+}
+
+__global__ __launch_bounds__(NT) void rasterize_kernel(const int* pts, const int* poly_off, const int* labels,
+                                                       int npoly, int h, int w, int64_t* mask) {
+  const long long total = (long long)h * w;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int y = (int)(i / w), x = (int)(i - (long long)y * w);
+    const float px = x + 0.5f, py = y + 0.5f;
+    int64_t v = 0;
+    for (int p = 0; p < npoly; ++p) {
+      const int b = poly_off[p], e = poly_off[p + 1];
+      bool in = false, edge = false;
+      for (int k = b, j = e - 1; k < e; j = k++) {
+        const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
+        edge |= on_segment(x, y, xj, yj, xi, yi);
+        if ((yi > py) != (yj > py)) {
+          const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
+          if (px < xc) in = !in;
+        }
+      }
+      if (in || edge) v = labels[p];
+    }
+    mask[i] = v;
+  }
+}
+
+// flip a [h][w][c] byte image / int64 mask: mode 1 = horizontal (cv2.flip(., 1)), 0 = vertical
+template <typename T>
+__global__ __launch_bounds__(NT) void flip_kernel(const T* src, T* dst, int h, int w, int c, int mode) {
+  const long long total = (long long)h * w * c;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % c);
+    const long long p = i / c;
+    const int y = (int)(p / w), x = (int)(p - (long long)y * w);
+    const int sy = mode == 0 ? h - 1 - y : y, sx = mode == 1 ? w - 1 - x : x;
+    dst[i] = src[((long long)sy * w + sx) * c + ch];
+  }
+}
+
+__device__ __forceinline__ uint8_t clip_u8(double v) {
+  v = v < 0.0 ? 0.0 : (v > 255.0 ? 255.0 : v);
+  return (uint8_t)v;  // astype(np.uint8) truncates
+}
+
+// the numpy pixel ops in the reference's order; flags bit 0 alpha, 1 beta, 2 noise, 3 gamma LUT
+__global__ __launch_bounds__(NT) void augment_kernel(uint8_t* img, long long n, int flags, double alpha,
+                                                     double beta, const float* noise, const uint8_t* lut) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    uint8_t v = img[i];
+    if (flags & 1) v = clip_u8((double)v * alpha);
+    if (flags & 2) v = clip_u8((double)v + beta);
+    if (flags & 4) v = clip_u8((double)((float)v + noise[i]));  // float32 image + float32 noise (:268)
+    if (flags & 8) v = lut[v];
+    img[i] = v;
+  }
+}
+
+// HWC uint8 -> CHW float32 / 255 (transforms.ToTensor), into out[c][h][w]
+__global__ __launch_bounds__(NT) void to_tensor_kernel(const uint8_t* img, int h, int w, int c, float* out) {
+  const long long hw = (long long)h * w, total = hw * c;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i / hw);
+    const long long p = i - ch * hw;
+    out[i] = (float)img[p * c + ch] / 255.f;
+  }
+}
+
+__global__ __launch_bounds__(NT) void resize_u8_kernel(const uint8_t* src, int hi, int wi, int c, uint8_t* dst,
+                                                       int ho, int wo) {
+  const long long total = (long long)ho * wo * c;
+  const float sy = (float)hi / ho, sx = (float)wi / wo;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % c);
+    const long long p = i / c;
+    const int y = (int)(p / wo), x = (int)(p - (long long)y * wo);
+    float fy = (y + 0.5f) * sy - 0.5f, fx = (x + 0.5f) * sx - 0.5f;
+    fy = fy < 0.f ? 0.f : fy;
+    fx = fx < 0.f ? 0.f : fx;
+    int y0 = (int)fy, x0 = (int)fx;
+    y0 = min(y0, hi - 1);
+    x0 = min(x0, wi - 1);
+    const int y1 = min(y0 + 1, hi - 1), x1 = min(x0 + 1, wi - 1);
+    const float ly = fy - y0, lx = fx - x0;
+    const float v = (1.f - ly) * ((1.f - lx) * src[((long long)y0 * wi + x0) * c + ch] +
+                                  lx * src[((long long)y0 * wi + x1) * c + ch]) +
+                    ly * ((1.f - lx) * src[((long long)y1 * wi + x0) * c + ch] +
+                          lx * src[((long long)y1 * wi + x1) * c + ch]);
+    const float r = floorf(v + 0.5f);
+    dst[i] = (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* labels, int npoly, int h, int w,
+                             int64_t* mask, void* stream) {
+  EUNET_REQUIRE(mask && h > 0 && w > 0 && npoly >= 0 && (npoly == 0 || (pts && poly_off && labels)),
+                "rasterize_polygons: bad args");
+  rasterize_kernel<<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(pts, poly_off, labels, npoly, h, w, mask);
+  EUNET_LAUNCH_CHECK("rasterize_polygons");
+  return EUNET_OK;
+}
+
+int eunet_flip_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, int mode, void* stream) {
+  EUNET_REQUIRE(src && dst && src != dst && h > 0 && w > 0 && c > 0 && (mode == 0 || mode == 1),
+                "flip_u8: bad args");
+  flip_kernel<uint8_t><<<grid1((long long)h * w * c), NT, 0, (hipStream_t)stream>>>(src, dst, h, w, c, mode);
+  EUNET_LAUNCH_CHECK("flip_u8");
+  return EUNET_OK;
+}
+
+int eunet_flip_mask(const int64_t* src, int64_t* dst, int h, int w, int mode, void* stream) {
+  EUNET_REQUIRE(src && dst && src != dst && h > 0 && w > 0 && (mode == 0 || mode == 1), "flip_mask: bad args");
+  flip_kernel<int64_t><<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(src, dst, h, w, 1, mode);
+  EUNET_LAUNCH_CHECK("flip_mask");
+  return EUNET_OK;
+}
+
+int eunet_augment_u8(uint8_t* img, long long n, int flags, double alpha, double beta, const float* noise,
+                     const uint8_t* lut, void* stream) {
+  EUNET_REQUIRE(img && n > 0 && (!(flags & 4) || noise) && (!(flags & 8) || lut), "augment_u8: bad args");
+  augment_kernel<<<grid1(n), NT, 0, (hipStream_t)stream>>>(img, n, flags, alpha, beta, noise, lut);
+  EUNET_LAUNCH_CHECK("augment_u8");
+  return EUNET_OK;
+}
+
+int eunet_to_tensor(const uint8_t* img, int h, int w, int c, float* out, void* stream) {
+  EUNET_REQUIRE(img && out && h > 0 && w > 0 && c > 0, "to_tensor: bad args");
+  to_tensor_kernel<<<grid1((long long)h * w * c), NT, 0, (hipStream_t)stream>>>(img, h, w, c, out);
+  EUNET_LAUNCH_CHECK("to_tensor");
+  return EUNET_OK;
+}
+
+int eunet_resize_u8(const uint8_t* src, int hi, int wi, int c, uint8_t* dst, int ho, int wo, void* stream) {
+  EUNET_REQUIRE(src && dst && hi > 0 && wi > 0 && ho > 0 && wo > 0 && c > 0, "resize_u8: bad args");
+  resize_u8_kernel<<<grid1((long long)ho * wo * c), NT, 0, (hipStream_t)stream>>>(src, hi, wi, c, dst, ho, wo);
+  EUNET_LAUNCH_CHECK("resize_u8");
+  return EUNET_OK;
+}
+
+}  // extern "C"

@@ -80,6 +80,12 @@ SIGNATURES = {
     "eunet_gate_bwd3": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
                         _f, _f, c_void_p],
     "eunet_dropout_affine": [_f, _f, _f, c_int, c_int, c_float, _f, _f, _f, c_void_p],
+    "eunet_rasterize_polygons": [_f, _f, _f, c_int, c_int, c_int, _f, c_void_p],
+    "eunet_flip_u8": [_f, _f, c_int, c_int, c_int, c_int, c_void_p],
+    "eunet_flip_mask": [_f, _f, c_int, c_int, c_int, c_void_p],
+    "eunet_augment_u8": [_f, c_int64, c_int, ctypes.c_double, ctypes.c_double, _f, _f, c_void_p],
+    "eunet_to_tensor": [_f, c_int, c_int, c_int, _f, c_void_p],
+    "eunet_resize_u8": [_f, c_int, c_int, c_int, _f, c_int, c_int, c_void_p],
     "eunet_consistency_tiles": [c_int, c_int, POINTER(c_int)],
     "eunet_consistency_fwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, c_void_p],
     "eunet_consistency_bwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, _f, _f,

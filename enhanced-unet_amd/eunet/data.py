@@ -1,0 +1,164 @@
+"""Device-side loader mirroring the reference CellDataset (dataset.py:21-361).
+
+    CellDataset(data_dir, split='train', transform=None, max_size=1024, device='cuda')
+    collate_fn(batch) -> {'images': [B,3,H,W] (device), 'batch_items': [...]}   # dataset.py:355-361
+
+Same file split (sorted *.jpg, 70/15/15, dataset.py:37-51), the same resize-to-/32
+sizes (:141-157), LabelMe 'live'/'dead' polygons scaled and truncated to int32 as the
+reference does (:173-188), the semantic mask with later instances overwriting earlier
+ones (:197-201), and the training augmentations drawn from Python's `random` in the
+reference's order, so a seeded run takes the same decisions (:204-294).  Per pixel
+everything runs in HIP (datapath.hip): polygon rasterisation, flips, the numpy pixel
+ops (brightness, contrast, noise, gamma LUT -- bit-exact with the reference's numpy
+lines), ToTensor.  Image decode stays PIL on the host (I/O).
+
+Not built (cv2 is absent, so their parity cannot be pinned): the cell-specific
+preprocessing (:58-131, LAB/CLAHE/Sobel/Laplacian/GaussianBlur), the HSV saturation,
+CLAHE, sharpening and HSV jitter augmentations (:255-294).  Their random draws are
+still consumed so the remaining decisions stay aligned with the reference's stream.
+cv2.fillPoly and cv2.resize are replaced by the kernels' documented rules (unpinned).
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+def reference_sizes(h: int, w: int, max_size: int):
+    """dataset.py:141-157: target (h, w) multiples of 32."""
+    if max(h, w) > max_size:
+        scale = max_size / max(h, w)
+        nh, nw = int(h * scale), int(w * scale)
+        return (nh // 32) * 32, (nw // 32) * 32
+    return (h // 32) * 32, (w // 32) * 32
+
+
+def gamma_lut(gamma: float) -> np.ndarray:
+    """dataset.py:273-275."""
+    inv_gamma = 1.0 / gamma
+    return np.array([((i / 255.0) ** inv_gamma) * 255 for i in np.arange(0, 256)]).astype(np.uint8)
+
+
+def load_labelme(json_path: str, scale_h: float, scale_w: float):
+    """dataset.py:161-195: (int32 polygons, labels 0 live / 1 dead, bboxes)."""
+    with open(json_path, "r", encoding="utf-8") as f:
+        ann = json.load(f)
+    polys, labels, bboxes = [], [], []
+    for shape in ann.get("shapes", []):
+        label = shape["label"].lower()
+        if label not in ("live", "dead"):
+            continue
+        pts = np.array(shape["points"], dtype=np.float32)
+        pts[:, 0] *= scale_w
+        pts[:, 1] *= scale_h
+        pts = pts.astype(np.int32)
+        polys.append(pts)
+        labels.append(0 if label == "live" else 1)
+        x_min, y_min = pts.min(axis=0)
+        x_max, y_max = pts.max(axis=0)
+        bboxes.append([x_min, y_min, x_max, y_max])
+    return polys, labels, bboxes
+
+
+class CellDataset:
+    def __init__(self, data_dir: str, split: str = "train", transform=None, max_size: int = 1024,
+                 device: str = "cuda"):
+        self.data_dir, self.split, self.transform, self.max_size = data_dir, split, transform, max_size
+        self.device = device
+        all_files = sorted(f for f in os.listdir(data_dir) if f.endswith(".jpg"))
+        n_total = len(all_files)
+        n_train, n_val = int(n_total * 0.7), int(n_total * 0.15)
+        if split == "train":
+            self.files = all_files[:n_train]
+        elif split == "val":
+            self.files = all_files[n_train:n_train + n_val]
+        else:
+            self.files = all_files[n_train + n_val:]
+
+    def __len__(self):
+        return len(self.files)
+
+    def _augment(self, img, mask):
+        """dataset.py:204-294 in order; img HWC uint8 and mask int64 on the device."""
+        if random.random() > 0.5:
+            img, mask = ops.flip_u8(img, 1), ops.flip_mask(mask, 1)
+        if random.random() > 0.5:
+            img, mask = ops.flip_u8(img, 0), ops.flip_mask(mask, 0)
+        c = ops.semantic_counts(mask.reshape(1, -1), mask.reshape(1, -1))[0, :, 0].tolist()  # #pixels per class
+        total = c[1] + c[2]
+        live_ratio = c[1] / total if total > 0 else 0.5
+        if random.random() > 0.3:
+            if live_ratio > 0.6:
+                alpha = random.uniform(0.8, 1.3)
+            elif live_ratio < 0.4:
+                alpha = random.uniform(0.6, 1.1)
+            else:
+                alpha = random.uniform(0.7, 1.3)
+            ops.augment_u8(img, alpha=alpha)
+        if random.random() > 0.3:
+            beta = random.uniform(-20, 40) if live_ratio < 0.4 else random.uniform(-30, 30)
+            ops.augment_u8(img, beta=beta)
+        if random.random() > 0.5:  # HSV saturation (cv2): not built, draw consumed
+            random.uniform(0.8, 1.3)
+        if random.random() > 0.4:  # CLAHE (cv2): not built, draw consumed
+            random.uniform(1.5, 3.0)
+        if random.random() > 0.5:
+            sigma = random.uniform(3, 10)
+            noise = np.random.normal(0, sigma, tuple(img.shape)).astype(np.float32)
+            ops.augment_u8(img, noise=torch.from_numpy(noise).to(img.device))
+        if random.random() > 0.5:
+            lut = torch.from_numpy(gamma_lut(random.uniform(0.7, 1.3))).to(img.device)
+            ops.augment_u8(img, lut=lut)
+        if random.random() > 0.6:  # sharpening (cv2.filter2D): not built, draw consumed
+            random.uniform(0.1, 0.3)
+        if random.random() > 0.6:  # HSV jitter (cv2): not built, draws consumed
+            random.uniform(-10, 10)
+            random.uniform(0.9, 1.1)
+        return img, mask
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        name = self.files[idx]
+        image = np.array(Image.open(os.path.join(self.data_dir, name)).convert("RGB"))
+        original_size = image.shape[:2]
+        img = torch.from_numpy(image).to(self.device)
+        h, w = reference_sizes(*original_size, self.max_size)
+        if (h, w) != tuple(original_size):
+            img = ops.resize_u8(img, h, w)
+        polys, labels, bboxes = load_labelme(os.path.join(self.data_dir, name.replace(".jpg", ".json")),
+                                             h / original_size[0], w / original_size[1])
+        mask = ops.rasterize_polygons(polys, [l + 1 for l in labels], h, w, img.device)
+        if self.split == "train":
+            img, mask = self._augment(img.contiguous(), mask)
+        tensor = self.transform(img) if self.transform else ops.to_tensor(img)
+        return {"image": tensor, "instance_polygons": polys, "instance_labels": labels, "bboxes": bboxes,
+                "semantic_mask": mask, "image_id": name, "original_size": original_size}
+
+
+def collate_fn(batch):
+    """dataset.py:355-361."""
+    return {"images": torch.stack([item["image"] for item in batch]), "batch_items": batch}
+
+
+class DataLoader:
+    """Minimal in-order / shuffled batch iterator over a CellDataset (num_workers=0 like the
+    reference's train_model loaders, train_eval.py:1073-1077)."""
+
+    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, collate_fn=collate_fn):
+        self.dataset, self.batch_size, self.shuffle, self.collate_fn = dataset, batch_size, shuffle, collate_fn
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        idx = list(range(len(self.dataset)))
+        if self.shuffle:
+            random.shuffle(idx)
+        for i in range(0, len(idx), self.batch_size):
+            yield self.collate_fn([self.dataset[j] for j in idx[i:i + self.batch_size]])

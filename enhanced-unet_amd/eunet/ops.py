@@ -358,3 +358,55 @@ def consistency_bwd(fused, b0, b1, c0, c1, gloss, gfused, g0, g1):
     n, k, h, w = fused.shape
     call("eunet_consistency_bwd", _ptr(fused), _ptr(b0), _ptr(b1), n, k, h, w, float(c0), float(c1), _ptr(gloss),
          _ptr(gfused), _ptr(g0), _ptr(g1), _stream())
+
+
+# ---- device-side data path (datapath.hip) ---------------------------------------------
+def rasterize_polygons(polys, labels, h, w, device):
+    """polys: list of int32 [n_i, 2] (x, y) arrays; labels: ints (1 live, 2 dead) -> int64 [h, w]."""
+    mask = torch.empty(h, w, dtype=torch.int64, device=device)
+    if not polys:
+        call("eunet_rasterize_polygons", None, None, None, 0, h, w, _ptr(mask), _stream())
+        return mask
+    import numpy as np
+    pts = torch.from_numpy(np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in polys])).to(device)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in polys])]).astype(np.int32), device=device)
+    lab = torch.tensor(np.asarray(labels, np.int32), device=device)
+    call("eunet_rasterize_polygons", _ptr(pts), _ptr(off), _ptr(lab), len(polys), h, w, _ptr(mask), _stream())
+    return mask
+
+
+def flip_u8(img, mode: int):
+    out = torch.empty_like(img)
+    h, w, c = img.shape
+    call("eunet_flip_u8", _ptr(img.contiguous()), _ptr(out), h, w, c, int(mode), _stream())
+    return out
+
+
+def flip_mask(mask, mode: int):
+    out = torch.empty_like(mask)
+    h, w = mask.shape
+    call("eunet_flip_mask", _ptr(mask.contiguous()), _ptr(out), h, w, int(mode), _stream())
+    return out
+
+
+def augment_u8(img, alpha=None, beta=None, noise=None, lut=None):
+    """In-place on a contiguous uint8 device tensor (reference order: alpha, beta, noise, LUT)."""
+    flags = (1 if alpha is not None else 0) | (2 if beta is not None else 0) | \
+        (4 if noise is not None else 0) | (8 if lut is not None else 0)
+    call("eunet_augment_u8", _ptr(img), img.numel(), flags, float(alpha or 0.0), float(beta or 0.0),
+         _ptr(noise), _ptr(lut), _stream())
+    return img
+
+
+def to_tensor(img):
+    h, w, c = img.shape
+    out = torch.empty(c, h, w, dtype=torch.float32, device=img.device)
+    call("eunet_to_tensor", _ptr(img.contiguous()), h, w, c, _ptr(out), _stream())
+    return out
+
+
+def resize_u8(img, ho, wo):
+    hi, wi, c = img.shape
+    out = torch.empty(ho, wo, c, dtype=torch.uint8, device=img.device)
+    call("eunet_resize_u8", _ptr(img.contiguous()), hi, wi, c, _ptr(out), ho, wo, _stream())
+    return out

@@ -279,6 +279,28 @@ int eunet_consistency_bwd(const float* fused, const float* br0, const float* br1
                           int h, int w, float c0, float c1, const float* gloss, float* gfused,
                           float* g0, float* g1, void* stream);
 
+/* ---- device-side data path (datapath.hip; dataset.py:133-321) ----------------
+ * rasterize: LabelMe polygons (int32 (x, y) vertices as dataset.py:185-188 truncates them;
+ * polygon i = pts[poly_off[i] .. poly_off[i+1]), label 1 live / 2 dead) -> int64 semantic
+ * mask [h][w], later polygons overwrite earlier ones (dataset.py:197-201).  Fill rule:
+ * even-odd at the pixel centre, plus every lattice pixel on an edge. */
+int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* labels, int npoly,
+                             int h, int w, int64_t* mask, void* stream);
+/* cv2.flip (dataset.py:208-222): mode 1 horizontal, 0 vertical; HWC uint8 / int64 mask */
+int eunet_flip_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, int mode, void* stream);
+int eunet_flip_mask(const int64_t* src, int64_t* dst, int h, int w, int mode, void* stream);
+/* numpy pixel augmentations in the reference's order, each rounded to uint8 as numpy does:
+ * flags bit0 brightness (:243), bit1 contrast (:251), bit2 + noise[n] fp32 (:266-268),
+ * bit3 gamma LUT[256] (:273-276) */
+int eunet_augment_u8(uint8_t* img, long long n, int flags, double alpha, double beta,
+                     const float* noise, const uint8_t* lut, void* stream);
+/* transforms.ToTensor (dataset.py:302-305): HWC uint8 -> CHW float32 / 255 */
+int eunet_to_tensor(const uint8_t* img, int h, int w, int c, float* out, void* stream);
+/* bilinear uint8 resize with cv2 INTER_LINEAR's half-pixel mapping (dataset.py:145-157);
+ * cv2's fixed-point weights are not reproduced (parity unpinned: cv2 is absent) */
+int eunet_resize_u8(const uint8_t* src, int hi, int wi, int c, uint8_t* dst, int ho, int wo,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+"""Device-side data path (datapath.hip) vs the reference loader's numpy expressions (oracle/data_ref.py).
+
+Pixel ops, flips and ToTensor are bit-exact; the polygon fill is checked against the
+build's documented rule (cv2.fillPoly itself is absent: parity unpinned).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import data_ref as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _img(seed, h=37, w=53):
+    return np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("alpha,beta,sigma,g", [(1.13, 17.4, 6.0, 0.8), (0.61, -25.0, 9.5, 1.27), (1.3, 39.9, 3.1, 1.0)])
+def test_pixel_augmentations_bit_exact(alpha, beta, sigma, g):
+    from eunet import data, ops
+    img = _img(1)
+    noise = np.random.default_rng(2).normal(0, sigma, img.shape).astype(np.float32)
+    ref = O.gamma(O.add_noise(O.contrast(O.brightness(img, alpha), beta), noise), g)
+    d = torch.from_numpy(img).to(DEV)
+    ops.augment_u8(d, alpha=alpha)
+    ops.augment_u8(d, beta=beta)
+    ops.augment_u8(d, noise=torch.from_numpy(noise).to(DEV))
+    ops.augment_u8(d, lut=torch.from_numpy(data.gamma_lut(g)).to(DEV))
+    assert np.array_equal(d.cpu().numpy(), ref)
+
+
+def test_flips_and_to_tensor_exact():
+    from eunet import ops
+    img = _img(3)
+    d = torch.from_numpy(img).to(DEV)
+    assert np.array_equal(ops.flip_u8(d, 1).cpu().numpy(), img[:, ::-1])
+    assert np.array_equal(ops.flip_u8(d, 0).cpu().numpy(), img[::-1])
+    m = torch.randint(0, 3, (37, 53), dtype=torch.int64)
+    assert torch.equal(ops.flip_mask(m.to(DEV), 1).cpu(), m.flip(1))
+    assert np.array_equal(ops.to_tensor(d).cpu().numpy(), O.to_tensor(img))
+
+
+def test_rasterize_matches_rule():
+    from eunet import ops
+    rng = np.random.default_rng(4)
+    polys, labels = [], []
+    for i in range(12):
+        c = rng.uniform(5, 60, 2)
+        ang = np.sort(rng.uniform(0, 2 * np.pi, rng.integers(3, 12)))
+        r = rng.uniform(2, 14, len(ang))
+        pts = np.stack([c[0] + r * np.cos(ang), c[1] + r * np.sin(ang)], 1).astype(np.float32).astype(np.int32)
+        polys.append(pts)
+        labels.append(1 + (i % 2))
+    polys.append(np.array([[10, 10], [20, 10], [20, 20], [10, 20]], np.int32))  # axis-aligned square
+    labels.append(1)
+    m = ops.rasterize_polygons(polys, labels, 64, 72, DEV).cpu().numpy()
+    ref = O.rasterize(polys, labels, 64, 72)
+    assert np.array_equal(m, ref)
+    assert (m[10:21, 10:21] == 1).all()  # a square's outline and interior are filled
+
+
+def test_cell_dataset_end_to_end(tmp_path):
+    """LabelMe directory -> device batches; same split, sizes and seeded augmentation decisions."""
+    from PIL import Image
+    from eunet.data import CellDataset, DataLoader, reference_sizes
+    rng = np.random.default_rng(5)
+    for i in range(10):
+        im = rng.integers(0, 256, (100, 130, 3), dtype=np.uint8)
+        Image.fromarray(im).save(tmp_path / f"img{i:02d}.jpg", quality=95)
+        shapes = [{"label": "Live", "points": [[10, 10], [40, 12], [35, 40], [12, 35]]},
+                  {"label": "dead", "points": [[60, 50], [90, 55], [70, 80]]},
+                  {"label": "debris", "points": [[0, 0], [5, 0], [5, 5]]}]
+        (tmp_path / f"img{i:02d}.json").write_text(json.dumps({"shapes": shapes}))
+    ds = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV)
+    assert len(ds) == 7 and len(CellDataset(str(tmp_path), "val", device=DEV)) == 1
+    random.seed(11)
+    np.random.seed(11)
+    item = ds[0]
+    h, w = reference_sizes(100, 130, 640)
+    assert item["image"].shape == (3, h, w) and item["semantic_mask"].shape == (h, w)
+    assert item["instance_labels"] == [0, 1]
+    assert set(torch.unique(item["semantic_mask"]).tolist()) <= {0, 1, 2}
+    assert float(item["image"].min()) >= 0.0 and float(item["image"].max()) <= 1.0
+    batch = next(iter(DataLoader(CellDataset(str(tmp_path), "val", device=DEV), batch_size=1)))
+    assert batch["images"].shape == (1, 3, h, w) and batch["images"].is_cuda

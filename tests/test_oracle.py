@@ -212,3 +212,14 @@ def test_dual_train_step_matches_reference(golden_dir):
                 flat = arr.reshape(-1)
                 ref_norm = float(g[f"{tag}_norm:{k}"])
                 assert abs(np.sqrt((flat ** 2).sum()) - ref_norm) < 1e-3 * ref_norm, (tag, k)
+
+
+def test_data_oracle_rules():
+    """oracle/data_ref.py: the reference's numpy pixel lines and the documented fill rule."""
+    from oracle import data_ref as O
+    img = np.arange(256, dtype=np.uint8).reshape(16, 16, 1)
+    assert O.brightness(img, 2.0)[15, 15, 0] == 255 and O.brightness(img, 0.5)[0, 3, 0] == 1
+    assert O.contrast(img, -10.0)[0, 5, 0] == 0
+    assert (O.gamma(img, 1.0) == img).all()
+    sq = O.rasterize([np.array([[2, 2], [5, 2], [5, 5], [2, 5]])], [2], 8, 8)
+    assert sq.sum() == 2 * 16 and (sq[2:6, 2:6] == 2).all()
