@@ -158,8 +158,9 @@ struct SmallWgArgs {
 
 // direct-conv wgrad as MFMA: dW[co][ci*9+t] = sum_p dY[p][co] im2col(x)[p][ci*9+t];
 // im2col (cin*9 columns padded to njt*16 <= 80) and the dY tile are staged in LDS per 8x32 tile
-template <typename T>
+template <typename T, int CI>  // CI = max input channels of the instance (4: enc1.0, 8: fusion_head.0)
 __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
+  constexpr int SCI = CI, SJT = (CI * 9 + 15) / 16;  // LDS sized per instance (occupancy)
   constexpr int E = Vec16<T>::N;
   __shared__ float xs[(STH + 2) * (STW + 2) * SCI];
   __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];         // dY tile [256 px][64 co]
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(const float* st, int tiles, int C, const float* gamma,
                                                          const float* beta, float eps, float mom, float* rm,
                                                          float* rv, float* mean_o, float* invstd_o, float* scale_o,
-                                                         float* shift_o) {
+                                                         float* shift_o, long long* nbt) {
   __shared__ double sh[NT];
   __shared__ double shb[2];
   const int c = blockIdx.x, tid = threadIdx.x;
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(const float* st, int ti
   }
   m2 = block_sum(m2);
   (void)shb;
+  if (tid == 0 && c == 0 && nbt != nullptr) *nbt += 1;  // BatchNorm2d.num_batches_tracked
   if (tid == 0) {
     const double var_b = m2 / n;
     const double var_u = n > 1.0 ? m2 / (n - 1.0) : var_b;
@@ -534,7 +536,8 @@ __global__ __launch_bounds__(NT) void colsum_stage1(const float* part, int rows,
   if (rg == 0 && col < cols) ws[(long long)blockIdx.y * cols + col] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
 }
 
-__global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, int cols, float* out) {
+__global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, int cols, float* out, int split,
+                                                    float* out_hi) {
   __shared__ double sh[4][64];
   const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int col = blockIdx.x * 64 + cl;
@@ -543,7 +546,13 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
     for (int r = rg; r < rb; r += 4) s += ws[(long long)r * cols + col];
   sh[rg][cl] = s;
   __syncthreads();
-  if (rg == 0 && col < cols) out[col] = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
+  if (rg == 0 && col < cols) {
+    const float v = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
+    if (out_hi != nullptr && col >= split)
+      out_hi[col - split] = v;
+    else
+      out[col] = v;
+  }
 }
 
 // gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [gamma xhat + beta > 0], folded per
@@ -807,12 +816,13 @@ static int colsum_rb(int rows) {
 
 size_t eunet_colsum_ws(int rows, int cols) { return (size_t)colsum_rb(rows) * cols * sizeof(double); }
 
-int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s) {
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s, int split,
+                    float* out_hi) {
   EUNET_REQUIRE(part && out && ws && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
   const int rb = colsum_rb(rows);
   const int chunk = cdiv(rows, rb);
   colsum_stage1<<<dim3(cdiv(cols, 64), rb), NT, 0, s>>>(part, rows, cols, ld, chunk, (double*)ws);
-  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, out);
+  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, out, split, out_hi);
   EUNET_LAUNCH_CHECK("colsum");
   return EUNET_OK;
 }
@@ -863,19 +873,26 @@ int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_pa
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv_small_wgrad: nsplit mismatch");
   dim3 grid(nsplit, cdiv(dy->c, 64));
   if (x->dtype == EUNET_BF16)
-    conv_small_wgrad_kernel<bf16_t><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    if (x->c <= 4)
+      conv_small_wgrad_kernel<bf16_t, 4><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    else
+      conv_small_wgrad_kernel<bf16_t, 8><<<grid, NT, 0, (hipStream_t)stream>>>(a);
   else
-    conv_small_wgrad_kernel<float><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    if (x->c <= 4)
+      conv_small_wgrad_kernel<float, 4><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    else
+      conv_small_wgrad_kernel<float, 8><<<grid, NT, 0, (hipStream_t)stream>>>(a);
   EUNET_LAUNCH_CHECK("conv_small_wgrad");
   return EUNET_OK;
 }
 
 int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, const float* beta, float eps,
                       float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
-                      float* shift, void* stream) {
+                      float* shift, int64_t* num_batches_tracked, void* stream) {
   EUNET_REQUIRE(stats && tiles > 0 && c > 0 && gamma && beta, "bn_finalize: bad args");
   bn_finalize_kernel<<<c, NT, 0, (hipStream_t)stream>>>(stats, tiles, c, gamma, beta, eps, momentum, run_mean,
-                                                        run_var, mean, invstd, scale, shift);
+                                                        run_var, mean, invstd, scale, shift,
+                                                        (long long*)num_batches_tracked);
   EUNET_LAUNCH_CHECK("bn_finalize");
   return EUNET_OK;
 }
@@ -990,6 +1007,12 @@ int eunet_colsum_ws_bytes(int rows, int cols, size_t* bytes) {
 
 int eunet_colsum(const float* part, int rows, int cols, float* out, void* ws, void* stream) {
   return eunet_colsum_ld(part, rows, cols, cols, out, ws, (hipStream_t)stream);
+}
+
+int eunet_colsum_split(const float* part, int rows, int cols, int split, float* out_lo, float* out_hi, void* ws,
+                       void* stream) {
+  EUNET_REQUIRE(out_hi && split > 0 && split < cols, "colsum_split: bad split");
+  return eunet_colsum_ld(part, rows, cols, cols, out_lo, ws, (hipStream_t)stream, split, out_hi);
 }
 
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,

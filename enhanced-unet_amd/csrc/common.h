@@ -129,6 +129,11 @@ __device__ __forceinline__ void up2_src(int o, int in, int& i0, int& i1, float& 
   l1 = s - (float)i0;
 }
 
+// deterministic fp64 column sum of a [rows][ld] partial matrix (bn_pool_up.hip); columns
+// >= split go to out_hi[col - split] when out_hi != nullptr
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s,
+                    int split = 0, float* out_hi = nullptr);
+
 // kernels with > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
 template <typename K>
 inline void allow_lds(K* kernel, size_t bytes) {

@@ -1146,11 +1146,8 @@ WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
 
 }  // namespace
 
-extern "C" int eunet_bn_finalize(const float*, int, int, const float*, const float*, float, float, float*, float*,
-                                 float*, float*, float*, float*, void*);
 extern "C" int eunet_bn_eval_affine(int, const float*, const float*, const float*, const float*, float, float*,
                                     float*, void*);
-int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s);
 extern "C" int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream);
 
 #define HEAD_DISPATCH(KERNEL, ...)                  \
@@ -1198,7 +1195,7 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     else HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_stats");
     int rc = eunet_bn_finalize(a.stats, L.grid, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
-                               wsf + L.scale, wsf + L.shift, stream);
+                               wsf + L.scale, wsf + L.shift, nullptr, stream);
     if (rc) return rc;
   } else {
     EUNET_REQUIRE(run_mean && run_var, "head_fwd: eval needs running stats");

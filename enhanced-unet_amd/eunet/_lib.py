@@ -39,7 +39,7 @@ SIGNATURES = {
     "eunet_conv_small_fwd": [_P, _f, _f, _P, _f, c_void_p],
     "eunet_conv_small_wgrad_splits": [_P, POINTER(c_int)],
     "eunet_conv_small_wgrad": [_P, _P, _f, _f, c_int, c_void_p],
-    "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_bn_eval_affine": [c_int, _f, _f, _f, _f, c_float, _f, _f, c_void_p],
     "eunet_bnrelu_pool": [_P, _f, _f, _P, _P, c_void_p],
     "eunet_bnrelu_upsample": [_P, _f, _f, _P, c_void_p],
@@ -56,6 +56,7 @@ SIGNATURES = {
     "eunet_bn_bwd_reduce": [_P, _P, _f, _f, _f, _f, _f, c_void_p],
     "eunet_colsum_ws_bytes": [c_int, c_int, POINTER(c_size_t)],
     "eunet_colsum": [_f, c_int, c_int, _f, _f, c_void_p],
+    "eunet_colsum_split": [_f, c_int, c_int, c_int, _f, _f, _f, c_void_p],
     "eunet_bn_bwd_apply": [_P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
     "eunet_pool_bwd_add": [_P, _P, _P, _P, c_void_p],
     "eunet_upsample_bwd": [_P, _P, c_void_p],

@@ -128,13 +128,11 @@ class DualEngine:
             part = _e(tiles * 2 * C, torch.float32, dev)
             ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
                               P[prefix + ".bias"], part)
-        red = _e(2 * C, torch.float32, dev)
-        ops.colsum(part, tiles, 2 * C, red)
-        sink.slot(prefix + ".bias", (C,)).copy_(red[:C])
-        sink.slot(prefix + ".weight", (C,)).copy_(red[C:])
+        dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
+        ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
         gy = torch.empty_like(y)
         ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                         P[prefix + ".bias"], red[:C], red[C:], ops.act(gy))
+                         P[prefix + ".bias"], dbeta, dgamma, ops.act(gy))
         return gy
 
     def _wgrad(self, name, xa: ops.Act, gy, sink, d=None):

@@ -81,8 +81,8 @@ class UNetEngine:
         if training:
             mean, invstd = _e(C, torch.float32, dev), _e(C, torch.float32, dev)
             ops.bn_finalize(stats, tiles, C, P[prefix + ".weight"], P[prefix + ".bias"], BN_EPS, BN_MOMENTUM,
-                            B[prefix + ".running_mean"], B[prefix + ".running_var"], mean, invstd, scale, shift)
-            B[prefix + ".num_batches_tracked"].add_(1)
+                            B[prefix + ".running_mean"], B[prefix + ".running_var"], mean, invstd, scale, shift,
+                            B[prefix + ".num_batches_tracked"])
             return dict(mean=mean, invstd=invstd, scale=scale, shift=shift)
         ops.bn_eval_affine(P[prefix + ".weight"], P[prefix + ".bias"], B[prefix + ".running_mean"],
                            B[prefix + ".running_var"], BN_EPS, scale, shift)
@@ -197,7 +197,6 @@ class UNetEngine:
         ya, yb, bna, bnb, X = s["ya"], s["yb"], s["bna"], s["bnb"], s["X"]
         N, H, W, C = yb.shape
         dev, dt = yb.device, self.dtype
-        red = _e(2 * C, torch.float32, dev)
 
         def bn_back(prefix, g, y, bn, part=None, tiles=0):
             if part is None:  # reduction not fused into the producer of g
@@ -205,12 +204,11 @@ class UNetEngine:
                 part = _e(tiles * 2 * C, torch.float32, dev)
                 ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
                                   P[prefix + ".bias"], part)
-            ops.colsum(part, tiles, 2 * C, red)
-            sink.slot(prefix + ".bias", (C,)).copy_(red[:C])
-            sink.slot(prefix + ".weight", (C,)).copy_(red[C:])
+            dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
+            ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
             gy = torch.empty_like(y)
             ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                             P[prefix + ".bias"], red[:C], red[C:], ops.act(gy))
+                             P[prefix + ".bias"], dbeta, dgamma, ops.act(gy))
             return gy
 
         def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False):

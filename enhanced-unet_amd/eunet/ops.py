@@ -123,9 +123,11 @@ def conv_small_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit):
          _stream())
 
 
-def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, scale, shift):
+def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, scale, shift,
+                num_batches_tracked=None):
     call("eunet_bn_finalize", _ptr(stats), tiles, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
-         _ptr(run_mean), _ptr(run_var), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _stream())
+         _ptr(run_mean), _ptr(run_var), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift),
+         _ptr(num_batches_tracked), _stream())
 
 
 def bn_eval_affine(gamma, beta, run_mean, run_var, eps, scale, shift):
@@ -196,11 +198,15 @@ def bn_bwd_reduce(g: Act, y: Act, mean, invstd, gamma, beta, part):
          _ptr(beta), _ptr(part), _stream())
 
 
-def colsum(part, rows, cols, out):
+def colsum(part, rows, cols, out, split=None, out_hi=None):
+    """Column sums of part [rows][cols] -> out (or out[:split] / out_hi[:cols - split])."""
     b = c_size_t()
     call("eunet_colsum_ws_bytes", rows, cols, ctypes.byref(b))
     ws = torch.empty(b.value, dtype=torch.uint8, device=part.device)
-    call("eunet_colsum", _ptr(part), rows, cols, _ptr(out), _ptr(ws), _stream())
+    if out_hi is None:
+        call("eunet_colsum", _ptr(part), rows, cols, _ptr(out), _ptr(ws), _stream())
+    else:
+        call("eunet_colsum_split", _ptr(part), rows, cols, int(split), _ptr(out), _ptr(out_hi), _ptr(ws), _stream())
 
 
 def bn_bwd_apply(g: Act, y: Act, mean, invstd, gamma, beta, dbeta, dgamma, gy: Act):

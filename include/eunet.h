@@ -101,10 +101,12 @@ int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_pa
 /* ---- BatchNorm2d train-mode statistics (models.py:220,223; eps 1e-5, momentum 0.1)
  * combine per-tile (sum, M2, count) partials (Chan, fp64); update running
  * stats with the UNBIASED variance; emit mean, invstd and the fused affine
- * scale = gamma*invstd, shift = beta - mean*scale. */
+ * scale = gamma*invstd, shift = beta - mean*scale; num_batches_tracked (nullable,
+ * int64) is incremented on the device. */
 int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, const float* beta,
                       float eps, float momentum, float* run_mean, float* run_var, float* mean,
-                      float* invstd, float* scale, float* shift, void* stream);
+                      float* invstd, float* scale, float* shift, int64_t* num_batches_tracked,
+                      void* stream);
 /* eval-mode affine from running stats */
 int eunet_bn_eval_affine(int c, const float* gamma, const float* beta, const float* run_mean,
                          const float* run_var, float eps, float* scale, float* shift, void* stream);
@@ -168,6 +170,10 @@ int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mea
 /* deterministic column sum of a [rows][cols] fp32 partial matrix (fp64 two-stage) */
 int eunet_colsum_ws_bytes(int rows, int cols, size_t* bytes);
 int eunet_colsum(const float* part, int rows, int cols, float* out, void* ws, void* stream);
+/* the same with columns >= split written to out_hi[col - split] (e.g. dbeta | dgamma straight
+ * into their two gradient slots) */
+int eunet_colsum_split(const float* part, int rows, int cols, int split, float* out_lo,
+                       float* out_hi, void* ws, void* stream);
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean,
                        const float* invstd, const float* gamma, const float* beta,
                        const float* dbeta, const float* dgamma, const eunet_act* gy,
