@@ -682,6 +682,65 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
   *(uint4*)(o + ((long long)(n * h + y) * w + x) * oct + oco + c) = Vec16<TO>::pack(acc);
 }
 
+// 2x2 low-res outputs per thread: the 6x6 high-res window they share is read once (36 vector
+// loads instead of 4 x 16), separable adjoint weights per row / column
+template <typename T, typename TO>
+__global__ __launch_bounds__(256) void up_bwd2x2_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
+                                                        int h, int w, int C) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w, hb = (h + 1) / 2, wb = (w + 1) / 2;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * hb * wb * U) return;
+  const int u = (int)(id % U);
+  long long p = id / U;
+  const int xb = (int)(p % wb); p /= wb;
+  const int yb = (int)(p % hb);
+  const int n = (int)(p / hb);
+  const int c = u * E, y0 = 2 * yb, x0 = 2 * xb;
+  float acc[2][2][E];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < E; ++j) acc[a][b][j] = 0.f;
+  float wxs[6][2];
+#pragma unroll
+  for (int dx = 0; dx < 6; ++dx) {
+    const int ox = 2 * x0 - 1 + dx;
+    const bool ok = ox >= 0 && ox < W2;
+    wxs[dx][0] = ok ? up2_adj_w(ox, w, x0) : 0.f;
+    wxs[dx][1] = ok && x0 + 1 < w ? up2_adj_w(ox, w, x0 + 1) : 0.f;
+  }
+#pragma unroll
+  for (int dy = 0; dy < 6; ++dy) {
+    const int oy = 2 * y0 - 1 + dy;
+    if (oy < 0 || oy >= H2) continue;
+    const float wy0 = up2_adj_w(oy, h, y0), wy1 = y0 + 1 < h ? up2_adj_w(oy, h, y0 + 1) : 0.f;
+#pragma unroll
+    for (int dx = 0; dx < 6; ++dx) {
+      const int ox = 2 * x0 - 1 + dx;
+      if (ox < 0 || ox >= W2) continue;
+      float f[E];
+      Vec16<T>::unpack(*(const uint4*)(g + ((long long)(n * H2 + oy) * W2 + ox) * gct + gco + c), f);
+      const float w00 = wy0 * wxs[dx][0], w01 = wy0 * wxs[dx][1], w10 = wy1 * wxs[dx][0], w11 = wy1 * wxs[dx][1];
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        acc[0][0][j] = fmaf(w00, f[j], acc[0][0][j]);
+        acc[0][1][j] = fmaf(w01, f[j], acc[0][1][j]);
+        acc[1][0][j] = fmaf(w10, f[j], acc[1][0][j]);
+        acc[1][1][j] = fmaf(w11, f[j], acc[1][1][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (y0 + a < h && x0 + b < w)
+        *(uint4*)(o + ((long long)(n * h + y0 + a) * w + x0 + b) * oct + oco + c) = Vec16<TO>::pack(acc[a][b]);
+}
+
 // fp32 K-channel (K <= 4) upsample backward for the head: g [N,2h,2w,K] -> o [N,h,w,K]
 __global__ void up_bwd_small_kernel(const float* g, float* o, int N, int h, int w, int K) {
   const int H2 = 2 * h, W2 = 2 * w;
@@ -1078,16 +1137,16 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
   }
   EUNET_REQUIRE(vec_ok(ghi) && vec_ok(glo) && ghi->dtype == glo->dtype, "upsample_bwd: vector layout");
   const int E = e16(ghi->dtype);
-  const long long total = (long long)glo->n * glo->h * glo->w * (glo->c / E);
+  const long long total = (long long)glo->n * ((glo->h + 1) / 2) * ((glo->w + 1) / 2) * (glo->c / E);
   const unsigned gr = (unsigned)((total + 255) / 256);
   if (ghi->dtype == EUNET_BF16)
-    up_bwd_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
+    up_bwd2x2_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c);
   else
-    up_bwd_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>((const float*)ghi->ptr, ghi->ctot, ghi->coff,
-                                                                     (float*)glo->ptr, glo->ctot, glo->coff, glo->n,
-                                                                     glo->h, glo->w, glo->c);
+    up_bwd2x2_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
+        (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
+        glo->w, glo->c);
   EUNET_LAUNCH_CHECK("upsample_bwd");
   return EUNET_OK;
 }

@@ -441,3 +441,19 @@ def test_conv3x3_per_sample_affine_and_gscale(dt):
     torch.cuda.synchronize()
     exp = (gx0.double() * gs.double()[:, None, None, :]).to(dt).double()
     assert rel(gx, exp) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("h,w", [(7, 9), (8, 16), (1, 3)])
+def test_upsample_bwd_odd_sizes(dt, h, w):
+    """2x2-per-thread adjoint of the x2 bilinear upsample at odd / tiny low-res sizes."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(13)
+    N, C = 2, 16
+    gh = torch.randn(N, 2 * h, 2 * w, C, generator=g, dtype=torch.float64).to(dt).double()
+    lo = torch.zeros(N, h, w, C, dtype=torch.float64).requires_grad_(True)
+    F.interpolate(nchw(lo), scale_factor=2, mode="bilinear", align_corners=False).backward(nchw(gh))
+    glo = torch.empty(N, h, w, C, dtype=dt, device=DEV)
+    ops.upsample_bwd(ops.act(gh.to(DEV, dt)), ops.act(glo))
+    torch.cuda.synchronize()
+    assert rel(glo, lo.grad) < TOL[dt]
