@@ -437,11 +437,11 @@ __global__ __launch_bounds__(NT) void head_bwd_gh_kernel(HeadArgs a) {
           }
         }
       }
-      if (pv) {
-        float* vp = a.v + p * ((K * 9 + 3) & ~3);
+      if (pv) {  // planar v[j][pixel] (coalesced gather in head_bwd_gu_kernel)
+        const long long P2 = (long long)a.N * 4 * a.h * a.w;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (4 * g + i < K * 9) vp[4 * g + i] = vj[i];
+          if (4 * g + i < K * 9) a.v[(long long)(4 * g + i) * P2 + p] = vj[i];
       }
       __syncthreads();
     }
@@ -465,9 +465,9 @@ __global__ void head_bwd_gu_kernel(HeadArgs a) {
     const int ky = t / 3, kx = t - ky * 3;
     const int py = oy - ky + 1, px = ox - kx + 1;
     if (py < 0 || py >= H2 || px < 0 || px >= W2) continue;
-    const float* vp = a.v + (((long long)n * H2 + py) * W2 + px) * ((K * 9 + 3) & ~3);
+    const long long P2 = (long long)a.N * H2 * W2, pix = ((long long)n * H2 + py) * W2 + px;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] += vp[k * 9 + t];
+    for (int k = 0; k < K; ++k) acc[k] += a.v[(long long)(k * 9 + t) * P2 + pix];
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) a.gu[id * K + k] = acc[k];
@@ -1056,10 +1056,13 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
         v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
         f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
         v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
-        if (pv) {
-          float* vp = a.v + (((long long)n * H2 + oy) * W2 + ox) * VLD;
-          if (4 * q < KJ) *(f32x4*)(vp + 4 * q) = v0;
-          if (16 + 4 * q < KJ) *(f32x4*)(vp + 16 + 4 * q) = v1;
+        if (pv) {  // planar v[j][pixel]: for each j the 16 lanes of a row write 64 contiguous bytes
+          const long long P2 = (long long)a.N * H2 * W2, pix = ((long long)n * H2 + oy) * W2 + ox;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (4 * q + i < KJ) a.v[(long long)(4 * q + i) * P2 + pix] = v0[i];
+            if (16 + 4 * q + i < KJ) a.v[(long long)(16 + 4 * q + i) * P2 + pix] = v1[i];
+          }
         }
         // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
