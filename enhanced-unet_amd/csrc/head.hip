@@ -1009,7 +1009,6 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  constexpr int VLD = (KJ + 3) & ~3;
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
