@@ -63,7 +63,7 @@ struct FwdArgs {
 // block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
 inline int env_order(const char* name, int dflt) {
   const char* v = getenv(name);
-  return (v && v[0] >= '0' && v[0] <= '2') ? v[0] - '0' : dflt;
+  return (v && v[0] >= '0' && v[0] <= '9') ? v[0] - '0' : dflt;
 }
 int conv_order() {
   static const int o = env_order("EUNET_CONV_ORDER", 0);
@@ -75,6 +75,10 @@ int wgrad_order() {
 }
 int conv_phase() {
   static const int o = env_order("EUNET_CONV_PHASE", 1);
+  return o;
+}
+int wgrad_pf() {
+  static const int o = env_order("EUNET_WGRAD_PF", 7);
   return o;
 }
 int wgrad_phase() {
@@ -827,10 +831,16 @@ __device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, in
 // to LDS (BN+ReLU applied to X there); the other block computes meanwhile.
 // MODE (diagnostic builds only, tools/conv_ablate.hip): 1 = stage only the first tile,
 // 2 = no MFMAs (VALU keeps the LDS reads alive).
-template <int MODE = 0>
+// PF (tile staging; EUNET_WGRAD_PF, A/B in profiles/r01_ab_wgrad_pf.txt):
+//   7 (default) X halo and dY both by LDS-DMA (global_load_lds, no staging VGPRs), then
+//     BN+ReLU applied to the halo in place; one global round trip per tile
+//   4 dY by LDS-DMA, X halo through registers in two halves
+//   0 X halo and dY through registers (three round trips)
+// Holding the next tile in registers across the k-loop (tried) spills: the 36 accumulators
+// take 144 of the 256 VGPRs two blocks per CU leave each wave.
+template <int MODE = 0, int PF = 7>
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* dbred = (float*)(smem + WSTAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int split, cob, kc;
   if (a.order == 1) {
@@ -852,7 +862,9 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbacc = 0.f;
+  float dbv[8];  // bias gradient: thread owns channels co0 + 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
   u32x4 rx[WX_ITERS], rd[WD_ITERS];
   if (a.phase && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
@@ -911,6 +923,57 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       *(u32x4*)(Xs + (oc * HPXP + hp) * 16) = v;
     }
   };
+  auto dma_d = [&](int tile) {  // dY tile straight into LDS: wave-instruction j = units 64j..64j+63
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+    char* Ds = smem + WX_LDS;
+    for (int j = wv; j < WD_ITERS * NTHR / 64; j += NTHR / 64) {
+      const int id = j * 64 + lane;
+      const int px = id >> 3, u = id & 7;
+      const int r = px / TW, c = px - r * TW;
+      const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
+      const void* src = (yy < a.H && xx < a.W && co < a.cout)
+                            ? (const void*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co)
+                            : (const void*)&g_conv_zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(Ds + j * 64 * 16), 16, 0, 0);
+    }
+  };
+  // X halo raw into LDS: slot s = oc * HPXP + hp, wave-instruction j = slots 64j..64j+63
+  auto dma_x = [&](int tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+    for (int j = wv; j < 8 * HPXP / 64; j += NTHR / 64) {
+      const int sl = j * 64 + lane, oc = sl / HPXP, hp = sl - oc * HPXP;
+      const int hy = hp / HW_, hx = hp - hy * HW_;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const int c = kc * KCW + oc * 8;
+      const void* src = (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
+                            ? (const void*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c)
+                            : (const void*)&g_conv_zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(smem + j * 64 * 16), 16, 0, 0);
+    }
+  };
+  auto bnrelu_x = [&](int tile) {  // BN+ReLU of the staged halo in place; padding stays 0
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+    for (int sl = tid; sl < 8 * HPXP; sl += NTHR) {
+      const int oc = sl / HPXP, hp = sl - oc * HPXP;
+      const int hy = hp / HW_, hx = hp - hy * HW_;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const int c = kc * KCW + oc * 8;
+      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
+        u32x4* q = (u32x4*)(smem + sl * 16);
+        float f[8];
+        const int cs = c + n * a.iss;
+        Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, *q), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], a.isc[cs + e], a.ish[cs + e]), 0.f);
+        *q = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
+      }
+    }
+  };
   auto lwrite_d = [&]() {
     char* Ds = smem + WX_LDS;
 #pragma unroll
@@ -919,7 +982,26 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
 
   for (int tile = t_begin; tile < t_end; ++tile) {
     constexpr int XH = WX_ITERS / 2;
-    if ((MODE & 1) == 0 || tile == t_begin) {
+    if (PF == 7 && ((MODE & 1) == 0 || tile == t_begin)) {  // X halo and dY both by LDS-DMA
+      __syncthreads();  // previous tile's LDS reads are done
+      dma_x(tile);
+      dma_d(tile);
+      __syncthreads();  // (its fence waits for the DMA)
+      if (a.isc != nullptr) {
+        bnrelu_x(tile);
+        __syncthreads();
+      }
+    }
+    if (PF == 4 && ((MODE & 1) == 0 || tile == t_begin)) {  // dY by LDS-DMA
+      gload_x(tile, 0, XH);
+      __syncthreads();  // previous tile's LDS reads are done
+      dma_d(tile);
+      lwrite_x(tile, 0, XH);
+      gload_x(tile, XH, WX_ITERS);
+      lwrite_x(tile, XH, WX_ITERS);
+      __syncthreads();  // (its fence also waits for the DMA)
+    }
+    if (PF == 0 && ((MODE & 1) == 0 || tile == t_begin)) {
       gload_x(tile, 0, XH);
       __syncthreads();  // previous tile's LDS reads are done
       lwrite_x(tile, 0, XH);
@@ -933,19 +1015,28 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     const char* Ds = Xs + WX_LDS;
     if (a.db != nullptr && kc == 0) {
       const bf16_t* d = (const bf16_t*)Ds;
-      for (int px = wv; px < TH * TW; px += 4) dbacc += bf2f(d[px * 64 + lane]);
+#pragma unroll
+      for (int i = 0; i < TH * TW / 32; ++i) {  // independent 16-B reads, no per-read wait
+        float f[8];
+        Vec16<bf16_t>::unpack(*(const uint4*)(d + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dbv[e] += f[e];
+      }
     }
-#pragma unroll 1
-    for (int ks = 0; ks < TH; ++ks) {
+    auto load_af = [&](int ks, bf16x8* f) {  // dY^T fragments of k-step ks (32 pixels x 4 co tiles)
       const int pxa = ks * TW + 8 * g + q4;
-      bf16x8 af[4];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa * 64 + ct * 16 + 4 * p4) * 2));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             LDS_PTR(s16x4, Ds + ((pxa + 4) * 64 + ct * 16 + 4 * p4) * 2));
-        af[ct] = cat_bf16x4(lo, hi);
+        f[ct] = cat_bf16x4(lo, hi);
       }
+    };
+#pragma unroll 1
+    for (int ks = 0; ks < TH; ++ks) {
+      bf16x8 af[4];
+      load_af(ks, af);
       const int oc = 2 * wv + (p4 >> 1);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -977,10 +1068,16 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[t][ct][e];
       }
   if (a.db != nullptr && kc == 0) {
-    dbred[wv * 64 + lane] = dbacc;  // dbred lies outside the tile stage
+    float* dbred = (float*)smem;  // [32 pixel groups][64 co], over the finished tile stage
     __syncthreads();
-    if (tid < 64 && co0 + tid < a.cout)
-      a.db[(long long)split * a.cout + co0 + tid] = dbred[tid] + dbred[64 + tid] + dbred[128 + tid] + dbred[192 + tid];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dbred[(tid >> 3) * 64 + (tid & 7) * 8 + e] = dbv[e];
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.cout) {
+      float t = 0.f;
+      for (int r = 0; r < 32; ++r) t += dbred[r * 64 + tid];
+      a.db[(long long)split * a.cout + co0 + tid] = t;
+    }
   }
 }
 
@@ -1175,8 +1272,19 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));
-    allow_lds(conv3x3_wgrad_bf16_kernel<0>, WG_LDS);
-    conv3x3_wgrad_bf16_kernel<0><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+    switch (wgrad_pf()) {
+      case 4:
+        allow_lds(conv3x3_wgrad_bf16_kernel<0, 4>, WG_LDS);
+        conv3x3_wgrad_bf16_kernel<0, 4><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+        break;
+      case 0:
+        allow_lds(conv3x3_wgrad_bf16_kernel<0, 0>, WG_LDS);
+        conv3x3_wgrad_bf16_kernel<0, 0><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+        break;
+      default:
+        allow_lds(conv3x3_wgrad_bf16_kernel<0, 7>, WG_LDS);
+        conv3x3_wgrad_bf16_kernel<0, 7><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+    }
   } else {
     dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
     const size_t lds = A_LDS_BYTES + TH * TW * 64 * 4 + 4 * 64 * 4;
