@@ -135,6 +135,24 @@ def pmc_traffic(args, kernel):
     return round(k["hbm_bytes_per_launch"]), f"profiles/{os.path.basename(PMC_SUMMARY)} ({d['correction']})"
 
 
+MFMA_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_mfma_summary.json")
+
+
+def pmc_mfma(kernel):
+    """MFMA-pipe busy fraction and effective clock of `kernel` from the committed
+    SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass of the default bench command
+    (tools/gpu_pmc_mfma.sh); None when absent."""
+    try:
+        with open(MFMA_SUMMARY) as f:
+            k = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not k:
+        return None
+    return {"mfma_busy_frac": round(k["mfma_busy_frac"], 4), "clock_ghz": round(k["clock_ghz"], 3),
+            "source": f"profiles/{os.path.basename(MFMA_SUMMARY)}"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,6 +215,10 @@ def main():
     pmc = pmc_traffic(args, "conv3x3_fwd_kernel")
     if pmc is not None:
         roof["traffic"], roof["traffic_source"] = pmc
+    mf = pmc_mfma("conv3x3_fwd_kernel") if (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16") \
+        and not args.dual else None
+    if mf is not None:
+        roof["pmc_mfma"] = mf
     if "conv3x3_wgrad" in ks:
         wg = ks["conv3x3_wgrad"]
         roof["wgrad_tflops"] = round(wg["flops"] / (wg["ms"] * 1e-3) / 1e12, 2)
