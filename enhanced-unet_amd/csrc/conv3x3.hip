@@ -23,6 +23,8 @@
 //   bf16 fragments (8 consecutive pixels) come from ds_read_b64_tr_b16.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -1122,6 +1124,325 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
+// ---------------------------------------------------------------------------
+// Persistent forward / dgrad for Cin == 64 (bf16): the 64-channel layers at full
+// resolution (enc1.3, dec2.3, enc2.0, and the dgrad of dec2.0) have only two
+// K-chunks per 16x32 tile, so in conv3x3_fwd_kernel the per-block staging round
+// trips and the epilogue are not amortised (MFMA-only diagnostic: 37 % of peak
+// on these shapes vs 74 % on 512-channel layers).  Here one block per CU (8 waves,
+// 2 per SIMD) keeps all 64 x 9 x 64 weights of its co-block resident in LDS for its
+// lifetime and walks tiles; the next tile's whole halo (both chunks) is loaded into
+// registers while the current tile's MFMAs run, so a tile costs one LDS write of
+// the halo, the MFMAs and the epilogue, with no exposed global latency.
+// Wave w computes rows 2w, 2w+1 (4 m-tiles) x 64 co (16 accumulators).  The
+// epilogue (bias, Dropout2d scale, BN partials, fused BN-backward reduction) is
+// the one of conv3x3_fwd_kernel; the output tile is staged as bf16 in the halo
+// region, so the per-tile outputs (stats, bpart) keep the 16x32 tile indexing.
+constexpr int K64_T = 512;                                   // threads
+#ifndef K64_UNROLL
+#define K64_UNROLL 3
+#endif
+#ifndef K64_PRE
+#define K64_PRE 0
+#endif
+#ifndef K64_SUNROLL
+#define K64_SUNROLL 2
+#endif
+constexpr int K64_CU = ((FHPX + 7) / 8) * 32;                // 2464 halo unit ids per chunk (whole 8-px groups)
+constexpr int K64_IT = (2 * K64_CU + K64_T - 1) / K64_T;     // 10
+constexpr int K64_B = 2 * B_LDS_BYTES;                       // 73728: both chunks' weights
+constexpr int K64_A = 2 * FA_BYTES;                          // 79872: both chunks' halo
+constexpr int K64_OLD = 72;                                  // bf16 row stride of the staged output tile
+constexpr int K64_LDS = K64_B + K64_A + (2 * 8 + 4 + 7) * 64 * 4;
+static_assert(K64_LDS <= 160 * 1024, "k64 LDS");
+static_assert(FTH * FTW * K64_OLD * 2 <= K64_A && K64_T * 16 * 4 <= K64_A, "k64 staging");
+
+// sum over the 16 lanes of a DPP row (every lane gets it): quad butterflies, then row rotates
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror 4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror 8
+  return v;
+}
+
+// ABL (diagnostic builds only, tools/conv_ablate.hip k64): 1 = halo staged once (no per-tile
+// global loads / LDS writes), 2 = no epilogue, 4 = no MFMAs, 8 = no output stores.
+template <int ABL = 0>
+__global__ __launch_bounds__(K64_T, 1) void conv3x3_k64_kernel(FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Bs = smem;
+  char* As = smem + K64_B;
+  float* red = (float*)(As + K64_A);  // [2][8 waves][64]
+  float* bprm = red + 2 * 8 * 64;     // [4][64] BN-backward constants
+  float* lbias = bprm + 4 * 64;       // [64] bias of the co-block
+  float* lcst = lbias + 64;           // [2 buffers][3][64]: input scale, shift (per sample), output gscale
+  constexpr int E = 8, UPX = 8, NCW = 8, MT = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q = lane >> 4, li = lane & 15;
+  const int ncob = a.cout_pad / BN;
+  const int cob = blockIdx.x % ncob, co0 = cob * BN;
+  const int tstride = gridDim.x / ncob;
+  const int tpi = a.tx * a.ty;
+  const bool bnb = a.bpart != nullptr;
+  const u32x4* wp = (const u32x4*)a.wp;
+
+  for (int id = tid; id < 2 * B_UNITS; id += K64_T) {
+    const int kc = id / B_UNITS, u = id - kc * B_UNITS;
+    *(u32x4*)(Bs + id * 16) = wp[((long long)(kc * 4 + u / (BN * 9)) * a.cout_pad + co0) * 9 + u % (BN * 9)];
+  }
+  if (tid < BN) lbias[tid] = (a.bias != nullptr && co0 + tid < a.cout) ? a.bias[co0 + tid] : 0.f;
+  if (tid < BN) lbias[tid] = (a.bias != nullptr && co0 + tid < a.cout) ? a.bias[co0 + tid] : 0.f;
+  if (bnb && tid < BN) {
+    const bool ok = co0 + tid < a.cout;
+    bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
+    bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
+    bprm[2 * BN + tid] = ok ? a.bgam[co0 + tid] : 0.f;
+    bprm[3 * BN + tid] = ok ? a.bbet[co0 + tid] : 0.f;
+  }
+
+  u32x4 ra[K64_IT];
+  unsigned rok = 0;  // bit i: unit i is inside the image (BN+ReLU applies; padding stays 0)
+  float rcst = 0.f;  // tid < 192: this thread's per-sample constant of the prefetched tile
+  auto gload = [&](int tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
+    if (tid < 3 * 64) {
+      const int j = tid >> 6, c = tid & 63;
+      if (j == 2)
+        rcst = (a.gsc != nullptr && co0 + c < a.cout) ? a.gsc[(long long)n * a.cout + co0 + c] : 1.f;
+      else if (a.isc != nullptr)
+        rcst = (j == 0 ? a.isc : a.ish)[c + n * a.iss];
+    }
+    rok = 0;
+#pragma unroll
+    for (int i = 0; i < K64_IT; ++i) {
+      const int id = tid + i * K64_T, kc = id >= K64_CU ? 1 : 0;
+      bool ok = false;
+      ra[i] = (u32x4){0u, 0u, 0u, 0u};
+      if (id < 2 * K64_CU) ra[i] = fwd_load_unit<bf16_t>(a, n, y0, x0, id - kc * K64_CU, kc, ok);
+      rok |= (unsigned)ok << i;
+    }
+  };
+  auto lwrite = [&](const float* cst) {  // cst: [3][64] constants of this tile (scale, shift from LDS)
+    const bool tr = a.isc != nullptr;
+#pragma unroll
+    for (int i = 0; i < K64_IT; ++i) {
+      const int id = tid + i * K64_T, kc = id >= K64_CU ? 1 : 0;
+      if (id >= 2 * K64_CU) continue;
+      int hp, qq;
+      fwd_unit(id - kc * K64_CU, hp, qq);
+      if (hp >= FHPX) continue;
+      u32x4 v = ra[i];
+      if (tr && ((rok >> i) & 1u)) {
+        const int c = kc * 32 + qq * 8;
+        float f[8];
+        Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], cst[c + j], cst[64 + c + j]), 0.f);
+        v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
+      }
+      *(u32x4*)(As + kc * FA_BYTES + (qq * FHPXP + hp) * 16) = v;
+    }
+  };
+
+  int tile = blockIdx.x / ncob, it = 0;
+  if (tile < a.ntiles) {
+    gload(tile);
+    if (tid < 3 * 64) lcst[tid] = rcst;
+  }
+  for (; tile < a.ntiles; tile += tstride, ++it) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
+    const float* cst = lcst + (it & 1) * 3 * 64;
+    __syncthreads();  // the previous tile's epilogue is done with the halo region; cst written
+    if ((ABL & 1) == 0 || tile == (int)blockIdx.x / ncob) lwrite(cst);
+    __syncthreads();
+    if ((ABL & 1) == 0 && tile + tstride < a.ntiles) gload(tile + tstride);  // in flight during the MFMAs
+
+    f32x4 acc[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll K64_UNROLL
+    for (int kt = 0; kt < 18; ++kt) {  // (chunk, tap)
+      const int kc = kt >= 9 ? 1 : 0, t = kt - 9 * kc, ky = t / 3, kx = t - 3 * ky;
+      const char* A_ = As + kc * FA_BYTES;
+      const char* B_ = Bs + kc * B_LDS_BYTES;
+      {
+        uint4 fb[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(B_ + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int hp = (2 * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
+          const uint4 fa = *(const uint4*)(A_ + (q * FHPXP + hp) * 16);
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            if constexpr ((ABL & 4) != 0)
+              acc[mt][nt][0] += __uint_as_float((fa.x ^ fb[nt].x) & 0x3f000000u);
+            else
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[nt]),
+                                                                    __builtin_bit_cast(bf16x8, fa), acc[mt][nt], 0, 0, 0);
+          }
+        }
+      }
+    }
+
+    if constexpr ((ABL & 2) != 0) {  // keep the accumulators alive, skip the epilogue
+      float t = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) t += acc[mt][nt][0] + acc[mt][nt][3];
+      if (t == 1234.5f) ((float*)a.stats)[tid] = t;
+      continue;
+    }
+    // ---- epilogue.  The MFMA operands are swapped (D^T = W^T X^T): lane (q, li) holds output
+    // channels nt*16 + 4q + i (i = 0..3) of pixel li of m-tile mt, so the bf16 tile is staged
+    // with one 8-byte LDS write per (mt, nt).  BN partials: each wave reduces its own 2 rows
+    // (sum, M2 about the wave mean) in registers; one thread per channel Chan-combines the 8
+    // waves -> a single barrier.
+    const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
+    const bool has_gsc = a.gsc != nullptr;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float bv = lbias[nt * 16 + 4 * q + i];
+        const float gv = has_gsc ? cst[128 + nt * 16 + 4 * q + i] : 1.f;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt][nt][i] = (acc[mt][nt][i] + bv) * gv;
+      }
+    const int nrow = max(0, min(2, vh - 2 * wv));
+    const int nw = nrow * vw;  // valid pixels of this wave
+    if (a.stats != nullptr) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bool ok = (mt >> 1) < nrow && (mt & 1) * 16 + li < vw;
+            v += ok ? acc[mt][nt][i] : 0.f;
+          }
+          v = row16_sum(v);
+          const float mw = nw > 0 ? v / (float)nw : 0.f;
+          float m2 = 0.f;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bool ok = (mt >> 1) < nrow && (mt & 1) * 16 + li < vw;
+            const float d = acc[mt][nt][i] - mw;
+            m2 += ok ? d * d : 0.f;
+          }
+          m2 = row16_sum(m2);
+          if (li == 0) {
+            red[wv * 64 + nt * 16 + 4 * q + i] = v;
+            red[NCW * 64 + wv * 64 + nt * 16 + 4 * q + i] = m2;
+          }
+        }
+    }
+    __syncthreads();  // every wave is done reading the halo; red is complete
+    if (a.stats != nullptr && tid < 64 && co0 + tid < a.cout) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NCW; ++w) sum += red[w * 64 + tid];
+      const float cnt = (float)(vh * vw), mean = sum / cnt;
+      float m2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NCW; ++w) {
+        const int nwv = max(0, min(2, vh - 2 * w)) * vw;
+        const float d = nwv > 0 ? red[w * 64 + tid] / (float)nwv - mean : 0.f;
+        m2 += red[NCW * 64 + w * 64 + tid] + (float)nwv * d * d;
+      }
+      a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
+      a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
+      if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
+    }
+    bf16_t* stg = (bf16_t*)As;  // [512 px][K64_OLD]
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int px = (2 * wv + (mt >> 1)) * FTW + (mt & 1) * 16 + li;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const uint32_t lo = (uint32_t)f2bf(acc[mt][nt][0]) | ((uint32_t)f2bf(acc[mt][nt][1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(acc[mt][nt][2]) | ((uint32_t)f2bf(acc[mt][nt][3]) << 16);
+        *(uint2*)(stg + px * K64_OLD + nt * 16 + 4 * q) = make_uint2(lo, hi);
+      }
+    }
+    __syncthreads();
+    bf16_t* yp = (bf16_t*)a.y;
+    const int ucol = tid % UPX;
+    float bs1[E], bs2[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { bs1[e] = 0.f; bs2[e] = 0.f; }
+    constexpr int SJ = FTH * FTW * UPX / K64_T;  // 8 output units per thread
+    uint4 ryb[SJ];                               // y of the fused BN-backward reduction, loaded
+    if (bnb && K64_PRE) {                        // before the stores (no store in the wait queue)
+#pragma unroll
+      for (int j = 0; j < SJ; ++j) {
+        const int id = tid + j * K64_T;
+        const int px = id / UPX, u = id - px * UPX;
+        const int r = px / FTW, c = px % FTW;
+        const int co = co0 + u * E;
+        ryb[j] = make_uint4(0, 0, 0, 0);
+        if (r < vh && c < vw && co < a.cout)
+          ryb[j] = *(const uint4*)((const bf16_t*)a.by + ((long long)(n * a.H + y0 + r) * a.W + x0 + c) * a.byct +
+                                   a.byco + co);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) {
+      const int id = tid + j * K64_T;
+      const int px = id / UPX, u = id - px * UPX;
+      const int r = px / FTW, c = px % FTW;
+      const int co = co0 + u * E;
+      if (r < vh && c < vw && co < a.cout) {
+        const uint4 packed = *(const uint4*)(stg + px * K64_OLD + u * E);
+        const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
+        if constexpr ((ABL & 8) == 0) *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
+        if (bnb) {
+          float gr[E], yv[E];
+          Vec16<bf16_t>::unpack(packed, gr);
+          Vec16<bf16_t>::unpack(K64_PRE ? ryb[j] : *(const uint4*)((const bf16_t*)a.by + pix * a.byct + a.byco + co), yv);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int cc = ucol * E + e;
+            const float xh = (yv[e] - bprm[cc]) * bprm[BN + cc];
+            const float gp = fmaf(bprm[2 * BN + cc], xh, bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
+            bs1[e] += gp;
+            bs2[e] = fmaf(gp, xh, bs2[e]);
+          }
+        }
+      }
+    }
+    if (bnb) {  // fixed-order block reduction of the per-thread channel sums
+      __syncthreads();
+      float* r2 = (float*)As;  // [K64_T][2E]
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        r2[tid * 2 * E + e] = bs1[e];
+        r2[tid * 2 * E + E + e] = bs2[e];
+      }
+      __syncthreads();
+      if (tid < 2 * BN) {
+        const int which = tid / BN, cc = tid % BN, u = cc / E, e = cc % E;
+        float t = 0.f;
+        for (int k = u; k < K64_T; k += UPX) t += r2[k * 2 * E + which * E + e];
+        if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
+      }
+    }
+    if (tid < 3 * 64 && tile + tstride < a.ntiles) lcst[((it + 1) & 1) * 3 * 64 + tid] = rcst;
+  }
+}
+
+int conv_k64() {
+  static const int o = env_order("EUNET_CONV_K64", 0);
+  return o;
+}
+
 int conv_dma() {
   static const int o = env_order("EUNET_CONV_DMA", 0);
   return o;
@@ -1139,6 +1460,14 @@ void launch_fwd_dma(const FwdArgs& a, int dtype, dim3 grid, void* stream) {
 }
 
 int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
+  if (dtype == EUNET_BF16 && a.cin == 64 && conv_k64()) {
+    const int ncob = a.cout_pad / BN;
+    const int per = std::max(1, std::min(a.ntiles, 256 / ncob));  // one resident block per CU
+    allow_lds(conv3x3_k64_kernel<0>, K64_LDS);
+    conv3x3_k64_kernel<0><<<dim3(per * ncob), K64_T, K64_LDS, (hipStream_t)stream>>>(a);
+    EUNET_LAUNCH_CHECK("conv3x3_fwd");
+    return EUNET_OK;
+  }
   dim3 grid(a.ntiles * (a.cout_pad / BN));
   switch (conv_dma()) {
     case 1: launch_fwd_dma<1>(a, dtype, grid, stream); break;

@@ -6,6 +6,7 @@
 #include "../enhanced-unet_amd/csrc/conv3x3.hip"
 #include "../enhanced-unet_amd/csrc/capi.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -91,6 +92,25 @@ static int wgrad_main(int N, int H, int W, int cin, int cout, int reps) {
   return 0;
 }
 
+template <int ABL>
+static float run_k64(const FwdArgs& a, int reps) {
+  const int ncob = a.cout_pad / BN;
+  const dim3 grid(std::max(1, std::min(a.ntiles, 256 / ncob)) * ncob);
+  allow_lds(conv3x3_k64_kernel<ABL>, K64_LDS);
+  conv3x3_k64_kernel<ABL><<<grid, K64_T, K64_LDS>>>(a);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < reps; ++i) conv3x3_k64_kernel<ABL><<<grid, K64_T, K64_LDS>>>(a);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 7 && std::string(argv[1]) == "wgrad")
     return wgrad_main(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
@@ -135,8 +155,33 @@ int main(int argc, char** argv) {
   a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr; a.order = 0; a.phase = 0;
   CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
   a.stats = stats;
+  if (getenv("ABLATE_ISC") != nullptr) {  // BN+ReLU operand transform on (scale 1, shift 0)
+    std::vector<float> one(cin, 1.f), zero(cin, 0.f);
+    float *sc, *sh;
+    CK(hipMalloc(&sc, cin * 4));
+    CK(hipMalloc(&sh, cin * 4));
+    CK(hipMemcpy(sc, one.data(), cin * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(sh, zero.data(), cin * 4, hipMemcpyHostToDevice));
+    a.isc = sc;
+    a.ish = sh;
+  }
   dim3 grid(a.ntiles * (cout / BN));
   const double flop = 2.0 * 9 * cin * cout * (double)N * H * W;
+  if (getenv("ABLATE_K64") != nullptr && cin == 64) {  // persistent Cin=64 kernel ablation
+    const char* nm[] = {"k64_full", "k64_stage_once", "k64_no_epi", "k64_mfma_lds_only", "k64_no_mfma",
+                        "k64_no_mfma_no_epi", "k64_no_store", "k64_no_stats"};
+    const float ts0 = run_k64<0>(a, reps);
+    float* st = a.stats;
+    a.stats = nullptr;
+    const float tns = run_k64<0>(a, reps);
+    a.stats = st;
+    const float ts[] = {ts0, run_k64<1>(a, reps), run_k64<2>(a, reps), run_k64<3>(a, reps),
+                        run_k64<4>(a, reps), run_k64<6>(a, reps), run_k64<8>(a, reps), tns};
+    printf("{\"shape\": [%d, %d, %d, %d, %d]", N, H, W, cin, cout);
+    for (int i = 0; i < 8; ++i) printf(", \"%s_ms\": %.4f, \"%s_tf\": %.1f", nm[i], ts[i], nm[i], flop / ts[i] / 1e9);
+    printf("}\n");
+    return 0;
+  }
   const float t0 = run<0>(a, grid, reps), t1 = run<1>(a, grid, reps), t2 = run<2>(a, grid, reps);
   const float t4 = run<4>(a, grid, reps), t5 = run<5>(a, grid, reps), t8 = run<8>(a, grid, reps);
   const float tdb = run<0, true, 8>(a, grid, reps), tdb5 = run<5, true, 8>(a, grid, reps);
