@@ -261,43 +261,40 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
 // ---------------------------------------------------------------------------
 // BatchNorm statistics: Chan-combine per-tile (sum, M2, count) in fp64
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void bn_finalize_kernel(const float* st, int tiles, int C, const float* gamma,
+constexpr int FNT = 1024;  // threads per channel block of bn_finalize (8 tiles per thread at 1024^2)
+__global__ __launch_bounds__(FNT) void bn_finalize_kernel(const float* st, int tiles, int C, const float* gamma,
                                                          const float* beta, float eps, float mom, float* rm,
                                                          float* rv, float* mean_o, float* invstd_o, float* scale_o,
                                                          float* shift_o, long long* nbt) {
-  __shared__ double sh[NT];
-  __shared__ double shb[2];
+  __shared__ double shn[FNT], shm[FNT], shq[FNT];
   const int c = blockIdx.x, tid = threadIdx.x;
   const float* cnt = st + (long long)2 * C * tiles;
-  double n = 0.0, s = 0.0;
-  for (int t = tid; t < tiles; t += NT) {
-    n += (double)cnt[t];
-    s += (double)st[((long long)t * 2) * C + c];
-  }
-  auto block_sum = [&](double v) -> double {
-    sh[tid] = v;
-    __syncthreads();
-    for (int o = NT / 2; o > 0; o >>= 1) {
-      if (tid < o) sh[tid] += sh[tid + o];
-      __syncthreads();
-    }
-    double r = sh[0];
-    __syncthreads();
-    return r;
+  // one pass: each thread Chan-merges its tiles (count, mean, M2) online, then a fixed-order tree
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  auto merge = [](double& n, double& mean, double& m2, double nb, double mb, double qb) {
+    const double nt = n + nb;
+    if (nb <= 0.0) return;
+    const double d = mb - mean;
+    mean += d * (nb / nt);
+    m2 += qb + d * d * (n * nb / nt);
+    n = nt;
   };
-  n = block_sum(n);
-  s = block_sum(s);
-  const double mean = s / n;
-  double m2 = 0.0;
-  for (int t = tid; t < tiles; t += NT) {
+  for (int t = tid; t < tiles; t += FNT) {
     const double nb = (double)cnt[t];
-    if (nb > 0.0) {
-      const double mb = (double)st[((long long)t * 2) * C + c] / nb;
-      m2 += (double)st[((long long)t * 2 + 1) * C + c] + nb * (mb - mean) * (mb - mean);
-    }
+    if (nb > 0.0)
+      merge(n, mean, m2, nb, (double)st[((long long)t * 2) * C + c] / nb, (double)st[((long long)t * 2 + 1) * C + c]);
   }
-  m2 = block_sum(m2);
-  (void)shb;
+  shn[tid] = n; shm[tid] = mean; shq[tid] = m2;
+  __syncthreads();
+  for (int o = FNT / 2; o > 0; o >>= 1) {
+    if (tid < o) {
+      double a_n = shn[tid], a_m = shm[tid], a_q = shq[tid];
+      merge(a_n, a_m, a_q, shn[tid + o], shm[tid + o], shq[tid + o]);
+      shn[tid] = a_n; shm[tid] = a_m; shq[tid] = a_q;
+    }
+    __syncthreads();
+  }
+  n = shn[0]; mean = shm[0]; m2 = shq[0];
   if (tid == 0 && c == 0 && nbt != nullptr) *nbt += 1;  // BatchNorm2d.num_batches_tracked
   if (tid == 0) {
     const double var_b = m2 / n;
@@ -468,12 +465,18 @@ __global__ __launch_bounds__(256) void bnrelu_conv1x1_kernel(const T* y, long lo
 // ---------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------
-constexpr int BWD_PIX = 1024;  // pixels per reduction tile
+// pixels per reduction tile: ~2048 tiles (whole-chip parallelism even for the 128^2 x 512-ch
+// levels), 64..1024 pixels each
+long long bwd_pix(long long P) {
+  long long pix = ((P / 2048 + 63) / 64) * 64;
+  return pix < 64 ? 64 : (pix > 1024 ? 1024 : pix);
+}
 
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
-                                                           const float* gamma, const float* beta, float* part) {
+                                                           const float* gamma, const float* beta, float* part,
+                                                           int tpix) {
   constexpr int E = Vec16<T>::N;
   __shared__ float red[2][NT][E];
   const int U = C / E;
@@ -487,8 +490,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, 
     s1[j] = 0.f; s2[j] = 0.f;
     if (sl < slots) { mu[j] = mean[c + j]; is[j] = istd[c + j]; ga[j] = gamma[c + j]; be[j] = beta[c + j]; }
   }
-  const long long p0 = (long long)blockIdx.x * BWD_PIX;
-  const long long p1 = min(P, p0 + BWD_PIX);
+  const long long p0 = (long long)blockIdx.x * tpix;
+  const long long p1 = min(P, p0 + tpix);
   if (sl < slots) {
     for (long long p = p0 + sl; p < p1; p += slots) {
       float gf[E], yf[E];
@@ -949,7 +952,7 @@ int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, 
                       float momentum, float* run_mean, float* run_var, float* mean, float* invstd, float* scale,
                       float* shift, int64_t* num_batches_tracked, void* stream) {
   EUNET_REQUIRE(stats && tiles > 0 && c > 0 && gamma && beta, "bn_finalize: bad args");
-  bn_finalize_kernel<<<c, NT, 0, (hipStream_t)stream>>>(stats, tiles, c, gamma, beta, eps, momentum, run_mean,
+  bn_finalize_kernel<<<c, FNT, 0, (hipStream_t)stream>>>(stats, tiles, c, gamma, beta, eps, momentum, run_mean,
                                                         run_var, mean, invstd, scale, shift,
                                                         (long long*)num_batches_tracked);
   EUNET_LAUNCH_CHECK("bn_finalize");
@@ -1033,7 +1036,7 @@ int eunet_bnrelu_conv1x1(const eunet_act* y, const float* scale, const float* sh
 int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles) {
   EUNET_REQUIRE(act_ok(y) && tiles, "bn_bwd_tiles: bad args");
   const long long P = (long long)y->n * y->h * y->w;
-  *tiles = (int)((P + BWD_PIX - 1) / BWD_PIX);
+  *tiles = (int)((P + bwd_pix(P) - 1) / bwd_pix(P));
   return EUNET_OK;
 }
 
@@ -1045,15 +1048,16 @@ int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mea
                 "bn_bwd_reduce: shape mismatch");
   EUNET_REQUIRE(y->c / e16(y->dtype) <= NT, "bn_bwd_reduce: too many channels");
   const long long P = (long long)y->n * y->h * y->w;
-  const unsigned tiles = (unsigned)((P + BWD_PIX - 1) / BWD_PIX);
+  const int tpix = (int)bwd_pix(P);
+  const unsigned tiles = (unsigned)((P + tpix - 1) / tpix);
   if (y->dtype == EUNET_BF16)
     bn_bwd_reduce_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, part);
+        gamma, beta, part, tpix);
   else
     bn_bwd_reduce_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>(
         (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, part);
+        gamma, beta, part, tpix);
   EUNET_LAUNCH_CHECK("bn_bwd_reduce");
   return EUNET_OK;
 }
