@@ -68,6 +68,56 @@ __device__ __forceinline__ void tile_coords(const HeadArgs& a, int tile, int& n,
   ox0 = (r % a.tx) * T2;
 }
 
+// The z region a 16x16 tile at 2H interpolates from: 10 x 10 pixels x K (<= 3) at H, edge-
+// clamped.  Each thread holds <= 2 of its values; the next tile's are loaded into registers
+// while the current tile computes, so fill_u no longer waits on global memory.
+constexpr int ZR = 10;
+__device__ __forceinline__ void zload(const HeadArgs& a, int tile, float (&zv)[2]) {
+  if (tile >= a.ntiles) return;
+  int n, oy0, ox0;
+  tile_coords(a, tile, n, oy0, ox0);
+  const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
+  const float* zb = a.z + (long long)n * a.h * a.w * a.K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + j * NT;
+    if (idx < ZR * ZR * a.K) {
+      const int k = idx % a.K, pix = idx / a.K, i = pix / ZR, c = pix - i * ZR;
+      const int yy = min(max(zy0 + i, 0), a.h - 1), xx = min(max(zx0 + c, 0), a.w - 1);
+      zv[j] = zb[((long long)yy * a.w + xx) * a.K + k];
+    }
+  }
+}
+
+// stage the prefetched z region, prefetch the next tile's, then u = up(z) over the 18x18 halo
+// from LDS (as fill_u; the caller syncs before and after)
+__device__ void stage_u(const HeadArgs& a, float* su, float* zs, float (&zv)[2], int tile, int oy0, int ox0) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = threadIdx.x + j * NT;
+    if (idx < ZR * ZR * a.K) zs[idx] = zv[j];
+  }
+  __syncthreads();
+  zload(a, tile + gridDim.x, zv);
+  const int H2 = 2 * a.h, W2 = 2 * a.w, zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
+  for (int i = threadIdx.x; i < 18 * 18; i += NT) {
+    const int hy = i / 18, hx = i - hy * 18;
+    const int oy = oy0 + hy - 1, ox = ox0 + hx - 1;
+    const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    up2_src(in ? oy : 0, a.h, y0, y1, ly);
+    up2_src(in ? ox : 0, a.w, x0, x1, lx);
+    const float* r0 = zs + ((y0 - zy0) * ZR) * a.K;
+    const float* r1 = zs + ((y1 - zy0) * ZR) * a.K;
+    const int c0 = (x0 - zx0) * a.K, c1 = (x1 - zx0) * a.K;
+    for (int k = 0; k < a.K; ++k)
+      su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
+                               ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
+                         : 0.f;
+  }
+}
+
 __device__ __forceinline__ float g_out(const HeadArgs& a, int K, int n, int k, int oy, int ox) {
   if (a.glog) return 0.25f * a.glog[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)];
   return a.gout2h[(((long long)n * K + k) * (2 * a.h) + oy) * (2 * a.w) + ox];
@@ -677,6 +727,7 @@ __device__ __forceinline__ float sum_x16(float v) {
 template <int K>
 __global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
   __shared__ float wn_s[4], wm_s[4][MID], wq_s[4][MID];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   bf16x8 Ah[4];
@@ -686,11 +737,13 @@ __global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
   float n = 0.f, mean[16], m2[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  float zv[2] = {0.f, 0.f};
+  zload(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int nn, oy0, ox0;
     tile_coords(a, tile, nn, oy0, ox0);
     __syncthreads();
-    fill_u(a, su, nn, oy0, ox0);
+    stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
@@ -758,6 +811,7 @@ __global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
 template <int K>
 __global__ __launch_bounds__(NT) void head_out_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float scs[MID], shs[MID];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   if (tid < MID) {
@@ -778,11 +832,13 @@ __global__ __launch_bounds__(NT) void head_out_mfma_kernel(HeadArgs a) {
   for (int k = 0; k < K; ++k) b2k[k] = a.b2[k];
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float zv[2] = {0.f, 0.f};
+  zload(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    fill_u(a, su, n, oy0, ox0);
+    stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
 #pragma unroll
     for (int rp = 0; rp < 2; ++rp) {
@@ -834,6 +890,7 @@ template <int K>
 __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = (K + 2) * MID + K;
   __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID];
   __shared__ float red[STRIDE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
@@ -863,11 +920,13 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   for (int k = 0; k < K; ++k) ab2[k] = 0.f;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float zv[2] = {0.f, 0.f};
+  zload(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    fill_u(a, su, n, oy0, ox0);
+    stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
 #pragma unroll 1
     for (int rr = 0; rr < 4; ++rr) {
@@ -950,6 +1009,7 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = MID * K * 9 + MID;
   constexpr int KJ = K * 9;
   __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float pP[MID], pQ[MID], pD[MID], pE[MID];
   __shared__ __attribute__((aligned(16))) bf16x8 fr[12][64];  // Ah[4], As[4], Av[jb][ch] per lane
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
@@ -1011,11 +1071,13 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
+  float zv[2] = {0.f, 0.f};
+  zload(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    fill_u(a, su, n, oy0, ox0);
+    stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
 #pragma unroll 1
     for (int rp = 0; rp < 2; ++rp) {
