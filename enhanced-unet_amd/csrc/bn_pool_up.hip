@@ -165,7 +165,6 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   __shared__ float xs[(STH + 2) * (STW + 2) * SCI];
   __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];         // dY tile [256 px][64 co]
   __shared__ __attribute__((aligned(16))) T cs[STH * STW * SJT * 16];  // im2col [256 px][icw]
-  __shared__ float dbs[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int split = blockIdx.x, co0 = blockIdx.y * 64;
   const int t_begin = split * a.per_split, t_end = min(a.ntiles, t_begin + a.per_split);
@@ -174,7 +173,9 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   f32x4 acc[SJT];
 #pragma unroll
   for (int j = 0; j < SJT; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbacc = 0.f;
+  float dbv[8];  // bias gradient: channels 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
   for (int tile = t_begin; tile < t_end; ++tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
@@ -209,7 +210,10 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       Elem<T>::st(cs + id, v);
     }
     __syncthreads();
-    for (int px = wv; px < STH * STW; px += 4) dbacc += Elem<T>::ld(gs + px * 64 + lane);
+#pragma unroll
+    for (int i = 0; i < STH * STW / 32; ++i)  // independent reads, no wait per element
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dbv[e] += Elem<T>::ld(gs + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8 + e);
     const int cw = wv * 16;
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
@@ -252,10 +256,15 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       }
     }
   __syncthreads();
-  dbs[wv][lane] = dbacc;
+  float(*dbs)[64] = (float(*)[64])gs;  // [32 pixel groups][64 co] over the finished dY tile
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dbs[tid >> 3][(tid & 7) * 8 + e] = dbv[e];
   __syncthreads();
-  if (a.db != nullptr && tid < 64 && co0 + tid < a.cout)
-    a.db[(long long)split * a.cout + co0 + tid] = dbs[0][tid] + dbs[1][tid] + dbs[2][tid] + dbs[3][tid];
+  if (a.db != nullptr && tid < 64 && co0 + tid < a.cout) {
+    float t = 0.f;
+    for (int r = 0; r < 32; ++r) t += dbs[r][tid];
+    a.db[(long long)split * a.cout + co0 + tid] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -768,6 +777,39 @@ __global__ void up_bwd_small_kernel(const float* g, float* o, int N, int h, int 
   for (int k = 0; k < K; ++k) o[id * K + k] = acc[k];
 }
 
+// K = 2 specialisation: separable row / column adjoint weights computed once per thread, one
+// 8-byte load per contributing high-res pixel
+__global__ __launch_bounds__(256) void up_bwd_k2_kernel(const float2* g, float2* o, int N, int h, int w) {
+  const int H2 = 2 * h, W2 = 2 * w;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * h * w) return;
+  const int x = (int)(id % w);
+  const int y = (int)((id / w) % h);
+  const int n = (int)(id / ((long long)w * h));
+  float wy[4], wx[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int oy = 2 * y - 1 + d, ox = 2 * x - 1 + d;
+    wy[d] = (oy >= 0 && oy < H2) ? up2_adj_w(oy, h, y) : 0.f;
+    wx[d] = (ox >= 0 && ox < W2) ? up2_adj_w(ox, w, x) : 0.f;
+  }
+  float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int dy = 0; dy < 4; ++dy) {
+    if (wy[dy] == 0.f) continue;
+    const float2* row = g + (long long)(n * H2 + 2 * y - 1 + dy) * W2;
+#pragma unroll
+    for (int dx = 0; dx < 4; ++dx) {
+      if (wx[dx] == 0.f) continue;
+      const float2 v = row[2 * x - 1 + dx];
+      const float ww = wy[dy] * wx[dx];
+      acc.x = fmaf(ww, v.x, acc.x);
+      acc.y = fmaf(ww, v.y, acc.y);
+    }
+  }
+  o[id] = acc;
+}
+
 // dec1 backward: gact = W^T gz; per-block partials of gW [K][C] and gb [K].
 // 8 lanes per pixel, lane group g owns channels 8g+64j (C <= 128); partial
 // sums stay in registers over the block's C1X_PIX pixels.
@@ -1134,8 +1176,12 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
   if (ghi->dtype == EUNET_F32 && glo->dtype == EUNET_F32 && ghi->ctot == ghi->c && glo->ctot == glo->c &&
       ghi->c <= 4 && ghi->coff == 0 && glo->coff == 0) {
     const long long total = (long long)glo->n * glo->h * glo->w;
-    up_bwd_small_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-        (const float*)ghi->ptr, (float*)glo->ptr, glo->n, glo->h, glo->w, glo->c);
+    if (ghi->c == 2)
+      up_bwd_k2_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+          (const float2*)ghi->ptr, (float2*)glo->ptr, glo->n, glo->h, glo->w);
+    else
+      up_bwd_small_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+          (const float*)ghi->ptr, (float*)glo->ptr, glo->n, glo->h, glo->w, glo->c);
     EUNET_LAUNCH_CHECK("upsample_bwd_small");
     return EUNET_OK;
   }

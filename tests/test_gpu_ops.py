@@ -514,3 +514,19 @@ def test_upsample_bwd_odd_sizes(dt, h, w):
     ops.upsample_bwd(ops.act(gh.to(DEV, dt)), ops.act(glo))
     torch.cuda.synchronize()
     assert rel(glo, lo.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("C", [1, 2, 3])
+@pytest.mark.parametrize("h,w", [(7, 9), (16, 24), (1, 3)])
+def test_upsample_bwd_small_channels(C, h, w):
+    """fp32 K-channel adjoint used for the head's logits (K = 2 has its own kernel)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(15)
+    N = 2
+    gh = torch.randn(N, 2 * h, 2 * w, C, generator=g, dtype=torch.float64)
+    lo = torch.zeros(N, h, w, C, dtype=torch.float64).requires_grad_(True)
+    F.interpolate(nchw(lo), scale_factor=2, mode="bilinear", align_corners=False).backward(nchw(gh))
+    glo = torch.empty(N, h, w, C, dtype=torch.float32, device=DEV)
+    ops.upsample_bwd(ops.act(gh.to(DEV, torch.float32)), ops.act(glo))
+    torch.cuda.synchronize()
+    assert rel(glo, lo.grad) < 1e-5
