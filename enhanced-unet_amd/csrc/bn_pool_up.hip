@@ -199,6 +199,7 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       *(uint4*)(gs + px * 64 + u * E) = v;
     }
     __syncthreads();
+#pragma unroll 4
     for (int id = tid; id < STH * STW * icw; id += NT) {
       const int px = id / icw, j = id - px * icw;
       float v = 0.f;
@@ -211,9 +212,16 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < STH * STW / 32; ++i)  // independent reads, no wait per element
+    for (int i = 0; i < STH * STW / 32; ++i) {  // independent 16-B reads, no wait per element
+      const T* src = gs + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) dbv[e] += Elem<T>::ld(gs + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8 + e);
+      for (int h = 0; h < 8 / E; ++h) {
+        float f[E];
+        Vec16<T>::unpack(*(const uint4*)(src + h * E), f);
+#pragma unroll
+        for (int e = 0; e < E; ++e) dbv[h * E + e] += f[e];
+      }
+    }
     const int cw = wv * 16;
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
