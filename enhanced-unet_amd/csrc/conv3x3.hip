@@ -60,6 +60,7 @@ struct FwdArgs {
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
   int order;         // block -> (tile, co-block) order: 0 XCD-grouped, 1 tile-fastest, 2 co-block-fastest
   int phase;         // 1: odd blocks start late (see conv3x3_fwd_kernel)
+  int pro1;          // 1: the first K-chunk is staged in one round trip (EUNET_CONV_PRO1)
 };
 
 // block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
@@ -73,6 +74,10 @@ int conv_order() {
 }
 int wgrad_order() {
   static const int o = env_order("EUNET_WGRAD_ORDER", 0);
+  return o;
+}
+int conv_pro1() {
+  static const int o = env_order("EUNET_CONV_PRO1", 1);
   return o;
 }
 int conv_phase() {
@@ -245,10 +250,6 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   const bool computes = !SPEC || wv < NCW;
 
   f32x4 acc[MT][4];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[A_IT];
   bool rok[A_IT];
@@ -401,6 +402,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   };
 
   uint4 fa0[MT], fb0[4];
+  const bool conv_pro1 = a.pro1 != 0;
   // Phase offset: the two blocks sharing a CU start (and, with equal work, keep running) in
   // lock-step, staging at the same time and leaving the MFMA pipes idle together.  Odd blocks
   // start ~2.5k clocks late so one block's staging overlaps the other's MFMAs (ablation:
@@ -427,10 +429,20 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     }
     CONV_LWRITE_A(0, 0, 0, A_IT);
     if constexpr (!BDMA) CONV_LWRITE_B(0, 0, B_IT);
+  } else if (conv_pro1) {  // first chunk in one round trip: the accumulators are not live yet
+    CONV_GLOAD_A(0, 0, A_IT);
+    if constexpr (DMA == 0) CONV_GLOAD_B(0, 0, B_IT);
+    else dma_b(0, 0);
+    CONV_LWRITE_A(0, 0, 0, A_IT);
+    if constexpr (DMA == 0) CONV_LWRITE_B(0, 0, B_IT);
   } else {
     stage(0, 0);
   }
   __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   if constexpr ((MODE & 4) != 0) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) fb0[nt] = *(const uint4*)(smem + FA_BYTES + (q * (BN * 9) + (nt * 16 + li) * 9) * 16);
@@ -1530,6 +1542,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
   a.order = conv_order();
   a.phase = conv_phase();
+  a.pro1 = conv_pro1();
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   return launch_fwd(a, x->dtype, stream);
@@ -1559,6 +1572,7 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
   a.order = conv_order();
   a.phase = conv_phase();
+  a.pro1 = conv_pro1();
   return launch_fwd(a, dy->dtype, stream);
 }
 

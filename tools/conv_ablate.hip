@@ -152,7 +152,7 @@ int main(int argc, char** argv) {
   a.y = y; a.yct = cout; a.yco = 0; a.cout = cout;
   a.tx = cdiv(W, FTW); a.ty = cdiv(H, FTH); a.ntiles = N * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
-  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr; a.order = 0; a.phase = 0;
+  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr; a.order = 0; a.phase = 0; a.pro1 = 0;
   CK(hipMalloc(&stats, (size_t)a.ntiles * (2 * cout + 1) * 4));
   a.stats = stats;
   if (getenv("ABLATE_ISC") != nullptr) {  // BN+ReLU operand transform on (scale 1, shift 0)
