@@ -60,7 +60,8 @@ struct FwdArgs {
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
   int order;         // block -> (tile, co-block) order: 0 XCD-grouped, 1 tile-fastest, 2 co-block-fastest
   int phase;         // 1: odd blocks start late (see conv3x3_fwd_kernel)
-  int pro1;          // 1: the first K-chunk is staged in one round trip (EUNET_CONV_PRO1)
+  int pro1;          // 1: the first K-chunk is staged in one round trip (EUNET_CONV_PRO1);
+                     // 2: also the later chunks' halo and weight halves load together
 };
 
 // block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
@@ -311,10 +312,21 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     }
   };
   constexpr int AH = A_IT / 2, BH = B_IT / 2;
+  const bool conv_st2 = a.pro1 == 2;
   auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
     if constexpr (DMA >= 1) dma_b(kc, buf);
     if (DMA >= 2 && a.isc == nullptr) {
       dma_a(kc, buf);
+    } else if (DMA == 0 && conv_st2) {  // halo and weight halves together: two round trips
+      CONV_GLOAD_A(kc, 0, AH);
+      CONV_GLOAD_B(kc, 0, BH);
+      CONV_LWRITE_A(kc, buf, 0, AH);
+      CONV_LWRITE_B(buf, 0, BH);
+      CONV_GLOAD_A(kc, AH, A_IT);
+      CONV_GLOAD_B(kc, BH, B_IT);
+      CONV_LWRITE_A(kc, buf, AH, A_IT);
+      CONV_LWRITE_B(buf, BH, B_IT);
+      return;
     } else {
       CONV_GLOAD_A(kc, 0, AH);
       CONV_LWRITE_A(kc, buf, 0, AH);
