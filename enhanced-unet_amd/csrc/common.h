@@ -46,6 +46,16 @@ int check_launch(const char* what);
 // ---------------------------------------------------------------------------
 // element conversion
 // ---------------------------------------------------------------------------
+// x + x[lane ^ 16] / x + x[lane ^ 32] on every lane with the gfx950 permlane swaps (VALU, no
+// LDS crossbar as __shfl_xor's ds_bpermute)
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 

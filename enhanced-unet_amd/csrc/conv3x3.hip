@@ -537,9 +537,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
           const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
           v += ok ? acc[mt][nt][i] : 0.f;
         }
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      s[nt] = v;
+      s[nt] = xor32_sum(xor16_sum(v));
     }
     if (q == 0 && computes)
 #pragma unroll
@@ -565,9 +563,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
           const float d = acc[mt][nt][i] - mb[nt];
           v += ok ? d * d : 0.f;
         }
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      s[nt] = v;
+      s[nt] = xor32_sum(xor16_sum(v));
     }
     if (q == 0 && computes)
 #pragma unroll
