@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--no-transform", action="store_true", help="forward without the BN+ReLU operand transform")
+    ap.add_argument("--no-stats", action="store_true", help="forward without BN partials")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = "cuda"
@@ -67,7 +69,9 @@ def main():
         st = torch.empty(tiles * (2 * cout + 1), device=dev)
         flops = 2.0 * 9 * cin * cout * a.batch * H * H
         xa, ya, gya, gxa = ops.act(x), ops.act(y), ops.act(gy), ops.act(gx)
-        t_f = timeit(lambda: ops.conv3x3_fwd(xa, wp, ya, bias=bias, scale=sc, shift=sh, stats=st), a.reps)
+        tsc, tsh = (None, None) if a.no_transform else (sc, sh)
+        tst = None if a.no_stats else st
+        t_f = timeit(lambda: ops.conv3x3_fwd(xa, wp, ya, bias=bias, scale=tsc, shift=tsh, stats=tst), a.reps)
         t_d = timeit(lambda: ops.conv3x3_fwd(gya, wpt, gxa), a.reps)
         ns = ops.conv3x3_wgrad_splits(gya, cin, dt)
         dwp = torch.empty(ns * cout * 9 * cin, device=dev)
