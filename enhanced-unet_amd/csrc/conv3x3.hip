@@ -829,7 +829,7 @@ constexpr int KCW = 64;                        // ci channels per wgrad block (b
 constexpr int WX_LDS = 8 * HPXP * 16;          // X halo [8 octants][HPXP][16 B]
 constexpr int WD_LDS = TH * TW * 64 * 2;       // dY tile [256 px][64 co] bf16
 constexpr int WSTAGE = WX_LDS + WD_LDS;        // 77824
-constexpr int WG_LDS = WSTAGE + 4 * 64 * 4;      // one stage + db reduction (2 blocks / CU)
+constexpr int WG_LDS = WSTAGE + 4 * 64 * 4;      // one stage + 1 KB (transform scales; 2 blocks / CU)
 constexpr int WX_IDS = ((HPX + 7) / 8) * 64;   // 2752: X unit ids (8 pixels x 8 octants per 64)
 constexpr int WX_ITERS = (WX_IDS + NTHR - 1) / NTHR;  // 11
 constexpr int WD_ITERS = TH * TW * 8 / NTHR;   // 8
@@ -863,6 +863,7 @@ __device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, in
 template <int MODE = 0, int PF = 7>
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lsc = (float*)(smem + WSTAGE);  // PF 7: [scale | shift][KCW] of the current tile
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int split, cob, kc;
   if (a.order == 1) {
@@ -988,10 +989,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
         u32x4* q = (u32x4*)(smem + sl * 16);
         float f[8];
-        const int cs = c + n * a.iss;
+        const float* sc = lsc + oc * 8;  // the tile's scale / shift rows, staged in LDS
         Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, *q), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], a.isc[cs + e], a.ish[cs + e]), 0.f);
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sc[KCW + e]), 0.f);
         *q = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
       }
     }
@@ -1005,9 +1006,17 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   for (int tile = t_begin; tile < t_end; ++tile) {
     constexpr int XH = WX_ITERS / 2;
     if (PF == 7 && ((MODE & 1) == 0 || tile == t_begin)) {  // X halo and dY both by LDS-DMA
+      // the block's 64 input channels' BN scale / shift for this tile's sample: one load per thread
+      // (tid < 128) instead of 16 per halo slot in the transform pass
+      float rsc = 0.f;
+      if (a.isc != nullptr && tid < 2 * KCW) {
+        const int c = kc * KCW + (tid % KCW);
+        if (c < a.cin) rsc = (tid < KCW ? a.isc : a.ish)[c + (tile / tpi) * a.iss];
+      }
       __syncthreads();  // previous tile's LDS reads are done
       dma_x(tile);
       dma_d(tile);
+      if (a.isc != nullptr && tid < 2 * KCW) lsc[tid] = rsc;
       __syncthreads();  // (its fence waits for the DMA)
       if (a.isc != nullptr) {
         bnrelu_x(tile);
