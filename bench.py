@@ -72,9 +72,16 @@ def cpu_baseline(args):
     tr.step(x, m)
     dt = time.perf_counter() - t0
     scale = (args.cpu_size / args.size) ** 2  # images of the benchmark size per sample
+    model = "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "?")
+    except OSError:
+        pass
     return {"value": round(scale / dt, 5), "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"1 oracle train step (PyTorch CPU fp32 restatement of Trainer.train_epoch), B=1, "
-                      f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s"}
+                      f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s on "
+                      f"{torch.get_num_threads()} threads of {os.cpu_count()} ({model})"}
 
 
 def dice_vs_cpu_ref(model, args, dev):
