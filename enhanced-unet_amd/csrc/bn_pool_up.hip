@@ -6,6 +6,8 @@
 // 212/236 (dec1), 220-224 (BN+ReLU), autograd of all of them.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int NT = 256;
@@ -372,6 +374,27 @@ __global__ void bnrelu_pool_kernel(const T* y, int N, int H, int W, int C, int y
     }
   const long long po = (long long)(n * Ho + yo) * Wo + xo;
   *(uint4*)(pool + po * pct + pco + c) = Vec16<T>::pack(m);
+}
+
+// z = relu(y * scale + shift), one 16-byte channel unit per thread and step: the activation of a
+// DoubleConv's first BN+ReLU (models.py:219-222), materialised once so the second conv's forward
+// and weight gradient read it without re-applying the transform per halo pixel
+template <typename T>
+__global__ __launch_bounds__(256) void bnrelu_kernel(const T* y, long long P, int C, int yct, int yco, const float* sc,
+                                                     const float* sh, T* out, int oct, int oco) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E;
+  const long long total = P * U;
+  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < total;
+       id += (long long)gridDim.x * blockDim.x) {
+    const long long p = id / U;
+    const int c = (int)(id - p * U) * E;
+    float f[E];
+    Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
+#pragma unroll
+    for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+    *(uint4*)(out + p * oct + oco + c) = Vec16<T>::pack(f);
+  }
 }
 
 // BN+ReLU -> bilinear x2 upsample (align_corners=False).  One thread per low-res pixel
@@ -1015,6 +1038,22 @@ int eunet_bn_eval_affine(int c, const float* gamma, const float* beta, const flo
   bn_eval_affine_kernel<<<cdiv(c, 256), 256, 0, (hipStream_t)stream>>>(c, gamma, beta, run_mean, run_var, eps,
                                                                         scale, shift);
   EUNET_LAUNCH_CHECK("bn_eval_affine");
+  return EUNET_OK;
+}
+
+int eunet_bnrelu(const eunet_act* y, const float* scale, const float* shift, const eunet_act* out, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(out) && scale && shift && vec_ok(y) && vec_ok(out), "bnrelu: bad args");
+  EUNET_REQUIRE(out->n == y->n && out->h == y->h && out->w == y->w && out->c == y->c && out->dtype == y->dtype,
+                "bnrelu: shape mismatch");
+  const long long P = (long long)y->n * y->h * y->w, total = P * (y->c / e16(y->dtype));
+  const unsigned g = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  if (y->dtype == EUNET_BF16)
+    bnrelu_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot, y->coff,
+                                                            scale, shift, (bf16_t*)out->ptr, out->ctot, out->coff);
+  else
+    bnrelu_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot, y->coff,
+                                                           scale, shift, (float*)out->ptr, out->ctot, out->coff);
+  EUNET_LAUNCH_CHECK("bnrelu");
   return EUNET_OK;
 }
 

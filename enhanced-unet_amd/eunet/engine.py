@@ -22,6 +22,8 @@ from __future__ import annotations
 
 from typing import Dict, Optional
 
+import os
+
 import torch
 
 from . import ops
@@ -30,6 +32,10 @@ from ._lib import EunetError
 BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+# DoubleConv's first BN+ReLU, za = relu(bn1(ya)), for the second conv (EUNET_MATERIALIZE_ZA):
+#   1 (default) one elementwise pass; conv .3's forward and weight gradient read za as is
+#   0 applied inside both operand stagings instead (nothing stored; A/B: profiles/r01_ab_za.txt)
+MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "1") != "0"
 
 
 class GradSink:
@@ -108,10 +114,16 @@ class UNetEngine:
             ops.conv3x3_fwd(X, wp, ops.act(ya), bias=P[p + ".0.bias"], stats=st)
         bna = self._bn(p + ".1", st, tiles, C, training, P, B)
         wp = ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
-        ops.conv3x3_fwd(ops.act(ya), wp, ops.act(yb), bias=P[p + ".3.bias"], scale=bna["scale"],
-                        shift=bna["shift"], stats=st)
+        za = None
+        if MATERIALIZE_ZA:  # one BN+ReLU pass; conv .3 forward and weight gradient read za as is
+            za = _e((N, H, W, C), self.dtype, dev)
+            ops.bnrelu(ops.act(ya), bna["scale"], bna["shift"], ops.act(za))
+            ops.conv3x3_fwd(ops.act(za), wp, ops.act(yb), bias=P[p + ".3.bias"], stats=st)
+        else:  # BN+ReLU applied while staging conv .3's operand tiles (forward and wgrad)
+            ops.conv3x3_fwd(ops.act(ya), wp, ops.act(yb), bias=P[p + ".3.bias"], scale=bna["scale"],
+                            shift=bna["shift"], stats=st)
         bnb = self._bn(p + ".4", st, tiles, C, training, P, B)
-        return dict(ya=ya, yb=yb, bna=bna, bnb=bnb, X=X)
+        return dict(ya=ya, za=za, yb=yb, bna=bna, bnb=bnb, X=X)
 
     # ---------------------------------------------------------------- forward
     def forward(self, x: torch.Tensor, training: bool, want: str = "logits"):
@@ -229,7 +241,10 @@ class UNetEngine:
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
         gyb = bn_back(p + ".4", G, yb, bnb)
-        wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
+        if s.get("za") is not None:
+            wgrad(p + ".3", ops.act(s["za"]), gyb)
+        else:
+            wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
         wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
         gaa = torch.empty_like(ya)
         ctiles = ops.conv3x3_tiles(ops.act(gaa))

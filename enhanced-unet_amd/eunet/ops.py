@@ -135,6 +135,10 @@ def bn_eval_affine(gamma, beta, run_mean, run_var, eps, scale, shift):
          float(eps), _ptr(scale), _ptr(shift), _stream())
 
 
+def bnrelu(y: Act, scale, shift, out: Act):
+    call("eunet_bnrelu", ctypes.byref(y), _ptr(scale), _ptr(shift), ctypes.byref(out), _stream())
+
+
 def bnrelu_pool(y: Act, scale, shift, act_out: Act | None, pooled: Act):
     call("eunet_bnrelu_pool", ctypes.byref(y), _ptr(scale), _ptr(shift), _ref(act_out), ctypes.byref(pooled),
          _stream())

@@ -111,6 +111,11 @@ int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, 
 int eunet_bn_eval_affine(int c, const float* gamma, const float* beta, const float* run_mean,
                          const float* run_var, float eps, float* scale, float* shift, void* stream);
 
+/* BN-apply + ReLU, out = relu(y * scale + shift) (models.py:219-222: the BatchNorm2d + ReLU between
+ * the two convs of a DoubleConv), materialised once for the second conv's forward and weight
+ * gradient (which then read it without applying the transform per staged halo pixel) */
+int eunet_bnrelu(const eunet_act* y, const float* scale, const float* shift, const eunet_act* out, void* stream);
+
 /* ---- fused BN-apply + ReLU consumers ----------------------------------------
  * pool: MaxPool2d(2) (models.py:214, 229-231); act (nullable) receives the
  * full-resolution activation (the skip tensor, written into its concat slot,

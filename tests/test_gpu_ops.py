@@ -530,3 +530,19 @@ def test_upsample_bwd_small_channels(C, h, w):
     ops.upsample_bwd(ops.act(gh.to(DEV, torch.float32)), ops.act(glo))
     torch.cuda.synchronize()
     assert rel(glo, lo.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bnrelu(dt):
+    """Materialised DoubleConv activation relu(y * scale + shift) on a channel slice."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(16)
+    N, H, W, C, CT, CO = 2, 9, 13, 48, 64, 8
+    ybuf = torch.randn(N, H, W, CT, generator=g).to(DEV, dt)
+    sc = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(C, generator=g) * 0.3).to(DEV)
+    out = torch.empty(N, H, W, C, dtype=dt, device=DEV)
+    ops.bnrelu(ops.act(ybuf, CO, C), sc, sh, ops.act(out))
+    torch.cuda.synchronize()
+    ref = torch.relu(ybuf[..., CO:CO + C].double() * sc.double() + sh.double())
+    assert rel(out, ref) < (1e-6 if dt == torch.float32 else 1e-2)

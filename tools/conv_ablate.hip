@@ -77,6 +77,16 @@ static int wgrad_main(int N, int H, int W, int cin, int cout, int reps) {
   a.isc = nullptr; a.ish = nullptr; a.iss = 0; a.order = 0; a.phase = 0;
   a.dy = dy; a.dct = cout; a.dco = 0; a.cout = cout;
   a.dw = dwp; a.db = dbp;
+  if (getenv("ABLATE_ISC") != nullptr) {  // BN+ReLU operand transform on (scale 1, shift 0)
+    std::vector<float> one(cin, 1.f), zero(cin, 0.f);
+    float *sc, *sh;
+    CK(hipMalloc(&sc, cin * 4));
+    CK(hipMalloc(&sh, cin * 4));
+    CK(hipMemcpy(sc, one.data(), cin * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(sh, zero.data(), cin * 4, hipMemcpyHostToDevice));
+    a.isc = sc;
+    a.ish = sh;
+  }
   a.tx = cdiv(W, TW); a.ty = cdiv(H, TH); a.ntiles = N * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, ns);
   a.nsplit = ns;
