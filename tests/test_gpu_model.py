@@ -216,3 +216,28 @@ def test_fp32_large_forward_vs_oracle():
     with torch.no_grad():
         out = m(x.to(DEV))
     assert _rel(out, ref) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_materialised_activation_is_exact(dtype, monkeypatch):
+    """The DoubleConv activation materialised once (eunet_bnrelu, default) and the BN+ReLU
+    applied inside conv .3's forward / wgrad operand staging round identically, so the
+    logits, the loss and every gradient agree bit for bit."""
+    from eunet import engine, synth
+    from eunet.losses import combined_loss
+    x, msk = synth.batch(2, 64, 64, start_index=3, num_classes=2, in_channels=1)
+    out = {}
+    for mat in (True, False):
+        monkeypatch.setattr(engine, "MATERIALIZE_ZA", mat)
+        m = _model(16, 1, 2, dtype)
+        m.train()
+        logits = m.forward_lowres(x.to(DEV))
+        loss = combined_loss(logits, msk.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        out[mat] = (logits.detach().clone(), loss.item(),
+                    {k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    assert torch.equal(out[True][0], out[False][0])
+    assert out[True][1] == out[False][1]
+    for k, g in out[True][2].items():
+        assert torch.equal(g, out[False][2][k]), k
