@@ -636,14 +636,69 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   }
 }
 
+// Fused BN-backward reduction in a gradient producer (the reduction half of bn_bwd_reduce for
+// the block whose output gradient g the kernel writes): each thread accumulates, for its 16-byte
+// channel unit, s1 += g', s2 += g' xhat over the pixels it writes (g' = stored g where
+// gamma xhat + beta > 0, xhat = (y - mean) istd); the block then sums its threads of equal unit
+// in fixed order into part[block][2][C].  Requires NT % U == 0 (U = C / E channel units).
+struct BnRed {
+  const void* y; int yct, yco;
+  const float* mean; const float* istd; const float* gamma; const float* beta;
+  float* part;
+};
+
 template <typename T>
-__global__ void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct, int gpco,
-                                    const T* gs, int gsct, int gsco, T* go, int goct, int goco, int N, int H, int W,
-                                    int C) {
+__device__ __forceinline__ void bnred_acc(const BnRed& r, long long pix, int c, const uint4& packed, float* s1,
+                                          float* s2) {
+  constexpr int E = Vec16<T>::N;
+  float gr[E], yv[E];
+  Vec16<T>::unpack(packed, gr);
+  Vec16<T>::unpack(*(const uint4*)((const T*)r.y + pix * r.yct + r.yco + c), yv);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const float xh = (yv[j] - r.mean[c + j]) * r.istd[c + j];
+    const float gp = fmaf(r.gamma[c + j], xh, r.beta[c + j]) > 0.f ? gr[j] : 0.f;
+    s1[j] += gp;
+    s2[j] = fmaf(gp, xh, s2[j]);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void bnred_block(const BnRed& r, int C, const float* s1, const float* s2) {
+  constexpr int E = Vec16<T>::N;
+  __shared__ float red[2][NT][E];
+  const int tid = threadIdx.x, U = C / E;
+#pragma unroll
+  for (int j = 0; j < E; ++j) { red[0][tid][j] = s1[j]; red[1][tid][j] = s2[j]; }
+  __syncthreads();
+  if (tid < U) {
+    float t1[E], t2[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) { t1[j] = 0.f; t2[j] = 0.f; }
+    for (int k = tid; k < NT; k += U)
+#pragma unroll
+      for (int j = 0; j < E; ++j) { t1[j] += red[0][k][j]; t2[j] += red[1][k][j]; }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      r.part[((long long)blockIdx.x * 2 + 0) * C + tid * E + j] = t1[j];
+      r.part[((long long)blockIdx.x * 2 + 1) * C + tid * E + j] = t2[j];
+    }
+  }
+}
+
+template <typename T, bool RED = false>
+__global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
+                                                          int gpco, const T* gs, int gsct, int gsco, T* go, int goct,
+                                                          int goco, int N, int H, int W, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E, Ho = H / 2, Wo = W / 2;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (long long)N * Ho * Wo * U) return;
+  float s1[E], s2[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  // grid-stride (the fused reduction runs on a capped grid: fewer partial rows); the stride is a
+  // multiple of U, so a thread keeps its channel unit
+  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < (long long)N * Ho * Wo * U;
+       id += (long long)gridDim.x * blockDim.x) {
   const int u = (int)(id % U);
   long long p = id / U;
   const int xo = (int)(p % Wo); p /= Wo;
@@ -679,8 +734,12 @@ __global__ void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const 
     }
 #pragma unroll
     for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
-    *(uint4*)(go + pix * goct + goco + c) = Vec16<T>::pack(o);
+    const uint4 packed = Vec16<T>::pack(o);
+    *(uint4*)(go + pix * goct + goco + c) = packed;
+    if constexpr (RED) bnred_acc<T>(br, pix, c, packed, s1, s2);
   }
+  }
+  if constexpr (RED) bnred_block<T>(br, C, s1, s2);
 }
 
 // adjoint of the x2 bilinear taps; per low-res row y the contributing
@@ -727,13 +786,16 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
 
 // 2x2 low-res outputs per thread: the 6x6 high-res window they share is read once (36 vector
 // loads instead of 4 x 16), separable adjoint weights per row / column
-template <typename T, typename TO>
+template <typename T, typename TO, bool RED = false>
 __global__ __launch_bounds__(256) void up_bwd2x2_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
-                                                        int h, int w, int C) {
+                                                        int h, int w, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E, H2 = 2 * h, W2 = 2 * w, hb = (h + 1) / 2, wb = (w + 1) / 2;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= (long long)N * hb * wb * U) return;
+  float s1[E], s2[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < (long long)N * hb * wb * U;
+       id += (long long)gridDim.x * blockDim.x) {
   const int u = (int)(id % U);
   long long p = id / U;
   const int xb = (int)(p % wb); p /= wb;
@@ -780,8 +842,14 @@ __global__ __launch_bounds__(256) void up_bwd2x2_kernel(const T* g, int gct, int
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
-      if (y0 + a < h && x0 + b < w)
-        *(uint4*)(o + ((long long)(n * h + y0 + a) * w + x0 + b) * oct + oco + c) = Vec16<TO>::pack(acc[a][b]);
+      if (y0 + a < h && x0 + b < w) {
+        const long long pix = (long long)(n * h + y0 + a) * w + x0 + b;
+        const uint4 packed = Vec16<TO>::pack(acc[a][b]);
+        *(uint4*)(o + pix * oct + oco + c) = packed;
+        if constexpr (RED) bnred_acc<TO>(br, pix, c, packed, s1, s2);
+      }
+  }
+  if constexpr (RED) bnred_block<TO>(br, C, s1, s2);
 }
 
 // fp32 K-channel (K <= 4) upsample backward for the head: g [N,2h,2w,K] -> o [N,h,w,K]
@@ -1208,7 +1276,7 @@ int eunet_pool_bwd_add(const eunet_act* act, const eunet_act* gpool, const eunet
   pool_bwd_add_kernel<T><<<gr, 256, 0, (hipStream_t)stream>>>(                                                  \
       (const T*)act->ptr, act->ctot, act->coff, (const T*)gpool->ptr, gpool->ctot, gpool->coff,                 \
       gskip ? (const T*)gskip->ptr : nullptr, gskip ? gskip->ctot : 0, gskip ? gskip->coff : 0, (T*)gout->ptr, \
-      gout->ctot, gout->coff, act->n, act->h, act->w, act->c)
+      gout->ctot, gout->coff, act->n, act->h, act->w, act->c, BnRed{})
   if (act->dtype == EUNET_BF16) PBA(bf16_t);
   else PBA(float);
 #undef PBA
@@ -1239,12 +1307,89 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
   if (ghi->dtype == EUNET_BF16)
     up_bwd2x2_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
-        glo->w, glo->c);
+        glo->w, glo->c, BnRed{});
   else
     up_bwd2x2_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
-        glo->w, glo->c);
+        glo->w, glo->c, BnRed{});
   EUNET_LAUNCH_CHECK("upsample_bwd");
+  return EUNET_OK;
+}
+
+// ---- gradient producers with the BN-backward reduction of the block they feed fused in ----
+namespace {
+bool bnr_ok(const eunet_act* g, const eunet_act* y) {
+  return act_ok(y) && vec_ok(y) && y->dtype == g->dtype && y->n == g->n && y->h == g->h && y->w == g->w &&
+         y->c == g->c && NT % (g->c / e16(g->dtype)) == 0;
+}
+long long pool_threads(const eunet_act* gout) {
+  return (long long)gout->n * (gout->h / 2) * (gout->w / 2) * (gout->c / e16(gout->dtype));
+}
+// fused-reduction grid, which is also the number of partial rows: at most cap blocks (each thread
+// then covers several outputs).  Measured: the max-pool adjoint prefers 2048 (fewer rows to write
+// and sum), the upsample adjoint, with more work per output, 8192 (more loads in flight).
+int bnr_grid(long long threads, int cap) { return (int)std::min<long long>((threads + NT - 1) / NT, cap); }
+long long up_threads(const eunet_act* glo) {
+  return (long long)glo->n * ((glo->h + 1) / 2) * ((glo->w + 1) / 2) * (glo->c / e16(glo->dtype));
+}
+}  // namespace
+
+int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows) {
+  EUNET_REQUIRE(act_ok(gout) && rows, "pool_bwd_add_bnr_rows: bad args");
+  *rows = (NT % (gout->c / e16(gout->dtype)) == 0) ? bnr_grid(pool_threads(gout), 2048) : 0;
+  return EUNET_OK;
+}
+
+int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
+                           const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(act) && act_ok(gpool) && act_ok(gout) && vec_ok(act) && vec_ok(gpool) && vec_ok(gout),
+                "pool_bwd_add_bnr: bad tensors");
+  if (gskip) EUNET_REQUIRE(act_ok(gskip) && vec_ok(gskip) && gskip->c == act->c, "pool_bwd_add_bnr: gskip");
+  EUNET_REQUIRE(gpool->h * 2 == act->h && gpool->w * 2 == act->w && gout->h == act->h && gout->w == act->w &&
+                    gpool->c == act->c && gout->c == act->c,
+                "pool_bwd_add_bnr: shapes");
+  EUNET_REQUIRE(bnr_ok(gout, y) && mean && invstd && gamma && beta && part,
+                "pool_bwd_add_bnr: y / BN args (and 256 %% channel units == 0)");
+  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, gamma, beta, part};
+  const unsigned gr = (unsigned)bnr_grid(pool_threads(gout), 2048);
+#define PBA(T)                                                                                                  \
+  pool_bwd_add_kernel<T, true><<<gr, NT, 0, (hipStream_t)stream>>>(                                             \
+      (const T*)act->ptr, act->ctot, act->coff, (const T*)gpool->ptr, gpool->ctot, gpool->coff,                 \
+      gskip ? (const T*)gskip->ptr : nullptr, gskip ? gskip->ctot : 0, gskip ? gskip->coff : 0, (T*)gout->ptr, \
+      gout->ctot, gout->coff, act->n, act->h, act->w, act->c, br)
+  if (act->dtype == EUNET_BF16) PBA(bf16_t);
+  else PBA(float);
+#undef PBA
+  EUNET_LAUNCH_CHECK("pool_bwd_add_bnr");
+  return EUNET_OK;
+}
+
+int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows) {
+  EUNET_REQUIRE(act_ok(glo) && rows, "upsample_bwd_bnr_rows: bad args");
+  *rows = (vec_ok(glo) && NT % (glo->c / e16(glo->dtype)) == 0) ? bnr_grid(up_threads(glo), 8192) : 0;
+  return EUNET_OK;
+}
+
+int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eunet_act* y, const float* mean,
+                           const float* invstd, const float* gamma, const float* beta, float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(ghi) && act_ok(glo) && vec_ok(ghi) && vec_ok(glo) && ghi->dtype == glo->dtype,
+                "upsample_bwd_bnr: bad tensors");
+  EUNET_REQUIRE(ghi->h == 2 * glo->h && ghi->w == 2 * glo->w && ghi->c == glo->c && ghi->n == glo->n,
+                "upsample_bwd_bnr: shapes");
+  EUNET_REQUIRE(bnr_ok(glo, y) && mean && invstd && gamma && beta && part,
+                "upsample_bwd_bnr: y / BN args (and 256 %% channel units == 0)");
+  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, gamma, beta, part};
+  const unsigned gr = (unsigned)bnr_grid(up_threads(glo), 8192);
+  if (ghi->dtype == EUNET_BF16)
+    up_bwd2x2_kernel<bf16_t, bf16_t, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
+        glo->w, glo->c, br);
+  else
+    up_bwd2x2_kernel<float, float, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+        (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
+        glo->w, glo->c, br);
+  EUNET_LAUNCH_CHECK("upsample_bwd_bnr");
   return EUNET_OK;
 }
 

@@ -36,6 +36,9 @@ BN_MOMENTUM = 0.1
 #   1 (default) one elementwise pass; conv .3's forward and weight gradient read za as is
 #   0 applied inside both operand stagings instead (nothing stored; A/B: profiles/r01_ab_za.txt)
 MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "1") != "0"
+# the BN-b backward reduction of a block fused into the kernel producing its output gradient
+# (upsample / max-pool adjoints) instead of a separate bn_bwd_reduce pass (EUNET_FUSE_BN_REDUCE=0)
+FUSE_BN_REDUCE = os.environ.get("EUNET_FUSE_BN_REDUCE", "1") != "0"
 
 
 class GradSink:
@@ -203,7 +206,8 @@ class UNetEngine:
         return S
 
     # --------------------------------------------------------------- backward
-    def _block_bwd(self, nm, G: torch.Tensor, S, P, sink: GradSink, need_gx: bool, small: bool):
+    def _block_bwd(self, nm, G: torch.Tensor, S, P, sink: GradSink, need_gx: bool, small: bool, gred=(None, 0)):
+        """gred: (part, rows) of the block's BN-b backward reduction when G's producer fused it."""
         p = f"{self.prefix}{nm}"
         s = S[nm]
         ya, yb, bna, bnb, X = s["ya"], s["yb"], s["bna"], s["bnb"], s["X"]
@@ -240,7 +244,7 @@ class UNetEngine:
             db = sink.slot(conv + ".bias", (C,))
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
-        gyb = bn_back(p + ".4", G, yb, bnb)
+        gyb = bn_back(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
         if s.get("za") is not None:
             wgrad(p + ".3", ops.act(s["za"]), gyb)
         else:
@@ -295,6 +299,31 @@ class UNetEngine:
         dev, dt = gz.device, self.dtype
         ch = [b, 2 * b, 4 * b, 8 * b]
         pre = self.prefix
+
+        def bnr_args(nm):
+            s = S[nm]
+            return (ops.act(s["yb"]), s["bnb"]["mean"], s["bnb"]["invstd"], P[f"{pre}{nm}.4.weight"],
+                    P[f"{pre}{nm}.4.bias"])
+
+        def up_bwd(ghi: ops.Act, glo: torch.Tensor, nm):
+            """g w.r.t. block nm's output from the upsample adjoint, its BN-b reduction fused."""
+            rows = ops.upsample_bwd_bnr_rows(ops.act(glo)) if FUSE_BN_REDUCE else 0
+            if not rows:
+                ops.upsample_bwd(ghi, ops.act(glo))
+                return None, 0
+            part = _e(rows * 2 * glo.shape[3], torch.float32, dev)
+            ops.upsample_bwd_bnr(ghi, ops.act(glo), *bnr_args(nm), part)
+            return part, rows
+
+        def pool_bwd(act_saved: ops.Act, gpool: ops.Act, gskip: ops.Act, gout: torch.Tensor, nm):
+            rows = ops.pool_bwd_add_bnr_rows(ops.act(gout)) if FUSE_BN_REDUCE else 0
+            if not rows:
+                ops.pool_bwd_add(act_saved, gpool, gskip, ops.act(gout))
+                return None, 0
+            part = _e(rows * 2 * gout.shape[3], torch.float32, dev)
+            ops.pool_bwd_add_bnr(act_saved, gpool, gskip, ops.act(gout), *bnr_args(nm), part)
+            return part, rows
+
         # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))
         s2 = S["dec2"]
         gd2 = torch.empty_like(s2["yb"])
@@ -312,35 +341,32 @@ class UNetEngine:
         g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False)
         del gd2
         g_d3 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
-        ops.upsample_bwd(ops.act(g_cat2, 0, ch[1]), ops.act(g_d3))
-        g_cat3 = self._block_bwd("dec3", g_d3, S, P, sink, need_gx=True, small=False)
+        red = up_bwd(ops.act(g_cat2, 0, ch[1]), g_d3, "dec3")
+        g_cat3 = self._block_bwd("dec3", g_d3, S, P, sink, need_gx=True, small=False, gred=red)
         del g_d3
         g_d4 = _e((N, H >> 2, W >> 2, ch[2]), dt, dev)
-        ops.upsample_bwd(ops.act(g_cat3, 0, ch[2]), ops.act(g_d4))
-        g_cat4 = self._block_bwd("dec4", g_d4, S, P, sink, need_gx=True, small=False)
+        red = up_bwd(ops.act(g_cat3, 0, ch[2]), g_d4, "dec4")
+        g_cat4 = self._block_bwd("dec4", g_d4, S, P, sink, need_gx=True, small=False, gred=red)
         del g_d4
         g_e4 = _e((N, H >> 3, W >> 3, ch[3]), dt, dev)
-        ops.upsample_bwd(ops.act(g_cat4, 0, ch[3]), ops.act(g_e4))
+        red = up_bwd(ops.act(g_cat4, 0, ch[3]), g_e4, "enc4")
         # ---- encoder (skip gradients + max-pool backward)
-        g_p3 = self._block_bwd("enc4", g_e4, S, P, sink, need_gx=True, small=False)
+        g_p3 = self._block_bwd("enc4", g_e4, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e4
         g_e3 = _e((N, H >> 2, W >> 2, ch[2]), dt, dev)
-        ops.pool_bwd_add(ops.act(S["cat4"], ch[3], ch[2]), ops.act(g_p3), ops.act(g_cat4, ch[3], ch[2]),
-                         ops.act(g_e3))
+        red = pool_bwd(ops.act(S["cat4"], ch[3], ch[2]), ops.act(g_p3), ops.act(g_cat4, ch[3], ch[2]), g_e3, "enc3")
         del g_p3, g_cat4
-        g_p2 = self._block_bwd("enc3", g_e3, S, P, sink, need_gx=True, small=False)
+        g_p2 = self._block_bwd("enc3", g_e3, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e3
         g_e2 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
-        ops.pool_bwd_add(ops.act(S["cat3"], ch[2], ch[1]), ops.act(g_p2), ops.act(g_cat3, ch[2], ch[1]),
-                         ops.act(g_e2))
+        red = pool_bwd(ops.act(S["cat3"], ch[2], ch[1]), ops.act(g_p2), ops.act(g_cat3, ch[2], ch[1]), g_e2, "enc2")
         del g_p2, g_cat3
-        g_p1 = self._block_bwd("enc2", g_e2, S, P, sink, need_gx=True, small=False)
+        g_p1 = self._block_bwd("enc2", g_e2, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e2
         g_e1 = _e((N, H, W, ch[0]), dt, dev)
-        ops.pool_bwd_add(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]),
-                         ops.act(g_e1))
+        red = pool_bwd(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]), g_e1, "enc1")
         del g_p1, g_cat2
-        self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True)
+        self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True, gred=red)
         return sink.finish()
 
 

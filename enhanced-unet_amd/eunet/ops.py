@@ -227,6 +227,31 @@ def upsample_bwd(ghi: Act, glo: Act):
     call("eunet_upsample_bwd", ctypes.byref(ghi), ctypes.byref(glo), _stream())
 
 
+def pool_bwd_add_bnr_rows(gout: Act) -> int:
+    r = c_int()
+    call("eunet_pool_bwd_add_bnr_rows", ctypes.byref(gout), ctypes.byref(r))
+    return r.value
+
+
+def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act, y: Act, mean, invstd, gamma, beta,
+                     part):
+    """pool_bwd_add + the BN-backward partial sums of the block whose output gradient gout is."""
+    call("eunet_pool_bwd_add_bnr", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), ctypes.byref(gout),
+         ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma), _ptr(beta), _ptr(part), _stream())
+
+
+def upsample_bwd_bnr_rows(glo: Act) -> int:
+    r = c_int()
+    call("eunet_upsample_bwd_bnr_rows", ctypes.byref(glo), ctypes.byref(r))
+    return r.value
+
+
+def upsample_bwd_bnr(ghi: Act, glo: Act, y: Act, mean, invstd, gamma, beta, part):
+    """upsample_bwd + the BN-backward partial sums of the block whose output gradient glo is."""
+    call("eunet_upsample_bwd_bnr", ctypes.byref(ghi), ctypes.byref(glo), ctypes.byref(y), _ptr(mean), _ptr(invstd),
+         _ptr(gamma), _ptr(beta), _ptr(part), _stream())
+
+
 def conv1x1_bwd_tiles(y: Act) -> int:
     t = c_int()
     call("eunet_conv1x1_bwd_tiles", ctypes.byref(y), ctypes.byref(t))

@@ -189,6 +189,17 @@ int eunet_pool_bwd_add(const eunet_act* act, const eunet_act* gpool, const eunet
                        const eunet_act* gout, void* stream);
 /* Upsample x2 backward (adjoint of the bilinear taps) */
 int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream);
+/* The two producers above with the reduction half of eunet_bn_bwd_reduce fused in: gout / glo is
+ * the gradient w.r.t. relu(bn(y)) of the DoubleConv output y (models.py:222-223), and
+ * part[rows][2][C] receives (sum g', sum g' xhat) per block, rows from the *_rows query (0: the
+ * channel count does not allow the fused form -- use the separate reduce). */
+int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows);
+int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
+                           const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
+                           const float* gamma, const float* beta, float* part, void* stream);
+int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows);
+int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eunet_act* y, const float* mean,
+                           const float* invstd, const float* gamma, const float* beta, float* part, void* stream);
 /* dec1 1x1 backward: gact = W^T gz (w.r.t. relu(bn(y))), part [tiles][K*C + K]
  * = per-tile (gW, gb) partials */
 int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles);

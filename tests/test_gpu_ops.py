@@ -546,3 +546,47 @@ def test_bnrelu(dt):
     torch.cuda.synchronize()
     ref = torch.relu(ybuf[..., CO:CO + C].double() * sc.double() + sh.double())
     assert rel(out, ref) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("kind", ["pool", "up"])
+def test_fused_bn_reduce_in_gradient_producers(dt, kind):
+    """pool_bwd_add / upsample_bwd with the BN-backward reduction fused in: the gradient equals
+    the plain kernel's bit for bit, the partial sums equal bn_bwd_reduce on that gradient."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(17)
+    N, C = 2, 64
+    h, w = (10, 14) if kind == "pool" else (7, 9)   # gradient (output) spatial size
+    gout = torch.empty(N, h, w, C, dtype=dt, device=DEV)
+    gref = torch.empty_like(gout)
+    y = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
+    mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    istd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    if kind == "pool":
+        act = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
+        gp = torch.randn(N, h // 2, w // 2, C, generator=g).to(DEV, dt)
+        gs = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
+        ops.pool_bwd_add(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gref))
+        rows = ops.pool_bwd_add_bnr_rows(ops.act(gout))
+        part = torch.empty(rows * 2 * C, device=DEV)
+        ops.pool_bwd_add_bnr(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gout), ops.act(y), mean, istd, gamma,
+                             beta, part)
+    else:
+        gh = torch.randn(N, 2 * h, 2 * w, C, generator=g).to(DEV, dt)
+        ops.upsample_bwd(ops.act(gh), ops.act(gref))
+        rows = ops.upsample_bwd_bnr_rows(ops.act(gout))
+        part = torch.empty(rows * 2 * C, device=DEV)
+        ops.upsample_bwd_bnr(ops.act(gh), ops.act(gout), ops.act(y), mean, istd, gamma, beta, part)
+    assert rows > 0
+    red = torch.empty(2 * C, device=DEV)
+    ops.colsum(part, rows, 2 * C, red)
+    tiles = ops.bn_bwd_tiles(ops.act(y))
+    p2 = torch.empty(tiles * 2 * C, device=DEV)
+    ops.bn_bwd_reduce(ops.act(gref), ops.act(y), mean, istd, gamma, beta, p2)
+    red2 = torch.empty(2 * C, device=DEV)
+    ops.colsum(p2, tiles, 2 * C, red2)
+    torch.cuda.synchronize()
+    assert torch.equal(gout, gref)
+    assert rel(red, red2) < 1e-5
