@@ -913,12 +913,22 @@ __global__ __launch_bounds__(256) void up_bwd_k2_kernel(const float2* g, float2*
 // 8 lanes per pixel, lane group g owns channels 8g+64j (C <= 128); partial
 // sums stay in registers over the block's C1X_PIX pixels.
 constexpr int C1X_PIX = 1024;
-template <typename T>
+// sum over the 8 pixel slots of a wave (lanes l, l^8, l^16, l^32, ...): DPP row rotate by 8 within
+// each 16-lane row, then the gfx950 permlane16 / permlane32 swaps (no ds_bpermute round trips)
+__device__ __forceinline__ float sum_slots8(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror 8
+  return xor32_sum(xor16_sum(v));
+}
+
+// BNR: also the BN-backward reduction (sum g', sum g' xhat) of y's BatchNorm over the produced
+// gradient (g' = the stored gradient where relu(bn(y)) > 0), per block into bpart[block][2][C]
+template <typename T, bool BNR = false>
 __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P, int C, int yct, int yco,
                                                          const float* sc, const float* sh, const float* w, int K,
-                                                         const float* gz, T* ga, int gct, int gco, float* part) {
+                                                         const float* gz, T* ga, int gct, int gco, float* part,
+                                                         const float* bmean, const float* bistd, float* bpart) {
   constexpr int E = Vec16<T>::N;
-  __shared__ float red[4][3 * 128 + 3];
+  __shared__ float red[4][3 * 128 + 3 + (BNR ? 2 * 128 : 0)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int stride = K * C + K;
   float aw[2][3][8], ab[3] = {0.f, 0.f, 0.f};
@@ -929,6 +939,7 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
 #pragma unroll
       for (int e = 0; e < 8; ++e) aw[j][k][e] = 0.f;
   float s8[2][8], t8[2][8], w8[2][3][8];  // this lane's channels 64j + 8g + e
+  float mu8[2][8], is8[2][8], bs1[2][8], bs2[2][8];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -937,6 +948,12 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
       const bool ok = c < C;
       s8[j][e] = ok ? sc[c] : 0.f;
       t8[j][e] = ok ? sh[c] : 0.f;
+      if constexpr (BNR) {
+        mu8[j][e] = ok ? bmean[c] : 0.f;
+        is8[j][e] = ok ? bistd[c] : 0.f;
+        bs1[j][e] = 0.f;
+        bs2[j][e] = 0.f;
+      }
 #pragma unroll
       for (int k = 0; k < 3; ++k) w8[j][k][e] = (ok && k < K) ? w[k * C + c] : 0.f;
     }
@@ -966,8 +983,25 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
         }
         go[e] = s;
       }
-      *(uint4*)(ga + p * gct + gco + c) = Vec16<T>::pack(go);
-      if constexpr (E == 4) *(uint4*)(ga + p * gct + gco + c + 4) = Vec16<T>::pack(go + 4);
+      const uint4 pk0 = Vec16<T>::pack(go);
+      *(uint4*)(ga + p * gct + gco + c) = pk0;
+      uint4 pk1 = pk0;
+      if constexpr (E == 4) {
+        pk1 = Vec16<T>::pack(go + 4);
+        *(uint4*)(ga + p * gct + gco + c + 4) = pk1;
+      }
+      if constexpr (BNR) {  // the stored (rounded) gradient, as bn_bwd_reduce would read it
+        float gr[8];
+        Vec16<T>::unpack(pk0, gr);
+        if constexpr (E == 4) Vec16<T>::unpack(pk1, gr + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (f[e] - mu8[j][e]) * is8[j][e];
+          const float gp = fmaf(f[e], s8[j][e], t8[j][e]) > 0.f ? gr[e] : 0.f;
+          bs1[j][e] += gp;
+          bs2[j][e] = fmaf(gp, xh, bs2[j][e]);
+        }
+      }
     }
   }
   // reduce over the 8 pixel slots of each wave (xor 8, 16, 32), then across waves
@@ -976,21 +1010,17 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float v = aw[j][k][e];
-        v += __shfl_xor(v, 8, 64);
-        v += __shfl_xor(v, 16, 64);
-        v += __shfl_xor(v, 32, 64);
-        aw[j][k][e] = v;
-      }
+      for (int e = 0; e < 8; ++e) aw[j][k][e] = k < K ? sum_slots8(aw[j][k][e]) : 0.f;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    float v = ab[k];
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    ab[k] = v;
-  }
+  for (int k = 0; k < 3; ++k) ab[k] = k < K ? sum_slots8(ab[k]) : 0.f;
+  if constexpr (BNR)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bs1[j][e] = sum_slots8(bs1[j][e]);
+        bs2[j][e] = sum_slots8(bs2[j][e]);
+      }
   if (lane < 8) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1003,10 +1033,25 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
         }
     if (lane == 0)
       for (int k = 0; k < K; ++k) red[wv][K * C + k] = ab[k];
+    if constexpr (BNR)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = 64 * j + 8 * g + e;
+          if (c < C) {
+            red[wv][stride + c] = bs1[j][e];
+            red[wv][stride + C + c] = bs2[j][e];
+          }
+        }
   }
   __syncthreads();
   for (int i = tid; i < stride; i += NT)
     part[(long long)blockIdx.x * stride + i] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  if constexpr (BNR)
+    for (int i = tid; i < 2 * C; i += NT)
+      bpart[(long long)blockIdx.x * 2 * C + i] =
+          red[0][stride + i] + red[1][stride + i] + red[2][stride + i] + red[3][stride + i];
 }
 
 }  // namespace
@@ -1411,13 +1456,37 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
     conv1x1_bwd_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
                                                                         y->coff, scale, shift, w, k, gz,
                                                                         (bf16_t*)gact->ptr, gact->ctot, gact->coff,
-                                                                        part);
+                                                                        part, nullptr, nullptr, nullptr);
   else
     conv1x1_bwd_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
                                                                        y->coff, scale, shift, w, k, gz,
                                                                        (float*)gact->ptr, gact->ctot, gact->coff,
-                                                                       part);
+                                                                       part, nullptr, nullptr, nullptr);
   EUNET_LAUNCH_CHECK("conv1x1_bwd");
+  return EUNET_OK;
+}
+
+int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* shift, const float* w, int k,
+                          const float* gz, const eunet_act* gact, float* part, const float* mean, const float* invstd,
+                          float* bn_part, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(gact) && vec_ok(y) && vec_ok(gact) && scale && shift && w && gz && part,
+                "conv1x1_bwd: bad args");
+  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 128 && y->c % 8 == 0 && gact->c == y->c && gact->dtype == y->dtype,
+                "conv1x1_bwd: K<=3, C<=128, C%8==0");
+  EUNET_REQUIRE(mean && invstd && bn_part, "conv1x1_bwd_bnr: BN args");
+  const long long P = (long long)y->n * y->h * y->w;
+  const unsigned tiles = (unsigned)((P + C1X_PIX - 1) / C1X_PIX);
+  if (y->dtype == EUNET_BF16)
+    conv1x1_bwd_kernel<bf16_t, true><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
+                                                                        y->coff, scale, shift, w, k, gz,
+                                                                        (bf16_t*)gact->ptr, gact->ctot, gact->coff,
+                                                                        part, mean, invstd, bn_part);
+  else
+    conv1x1_bwd_kernel<float, true><<<tiles, NT, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
+                                                                       y->coff, scale, shift, w, k, gz,
+                                                                       (float*)gact->ptr, gact->ctot, gact->coff,
+                                                                       part, mean, invstd, bn_part);
+  EUNET_LAUNCH_CHECK("conv1x1_bwd_bnr");
   return EUNET_OK;
 }
 

@@ -67,6 +67,7 @@ SIGNATURES = {
     "eunet_upsample_bwd_bnr": [_P, _P, _P, _f, _f, _f, _f, _f, c_void_p],
     "eunet_conv1x1_bwd_tiles": [_P, POINTER(c_int)],
     "eunet_conv1x1_bwd": [_P, _f, _f, _f, c_int, _f, _P, _f, c_void_p],
+    "eunet_conv1x1_bwd_bnr": [_P, _f, _f, _f, c_int, _f, _P, _f, _f, _f, _f, c_void_p],
     "eunet_semantic_counts": [_f, _f, c_int, c_int64, _f, c_void_p],
     "eunet_binary_overlap": [_f, _f, c_int64, _f, c_void_p],
     "eunet_resize_bilinear": [_f, c_int, c_int, c_int, _f, c_int, c_int, c_float, c_float, c_int, c_int,

@@ -24,7 +24,7 @@ from typing import List, Optional
 
 import torch
 
-from . import ops
+from . import engine, ops
 from .engine import BN_EPS, BN_MOMENTUM, GradSink, UNetEngine, _e
 
 DROP_P = (0.2, 0.15)   # models.py:287, 291
@@ -170,15 +170,22 @@ class DualEngine:
         g3 = torch.empty_like(y3)
         ct = ops.conv1x1_bwd_tiles(ops.act(y3))
         part = _e(ct * (K * C3 + K), torch.float32, dev)
-        ops.conv1x1_bwd(ops.act(y3), h3["scale"], h3["shift"], P["fusion_head.11.weight"].reshape(K, C3).contiguous(),
-                        K, gz, ops.act(g3), part)
+        w11 = P["fusion_head.11.weight"].reshape(K, C3).contiguous()
+        red3 = (None, 0)
+        if engine.FUSE_BN_REDUCE:
+            bpart = _e(ct * 2 * C3, torch.float32, dev)
+            ops.conv1x1_bwd_bnr(ops.act(y3), h3["scale"], h3["shift"], w11, K, gz, ops.act(g3), part,
+                                h3["mean"], h3["invstd"], bpart)
+            red3 = (bpart, ct)
+        else:
+            ops.conv1x1_bwd(ops.act(y3), h3["scale"], h3["shift"], w11, K, gz, ops.act(g3), part)
         red = _e(K * C3 + K, torch.float32, dev)
         ops.colsum(part, ct, K * C3 + K, red)
         sink.slot("fusion_head.11.weight", (K, C3, 1, 1)).copy_(red[:K * C3].view(K, C3, 1, 1))
         sink.slot("fusion_head.11.bias", (K,)).copy_(red[K * C3:])
         sink.ready(["fusion_residual.weight", "fusion_residual.bias", "fusion_head.11.weight", "fusion_head.11.bias"])
         # ---- conv 128->64 (fusion_head.8/.9)
-        gy3 = self._bn_back("fusion_head.9", g3, y3, h3, P, sink)
+        gy3 = self._bn_back("fusion_head.9", g3, y3, h3, P, sink, part=red3[0], tiles=red3[1])
         del g3
         self._wgrad("fusion_head.8.weight", ops.act(y2), gy3, sink, d2)
         gg2 = torch.empty_like(y2)

@@ -330,15 +330,23 @@ class UNetEngine:
         yb_act = ops.act(s2["yb"])
         tiles = ops.conv1x1_bwd_tiles(yb_act)
         part = _e(tiles * (K * b + K), torch.float32, dev)
-        ops.conv1x1_bwd(yb_act, s2["bnb"]["scale"], s2["bnb"]["shift"], P[pre + "dec1.weight"].reshape(K, b).contiguous(),
-                        K, gz, ops.act(gd2), part)
+        w1 = P[pre + "dec1.weight"].reshape(K, b).contiguous()
+        bnb2 = s2["bnb"]
+        red2 = (None, 0)
+        if FUSE_BN_REDUCE:
+            bpart = _e(tiles * 2 * b, torch.float32, dev)
+            ops.conv1x1_bwd_bnr(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part,
+                                bnb2["mean"], bnb2["invstd"], bpart)
+            red2 = (bpart, tiles)
+        else:
+            ops.conv1x1_bwd(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part)
         red = _e(K * b + K, torch.float32, dev)
         ops.colsum(part, tiles, K * b + K, red)
         sink.slot(pre + "dec1.weight", (K, b, 1, 1)).copy_(red[:K * b].view(K, b, 1, 1))
         sink.slot(pre + "dec1.bias", (K,)).copy_(red[K * b:])
         sink.ready([pre + "dec1.weight", pre + "dec1.bias"])
         # ---- decoder
-        g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False)
+        g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False, gred=red2)
         del gd2
         g_d3 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
         red = up_bwd(ops.act(g_cat2, 0, ch[1]), g_d3, "dec3")

@@ -263,6 +263,12 @@ def conv1x1_bwd(y: Act, scale, shift, w, k, gz, gact: Act, part):
          ctypes.byref(gact), _ptr(part), _stream())
 
 
+def conv1x1_bwd_bnr(y: Act, scale, shift, w, k, gz, gact: Act, part, mean, invstd, bn_part):
+    """conv1x1_bwd + the BN-backward partial sums [tiles][2][C] of y's BatchNorm over gact."""
+    call("eunet_conv1x1_bwd_bnr", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),
+         ctypes.byref(gact), _ptr(part), _ptr(mean), _ptr(invstd), _ptr(bn_part), _stream())
+
+
 # ---- evaluation path (evalpath.hip) ------------------------------------------------
 def semantic_counts(pred, gt):
     """pred, gt int64 [n, ...] -> counts int64 [n, 3, 3] = (#pred==c, #gt==c, #both==c)."""

@@ -206,6 +206,12 @@ int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles);
 int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift,
                       const float* w, int k, const float* gz, const eunet_act* gact, float* part,
                       void* stream);
+/* the same, also writing the BN-backward partial sums of y's BatchNorm over the gradient it
+ * produces (what eunet_bn_bwd_reduce would compute from gact): bn_part [tiles][2][C] = per-tile
+ * (sum g', sum g' xhat), g' = gact where relu(bn(y)) > 0 (scale/shift are that BN's affine form). */
+int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* shift,
+                          const float* w, int k, const float* gz, const eunet_act* gact, float* part,
+                          const float* mean, const float* invstd, float* bn_part, void* stream);
 
 /* ---- evaluation path (evalpath.hip) ---------------------------------------
  * Semantic metric counts (metrics.py:29-58, calculate_semantic_metrics): pred, gt

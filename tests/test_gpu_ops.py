@@ -270,6 +270,43 @@ def test_conv1x1_bwd(dt):
     assert rel(red[K * C:], gz.sum(dim=(0, 1, 2))) < 1e-4
 
 
+@pytest.mark.parametrize("dt,C,K", [(torch.bfloat16, 64, 2), (torch.bfloat16, 128, 2), (torch.bfloat16, 128, 3),
+                                    (torch.float32, 64, 3)])
+def test_conv1x1_bwd_fused_bn_reduce(dt, C, K):
+    """conv1x1_bwd with y's BN-backward reduction fused in: gact and the (gW, gb) partials equal the
+    plain kernel's bit for bit; the BN partial sums match bn_bwd_reduce on the stored gact."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(23)
+    N, H, W = 2, 12, 40
+    yd = torch.randn(N, H, W, C, generator=g).to(DEV, dt)
+    mean = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    istd = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    sc = gamma * istd
+    sh = beta - mean * sc
+    w = (torch.randn(K, C, generator=g) / 4).to(DEV)
+    gz = torch.randn(N, H, W, K, generator=g).to(DEV)
+    tiles = ops.conv1x1_bwd_tiles(ops.act(yd))
+    ga1, ga2 = torch.empty_like(yd), torch.empty_like(yd)
+    p1 = torch.empty(tiles * (K * C + K), device=DEV)
+    p2 = torch.empty_like(p1)
+    bp = torch.empty(tiles * 2 * C, device=DEV)
+    ops.conv1x1_bwd(ops.act(yd), sc, sh, w, K, gz, ops.act(ga1), p1)
+    ops.conv1x1_bwd_bnr(ops.act(yd), sc, sh, w, K, gz, ops.act(ga2), p2, mean, istd, bp)
+    red = torch.empty(2 * C, device=DEV)
+    ops.colsum(bp, tiles, 2 * C, red)
+    bt = ops.bn_bwd_tiles(ops.act(yd))
+    bp2 = torch.empty(bt * 2 * C, device=DEV)
+    ops.bn_bwd_reduce(ops.act(ga1), ops.act(yd), mean, istd, gamma, beta, bp2)
+    red2 = torch.empty(2 * C, device=DEV)
+    ops.colsum(bp2, bt, 2 * C, red2)
+    torch.cuda.synchronize()
+    assert torch.equal(ga1, ga2)
+    assert torch.equal(p1, p2)
+    assert rel(red, red2) < 1e-5
+
+
 def _head_ref(z, w1, b1, gamma, beta, w2, b2):
     u = F.interpolate(z, scale_factor=2, mode="bilinear", align_corners=False)
     h = F.conv2d(u, w1, b1, padding=1)

@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out
 TAG=${TAG:-ab}
 IFS=';' read -ra CF <<< "${CONFIGS:-X=0}"
-for rep in 1 2; do
+for rep in $(seq ${REPS:-2}); do
   for v in "${CF[@]}"; do
     env $v timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline --dice-size 0 ${BENCH_ARGS:-} \
       > gpurun_out/bench_${TAG}.log 2>&1
