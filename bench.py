@@ -39,6 +39,12 @@ PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}  # MI355X_MICROARCH.md dense MFMA 
 HBM_PEAK_GBS = 8000.0
 
 
+# The loss stays on the device (Trainer.train_epoch accumulates it there and reads it once per
+# epoch), so the host queues step k+1 while step k runs.  EUNET_BENCH_SYNC_LOSS=1 reads
+# loss.item() every step as the reference's loop does: ~0.7 ms/step of idle GPU (profiles/r01_ab_sync.txt).
+SYNC_LOSS = os.environ.get("EUNET_BENCH_SYNC_LOSS", "0") == "1"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -195,7 +201,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            tr.step(x, m)
+            tr.step(x, m, sync_loss=SYNC_LOSS)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     if world > 1:
@@ -210,7 +216,7 @@ def main():
             dist.destroy_process_group()
         return
     imgs = world * args.batch * args.steps
-    fam = ks.get("conv3x3_fwd", {"ms": float("nan"), "flops": 0.0, "launches": 0})
+    fam = ks.get("conv3x3_fwd", {"ms": 0.0, "flops": 0.0, "launches": 0, "bytes": 0.0})
     achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12 if fam["ms"] else None
     peak = PEAK_TFLOPS[args.dtype]
     roof = {"kernel": "conv3x3_fwd_kernel (implicit-GEMM MFMA, fwd + dgrad launches)", "bound": "mfma",

@@ -6,6 +6,8 @@ C-ABI launches on -- and credited with their algorithmic FLOPs / bytes.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 _active = None
@@ -34,10 +36,13 @@ class KernelTimer:
         return out
 
 
+_OFF = os.environ.get("EUNET_KPROF", "1") == "0"  # diagnostic: measure the event overhead itself
+
+
 def timed(family: str, flops: float, nbytes: float = 0.0):
     """Context manager used around a launch; no-op when no timer is active."""
     t = _active
-    if t is None:
+    if t is None or _OFF:
         return _Null
     return _Rec(t, family, flops, nbytes)
 

@@ -138,16 +138,15 @@ class Trainer:
 
     def train_epoch(self, dataloader):
         self.model.train()
-        total = 0.0
+        total = None  # device-side running sum: one host sync per epoch, not per step
         n = 0
         for batch in dataloader:
             images = batch["images"].to(self.device, non_blocking=True)
-            _, _, h, w = images.shape
-            h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
             masks = self._masks(batch, self.device, 0, 0)
-            total += self.step(images, masks)
+            loss = self.step(images, masks, sync_loss=False).double()
+            total = loss if total is None else total + loss
             n += 1
-        return total / max(1, n)
+        return float(total.item()) / n if n else 0.0
 
     def epoch_lr_step(self, epoch: int) -> float:
         """train_model's per-epoch stepping (train_eval.py:1104-1111).  The reference steps the

@@ -241,3 +241,24 @@ def test_materialised_activation_is_exact(dtype, monkeypatch):
     assert out[True][1] == out[False][1]
     for k, g in out[True][2].items():
         assert torch.equal(g, out[False][2][k]), k
+
+
+def test_train_epoch_device_loss_sum():
+    """Trainer.train_epoch keeps the running loss on the device (one sync per epoch) and returns
+    what the reference's per-step `total += loss.item()` loop returns (train_eval.py train_epoch),
+    with the same parameters afterwards (the kernels reduce in a fixed order)."""
+    from eunet import synth
+    from eunet.train_eval import Trainer
+    batches = []
+    for i in range(3):
+        x, msk = synth.batch(2, 64, 64, start_index=2 * i, num_classes=2, in_channels=1)
+        batches.append({"images": x, "batch_items": [{"semantic_mask": mm} for mm in msk]})
+    ta = Trainer(_model(16, 1, 2, "bf16"), DEV, "enhanced_unet", total_epochs=50)
+    tb = Trainer(_model(16, 1, 2, "bf16"), DEV, "enhanced_unet", total_epochs=50)
+    avg = ta.train_epoch(batches)
+    tot = 0.0
+    for b in batches:
+        tot += tb.step(b["images"].to(DEV), tb._masks(b, DEV, 0, 0))
+    assert avg == tot / len(batches)
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
