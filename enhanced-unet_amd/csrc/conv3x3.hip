@@ -213,13 +213,24 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
 // PIPE: the 9 taps of a chunk are software-pipelined -- the fragments of tap t+1 are read
 //   from LDS into a second register set while tap t's MFMAs run (one wave per SIMD with DB,
 //   so no other wave hides the ds_read latency; 512 registers per lane leave room for it).
+// GB (bf16, no operand transform): the weight fragments are read straight from global memory
+//   (L2-resident packed weights, prefetched three taps ahead in registers) and LDS holds only
+//   the input halo, double-buffered (2 x 39 KB, still two blocks per CU).  The next chunk's
+//   halo is staged by LDS-DMA during the current chunk's MFMAs, so a block never waits on a
+//   staging round trip inside the K loop and no staging VGPRs / LDS writes are issued.
+//   Opt-in (EUNET_CONV_GB=1), slower: conv fwd+dgrad 16.0 vs 11.3 ms/step.  The weight loads
+//   share vmcnt with the DMA, so the first fragment load issued after the DMA waits for the
+//   whole halo (4.3 ms of the loss: a diagnostic build without the DMA ran 11.8); B from L2
+//   instead of LDS costs another ~1.4 ms (fixed-address weights: 14.6).  profiles/r01_ab_conv_gb.txt
 __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised)
+constexpr int FWD_LDS_GB = 2 * FA_BYTES;  // 79872
 
 template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, int DMA = 0,
-          bool PIPE = false>
+          bool PIPE = false, bool GB = false>
 __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
   static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
   static_assert(!BDMA || (DB && !SPEC), "BDMA needs the double-buffered block");
+  static_assert(!GB || (sizeof(T) == 2 && !DB && NW == 4 && DMA == 0 && MODE == 0), "GB: bf16 single-stage block");
   constexpr int NTH = 64 * NW;
   constexpr int NCW = SPEC ? 4 : NW;          // computing waves
   constexpr int NLT = SPEC ? 256 : NTH;       // staging threads
@@ -413,6 +424,92 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
     }
   };
 
+  if constexpr (GB) {
+    if (a.phase && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(40);
+    // buffer descriptors: 32-bit per-lane offsets, wave-uniform parts in soffset (host checks
+    // that the input fits 2^31 bytes and that cin is a whole number of chunks)
+    const int kstr = 4 * a.cout_pad * 9 * 16;  // bytes per K-chunk of packed weights
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.wp, (short)0, a.nkc * kstr, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, (short)0, (int)((long long)a.N * a.H * a.W * a.xct * 2), 0x00020000);
+    const unsigned wlane = (unsigned)((q * a.cout_pad + co0 + li) * 9 * 16);
+    auto ldb = [&](int kc, int t, uint4 (&fb)[4]) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        fb[nt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, wlane, kc * kstr + (nt * 16 * 9 + t) * 16, 0));
+    };
+    constexpr int NDMA = 4 * (FHPXP / 64) / NW;  // 10 halo wave-instructions per wave
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    auto dma_halo = [&](int kc, int buf) {
+      constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
+      char* As_ = smem + buf * FA_BYTES;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));  // opaque: the per-lane offsets are recomputed per chunk, not held
+#pragma unroll
+      for (int jj = 0; jj < NDMA; ++jj) {
+        const int j = wvu + jj * NW;
+        const int qq = j / (FHPXP / 64), hp0 = (j % (FHPXP / 64)) * 64, hp = hp0 + ln;
+        const int hy = hp / FHW, hx = hp - hy * FHW;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        const bool ok = (hp < FHPX) & (yy >= 0) & (yy < a.H) & (xx >= 0) & (xx < a.W);
+        // out-of-image / plane-padding lanes read past the descriptor's range: zero fill
+        const unsigned off = ok ? (unsigned)((((n * a.H + yy) * a.W + xx) * a.xct + a.xco + qq * E) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(As_ + (qq * FHPXP + hp0) * 16),
+                                                 16, off, kc * KC * 2, 0, 0);
+      }
+    };
+    constexpr int PD = 3;  // weight-fragment prefetch distance (taps)
+    uint4 fb[PD][4];
+    dma_halo(0, 0);
+#pragma unroll
+    for (int t = 0; t < PD; ++t) ldb(0, t, fb[t]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kc = 0; kc < a.nkc; ++kc) {
+      const char* As = smem + (kc & 1) * FA_BYTES;
+      // tap rows not unrolled (as in the staged path): bounds how far the scheduler hoists the
+      // fragment reads; with PD = 3 the prefetch slot of tap (ky, kx) is kx
+#pragma unroll 1
+      for (int ky = 0; ky < 3; ++ky) {
+        const unsigned abase = (unsigned)(uintptr_t)(As + (q * FHPXP + (RPW * wv + ky) * FHW + li) * 16);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          // The fragment reads are inline asm: the compiler cannot prove they miss the LDS-DMA
+          // writes into the other buffer and would otherwise wait for every outstanding load
+          // (DMA and weight prefetch alike) before them.  lgkmcnt is waited on by hand.
+          u32x4 fa[MT];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                         : "=v"(fa[mt])
+                         : "v"(abase), "i"((((mt >> 1) * FHW + (mt & 1) * 16 + kx) * 16)));
+          static_assert(MT == 8, "GB: eight fragment registers tied to the wait");
+          // the wait names the fragments as operands, so no MFMA can be scheduled above it
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
+                         "+v"(fa[7])::"memory");
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, fa[mt]), __builtin_bit_cast(bf16x8, fb[kx][nt]), acc[mt][nt], 0, 0, 0);
+          // refill this slot with tap (ky+1, kx), the next chunk's first row after ky = 2; the
+          // last chunk re-reads its own weights instead of branching, so the wait counts stay static
+          ldb(min(ky < 2 ? kc : kc + 1, a.nkc - 1), ((ky + 1) % 3) * 3 + kx, fb[kx]);
+          if (kx == 0 && ky == 0 && kc + 1 < a.nkc) dma_halo(kc + 1, (kc + 1) & 1);
+        }
+      }
+      // the DMA was issued before the 32 fragment loads of taps 1..8: vmcnt <= 12 covers it
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      __syncthreads();
+    }
+  } else {  // register / LDS-staged K loop (every other variant)
   uint4 fa0[MT], fb0[4];
   const bool conv_pro1 = a.pro1 != 0;
   // Phase offset: the two blocks sharing a CU start (and, with equal work, keep running) in
@@ -501,6 +598,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
       chunk(smem, smem + FA_BYTES, fa0, fb0);
     }
   }
+  }  // !GB
 #undef CONV_GLOAD_A
 #undef CONV_GLOAD_B
 #undef CONV_LWRITE_A
@@ -1477,6 +1575,11 @@ int conv_dma() {
   return o;
 }
 
+int conv_gb() {  // EUNET_CONV_GB: weight fragments from global, halo double-buffered by LDS-DMA
+  static const int o = env_order("EUNET_CONV_GB", 0);
+  return o;
+}
+
 template <int DMA>
 void launch_fwd_dma(const FwdArgs& a, int dtype, dim3 grid, void* stream) {
   if (dtype == EUNET_BF16) {
@@ -1498,6 +1601,16 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
     return EUNET_OK;
   }
   dim3 grid(a.ntiles * (a.cout_pad / BN));
+  const bool gb_ok = dtype == EUNET_BF16 && a.isc == nullptr && a.cin % KCh<bf16_t>::v == 0 &&
+                     (long long)a.N * a.H * a.W * a.xct * 2 < (1LL << 31) &&
+                     (long long)a.nkc * 4 * a.cout_pad * 9 * 16 < (1LL << 31);
+  if (gb_ok && conv_gb()) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, 0, false, true>, FWD_LDS_GB);
+    conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, 0, false, true>
+        <<<grid, FT, FWD_LDS_GB, (hipStream_t)stream>>>(a);
+    EUNET_LAUNCH_CHECK("conv3x3_fwd");
+    return EUNET_OK;
+  }
   switch (conv_dma()) {
     case 1: launch_fwd_dma<1>(a, dtype, grid, stream); break;
     case 2: launch_fwd_dma<2>(a, dtype, grid, stream); break;
