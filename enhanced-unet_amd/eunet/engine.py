@@ -110,21 +110,22 @@ class UNetEngine:
         ya = _e((N, H, W, C), self.dtype, dev)
         yb = _e((N, H, W, C), self.dtype, dev)
         st, tiles = self._stats_buf(ya) if training else (None, 0)
+        enc = "conv3x3_fwd.encoder" if nm.startswith("enc") else None  # bench: the encoder's MFMA convs
         if small:
             ops.conv_small_fwd(X, P[p + ".0.weight"], P[p + ".0.bias"], ops.act(ya), st)
         else:
             wp = ops.conv3x3_pack(P[p + ".0.weight"], self.dtype, flip=False)
-            ops.conv3x3_fwd(X, wp, ops.act(ya), bias=P[p + ".0.bias"], stats=st)
+            ops.conv3x3_fwd(X, wp, ops.act(ya), bias=P[p + ".0.bias"], stats=st, sub=enc)
         bna = self._bn(p + ".1", st, tiles, C, training, P, B)
         wp = ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
         za = None
         if MATERIALIZE_ZA:  # one BN+ReLU pass; conv .3 forward and weight gradient read za as is
             za = _e((N, H, W, C), self.dtype, dev)
             ops.bnrelu(ops.act(ya), bna["scale"], bna["shift"], ops.act(za))
-            ops.conv3x3_fwd(ops.act(za), wp, ops.act(yb), bias=P[p + ".3.bias"], stats=st)
+            ops.conv3x3_fwd(ops.act(za), wp, ops.act(yb), bias=P[p + ".3.bias"], stats=st, sub=enc)
         else:  # BN+ReLU applied while staging conv .3's operand tiles (forward and wgrad)
             ops.conv3x3_fwd(ops.act(ya), wp, ops.act(yb), bias=P[p + ".3.bias"], scale=bna["scale"],
-                            shift=bna["shift"], stats=st)
+                            shift=bna["shift"], stats=st, sub=enc)
         bnb = self._bn(p + ".4", st, tiles, C, training, P, B)
         return dict(ya=ya, za=za, yb=yb, bna=bna, bnb=bnb, X=X)
 

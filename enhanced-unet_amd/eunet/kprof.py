@@ -39,12 +39,13 @@ class KernelTimer:
 _OFF = os.environ.get("EUNET_KPROF", "1") == "0"  # diagnostic: measure the event overhead itself
 
 
-def timed(family: str, flops: float, nbytes: float = 0.0):
-    """Context manager used around a launch; no-op when no timer is active."""
+def timed(family: str, flops: float, nbytes: float = 0.0, sub: str | None = None):
+    """Context manager used around a launch; no-op when no timer is active.
+    sub: a second family the same events are credited to (a subset of `family`)."""
     t = _active
     if t is None or _OFF:
         return _Null
-    return _Rec(t, family, flops, nbytes)
+    return _Rec(t, family, flops, nbytes, sub)
 
 
 class _NullCtx:
@@ -59,10 +60,10 @@ _Null = _NullCtx()
 
 
 class _Rec:
-    __slots__ = ("t", "fam", "flops", "nbytes", "e0")
+    __slots__ = ("t", "fam", "flops", "nbytes", "e0", "sub")
 
-    def __init__(self, t, fam, flops, nbytes):
-        self.t, self.fam, self.flops, self.nbytes = t, fam, flops, nbytes
+    def __init__(self, t, fam, flops, nbytes, sub=None):
+        self.t, self.fam, self.flops, self.nbytes, self.sub = t, fam, flops, nbytes, sub
 
     def __enter__(self):
         self.e0 = torch.cuda.Event(enable_timing=True)
@@ -73,4 +74,6 @@ class _Rec:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         self.t.records.setdefault(self.fam, []).append((self.e0, e1, self.flops, self.nbytes))
+        if self.sub is not None:
+            self.t.records.setdefault(self.sub, []).append((self.e0, e1, self.flops, self.nbytes))
         return False

@@ -68,13 +68,14 @@ def conv3x3_tiles(y_act: Act) -> int:
     return t.value
 
 
-def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None, nstride=0):
-    """nstride > 0: scale/shift are per-sample [N][nstride] (BN+ReLU+Dropout2d folded)."""
+def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None, nstride=0, sub=None):
+    """nstride > 0: scale/shift are per-sample [N][nstride] (BN+ReLU+Dropout2d folded).
+    sub: optional kprof sub-family the launch is also credited to (e.g. the encoder forward convs)."""
     flops = 2.0 * 9 * x.c * y.c * x.n * x.h * x.w
     esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
     # algorithmic HBM bytes: read x once, write y once, read the packed weights once
     nbytes = float(esz * x.n * x.h * x.w * (x.c + y.c) + wp.numel() * wp.element_size())
-    with kprof.timed("conv3x3_fwd", flops, nbytes):
+    with kprof.timed("conv3x3_fwd", flops, nbytes, sub=sub):
         call("eunet_conv3x3_fwd", ctypes.byref(x), _ptr(scale), _ptr(shift), int(nstride), _ptr(wp), _ptr(bias),
              ctypes.byref(y), _ptr(stats), _stream())
 
