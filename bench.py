@@ -16,7 +16,16 @@ Also reported on the same JSON line:
                   events on the launch stream over the timed region, vs the
                   gfx950 dense MFMA peak of the dtype;
   cpu_baseline -- the oracle (PyTorch CPU restatement of the reference step)
-                  on the host cores, bounded sample, rank 0 at N=1 only.
+                  on the host cores, bounded sample (1 warm-up + 3 timed steps), rank 0 at
+                  N=1 only;
+  parity       -- after the timed region, untimed: a fresh model of the same configuration
+                  is trained for --dice-steps seeded steps on distinct synthetic batches
+                  (so it segments the cells instead of sitting in a degenerate state), then
+                  on held-out tiles its GPU logits (the bench dtype and fp32) are compared
+                  with the fp64 CPU oracle on the same weights (logits_rel_err_vs_cpu), and
+                  its GPU masks with the fp32 CPU oracle's masks (dice_vs_cpu_ref).
+
+    python bench.py --dtype fp32 --size 512 --batch 8     # BASELINE configs[1] (fp32 MFMA path)
 """
 from __future__ import annotations
 
@@ -55,15 +64,18 @@ def parse():
     ap.add_argument("--base", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-size", type=int, default=1024, help="CPU baseline sample: one B=1 step at this size")
+    ap.add_argument("--cpu-size", type=int, default=512,
+                    help="CPU baseline sample: 1 warm-up + 3 timed B=1 steps at this size")
     ap.add_argument("--dice-size", type=int, default=1024, help="Dice-vs-CPU-reference image side (0 = skip)")
+    ap.add_argument("--dice-steps", type=int, default=80, help="training steps of the parity model")
     ap.add_argument("--dual", action="store_true",
                     help="dual-branch model + deep supervision (BASELINE configs[4]: --dual --base 96 --size 2048)")
     return ap.parse_args()
 
 
 def cpu_baseline(args):
-    """Oracle train step on the host CPU: one image, B=1 (bounded ~10-30 s)."""
+    """Oracle train step on the host CPU (BASELINE.md 'CPU-baseline plan'): B=1 at --cpu-size,
+    1 warm-up step + 3 timed steps on distinct seeded tiles (bounded ~10-30 s)."""
     from oracle import eunet_ref as R
     from eunet import synth
     # the box exports OMP_NUM_THREADS = this job's CPU share; os.cpu_count() is the whole host
@@ -71,12 +83,14 @@ def cpu_baseline(args):
     torch.set_num_threads(threads)
     S = R.formula_weights(args.base, 1, 2, dtype=torch.float32)
     tr = R.OracleTrainer(S, total_epochs=50)
-    xw, mw = synth.batch(1, 64, 64, start_index=0)
+    xw, mw = synth.batch(1, args.cpu_size, args.cpu_size, start_index=0)
     tr.step(xw, mw)  # warm-up (allocator / oneDNN init), not timed
-    x, m = synth.batch(1, args.cpu_size, args.cpu_size, start_index=0)
+    steps = 3
+    batches = [synth.batch(1, args.cpu_size, args.cpu_size, start_index=1 + i) for i in range(steps)]
     t0 = time.perf_counter()
-    tr.step(x, m)
-    dt = time.perf_counter() - t0
+    for x, m in batches:
+        tr.step(x, m)
+    dt = (time.perf_counter() - t0) / steps
     scale = (args.cpu_size / args.size) ** 2  # images of the benchmark size per sample
     model = "?"
     try:
@@ -85,47 +99,108 @@ def cpu_baseline(args):
     except OSError:
         pass
     return {"value": round(scale / dt, 5), "unit": "img/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"1 oracle train step (PyTorch CPU fp32 restatement of Trainer.train_epoch), B=1, "
-                      f"{args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2; {dt:.2f} s on "
-                      f"{torch.get_num_threads()} threads of {os.cpu_count()} ({model})"}
+            "sample": f"oracle train steps (PyTorch CPU fp32 restatement of Trainer.train_epoch, fixture-"
+                      f"pinned), B=1, {args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2: 1 warm-up + "
+                      f"3 timed, {dt:.2f} s/step on {torch.get_num_threads()} threads of {os.cpu_count()} "
+                      f"({model}); value scaled to {args.size}x{args.size} images by pixel count"}
+
+
+def train_parity_model(args, dev):
+    """A model of the bench configuration trained for args.dice_steps seeded steps (LR at the
+    end of the reference warmup, 4e-3) on distinct synthetic 256^2 batches of 4: the parity legs
+    then compare a network that actually segments the cells (untimed)."""
+    from eunet import synth
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    torch.manual_seed(1)
+    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=args.base, dtype=args.dtype).to(dev)
+    tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
+    for e in range(tr.warmup_epochs + 1):
+        tr.epoch_lr_step(e)
+    for s in range(args.dice_steps):
+        x, m = synth.batch(4, 256, 256, start_index=10000 + 4 * s, num_classes=2, in_channels=1, device=dev)
+        tr.step(x, m, sync_loss=False)
+    torch.cuda.synchronize()
+    return model
+
+
+def _cpu_state(model):
+    return {k: (v.detach().double().cpu() if v.is_floating_point() else v.cpu()) for k, v in model.state_dict().items()}
+
+
+def logits_rel_err_vs_cpu(model, args, dev):
+    """logits rel-err vs the CPU path.  Held-out 256^2 tile, eval mode, the trained
+    parity model's weights: GPU forward_lowres (bench dtype and fp32) vs the fp64 oracle forward
+    + the reference's bilinear 2H->H resize.  Per pixel |a-b| / max(|b|, 1e-3 max|b|) and the
+    max-normalised max|a-b| / max|b|."""
+    from eunet import synth
+    from oracle import eunet_ref as R
+    x, _ = synth.batch(1, 256, 256, start_index=200000, num_classes=2, in_channels=1)
+    S = _cpu_state(model)
+    with torch.no_grad():
+        ref = torch.nn.functional.interpolate(R.forward(S, x.double(), training=False), size=(256, 256),
+                                              mode="bilinear", align_corners=False)
+    out = {}
+    dtype0 = args.dtype
+    model.eval()
+    for dt in dict.fromkeys((dtype0, "fp32")):
+        model.set_dtype(dt)
+        with torch.no_grad():
+            lg = model.forward_lowres(x.to(dev)).double().cpu()
+        d = (lg - ref).abs()
+        out[dt] = {"per_pixel": float((d / ref.abs().clamp_min(1e-3 * float(ref.abs().max()))).max()),
+                   "max_normalised": float(d.max() / ref.abs().max())}
+    model.set_dtype(dtype0)
+    model.train()
+    out["sample"] = "held-out 256x256 tile, eval mode, trained parity model; vs fp64 CPU oracle (gate: fp32 <= 1e-3)"
+    return out
 
 
 def dice_vs_cpu_ref(model, args, dev):
-    """The metric's "Dice vs CPU ref": the trained model (its compute dtype) predicts a held-out
-    synthetic tile on the GPU (eval mode, Evaluator._run_model_single + the reference's
-    probability->mask rules, all HIP); the oracle runs the same weights in fp32 on the CPU
-    (reference path: full 2H forward, bilinear resize, softmax, mask rules).  Reported:
-    calculate_semantic_metrics(gpu_mask, cpu_mask) (GPU-counted), pixel agreement, max |dprob|."""
+    """The metric's "Dice vs CPU ref": the trained parity model predicts a held-out synthetic tile
+    on the GPU (eval mode, Evaluator._run_model_single + the reference's probability->mask rules,
+    all HIP), in the bench dtype and in fp32; the oracle runs the same weights in fp32 on the CPU
+    (reference path: full 2H forward, bilinear resize, softmax, mask rules).  Reported per GPU
+    dtype: calculate_semantic_metrics(gpu_mask, cpu_mask) (GPU-counted), pixel agreement,
+    max |dprob|, live-class soft Dice; and how well each predicts the synthetic ground truth."""
     from eunet import metrics, ops, synth
     from eunet.evaluator import Evaluator
     from oracle import evalpath_ref as E
     n = args.dice_size
     x, gt = synth.batch(1, n, n, start_index=100000, num_classes=2, in_channels=1)
-    ev = Evaluator(model, dev, "enhanced_unet")
-    model.eval()
-    with torch.no_grad():
-        probs = ev._run_model_single(x[0].to(dev))
-        gpu_mask = ops.probs_to_mask(probs)
-    model.train()
-    S = {k: (v.detach().float().cpu() if v.is_floating_point() else v.cpu()) for k, v in model.state_dict().items()}
+    S = {k: (v.float() if v.is_floating_point() else v) for k, v in _cpu_state(model).items()}
     t0 = time.perf_counter()
     with torch.no_grad():
         ref_probs = E.run_model_single(S, x[0])
     cpu_mask = E.convert_probs_to_mask(ref_probs.numpy())
-    dt = time.perf_counter() - t0
-    m = metrics.calculate_semantic_metrics(gpu_mask, cpu_mask)
-    m_gt = metrics.calculate_semantic_metrics(gpu_mask, gt[0])
-    agree = float((gpu_mask.cpu().numpy() == cpu_mask).mean())
-    pg, pc = probs[1].double().cpu(), ref_probs[1].double()  # live-class probabilities
-    soft = float(2 * (pg * pc).sum() / ((pg * pg).sum() + (pc * pc).sum()))
-    return {"sem_mean_dice": round(m["sem_mean_dice"], 6), "sem_live_dice": round(m["sem_live_dice"], 6),
-            "sem_background_dice": round(m["sem_background_dice"], 6), "pixel_agreement": round(agree, 7),
-            "max_abs_prob_diff": round(float((probs.cpu() - ref_probs).abs().max()), 6),
-            "live_soft_dice": round(soft, 7),
-            "live_pixels_gpu": int((gpu_mask == 1).sum()), "live_pixels_cpu": int((cpu_mask == 1).sum()),
-            "gpu_vs_synthetic_gt_live_dice": round(m_gt["sem_live_dice"], 6),
-            "sample": f"1 held-out {n}x{n} synthetic tile after the timed steps; GPU {args.dtype} vs CPU fp32 "
-                      f"oracle ({dt:.1f} s)"}
+    dt_cpu = time.perf_counter() - t0
+    ev = Evaluator(model, dev, "enhanced_unet")
+    out = {}
+    dtype0 = args.dtype
+    model.eval()
+    for dt in dict.fromkeys((dtype0, "fp32")):
+        model.set_dtype(dt)
+        with torch.no_grad():
+            probs = ev._run_model_single(x[0].to(dev))
+            gpu_mask = ops.probs_to_mask(probs)
+        m = metrics.calculate_semantic_metrics(gpu_mask, cpu_mask)
+        m_gt = metrics.calculate_semantic_metrics(gpu_mask, gt[0])
+        pg, pc = probs[1].double().cpu(), ref_probs[1].double()  # live-class probabilities
+        out[dt] = {"sem_mean_dice": round(m["sem_mean_dice"], 6), "sem_live_dice": round(m["sem_live_dice"], 6),
+                   "sem_background_dice": round(m["sem_background_dice"], 6),
+                   "pixel_agreement": round(float((gpu_mask.cpu().numpy() == cpu_mask).mean()), 7),
+                   "max_abs_prob_diff": round(float((probs.cpu() - ref_probs).abs().max()), 6),
+                   "live_soft_dice": round(float(2 * (pg * pc).sum() / ((pg * pg).sum() + (pc * pc).sum())), 7),
+                   "live_pixels_gpu": int((gpu_mask == 1).sum()),
+                   "gpu_vs_synthetic_gt_live_dice": round(m_gt["sem_live_dice"], 6)}
+    model.set_dtype(dtype0)
+    model.train()
+    m_ref = metrics.calculate_semantic_metrics(cpu_mask, gt[0])
+    out.update({"live_pixels_cpu": int((cpu_mask == 1).sum()),
+                "cpu_vs_synthetic_gt_live_dice": round(m_ref["sem_live_dice"], 6),
+                "sample": f"1 held-out {n}x{n} synthetic tile; model trained {args.dice_steps} steps (untimed); "
+                          f"GPU vs CPU fp32 oracle ({dt_cpu:.1f} s)"})
+    return out
 
 
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
@@ -164,6 +239,16 @@ def pmc_mfma(kernel):
         return None
     return {"mfma_busy_frac": round(k["mfma_busy_frac"], 4), "clock_ghz": round(k["clock_ghz"], 3),
             "source": f"profiles/{os.path.basename(MFMA_SUMMARY)}"}
+
+
+def _config_tag(args):
+    if args.dual:
+        return "(BASELINE configs[4])"
+    if (args.base, args.size, args.batch, args.dtype) == (64, 512, 8, "fp32"):
+        return "(BASELINE configs[1])"
+    if (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16"):
+        return "(BASELINE configs[2]; configs[3] at N=8)"
+    return "(custom)"
 
 
 def main():
@@ -247,7 +332,11 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
-    dice = dice_vs_cpu_ref(model, args, dev) if args.dice_size > 0 and not args.dual else None
+    dice = logits_err = None
+    if args.dice_size > 0 and not args.dual:
+        pmodel = train_parity_model(args, dev)
+        logits_err = logits_rel_err_vs_cpu(pmodel, args, dev)
+        dice = dice_vs_cpu_ref(pmodel, args, dev)
     from oracle.eunet_ref import flops_per_pixel
     from oracle.dual_ref import dual_flops_per_pixel
     fpp = dual_flops_per_pixel(args.base, 1, 2) if args.dual else flops_per_pixel(args.base, 1, 2)
@@ -267,12 +356,12 @@ def main():
         "data": "synthetic bright-field tiles (eunet.synth, seeded), random-init weights",
         "config": {"workload": (f"dual-branch + deep supervision, " if args.dual else "") +
                                f"base_ch={args.base}, 1x{args.size}x{args.size} 1-ch->2-cls, batch "
-                               f"{args.batch}/GPU, {args.dtype} " +
-                               ("(BASELINE configs[4])" if args.dual else "(BASELINE configs[2]; configs[3] at N=8)"),
+                               f"{args.batch}/GPU, {args.dtype} " + _config_tag(args),
                    "global_batch": world * args.batch, "image_size": args.size, "parallelism": f"dp{world}"},
         "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
         "roofline": roof,
         "cpu_baseline": cpu,
+        "logits_rel_err_vs_cpu": logits_err,
         "dice_vs_cpu_ref": dice,
     }
     print(json.dumps(line), flush=True)

@@ -4,10 +4,10 @@
 // BasicUNet models.py:203-211) and their autograd (dgrad / wgrad).
 //
 // Forward (and dgrad, which is the same kernel on W'[ci][co][8-t]):
-//   GEMM  M = output pixels (8x32 tile per block), N = Cout (64 per block),
+//   GEMM  M = output pixels (16x32 tile per block), N = Cout (64 per block),
 //         K = 9 taps x Cin, consumed one Cin chunk (KC channels) at a time.
-//   The chunk's input halo tile [(8+2) x (32+2) px][KC] is staged once in LDS
-//   and re-read by all 9 taps (no im2col, 1.4x halo over-read instead of 9x),
+//   The chunk's input halo tile [(16+2) x (32+2) px][KC] is staged once in LDS
+//   and re-read by all 9 taps (no im2col, 1.2x halo over-read instead of 9x),
 //   together with the chunk's weights [64 co][9 taps][KC].
 //   bf16: v_mfma_f32_16x16x32_bf16 (fp32 accumulate), KC = 32.
 //   f32 : v_mfma_f32_16x16x4_f32 (exact fp32 fma chain), KC = 16.
@@ -21,15 +21,19 @@
 // Wgrad: dW[co][t][ci] = sum_p dY[p][co] * X~[p+d_t][ci], pixels are the GEMM K.
 //   Block = (pixel-tile split, 64 co, KC ci); dY tile and X halo staged in LDS;
 //   bf16 fragments (8 consecutive pixels) come from ds_read_b64_tr_b16.
-#include <stdlib.h>
-
+//
+// The library takes no configuration from the environment: the alternatives measured
+// against these kernels (double buffering, 8 waves, producer/consumer waves, LDS-DMA
+// staging, weight fragments from L2, tap pipelining, a persistent Cin=64 kernel, other
+// block orders) are recorded in DESIGN.md §4 and profiles/r01_*; their code lives in the
+// git history (round 1), not in this file.
 #include <algorithm>
 
 #include "common.h"
 
 namespace {
 
-constexpr int TH = 8, TW = 32;            // output tile (pixels)
+constexpr int TH = 8, TW = 32;            // wgrad output tile (pixels)
 constexpr int HW_ = TW + 2, HH_ = TH + 2;  // halo tile
 constexpr int HPX = HH_ * HW_;            // 340 halo pixels
 constexpr int HPXP = 352;                 // padded plane (multiple of 16)
@@ -38,7 +42,6 @@ constexpr int NTHR = 256;
 constexpr int A_UNITS = 4 * HPX;          // 16-B units in one halo chunk
 constexpr int A_ITERS = (A_UNITS + NTHR - 1) / NTHR;  // 6
 constexpr int B_UNITS = 4 * BN * 9;       // 2304
-constexpr int B_ITERS = B_UNITS / NTHR;   // 9
 constexpr int A_LDS_BYTES = 4 * HPXP * 16;  // 22528
 constexpr int B_LDS_BYTES = B_UNITS * 16;   // 36864
 
@@ -58,43 +61,13 @@ struct FwdArgs {
   const float* bmean; const float* bistd; const float* bgam; const float* bbet;
   float* bpart;
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
-  int order;         // block -> (tile, co-block) order: 0 XCD-grouped, 1 tile-fastest, 2 co-block-fastest
-  int phase;         // 1: odd blocks start late (see conv3x3_fwd_kernel)
-  int pro1;          // 1: the first K-chunk is staged in one round trip (EUNET_CONV_PRO1);
-                     // 2: also the later chunks' halo and weight halves load together
+  int pro1;          // 1 (always, set by the launcher): the first K-chunk is staged in one round trip.
+                     // Kept a runtime flag: with the halved-staging prologue still compiled in, the
+                     // register allocator fits the kernel in 256 VGPRs without spills (a compile-time
+                     // constant here produces SGPR / VGPR spills).
 };
 
-// block order of the conv kernels (EUNET_CONV_ORDER / EUNET_WGRAD_ORDER, read once per process)
-inline int env_order(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && v[0] >= '0' && v[0] <= '9') ? v[0] - '0' : dflt;
-}
-int conv_order() {
-  static const int o = env_order("EUNET_CONV_ORDER", 0);
-  return o;
-}
-int wgrad_order() {
-  static const int o = env_order("EUNET_WGRAD_ORDER", 0);
-  return o;
-}
-int conv_pro1() {
-  static const int o = env_order("EUNET_CONV_PRO1", 1);
-  return o;
-}
-int conv_phase() {
-  static const int o = env_order("EUNET_CONV_PHASE", 1);
-  return o;
-}
-int wgrad_pf() {
-  static const int o = env_order("EUNET_WGRAD_PF", 7);
-  return o;
-}
-int wgrad_phase() {
-  static const int o = env_order("EUNET_WGRAD_PHASE", 1);
-  return o;
-}
-
-// stage one halo unit (pixel hp, quarter q) of chunk kc into registers
+// stage one halo unit (pixel hp, quarter q) of chunk kc into registers (f32 wgrad)
 template <typename T>
 __device__ __forceinline__ uint4 load_halo_unit(const FwdArgs& a, int n, int y0, int x0, int id, int kc,
                                                 bool& ok) {
@@ -126,26 +99,25 @@ __device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int
   *(uint4*)(lds + (q * HPXP + hp) * 16) = v;
 }
 
-// Forward v3: 256 threads = 4 waves (one per SIMD), output tile 16 x 32 px x 64 co;
+// Forward: 256 threads = 4 waves (one per SIMD), output tile 16 x 32 px x 64 co;
 // wave w computes rows 4w..4w+3 (128 px = 8 m-tiles) x 64 co = 32 accumulators,
-// so each tap issues 8 A + 4 B 16-byte LDS reads for 32 MFMAs (LDS well below
-// its 256 B/clk).  LDS is double-buffered (2 x 75 KB): the next chunk's global
-// loads go to registers before the current chunk's MFMAs and are written (with
-// the BN+ReLU transform) into the other buffer after them -> one barrier per
-// K-chunk.  Halo units are loaded 8 pixels x 4 quarters per 32 lanes so the
-// LDS writes are conflict-free.  The epilogue stages the tile through LDS and
-// stores whole 16-byte vectors.
+// so each tap issues 8 A + 4 B 16-byte LDS reads for 32 MFMAs.  Two blocks per CU
+// (75 KB of LDS each, one stage): a block's staging overlaps the other block's
+// MFMAs.  The first K-chunk is staged in one global round trip (the accumulators
+// are not live yet), later chunks in halves to bound the staging registers.  Halo
+// units are loaded 8 pixels x 4 quarters per 32 lanes so the LDS writes are
+// conflict-free.  The epilogue stages the tile through LDS and stores whole
+// 16-byte vectors.
 constexpr int FTH = 16, FTW = 32;            // output tile
 constexpr int FHW = FTW + 2;                 // 34
 constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
-constexpr int FHPXP = 640;                   // plane stride (10 x 64 units: whole LDS-DMA wave-instructions)
-constexpr int FT = 256;                      // threads of the production (NW = 4) forward block
+constexpr int FHPXP = 640;                   // plane stride
+constexpr int FT = 256;                      // threads of the forward block
 constexpr int FA_UNITS = 4 * FHPX;           // 2448
-constexpr int FA_BYTES = 4 * FHPXP * 16;     // 39936
-constexpr int STAGE_BYTES = FA_BYTES + B_LDS_BYTES;  // 76800
+constexpr int FA_BYTES = 4 * FHPXP * 16;     // 40960
+constexpr int STAGE_BYTES = FA_BYTES + B_LDS_BYTES;  // 77824
 constexpr int OUT_LD = 68;                   // fp32 row stride of the output staging tile
-constexpr int FWD_LDS_DB = 2 * STAGE_BYTES;  // 153600: one block / CU, double-buffered
-constexpr int FWD_LDS = STAGE_BYTES;         // 76800: two blocks / CU
+constexpr int FWD_LDS = STAGE_BYTES;         // two blocks / CU
 
 // XCD-aware block order: hardware block b runs on XCD b % 8.  Logical block L =
 // (tile, co-block) with the co-block fastest; each XCD gets a contiguous range of L,
@@ -195,417 +167,126 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
   *(u32x4*)(lds + (q * FHPXP + hp) * 16) = v;
 }
 
-// MODE: 0 = production.  Diagnostic builds only (tools/conv_ablate.hip):
-//   1 = no global loads / LDS writes inside the K loop, 2 = no MFMAs (VALU keeps the
-//   LDS reads alive), 4 = LDS fragments read once before the loop (MFMA-only loop),
-//   8 = plain tile-fastest block order instead of xcd_map, 16 / 32 = odd blocks start
-//   ~2.5k / ~5k clocks late (phase offset between the two blocks of a CU).
-// NW = waves per block (4: 128 px x 64 co per wave; 8: 64 px x 64 co per wave).
-// DB: true = one block per CU, double-buffered LDS (next chunk prefetched into
-//   registers during the MFMAs, one barrier per chunk); false = two blocks per CU,
-//   one LDS stage each (a block's staging overlaps the other block's MFMAs).
-// SPEC (with DB, NW = 8): waves 0-3 only compute (128 px x 64 co each), waves 4-7 only
-//   stage the next chunk (global -> registers -> BN+ReLU -> LDS) into the other buffer.
-// BDMA (with DB): the weight tile is staged by LDS-DMA (global_load_lds_dwordx4, no VGPR round
-//   trip); the packed layout makes every 64-unit wave-instruction one contiguous 1 KiB run.
-// DMA (single-stage path): 1 = weights by LDS-DMA, 2 = also the input halo when it needs no
-//   BN+ReLU transform (out-of-image / padded-channel lanes read a global zero vector).
-// PIPE: the 9 taps of a chunk are software-pipelined -- the fragments of tap t+1 are read
-//   from LDS into a second register set while tap t's MFMAs run (one wave per SIMD with DB,
-//   so no other wave hides the ds_read latency; 512 registers per lane leave room for it).
-// GB (bf16, no operand transform): the weight fragments are read straight from global memory
-//   (L2-resident packed weights, prefetched three taps ahead in registers) and LDS holds only
-//   the input halo, double-buffered (2 x 39 KB, still two blocks per CU).  The next chunk's
-//   halo is staged by LDS-DMA during the current chunk's MFMAs, so a block never waits on a
-//   staging round trip inside the K loop and no staging VGPRs / LDS writes are issued.
-//   Opt-in (EUNET_CONV_GB=1), slower: conv fwd+dgrad 16.0 vs 11.3 ms/step.  The weight loads
-//   share vmcnt with the DMA, so the first fragment load issued after the DMA waits for the
-//   whole halo (4.3 ms of the loss: a diagnostic build without the DMA ran 11.8); B from L2
-//   instead of LDS costs another ~1.4 ms (fixed-address weights: 14.6).  profiles/r01_ab_conv_gb.txt
-__device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised)
-constexpr int FWD_LDS_GB = 2 * FA_BYTES;  // 79872
-
-template <typename T, int MODE = 0, bool DB = false, int NW = 4, bool SPEC = false, bool BDMA = false, int DMA = 0,
-          bool PIPE = false, bool GB = false>
-__global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArgs a) {
-  static_assert(!SPEC || (DB && NW == 8), "SPEC needs the double-buffered 8-wave block");
-  static_assert(!BDMA || (DB && !SPEC), "BDMA needs the double-buffered block");
-  static_assert(!GB || (sizeof(T) == 2 && !DB && NW == 4 && DMA == 0 && MODE == 0), "GB: bf16 single-stage block");
-  constexpr int NTH = 64 * NW;
-  constexpr int NCW = SPEC ? 4 : NW;          // computing waves
-  constexpr int NLT = SPEC ? 256 : NTH;       // staging threads
-  constexpr int RPW = FTH / NCW;              // output rows per computing wave
+template <typename T>
+__global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
+  constexpr int NW = 4;                       // waves
+  constexpr int RPW = FTH / NW;               // output rows per wave
   constexpr int MT = 2 * RPW;                 // 16-px m-tiles per wave
-  constexpr int A_IT = (FA_UNITS + NLT - 1) / NLT;
-  constexpr int B_IT = (B_UNITS + NLT - 1) / NLT;
-  constexpr bool B_TAIL = B_UNITS % NLT != 0;
-  constexpr int NPASS = DB ? 1 : 2;           // epilogue staging passes (LDS budget)
+  constexpr int A_IT = (FA_UNITS + FT - 1) / FT;
+  constexpr int B_IT = (B_UNITS + FT - 1) / FT;
+  constexpr bool B_TAIL = B_UNITS % FT != 0;
+  constexpr int NPASS = 2;                    // epilogue staging passes (LDS budget)
   constexpr int PROWS = FTH / NPASS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int tile, cob;
-  if ((MODE & 8) != 0 || a.order == 1) {  // tile-fastest: co-block-major
-    tile = blockIdx.x % a.ntiles;
-    cob = blockIdx.x / a.ntiles;
-  } else if (a.order == 2) {  // co-block-fastest identity order
-    cob = blockIdx.x % (a.cout_pad / BN);
-    tile = blockIdx.x / (a.cout_pad / BN);
-  } else {  // XCD-grouped
-    xcd_map(blockIdx.x, a.ntiles, a.cout_pad / BN, tile, cob);
-  }
+  xcd_map(blockIdx.x, a.ntiles, a.cout_pad / BN, tile, cob);
   const int tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
   const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
   const int co0 = cob * BN;
   const int q = lane >> 4, li = lane & 15;
-  const int lt = SPEC ? tid - 256 : tid;  // staging thread index
-  const bool computes = !SPEC || wv < NCW;
 
   f32x4 acc[MT][4];
-
   u32x4 ra[A_IT];
   bool rok[A_IT];
   u32x4 rb[B_IT];
   const u32x4* wp = (const u32x4*)a.wp;
+  char* const As = smem;
+  char* const Bs = smem + FA_BYTES;
 
-#define CONV_BUNIT(ID_, KC_) \
-  wp[((long long)((KC_) * 4 + (ID_) / (BN * 9)) * a.cout_pad + co0) * 9 + (ID_) % (BN * 9)]
-#define CONV_GLOAD_A(KC_, I0_, I1_)                                                           \
-  do {                                                                                        \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        ra[i] = fwd_load_unit<T>(a, n, y0, x0, lt + i * NLT, (KC_), rok[i]);                  \
-  } while (0)
-#define CONV_GLOAD_B(KC_, I0_, I1_)                                                           \
-  do {                                                                                        \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
-      const int id_ = lt + i * NLT;                                                           \
-      if (!B_TAIL || id_ < B_UNITS) rb[i] = CONV_BUNIT(id_, KC_);                             \
-    }                                                                                         \
-  } while (0)
-#define CONV_LWRITE_A(KC_, BUF_, I0_, I1_)                                                    \
-  do {                                                                                        \
-    char* As_ = smem + (BUF_) * STAGE_BYTES;                                                  \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i)                                     \
-        fwd_store_unit<T>(a, As_, n, lt + i * NLT, (KC_), ra[i], rok[i]);                     \
-  } while (0)
-#define CONV_LWRITE_B(BUF_, I0_, I1_)                                                         \
-  do {                                                                                        \
-    char* Bs_ = smem + (BUF_) * STAGE_BYTES + FA_BYTES;                                       \
-    _Pragma("unroll") for (int i = (I0_); i < (I1_); ++i) {                                   \
-      const int id_ = lt + i * NLT;                                                           \
-      if (!B_TAIL || id_ < B_UNITS) *(u32x4*)(Bs_ + id_ * 16) = rb[i];                        \
-    }                                                                                         \
-  } while (0)
-
-  auto dma_b = [&](int kc, int buf) {
-    char* Bs_ = smem + buf * STAGE_BYTES + FA_BYTES;
-// (wave-strided: not unrolled)
-    for (int j = wv; j < B_UNITS / 64; j += NW) {
-      const u32x4* src = &CONV_BUNIT(j * 64 + lane, kc);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(Bs_ + j * 64 * 16), 16, 0, 0);
+  auto gload_a = [&](int kc, int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) ra[i] = fwd_load_unit<T>(a, n, y0, x0, tid + i * FT, kc, rok[i]);
+  };
+  auto gload_b = [&](int kc, int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int id = tid + i * FT;
+      if (!B_TAIL || id < B_UNITS) rb[i] = wp[((long long)(kc * 4 + id / (BN * 9)) * a.cout_pad + co0) * 9 + id % (BN * 9)];
     }
   };
-  auto dma_a = [&](int kc, int buf) {  // halo tile by LDS-DMA: wave-instruction j = quarter j/10, 64 pixels
-    constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-    char* As_ = smem + buf * STAGE_BYTES;
-    for (int j = wv; j < 4 * (FHPXP / 64); j += NW) {
-      const int qq = j / (FHPXP / 64), hp0 = (j % (FHPXP / 64)) * 64, hp = hp0 + lane;
-      const int hy = hp / FHW, hx = hp - hy * FHW;
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      const int c = kc * KC + qq * E;
-      const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin;
-      const void* src = ok ? (const void*)((const T*)a.x + (((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c))
-                           : (const void*)&g_conv_zero;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(As_ + (qq * FHPXP + hp0) * 16), 16, 0,
-                                       0);
+  auto lwrite_a = [&](int kc, int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) fwd_store_unit<T>(a, As, n, tid + i * FT, kc, ra[i], rok[i]);
+  };
+  auto lwrite_b = [&](int i0, int i1) {
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int id = tid + i * FT;
+      if (!B_TAIL || id < B_UNITS) *(u32x4*)(Bs + id * 16) = rb[i];
     }
   };
   constexpr int AH = A_IT / 2, BH = B_IT / 2;
-  const bool conv_st2 = a.pro1 == 2;
-  auto stage = [&](int kc, int buf) {  // single-stage path: staged in halves to bound registers
-    if constexpr (DMA >= 1) dma_b(kc, buf);
-    if (DMA >= 2 && a.isc == nullptr) {
-      dma_a(kc, buf);
-    } else if (DMA == 0 && conv_st2) {  // halo and weight halves together: two round trips
-      CONV_GLOAD_A(kc, 0, AH);
-      CONV_GLOAD_B(kc, 0, BH);
-      CONV_LWRITE_A(kc, buf, 0, AH);
-      CONV_LWRITE_B(buf, 0, BH);
-      CONV_GLOAD_A(kc, AH, A_IT);
-      CONV_GLOAD_B(kc, BH, B_IT);
-      CONV_LWRITE_A(kc, buf, AH, A_IT);
-      CONV_LWRITE_B(buf, BH, B_IT);
-      return;
-    } else {
-      CONV_GLOAD_A(kc, 0, AH);
-      CONV_LWRITE_A(kc, buf, 0, AH);
-      CONV_GLOAD_A(kc, AH, A_IT);
-      CONV_LWRITE_A(kc, buf, AH, A_IT);
-    }
-    if constexpr (DMA == 0) {
-      CONV_GLOAD_B(kc, 0, BH);
-      CONV_LWRITE_B(buf, 0, BH);
-      CONV_GLOAD_B(kc, BH, B_IT);
-      CONV_LWRITE_B(buf, BH, B_IT);
-    }
-  };
-  auto ldfrag = [&](const char* As, const char* Bs, int t, uint4 (&fa)[MT], uint4 (&fb)[4]) {
-    const int ky = t / 3, kx = t - ky * 3;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
-      fa[mt] = *(const uint4*)(As + (q * FHPXP + hp) * 16);
-    }
-  };
-  auto mm = [&](const uint4 (&fa)[MT], const uint4 (&fb)[4]) {
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        if constexpr (sizeof(T) == 2) {
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[mt]),
-                                                                __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
-        } else {
-          const uint4 A_ = fa[mt], B_ = fb[nt];
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
-        }
-      }
-  };
-  auto chunk_pipe = [&](const char* As, const char* Bs) {
-    uint4 fa[2][MT], fb[2][4];
-    ldfrag(As, Bs, 0, fa[0], fb[0]);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) ldfrag(As, Bs, t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
-      mm(fa[t & 1], fb[t & 1]);
-    }
-  };
-  auto chunk = [&](const char* As, const char* Bs, const uint4 (&fa0)[MT], const uint4 (&fb0)[4]) {
-    if constexpr (PIPE) {
-      chunk_pipe(As, Bs);
-      return;
-    }
+  auto chunk = [&]() {
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int t = ky * 3 + kx;
-      uint4 fb[4];
+      for (int kx = 0; kx < 3; ++kx) {
+        const int t = ky * 3 + kx;
+        uint4 fb[4];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        fb[nt] = (MODE & 4) ? fb0[nt] : *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
+        for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
-        const uint4 fa = (MODE & 4) ? fa0[mt] : *(const uint4*)(As + (q * FHPXP + hp) * 16);
+        for (int mt = 0; mt < MT; ++mt) {
+          const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
+          const uint4 fa = *(const uint4*)(As + (q * FHPXP + hp) * 16);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          if constexpr ((MODE & 2) != 0) {
-            acc[mt][nt][0] += __uint_as_float((fa.x ^ fb[nt].x) & 0x3f000000u);
-          } else if constexpr (sizeof(T) == 2) {
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
-          } else {
-            const uint4 A_ = fa, B_ = fb[nt];
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(A_.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
+          for (int nt = 0; nt < 4; ++nt) {
+            if constexpr (sizeof(T) == 2) {
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
+            } else {
+              const uint4 B_ = fb[nt];
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.x), __uint_as_float(B_.x), acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.y), __uint_as_float(B_.y), acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.z), __uint_as_float(B_.z), acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(fa.w), __uint_as_float(B_.w), acc[mt][nt], 0, 0, 0);
+            }
           }
         }
       }
-    }
   };
 
-  if constexpr (GB) {
-    if (a.phase && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(40);
-    // buffer descriptors: 32-bit per-lane offsets, wave-uniform parts in soffset (host checks
-    // that the input fits 2^31 bytes and that cin is a whole number of chunks)
-    const int kstr = 4 * a.cout_pad * 9 * 16;  // bytes per K-chunk of packed weights
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.wp, (short)0, a.nkc * kstr, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.x, (short)0, (int)((long long)a.N * a.H * a.W * a.xct * 2), 0x00020000);
-    const unsigned wlane = (unsigned)((q * a.cout_pad + co0 + li) * 9 * 16);
-    auto ldb = [&](int kc, int t, uint4 (&fb)[4]) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        fb[nt] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rw, wlane, kc * kstr + (nt * 16 * 9 + t) * 16, 0));
-    };
-    constexpr int NDMA = 4 * (FHPXP / 64) / NW;  // 10 halo wave-instructions per wave
-    const int wvu = __builtin_amdgcn_readfirstlane(wv);
-    auto dma_halo = [&](int kc, int buf) {
-      constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-      char* As_ = smem + buf * FA_BYTES;
-      int ln = lane;
-      asm volatile("" : "+v"(ln));  // opaque: the per-lane offsets are recomputed per chunk, not held
-#pragma unroll
-      for (int jj = 0; jj < NDMA; ++jj) {
-        const int j = wvu + jj * NW;
-        const int qq = j / (FHPXP / 64), hp0 = (j % (FHPXP / 64)) * 64, hp = hp0 + ln;
-        const int hy = hp / FHW, hx = hp - hy * FHW;
-        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        const bool ok = (hp < FHPX) & (yy >= 0) & (yy < a.H) & (xx >= 0) & (xx < a.W);
-        // out-of-image / plane-padding lanes read past the descriptor's range: zero fill
-        const unsigned off = ok ? (unsigned)((((n * a.H + yy) * a.W + xx) * a.xct + a.xco + qq * E) * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(As_ + (qq * FHPXP + hp0) * 16),
-                                                 16, off, kc * KC * 2, 0, 0);
-      }
-    };
-    constexpr int PD = 3;  // weight-fragment prefetch distance (taps)
-    uint4 fb[PD][4];
-    dma_halo(0, 0);
-#pragma unroll
-    for (int t = 0; t < PD; ++t) ldb(0, t, fb[t]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int kc = 0; kc < a.nkc; ++kc) {
-      const char* As = smem + (kc & 1) * FA_BYTES;
-      // tap rows not unrolled (as in the staged path): bounds how far the scheduler hoists the
-      // fragment reads; with PD = 3 the prefetch slot of tap (ky, kx) is kx
-#pragma unroll 1
-      for (int ky = 0; ky < 3; ++ky) {
-        const unsigned abase = (unsigned)(uintptr_t)(As + (q * FHPXP + (RPW * wv + ky) * FHW + li) * 16);
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          // The fragment reads are inline asm: the compiler cannot prove they miss the LDS-DMA
-          // writes into the other buffer and would otherwise wait for every outstanding load
-          // (DMA and weight prefetch alike) before them.  lgkmcnt is waited on by hand.
-          u32x4 fa[MT];
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            asm volatile("ds_read_b128 %0, %1 offset:%2"
-                         : "=v"(fa[mt])
-                         : "v"(abase), "i"((((mt >> 1) * FHW + (mt & 1) * 16 + kx) * 16)));
-          static_assert(MT == 8, "GB: eight fragment registers tied to the wait");
-          // the wait names the fragments as operands, so no MFMA can be scheduled above it
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]), "+v"(fa[6]),
-                         "+v"(fa[7])::"memory");
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt)
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                  __builtin_bit_cast(bf16x8, fa[mt]), __builtin_bit_cast(bf16x8, fb[kx][nt]), acc[mt][nt], 0, 0, 0);
-          // refill this slot with tap (ky+1, kx), the next chunk's first row after ky = 2; the
-          // last chunk re-reads its own weights instead of branching, so the wait counts stay static
-          ldb(min(ky < 2 ? kc : kc + 1, a.nkc - 1), ((ky + 1) % 3) * 3 + kx, fb[kx]);
-          if (kx == 0 && ky == 0 && kc + 1 < a.nkc) dma_halo(kc + 1, (kc + 1) & 1);
-        }
-      }
-      // the DMA was issued before the 32 fragment loads of taps 1..8: vmcnt <= 12 covers it
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      __syncthreads();
-    }
-  } else {  // register / LDS-staged K loop (every other variant)
-  uint4 fa0[MT], fb0[4];
-  const bool conv_pro1 = a.pro1 != 0;
   // Phase offset: the two blocks sharing a CU start (and, with equal work, keep running) in
   // lock-step, staging at the same time and leaving the MFMA pipes idle together.  Odd blocks
   // start ~2.5k clocks late so one block's staging overlaps the other's MFMAs (ablation:
-  // +15-20 % on every layer shape).
-  if ((MODE & 48) != 0 || a.phase) {
-    if (blockIdx.x & 1) {
-#pragma unroll 1
-      for (int i = 0; i < ((MODE & 32) ? 2 : 1); ++i) __builtin_amdgcn_s_sleep(40);
-    }
-  }
-  if constexpr (SPEC) {
-    if (!computes) {
-      CONV_GLOAD_A(0, 0, A_IT);
-      CONV_GLOAD_B(0, 0, B_IT);
-      CONV_LWRITE_A(0, 0, 0, A_IT);
-      CONV_LWRITE_B(0, 0, B_IT);
-    }
-  } else if constexpr (DB) {
-    CONV_GLOAD_A(0, 0, A_IT);
-    if constexpr (BDMA) {
-      dma_b(0, 0);
-    } else {
-      CONV_GLOAD_B(0, 0, B_IT);
-    }
-    CONV_LWRITE_A(0, 0, 0, A_IT);
-    if constexpr (!BDMA) CONV_LWRITE_B(0, 0, B_IT);
-  } else if (conv_pro1) {  // first chunk in one round trip: the accumulators are not live yet
-    CONV_GLOAD_A(0, 0, A_IT);
-    if constexpr (DMA == 0) CONV_GLOAD_B(0, 0, B_IT);
-    else dma_b(0, 0);
-    CONV_LWRITE_A(0, 0, 0, A_IT);
-    if constexpr (DMA == 0) CONV_LWRITE_B(0, 0, B_IT);
+  // +15-20 % on every layer shape, profiles/r01_ab_phase.txt).
+  if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
+  auto stage_halves = [&](int kc) {
+    gload_a(kc, 0, AH);
+    lwrite_a(kc, 0, AH);
+    gload_a(kc, AH, A_IT);
+    lwrite_a(kc, AH, A_IT);
+    gload_b(kc, 0, BH);
+    lwrite_b(0, BH);
+    gload_b(kc, BH, B_IT);
+    lwrite_b(BH, B_IT);
+  };
+  if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
+    gload_a(0, 0, A_IT);
+    gload_b(0, 0, B_IT);
+    lwrite_a(0, 0, A_IT);
+    lwrite_b(0, B_IT);
   } else {
-    stage(0, 0);
+    stage_halves(0);
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if constexpr ((MODE & 4) != 0) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) fb0[nt] = *(const uint4*)(smem + FA_BYTES + (q * (BN * 9) + (nt * 16 + li) * 9) * 16);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-      fa0[mt] = *(const uint4*)(smem + (q * FHPXP + (RPW * wv + (mt >> 1)) * FHW + (mt & 1) * 16 + li) * 16);
-  }
   for (int kc = 0; kc < a.nkc; ++kc) {
-    if constexpr (SPEC) {
-      const int cur = kc & 1;
-      if (computes) {
-        chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
-      } else if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
-        CONV_GLOAD_A(kc + 1, 0, A_IT);
-        CONV_GLOAD_B(kc + 1, 0, B_IT);
-        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, A_IT);
-        CONV_LWRITE_B(cur ^ 1, 0, B_IT);
-      }
+    if (kc > 0) {
+      __syncthreads();  // every wave is done reading the stage
+      stage_halves(kc);
       __syncthreads();
-    } else if constexpr (DB) {
-      const int cur = kc & 1;
-      if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
-        if constexpr (BDMA) {
-          dma_b(kc + 1, cur ^ 1);
-        } else {
-          CONV_GLOAD_B(kc + 1, 0, B_IT);
-        }
-        CONV_GLOAD_A(kc + 1, 0, A_IT);
-      }
-      chunk(smem + cur * STAGE_BYTES, smem + cur * STAGE_BYTES + FA_BYTES, fa0, fb0);
-      if ((MODE & 1) == 0 && kc + 1 < a.nkc) {
-        CONV_LWRITE_A(kc + 1, cur ^ 1, 0, A_IT);
-        if constexpr (!BDMA) CONV_LWRITE_B(cur ^ 1, 0, B_IT);
-      }
-      __syncthreads();
-    } else {
-      if (kc > 0) {
-        if ((MODE & 1) == 0) {
-          __syncthreads();  // every wave is done reading the stage
-          stage(kc, 0);
-        }
-        __syncthreads();
-      }
-      chunk(smem, smem + FA_BYTES, fa0, fb0);
     }
+    chunk();
   }
-  }  // !GB
-#undef CONV_GLOAD_A
-#undef CONV_GLOAD_B
-#undef CONV_LWRITE_A
-#undef CONV_LWRITE_B
-#undef CONV_BUNIT
 
   // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
+  constexpr int NCW = NW, NTH = FT;
   const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -621,7 +302,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
   float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NCW][64] x 2
   float* bprm = red + 2 * NCW * 64;                             // [4][64] BN-backward constants
-  static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= (DB ? FWD_LDS_DB : FWD_LDS), "epilogue LDS");
+  static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= FWD_LDS, "epilogue LDS");
   __syncthreads();  // all waves are done with the K loop's LDS
   if (a.stats != nullptr) {
     float s[4];
@@ -637,7 +318,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
         }
       s[nt] = xor32_sum(xor16_sum(v));
     }
-    if (q == 0 && computes)
+    if (q == 0)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) red[wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
@@ -663,7 +344,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
         }
       s[nt] = xor32_sum(xor16_sum(v));
     }
-    if (q == 0 && computes)
+    if (q == 0)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) red[NCW * 64 + wv * 64 + nt * 16 + li] = s[nt];
     __syncthreads();
@@ -697,7 +378,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   }
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
-    if (computes && RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
+    if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -757,6 +438,7 @@ __global__ __launch_bounds__(64 * NW, DB ? 1 : 2) void conv3x3_fwd_kernel(FwdArg
   }
 }
 
+
 // ---------------------------------------------------------------------------
 // weight packing: torch [Cout][Cin][3][3] fp32 -> [Cin_p/KC][4][Cout_p][9][E]
 // transpose_flip: pack W'[o=ci][i=co][t] = W[co][ci][8-t] (dgrad operand)
@@ -795,12 +477,10 @@ struct WgArgs {
   const void* dy; int dct, dco, cout;
   float* dw; float* db;
   int tx, ty, ntiles, per_split, nsplit;
-  int order;  // 0 XCD-grouped (wg_map), 1 identity
-  int phase;  // 1: odd blocks start late (see conv3x3_fwd_kernel)
 };
 
 template <typename T>
-__global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
+__global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {  // f32 path
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   constexpr int DY_UNITS_PX = 64 / E;                 // 16-B units per pixel row of dY tile
   constexpr int DY_UNITS = TH * TW * DY_UNITS_PX;     // 2048 (bf16) / 4096 (f32)
@@ -920,6 +600,8 @@ __global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {
   }
 }
 
+__device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised): LDS-DMA source of padding
+
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
 // w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
 // 32-pixel k-step costs 8 + 18 transposed fragment reads for 36 MFMAs.
@@ -949,29 +631,17 @@ __device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, in
 // (36 accumulators).  Two blocks per CU: a tile's X halo / dY loads are all
 // issued before the barrier that ends the previous tile's MFMAs, then written
 // to LDS (BN+ReLU applied to X there); the other block computes meanwhile.
-// MODE (diagnostic builds only, tools/conv_ablate.hip): 1 = stage only the first tile,
-// 2 = no MFMAs (VALU keeps the LDS reads alive).
-// PF (tile staging; EUNET_WGRAD_PF, A/B in profiles/r01_ab_wgrad_pf.txt):
-//   7 (default) X halo and dY both by LDS-DMA (global_load_lds, no staging VGPRs), then
-//     BN+ReLU applied to the halo in place; one global round trip per tile
-//   4 dY by LDS-DMA, X halo through registers in two halves
-//   0 X halo and dY through registers (three round trips)
-// Holding the next tile in registers across the k-loop (tried) spills: the 36 accumulators
-// take 144 of the 256 VGPRs two blocks per CU leave each wave.
-template <int MODE = 0, int PF = 7>
+// Tile staging: X halo and dY both by LDS-DMA (global_load_lds, no staging VGPRs), then
+// BN+ReLU applied to the halo in place; one global round trip per tile (register-staged
+// variants measured slower: profiles/r01_ab_wgrad_pf.txt).  Holding the next tile in
+// registers across the k-loop (tried) spills: the 36 accumulators take 144 of the 256
+// VGPRs two blocks per CU leave each wave.
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* lsc = (float*)(smem + WSTAGE);  // PF 7: [scale | shift][KCW] of the current tile
+  float* lsc = (float*)(smem + WSTAGE);  // [scale | shift][KCW] of the current tile
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int split, cob, kc;
-  if (a.order == 1) {
-    const int ncib = cdiv(a.cin, KCW), ncob = cdiv(a.cout, 64);
-    kc = blockIdx.x % ncib;
-    cob = (blockIdx.x / ncib) % ncob;
-    split = blockIdx.x / (ncib * ncob);
-  } else {
-    wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
-  }
+  wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
   const int co0 = cob * 64;
   const int t_begin = split * a.per_split;
   const int t_end = min(a.ntiles, t_begin + a.per_split);
@@ -986,64 +656,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   float dbv[8];  // bias gradient: thread owns channels co0 + 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i
 #pragma unroll
   for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
-  u32x4 rx[WX_ITERS], rd[WD_ITERS];
-  if (a.phase && (blockIdx.x & 1)) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
+  if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
-  auto gload_x = [&](int tile, int i0, int i1) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-#pragma unroll
-    for (int i = i0; i < i1; ++i) {
-      const int id = tid + i * NTHR;
-      const int hp = (id >> 6) * 8 + (id & 7), oc = (id >> 3) & 7;
-      const int hy = hp / HW_, hx = hp - hy * HW_;
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      const int c = kc * KCW + oc * 8;
-      rx[i] = (u32x4){0u, 0u, 0u, 0u};
-      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
-        rx[i] = *(const u32x4*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
-    }
-  };
-  auto gload_d = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-#pragma unroll
-    for (int i = 0; i < WD_ITERS; ++i) {
-      const int id = tid + i * NTHR;
-      const int px = id >> 3, u = id & 7;
-      const int r = px / TW, c = px - r * TW;
-      const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
-      rd[i] = (u32x4){0u, 0u, 0u, 0u};
-      if (yy < a.H && xx < a.W && co < a.cout)
-        rd[i] = *(const u32x4*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
-    }
-  };
-  auto lwrite_x = [&](int tile, int i0, int i1) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-    char* Xs = smem;
-#pragma unroll
-    for (int i = i0; i < i1; ++i) {
-      const int id = tid + i * NTHR;
-      const int hp = (id >> 6) * 8 + (id & 7), oc = (id >> 3) & 7;
-      if (hp >= HPX) continue;
-      u32x4 v = rx[i];
-      if (a.isc != nullptr) {
-        const int hy = hp / HW_, hx = hp - hy * HW_;
-        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        const int c = kc * KCW + oc * 8;
-        if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {  // padding stays 0
-          float f[8];
-          const int cs = c + n * a.iss;
-          Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[cs + j], a.ish[cs + j]), 0.f);
-          v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
-        }
-      }
-      *(u32x4*)(Xs + (oc * HPXP + hp) * 16) = v;
-    }
-  };
   auto dma_d = [&](int tile) {  // dY tile straight into LDS: wave-instruction j = units 64j..64j+63
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
@@ -1095,15 +709,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       }
     }
   };
-  auto lwrite_d = [&]() {
-    char* Ds = smem + WX_LDS;
-#pragma unroll
-    for (int i = 0; i < WD_ITERS; ++i) *(u32x4*)(Ds + (tid + i * NTHR) * 16) = rd[i];
-  };
-
   for (int tile = t_begin; tile < t_end; ++tile) {
-    constexpr int XH = WX_ITERS / 2;
-    if (PF == 7 && ((MODE & 1) == 0 || tile == t_begin)) {  // X halo and dY both by LDS-DMA
+    {  // X halo and dY both by LDS-DMA
       // the block's 64 input channels' BN scale / shift for this tile's sample: one load per thread
       // (tid < 128) instead of 16 per halo slot in the transform pass
       float rsc = 0.f;
@@ -1120,25 +727,6 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         bnrelu_x(tile);
         __syncthreads();
       }
-    }
-    if (PF == 4 && ((MODE & 1) == 0 || tile == t_begin)) {  // dY by LDS-DMA
-      gload_x(tile, 0, XH);
-      __syncthreads();  // previous tile's LDS reads are done
-      dma_d(tile);
-      lwrite_x(tile, 0, XH);
-      gload_x(tile, XH, WX_ITERS);
-      lwrite_x(tile, XH, WX_ITERS);
-      __syncthreads();  // (its fence also waits for the DMA)
-    }
-    if (PF == 0 && ((MODE & 1) == 0 || tile == t_begin)) {
-      gload_x(tile, 0, XH);
-      __syncthreads();  // previous tile's LDS reads are done
-      lwrite_x(tile, 0, XH);
-      gload_x(tile, XH, WX_ITERS);
-      lwrite_x(tile, XH, WX_ITERS);
-      gload_d(tile);
-      lwrite_d();
-      __syncthreads();
     }
     const char* Xs = smem;
     const char* Ds = Xs + WX_LDS;
@@ -1177,10 +765,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         const bf16x8 bfr = cat_bf16x4(lo, hi);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) {
-          if constexpr ((MODE & 2) != 0)
-            acc[t][ct][0] += __uint_as_float((__builtin_bit_cast(u32x4, af[ct]).x ^ __builtin_bit_cast(u32x4, bfr).x) & 0x3f000000u);
-          else
-            acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
         }
       }
     }
@@ -1251,370 +836,14 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
-// ---------------------------------------------------------------------------
-// Persistent forward / dgrad for Cin == 64 (bf16): the 64-channel layers at full
-// resolution (enc1.3, dec2.3, enc2.0, and the dgrad of dec2.0) have only two
-// K-chunks per 16x32 tile, so in conv3x3_fwd_kernel the per-block staging round
-// trips and the epilogue are not amortised (MFMA-only diagnostic: 37 % of peak
-// on these shapes vs 74 % on 512-channel layers).  Here one block per CU (8 waves,
-// 2 per SIMD) keeps all 64 x 9 x 64 weights of its co-block resident in LDS for its
-// lifetime and walks tiles; the next tile's whole halo (both chunks) is loaded into
-// registers while the current tile's MFMAs run, so a tile costs one LDS write of
-// the halo, the MFMAs and the epilogue, with no exposed global latency.
-// Wave w computes rows 2w, 2w+1 (4 m-tiles) x 64 co (16 accumulators).  The
-// epilogue (bias, Dropout2d scale, BN partials, fused BN-backward reduction) is
-// the one of conv3x3_fwd_kernel; the output tile is staged as bf16 in the halo
-// region, so the per-tile outputs (stats, bpart) keep the 16x32 tile indexing.
-constexpr int K64_T = 512;                                   // threads
-#ifndef K64_UNROLL
-#define K64_UNROLL 3
-#endif
-#ifndef K64_PRE
-#define K64_PRE 0
-#endif
-#ifndef K64_SUNROLL
-#define K64_SUNROLL 2
-#endif
-constexpr int K64_CU = ((FHPX + 7) / 8) * 32;                // 2464 halo unit ids per chunk (whole 8-px groups)
-constexpr int K64_IT = (2 * K64_CU + K64_T - 1) / K64_T;     // 10
-constexpr int K64_B = 2 * B_LDS_BYTES;                       // 73728: both chunks' weights
-constexpr int K64_A = 2 * FA_BYTES;                          // 79872: both chunks' halo
-constexpr int K64_OLD = 72;                                  // bf16 row stride of the staged output tile
-constexpr int K64_LDS = K64_B + K64_A + (2 * 8 + 4 + 7) * 64 * 4;
-static_assert(K64_LDS <= 160 * 1024, "k64 LDS");
-static_assert(FTH * FTW * K64_OLD * 2 <= K64_A && K64_T * 16 * 4 <= K64_A, "k64 staging");
-
-// sum over the 16 lanes of a DPP row (every lane gets it): quad butterflies, then row rotates
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror 4
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror 8
-  return v;
-}
-
-// ABL (diagnostic builds only, tools/conv_ablate.hip k64): 1 = halo staged once (no per-tile
-// global loads / LDS writes), 2 = no epilogue, 4 = no MFMAs, 8 = no output stores.
-template <int ABL = 0>
-__global__ __launch_bounds__(K64_T, 1) void conv3x3_k64_kernel(FwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Bs = smem;
-  char* As = smem + K64_B;
-  float* red = (float*)(As + K64_A);  // [2][8 waves][64]
-  float* bprm = red + 2 * 8 * 64;     // [4][64] BN-backward constants
-  float* lbias = bprm + 4 * 64;       // [64] bias of the co-block
-  float* lcst = lbias + 64;           // [2 buffers][3][64]: input scale, shift (per sample), output gscale
-  constexpr int E = 8, UPX = 8, NCW = 8, MT = 4;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int q = lane >> 4, li = lane & 15;
-  const int ncob = a.cout_pad / BN;
-  const int cob = blockIdx.x % ncob, co0 = cob * BN;
-  const int tstride = gridDim.x / ncob;
-  const int tpi = a.tx * a.ty;
-  const bool bnb = a.bpart != nullptr;
-  const u32x4* wp = (const u32x4*)a.wp;
-
-  for (int id = tid; id < 2 * B_UNITS; id += K64_T) {
-    const int kc = id / B_UNITS, u = id - kc * B_UNITS;
-    *(u32x4*)(Bs + id * 16) = wp[((long long)(kc * 4 + u / (BN * 9)) * a.cout_pad + co0) * 9 + u % (BN * 9)];
-  }
-  if (tid < BN) lbias[tid] = (a.bias != nullptr && co0 + tid < a.cout) ? a.bias[co0 + tid] : 0.f;
-  if (tid < BN) lbias[tid] = (a.bias != nullptr && co0 + tid < a.cout) ? a.bias[co0 + tid] : 0.f;
-  if (bnb && tid < BN) {
-    const bool ok = co0 + tid < a.cout;
-    bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
-    bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
-    bprm[2 * BN + tid] = ok ? a.bgam[co0 + tid] : 0.f;
-    bprm[3 * BN + tid] = ok ? a.bbet[co0 + tid] : 0.f;
-  }
-
-  u32x4 ra[K64_IT];
-  unsigned rok = 0;  // bit i: unit i is inside the image (BN+ReLU applies; padding stays 0)
-  float rcst = 0.f;  // tid < 192: this thread's per-sample constant of the prefetched tile
-  auto gload = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
-    if (tid < 3 * 64) {
-      const int j = tid >> 6, c = tid & 63;
-      if (j == 2)
-        rcst = (a.gsc != nullptr && co0 + c < a.cout) ? a.gsc[(long long)n * a.cout + co0 + c] : 1.f;
-      else if (a.isc != nullptr)
-        rcst = (j == 0 ? a.isc : a.ish)[c + n * a.iss];
-    }
-    rok = 0;
-#pragma unroll
-    for (int i = 0; i < K64_IT; ++i) {
-      const int id = tid + i * K64_T, kc = id >= K64_CU ? 1 : 0;
-      bool ok = false;
-      ra[i] = (u32x4){0u, 0u, 0u, 0u};
-      if (id < 2 * K64_CU) ra[i] = fwd_load_unit<bf16_t>(a, n, y0, x0, id - kc * K64_CU, kc, ok);
-      rok |= (unsigned)ok << i;
-    }
-  };
-  auto lwrite = [&](const float* cst) {  // cst: [3][64] constants of this tile (scale, shift from LDS)
-    const bool tr = a.isc != nullptr;
-#pragma unroll
-    for (int i = 0; i < K64_IT; ++i) {
-      const int id = tid + i * K64_T, kc = id >= K64_CU ? 1 : 0;
-      if (id >= 2 * K64_CU) continue;
-      int hp, qq;
-      fwd_unit(id - kc * K64_CU, hp, qq);
-      if (hp >= FHPX) continue;
-      u32x4 v = ra[i];
-      if (tr && ((rok >> i) & 1u)) {
-        const int c = kc * 32 + qq * 8;
-        float f[8];
-        Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], cst[c + j], cst[64 + c + j]), 0.f);
-        v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
-      }
-      *(u32x4*)(As + kc * FA_BYTES + (qq * FHPXP + hp) * 16) = v;
-    }
-  };
-
-  int tile = blockIdx.x / ncob, it = 0;
-  if (tile < a.ntiles) {
-    gload(tile);
-    if (tid < 3 * 64) lcst[tid] = rcst;
-  }
-  for (; tile < a.ntiles; tile += tstride, ++it) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
-    const float* cst = lcst + (it & 1) * 3 * 64;
-    __syncthreads();  // the previous tile's epilogue is done with the halo region; cst written
-    if ((ABL & 1) == 0 || tile == (int)blockIdx.x / ncob) lwrite(cst);
-    __syncthreads();
-    if ((ABL & 1) == 0 && tile + tstride < a.ntiles) gload(tile + tstride);  // in flight during the MFMAs
-
-    f32x4 acc[MT][4];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll K64_UNROLL
-    for (int kt = 0; kt < 18; ++kt) {  // (chunk, tap)
-      const int kc = kt >= 9 ? 1 : 0, t = kt - 9 * kc, ky = t / 3, kx = t - 3 * ky;
-      const char* A_ = As + kc * FA_BYTES;
-      const char* B_ = Bs + kc * B_LDS_BYTES;
-      {
-        uint4 fb[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(B_ + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int hp = (2 * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
-          const uint4 fa = *(const uint4*)(A_ + (q * FHPXP + hp) * 16);
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            if constexpr ((ABL & 4) != 0)
-              acc[mt][nt][0] += __uint_as_float((fa.x ^ fb[nt].x) & 0x3f000000u);
-            else
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[nt]),
-                                                                    __builtin_bit_cast(bf16x8, fa), acc[mt][nt], 0, 0, 0);
-          }
-        }
-      }
-    }
-
-    if constexpr ((ABL & 2) != 0) {  // keep the accumulators alive, skip the epilogue
-      float t = 0.f;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) t += acc[mt][nt][0] + acc[mt][nt][3];
-      if (t == 1234.5f) ((float*)a.stats)[tid] = t;
-      continue;
-    }
-    // ---- epilogue.  The MFMA operands are swapped (D^T = W^T X^T): lane (q, li) holds output
-    // channels nt*16 + 4q + i (i = 0..3) of pixel li of m-tile mt, so the bf16 tile is staged
-    // with one 8-byte LDS write per (mt, nt).  BN partials: each wave reduces its own 2 rows
-    // (sum, M2 about the wave mean) in registers; one thread per channel Chan-combines the 8
-    // waves -> a single barrier.
-    const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
-    const bool has_gsc = a.gsc != nullptr;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float bv = lbias[nt * 16 + 4 * q + i];
-        const float gv = has_gsc ? cst[128 + nt * 16 + 4 * q + i] : 1.f;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt][nt][i] = (acc[mt][nt][i] + bv) * gv;
-      }
-    const int nrow = max(0, min(2, vh - 2 * wv));
-    const int nw = nrow * vw;  // valid pixels of this wave
-    if (a.stats != nullptr) {
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const bool ok = (mt >> 1) < nrow && (mt & 1) * 16 + li < vw;
-            v += ok ? acc[mt][nt][i] : 0.f;
-          }
-          v = row16_sum(v);
-          const float mw = nw > 0 ? v / (float)nw : 0.f;
-          float m2 = 0.f;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const bool ok = (mt >> 1) < nrow && (mt & 1) * 16 + li < vw;
-            const float d = acc[mt][nt][i] - mw;
-            m2 += ok ? d * d : 0.f;
-          }
-          m2 = row16_sum(m2);
-          if (li == 0) {
-            red[wv * 64 + nt * 16 + 4 * q + i] = v;
-            red[NCW * 64 + wv * 64 + nt * 16 + 4 * q + i] = m2;
-          }
-        }
-    }
-    __syncthreads();  // every wave is done reading the halo; red is complete
-    if (a.stats != nullptr && tid < 64 && co0 + tid < a.cout) {
-      float sum = 0.f;
-#pragma unroll
-      for (int w = 0; w < NCW; ++w) sum += red[w * 64 + tid];
-      const float cnt = (float)(vh * vw), mean = sum / cnt;
-      float m2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NCW; ++w) {
-        const int nwv = max(0, min(2, vh - 2 * w)) * vw;
-        const float d = nwv > 0 ? red[w * 64 + tid] / (float)nwv - mean : 0.f;
-        m2 += red[NCW * 64 + w * 64 + tid] + (float)nwv * d * d;
-      }
-      a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
-      a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
-      if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
-    }
-    bf16_t* stg = (bf16_t*)As;  // [512 px][K64_OLD]
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int px = (2 * wv + (mt >> 1)) * FTW + (mt & 1) * 16 + li;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const uint32_t lo = (uint32_t)f2bf(acc[mt][nt][0]) | ((uint32_t)f2bf(acc[mt][nt][1]) << 16);
-        const uint32_t hi = (uint32_t)f2bf(acc[mt][nt][2]) | ((uint32_t)f2bf(acc[mt][nt][3]) << 16);
-        *(uint2*)(stg + px * K64_OLD + nt * 16 + 4 * q) = make_uint2(lo, hi);
-      }
-    }
-    __syncthreads();
-    bf16_t* yp = (bf16_t*)a.y;
-    const int ucol = tid % UPX;
-    float bs1[E], bs2[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) { bs1[e] = 0.f; bs2[e] = 0.f; }
-    constexpr int SJ = FTH * FTW * UPX / K64_T;  // 8 output units per thread
-    uint4 ryb[SJ];                               // y of the fused BN-backward reduction, loaded
-    if (bnb && K64_PRE) {                        // before the stores (no store in the wait queue)
-#pragma unroll
-      for (int j = 0; j < SJ; ++j) {
-        const int id = tid + j * K64_T;
-        const int px = id / UPX, u = id - px * UPX;
-        const int r = px / FTW, c = px % FTW;
-        const int co = co0 + u * E;
-        ryb[j] = make_uint4(0, 0, 0, 0);
-        if (r < vh && c < vw && co < a.cout)
-          ryb[j] = *(const uint4*)((const bf16_t*)a.by + ((long long)(n * a.H + y0 + r) * a.W + x0 + c) * a.byct +
-                                   a.byco + co);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < SJ; ++j) {
-      const int id = tid + j * K64_T;
-      const int px = id / UPX, u = id - px * UPX;
-      const int r = px / FTW, c = px % FTW;
-      const int co = co0 + u * E;
-      if (r < vh && c < vw && co < a.cout) {
-        const uint4 packed = *(const uint4*)(stg + px * K64_OLD + u * E);
-        const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
-        if constexpr ((ABL & 8) == 0) *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
-        if (bnb) {
-          float gr[E], yv[E];
-          Vec16<bf16_t>::unpack(packed, gr);
-          Vec16<bf16_t>::unpack(K64_PRE ? ryb[j] : *(const uint4*)((const bf16_t*)a.by + pix * a.byct + a.byco + co), yv);
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const int cc = ucol * E + e;
-            const float xh = (yv[e] - bprm[cc]) * bprm[BN + cc];
-            const float gp = fmaf(bprm[2 * BN + cc], xh, bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
-            bs1[e] += gp;
-            bs2[e] = fmaf(gp, xh, bs2[e]);
-          }
-        }
-      }
-    }
-    if (bnb) {  // fixed-order block reduction of the per-thread channel sums
-      __syncthreads();
-      float* r2 = (float*)As;  // [K64_T][2E]
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        r2[tid * 2 * E + e] = bs1[e];
-        r2[tid * 2 * E + E + e] = bs2[e];
-      }
-      __syncthreads();
-      if (tid < 2 * BN) {
-        const int which = tid / BN, cc = tid % BN, u = cc / E, e = cc % E;
-        float t = 0.f;
-        for (int k = u; k < K64_T; k += UPX) t += r2[k * 2 * E + which * E + e];
-        if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
-      }
-    }
-    if (tid < 3 * 64 && tile + tstride < a.ntiles) lcst[((it + 1) & 1) * 3 * 64 + tid] = rcst;
-  }
-}
-
-int conv_k64() {
-  static const int o = env_order("EUNET_CONV_K64", 0);
-  return o;
-}
-
-int conv_dma() {
-  static const int o = env_order("EUNET_CONV_DMA", 0);
-  return o;
-}
-
-int conv_gb() {  // EUNET_CONV_GB: weight fragments from global, halo double-buffered by LDS-DMA
-  static const int o = env_order("EUNET_CONV_GB", 0);
-  return o;
-}
-
-template <int DMA>
-void launch_fwd_dma(const FwdArgs& a, int dtype, dim3 grid, void* stream) {
-  if (dtype == EUNET_BF16) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, DMA>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, DMA><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
-  } else {
-    allow_lds(conv3x3_fwd_kernel<float, 0, false, 4, false, false, DMA>, FWD_LDS);
-    conv3x3_fwd_kernel<float, 0, false, 4, false, false, DMA><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
-  }
-}
-
 int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
-  if (dtype == EUNET_BF16 && a.cin == 64 && conv_k64()) {
-    const int ncob = a.cout_pad / BN;
-    const int per = std::max(1, std::min(a.ntiles, 256 / ncob));  // one resident block per CU
-    allow_lds(conv3x3_k64_kernel<0>, K64_LDS);
-    conv3x3_k64_kernel<0><<<dim3(per * ncob), K64_T, K64_LDS, (hipStream_t)stream>>>(a);
-    EUNET_LAUNCH_CHECK("conv3x3_fwd");
-    return EUNET_OK;
-  }
   dim3 grid(a.ntiles * (a.cout_pad / BN));
-  const bool gb_ok = dtype == EUNET_BF16 && a.isc == nullptr && a.cin % KCh<bf16_t>::v == 0 &&
-                     (long long)a.N * a.H * a.W * a.xct * 2 < (1LL << 31) &&
-                     (long long)a.nkc * 4 * a.cout_pad * 9 * 16 < (1LL << 31);
-  if (gb_ok && conv_gb()) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, 0, false, true>, FWD_LDS_GB);
-    conv3x3_fwd_kernel<bf16_t, 0, false, 4, false, false, 0, false, true>
-        <<<grid, FT, FWD_LDS_GB, (hipStream_t)stream>>>(a);
-    EUNET_LAUNCH_CHECK("conv3x3_fwd");
-    return EUNET_OK;
-  }
-  switch (conv_dma()) {
-    case 1: launch_fwd_dma<1>(a, dtype, grid, stream); break;
-    case 2: launch_fwd_dma<2>(a, dtype, grid, stream); break;
-    default: launch_fwd_dma<0>(a, dtype, grid, stream); break;
+  if (dtype == EUNET_BF16) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else {
+    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
+    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
   }
   EUNET_LAUNCH_CHECK("conv3x3_fwd");
   return EUNET_OK;
@@ -1670,9 +899,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
   a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
-  a.order = conv_order();
-  a.phase = conv_phase();
-  a.pro1 = conv_pro1();
+  a.pro1 = 1;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
   return launch_fwd(a, x->dtype, stream);
@@ -1700,9 +927,7 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
   a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
-  a.order = conv_order();
-  a.phase = conv_phase();
-  a.pro1 = conv_pro1();
+  a.pro1 = 1;
   return launch_fwd(a, dy->dtype, stream);
 }
 
@@ -1740,24 +965,11 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;
-  a.order = wgrad_order();
-  a.phase = wgrad_phase();
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));
-    switch (wgrad_pf()) {
-      case 4:
-        allow_lds(conv3x3_wgrad_bf16_kernel<0, 4>, WG_LDS);
-        conv3x3_wgrad_bf16_kernel<0, 4><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
-        break;
-      case 0:
-        allow_lds(conv3x3_wgrad_bf16_kernel<0, 0>, WG_LDS);
-        conv3x3_wgrad_bf16_kernel<0, 0><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
-        break;
-      default:
-        allow_lds(conv3x3_wgrad_bf16_kernel<0, 7>, WG_LDS);
-        conv3x3_wgrad_bf16_kernel<0, 7><<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
-    }
+    allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
+    conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
   } else {
     dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
     const size_t lds = A_LDS_BYTES + TH * TW * 64 * 4 + 4 * 64 * 4;

@@ -61,6 +61,32 @@ __global__ __launch_bounds__(NT) void rasterize_kernel(const int* pts, const int
   }
 }
 
+// one uint8 mask per polygon (dataset.py:184-186: cv2.fillPoly(mask, [points], 1)), same fill rule,
+// with the training flips (dataset.py:209-222: every instance mask flipped like the image) applied
+// as a mirrored read: out[i][y][x] = raster_i[flip_v ? h-1-y : y][flip_h ? w-1-x : x]
+__global__ __launch_bounds__(NT) void rasterize_instances_kernel(const int* pts, const int* poly_off, int npoly, int h,
+                                                                 int w, int flip_h, int flip_v, uint8_t* masks) {
+  const long long hw = (long long)h * w, total = hw * npoly;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int p = (int)(i / hw);
+    const long long r = i - (long long)p * hw;
+    const int yo = (int)(r / w), xo = (int)(r - (long long)yo * w);
+    const int y = flip_v ? h - 1 - yo : yo, x = flip_h ? w - 1 - xo : xo;
+    const float px = x + 0.5f, py = y + 0.5f;
+    const int b = poly_off[p], e = poly_off[p + 1];
+    bool in = false, edge = false;
+    for (int k = b, j = e - 1; k < e; j = k++) {
+      const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
+      edge |= on_segment(x, y, xj, yj, xi, yi);
+      if ((yi > py) != (yj > py)) {
+        const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
+        if (px < xc) in = !in;
+      }
+    }
+    masks[i] = (in || edge) ? 1 : 0;
+  }
+}
+
 // flip a [h][w][c] byte image / int64 mask: mode 1 = horizontal (cv2.flip(., 1)), 0 = vertical
 template <typename T>
 __global__ __launch_bounds__(NT) void flip_kernel(const T* src, T* dst, int h, int w, int c, int mode) {
@@ -137,6 +163,15 @@ int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* lab
                 "rasterize_polygons: bad args");
   rasterize_kernel<<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(pts, poly_off, labels, npoly, h, w, mask);
   EUNET_LAUNCH_CHECK("rasterize_polygons");
+  return EUNET_OK;
+}
+
+int eunet_rasterize_instances(const int* pts, const int* poly_off, int npoly, int h, int w, int flip_h,
+                              int flip_v, uint8_t* masks, void* stream) {
+  EUNET_REQUIRE(masks && h > 0 && w > 0 && npoly > 0 && pts && poly_off, "rasterize_instances: bad args");
+  rasterize_instances_kernel<<<grid1((long long)h * w * npoly), NT, 0, (hipStream_t)stream>>>(
+      pts, poly_off, npoly, h, w, flip_h, flip_v, masks);
+  EUNET_LAUNCH_CHECK("rasterize_instances");
   return EUNET_OK;
 }
 

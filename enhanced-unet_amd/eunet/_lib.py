@@ -22,6 +22,14 @@ class Act(ctypes.Structure):
                 ("ctot", c_int), ("coff", c_int), ("dtype", c_int)]
 
 
+class LossParams(ctypes.Structure):
+    """eunet_loss_params (include/eunet.h): the loss configuration of one combined-loss call."""
+    _fields_ = [("ce_weight", c_float * 3), ("alpha", c_float * 3), ("gamma", c_float), ("ignore_index", c_int),
+                ("dice_weight", c_float * 3), ("tversky_weight", c_float * 3), ("tversky_alpha", c_float),
+                ("w_focal", c_float), ("w_dice", c_float), ("w_tversky", c_float), ("class_div", c_float),
+                ("focal_norm", c_int)]
+
+
 _P = POINTER(Act)
 _f = c_void_p  # float* / void* device pointers are passed as integers
 
@@ -50,9 +58,11 @@ SIGNATURES = {
                        _f, _f, _f, _f, _f, _f, c_int, _f, c_void_p],
     "eunet_head_bwd": [_f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f, _f,
                        _f, _f, _f, _f, _f, _f, c_int, _f, c_void_p],
+    "eunet_loss_reference_params": [POINTER(LossParams)],
+    "eunet_loss_sums_len": [c_int, c_int, POINTER(c_int)],
     "eunet_loss_workspace_bytes": [c_int, c_int, c_int, c_int, POINTER(c_size_t)],
-    "eunet_loss_fwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, _f, c_void_p],
-    "eunet_loss_bwd": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, _f, c_void_p],
+    "eunet_loss_fwd": [_f, _f, c_int, c_int, c_int, c_int, POINTER(LossParams), _f, _f, _f, _f, c_void_p],
+    "eunet_loss_bwd": [_f, _f, c_int, c_int, c_int, c_int, POINTER(LossParams), _f, _f, _f, c_void_p],
     "eunet_bn_bwd_tiles": [_P, POINTER(c_int)],
     "eunet_bn_bwd_reduce": [_P, _P, _f, _f, _f, _f, _f, c_void_p],
     "eunet_colsum_ws_bytes": [c_int, c_int, POINTER(c_size_t)],
@@ -88,6 +98,7 @@ SIGNATURES = {
                         _f, _f, c_void_p],
     "eunet_dropout_affine": [_f, _f, _f, c_int, c_int, c_float, _f, _f, _f, c_void_p],
     "eunet_rasterize_polygons": [_f, _f, _f, c_int, c_int, c_int, _f, c_void_p],
+    "eunet_rasterize_instances": [_f, _f, c_int, c_int, c_int, c_int, c_int, _f, c_void_p],
     "eunet_flip_u8": [_f, _f, c_int, c_int, c_int, c_int, c_void_p],
     "eunet_flip_mask": [_f, _f, c_int, c_int, c_int, c_void_p],
     "eunet_augment_u8": [_f, c_int64, c_int, ctypes.c_double, ctypes.c_double, _f, _f, c_void_p],
@@ -146,5 +157,5 @@ def version() -> str:
     return load().eunet_version().decode()
 
 
-__all__ = ["Act", "load", "call", "EunetError", "EUNET_F32", "EUNET_BF16", "exported_symbols",
+__all__ = ["Act", "LossParams", "load", "call", "EunetError", "EUNET_F32", "EUNET_BF16", "exported_symbols",
            "c_int", "c_size_t", "c_float", "c_int64"]

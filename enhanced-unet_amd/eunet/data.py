@@ -6,7 +6,7 @@
 Same file split (sorted *.jpg, 70/15/15, dataset.py:37-51), the same resize-to-/32
 sizes (:141-157), LabelMe 'live'/'dead' polygons scaled and truncated to int32 as the
 reference does (:173-188), the semantic mask with later instances overwriting earlier
-ones (:197-201), and the training augmentations drawn from Python's `random` in the
+ones (:197-201), per-instance uint8 masks flipped with the image (:184-193, 209-222), and the training augmentations drawn from Python's `random` in the
 reference's order, so a seeded run takes the same decisions (:204-294).  Per pixel
 everything runs in HIP (datapath.hip): polygon rasterisation, flips, the numpy pixel
 ops (brightness, contrast, noise, gamma LUT -- bit-exact with the reference's numpy
@@ -85,11 +85,16 @@ class CellDataset:
         return len(self.files)
 
     def _augment(self, img, mask):
-        """dataset.py:204-294 in order; img HWC uint8 and mask int64 on the device."""
+        """dataset.py:204-294 in order; img HWC uint8 and mask int64 on the device.  Returns
+        (img, mask, (flip_h, flip_v)): the flips are applied to the instance masks as well
+        (dataset.py:212-213, 220-221), by rasterize_instances."""
+        flip_h = flip_v = False
         if random.random() > 0.5:
             img, mask = ops.flip_u8(img, 1), ops.flip_mask(mask, 1)
+            flip_h = True
         if random.random() > 0.5:
             img, mask = ops.flip_u8(img, 0), ops.flip_mask(mask, 0)
+            flip_v = True
         c = ops.semantic_counts(mask.reshape(1, -1), mask.reshape(1, -1))[0, :, 0].tolist()  # #pixels per class
         total = c[1] + c[2]
         live_ratio = c[1] / total if total > 0 else 0.5
@@ -120,7 +125,7 @@ class CellDataset:
         if random.random() > 0.6:  # HSV jitter (cv2): not built, draws consumed
             random.uniform(-10, 10)
             random.uniform(0.9, 1.1)
-        return img, mask
+        return img, mask, (flip_h, flip_v)
 
     def __getitem__(self, idx):
         from PIL import Image
@@ -134,10 +139,13 @@ class CellDataset:
         polys, labels, bboxes = load_labelme(os.path.join(self.data_dir, name.replace(".jpg", ".json")),
                                              h / original_size[0], w / original_size[1])
         mask = ops.rasterize_polygons(polys, [l + 1 for l in labels], h, w, img.device)
+        flips = (False, False)
         if self.split == "train":
-            img, mask = self._augment(img.contiguous(), mask)
+            img, mask, flips = self._augment(img.contiguous(), mask)
+        instance_masks = list(ops.rasterize_instances(polys, h, w, img.device, flip_h=flips[0], flip_v=flips[1]))
         tensor = self.transform(img) if self.transform else ops.to_tensor(img)
-        return {"image": tensor, "instance_polygons": polys, "instance_labels": labels, "bboxes": bboxes,
+        # dataset.py:313-321; bboxes stay in the unflipped frame, as the reference leaves them
+        return {"image": tensor, "instance_masks": instance_masks, "instance_labels": labels, "bboxes": bboxes,
                 "semantic_mask": mask, "image_id": name, "original_size": original_size}
 
 

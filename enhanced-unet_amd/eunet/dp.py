@@ -6,7 +6,10 @@ its own B samples) and has exactly one exchange step per iteration: the
 gradient all-reduce (backend 'nccl' == RCCL over xGMI on MI355X; 'gloo' for
 the CPU tests).  BatchNorm stays per replica, as under DDP without SyncBN;
 running statistics are broadcast from rank 0 before each forward
-(DDP broadcast_buffers semantics).
+(DDP broadcast_buffers semantics) as ONE collective on a persistent flat buffer: at
+construction every floating-point module buffer is re-pointed at a slice of that buffer
+(the HIP kernels update running statistics through those views), so the per-step sync
+is a single async broadcast with no host-side concatenation or scatter copies.
 
 Overlap: parameter gradients are written by the HIP backward straight into a
 flat fp32 buffer laid out in backward-production order (head, dec1, dec2 ...
@@ -104,19 +107,35 @@ class DataParallel:
         with torch.no_grad():  # identical initial replicas
             for n in self.order:
                 dist.broadcast(params[n].data, src=0, group=group)
+        self.flat_buffers = self._flatten_buffers(model)
         self._sync_buffers()
         model.grad_sink_factory = lambda: BucketSink(self)
 
-    def _sync_buffers(self):
-        bufs = [b for _, b in self.model.named_buffers() if b.dtype.is_floating_point]
-        if not bufs or self.world == 1:
-            return
-        flat = torch.cat([b.reshape(-1) for b in bufs])
-        dist.broadcast(flat, src=0, group=self.group)
+    @staticmethod
+    def _flatten_buffers(model):
+        """Re-point every floating-point buffer (BN running_mean / running_var) at a slice of one
+        flat tensor; returns it (None without such buffers)."""
+        entries = [(mod, name, b) for mod in model.modules() for name, b in mod._buffers.items()
+                   if b is not None and b.dtype.is_floating_point]
+        if not entries:
+            return None
+        dt, dev = entries[0][2].dtype, entries[0][2].device
+        if any(b.dtype != dt or b.device != dev for _, _, b in entries):
+            raise RuntimeError("DataParallel: floating-point buffers must share one dtype and device")
+        flat = torch.empty(sum(b.numel() for _, _, b in entries), dtype=dt, device=dev)
         off = 0
-        for b in bufs:
-            b.copy_(flat[off:off + b.numel()].view_as(b))
-            off += b.numel()
+        with torch.no_grad():
+            for mod, name, b in entries:
+                view = flat[off:off + b.numel()].view_as(b)
+                view.copy_(b)
+                mod._buffers[name] = view
+                off += b.numel()
+        return flat
+
+    def _sync_buffers(self):
+        if self.flat_buffers is None or self.world == 1:
+            return
+        dist.broadcast(self.flat_buffers, src=0, group=self.group)  # nccl: stream-ordered, no host wait
 
     def before_forward(self):
         if self.broadcast_buffers:

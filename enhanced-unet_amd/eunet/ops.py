@@ -174,22 +174,35 @@ def head_bwd(z, n, h, w, k, w1, b1, gamma, beta, w2, mean, invstd, g_logits, g_o
          _ptr(gbeta), _ptr(gw2), _ptr(gb2), DTYPES[dtype], _ptr(ws), _stream())
 
 
+def loss_reference_params() -> _lib.LossParams:
+    p = _lib.LossParams()
+    call("eunet_loss_reference_params", ctypes.byref(p))
+    return p
+
+
+def loss_sums_len(n, k):
+    v = c_int()
+    call("eunet_loss_sums_len", n, k, ctypes.byref(v))
+    return v.value
+
+
 def loss_workspace_bytes(n, k, h, w):
     b = c_size_t()
     call("eunet_loss_workspace_bytes", n, k, h, w, ctypes.byref(b))
     return b.value
 
 
-def loss_fwd(logits, target, sums, loss, parts, ws):
+def loss_fwd(logits, target, params, sums, loss, parts, ws):
+    """params: _lib.LossParams or None (the reference Trainer's configuration)."""
     n, k, h, w = logits.shape
-    call("eunet_loss_fwd", _ptr(logits), _ptr(target), n, k, h, w, _ptr(sums), _ptr(loss), _ptr(parts), _ptr(ws),
-         _stream())
+    call("eunet_loss_fwd", _ptr(logits), _ptr(target), n, k, h, w, _ref(params), _ptr(sums), _ptr(loss),
+         _ptr(parts), _ptr(ws), _stream())
 
 
-def loss_bwd(logits, target, sums, gloss, glogits):
+def loss_bwd(logits, target, params, sums, gloss, glogits):
     n, k, h, w = logits.shape
-    call("eunet_loss_bwd", _ptr(logits), _ptr(target), n, k, h, w, _ptr(sums), _ptr(gloss), _ptr(glogits),
-         _stream())
+    call("eunet_loss_bwd", _ptr(logits), _ptr(target), n, k, h, w, _ref(params), _ptr(sums), _ptr(gloss),
+         _ptr(glogits), _stream())
 
 
 def bn_bwd_tiles(y: Act) -> int:
@@ -415,6 +428,19 @@ def rasterize_polygons(polys, labels, h, w, device):
     lab = torch.tensor(np.asarray(labels, np.int32), device=device)
     call("eunet_rasterize_polygons", _ptr(pts), _ptr(off), _ptr(lab), len(polys), h, w, _ptr(mask), _stream())
     return mask
+
+
+def rasterize_instances(polys, h, w, device, flip_h: bool = False, flip_v: bool = False):
+    """One uint8 [h, w] mask per polygon (stacked [n, h, w]), mirrored by the training flips."""
+    if not polys:
+        return torch.zeros(0, h, w, dtype=torch.uint8, device=device)
+    import numpy as np
+    pts = torch.from_numpy(np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in polys])).to(device)
+    off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in polys])]).astype(np.int32), device=device)
+    masks = torch.empty(len(polys), h, w, dtype=torch.uint8, device=device)
+    call("eunet_rasterize_instances", _ptr(pts), _ptr(off), len(polys), h, w, int(flip_h), int(flip_v), _ptr(masks),
+         _stream())
+    return masks
 
 
 def flip_u8(img, mode: int):

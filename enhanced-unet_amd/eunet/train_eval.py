@@ -25,18 +25,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .losses import combined_loss, consistency_loss
+from . import losses as L
+from .losses import CrossEntropyLoss, FocalLoss, check_targets, combined_loss, consistency_loss  # noqa: F401
 from .models import EnhancedUNet
-
-
-class FocalLoss(nn.Module):
-    """API mirror of train_eval.FocalLoss (train_eval.py:28-60) for the Enhanced-UNet
-    configuration (alpha [1,8,5], gamma 5, CE weights [1,20,10]); computed by the
-    fused loss kernel.  inputs [N,K,H,W], targets [N,H,W] -> mean focal term."""
-
-    def forward(self, inputs, targets):
-        _, parts = combined_loss(inputs, targets, return_parts=True)
-        return parts[:, 0].mean()
 
 
 class Trainer:
@@ -47,6 +38,11 @@ class Trainer:
         self.total_epochs = max(1, total_epochs)
         if model_name != "enhanced_unet":
             raise ValueError("this build implements the enhanced_unet training path only")
+        # train_eval.py:74-80: the focal and CE modules with the reference's class weights
+        class_weights = torch.tensor([1.0, 20.0, 10.0]).to(device)
+        alpha = [1.0, 8.0, 5.0]
+        self.focal_loss = FocalLoss(alpha=alpha, gamma=5.0, ignore_index=None, class_weights=class_weights)
+        self.ce_loss = CrossEntropyLoss(weight=class_weights)
         self.dice_loss_weight = 2.5
         self.focal_loss_weight = 2.5
         self.tversky_loss_weight = 1.0
@@ -68,23 +64,34 @@ class Trainer:
         self.dp = None  # eunet.dp.DataParallel when training on several GPUs
 
     # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
+    def loss_params(self):
+        """The combined loss as _compute_combined_loss forms it from this Trainer's attributes
+        (train_eval.py:183-197): self.focal_loss's alpha / gamma / class_weights / ignore_index,
+        Dice / Tversky class weights, the three term weights, num_classes = 3."""
+        f = self.focal_loss
+        return L.make_params(ce_weight=f.class_weights, alpha=f.alpha, gamma=f.gamma, ignore_index=f.ignore_index,
+                             w_focal=self.focal_loss_weight, w_dice=self.dice_loss_weight,
+                             w_tversky=self.tversky_loss_weight, class_div=3.0)
+
     def _compute_combined_loss(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-        return combined_loss(logits.unsqueeze(0), target.long().to(logits.device).unsqueeze(0))
+        return combined_loss(logits.unsqueeze(0), target.long().to(logits.device).unsqueeze(0),
+                             params=self.loss_params())
 
     def dice_loss(self, pred, target, num_classes=3):
-        return combined_loss(pred, target, return_parts=True)[1][:, 1].mean()
+        return L.dice_loss(pred, target, num_classes)
 
     def tversky_loss(self, pred, target, num_classes=3, alpha=0.7):
-        return combined_loss(pred, target, return_parts=True)[1][:, 2].mean()
+        return L.tversky_loss(pred, target, num_classes, alpha)
 
     def aux_loss(self, fused, aux_outputs, masks):
         """Batched train_eval.py:326-337 with _apply_auxiliary_supervision (:199-234):
         (1/B) sum_i [CL(fused_i) + sum_b w_b (CL(branch_b,i) + consistency_weight MSE(p_b,i, p_f,i))]."""
-        loss = combined_loss(fused, masks)
+        prm = self.loss_params()
+        loss = combined_loss(fused, masks, params=prm)
         if not aux_outputs or not self.aux_branch_weights:
             return loss
         for name, w in self.aux_branch_weights.items():
-            loss = loss + w * combined_loss(aux_outputs[name], masks)
+            loss = loss + w * combined_loss(aux_outputs[name], masks, params=prm)
         if self.consistency_weight > 0:
             (n0, w0), (n1, w1) = list(self.aux_branch_weights.items())
             loss = loss + consistency_loss(fused, aux_outputs[n0], aux_outputs[n1], self.consistency_weight * w0,
@@ -128,13 +135,17 @@ class Trainer:
             else:
                 out = self.model(images)
                 logits = F.interpolate(out, size=masks.shape[-2:], mode="bilinear", align_corners=False)
-            loss = combined_loss(logits, masks)
+            loss = combined_loss(logits, masks, params=self.loss_params())
         loss.backward()
         if self.dp is not None:
             self.dp.after_backward()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1.0, foreach=True)
         self.optimizer.step()
-        return loss.item() if sync_loss else loss.detach()
+        if not sync_loss:
+            return loss.detach()
+        value = loss.item()
+        check_targets()  # out-of-range targets surface at this sync, as the reference's device assert would
+        return value
 
     def train_epoch(self, dataloader):
         self.model.train()
@@ -146,7 +157,9 @@ class Trainer:
             loss = self.step(images, masks, sync_loss=False).double()
             total = loss if total is None else total + loss
             n += 1
-        return float(total.item()) / n if n else 0.0
+        value = float(total.item()) / n if n else 0.0
+        check_targets()
+        return value
 
     def epoch_lr_step(self, epoch: int) -> float:
         """train_model's per-epoch stepping (train_eval.py:1104-1111).  The reference steps the
@@ -176,9 +189,10 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
     each train_epoch, semantic validation every 3 epochs, best-mIoU checkpoint in the reference's
     dict format ('checkpoints/<model>/best_model.pth'), early stop after patience 10 (epoch > 25).
 
-    The reference builds its loaders from CellDataset (cv2 / PIL LabelMe pipeline, dataset.py),
-    which this build does not provide: pass train_loader / val_loader yielding the collate_fn batch
-    dict ({'images', 'batch_items': [{'semantic_mask'}]}), e.g. eunet.synth.loader."""
+    Without train_loader / val_loader it builds the reference's loaders (train_eval.py:1054-1075):
+    eunet.data.CellDataset(data_dir, 'train' / 'val', max_size=640), batch 2 on cuda (1 otherwise),
+    the train split shuffled, val batch 1.  Any iterable of collate_fn batch dicts
+    ({'images', 'batch_items': [{'semantic_mask'}]}) may be passed instead, e.g. eunet.synth.loader."""
     import os
     from .models import get_model
     save_dir = save_dir or os.path.join("checkpoints", model_name)
@@ -187,8 +201,15 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
     if os.path.exists(checkpoint_path) and skip_training:
         return checkpoint_path
     if train_loader is None:
-        raise NotImplementedError("CellDataset (dataset.py, cv2/PIL LabelMe loader) is not part of this build: "
-                                  "pass train_loader/val_loader")
+        from .data import CellDataset, DataLoader, collate_fn
+        if data_dir is None:
+            raise ValueError("train_model needs data_dir (a LabelMe directory) or explicit loaders")
+        batch_size = 2 if str(device).startswith("cuda") else 1  # train_eval.py:1058-1059
+        train_loader = DataLoader(CellDataset(data_dir, split="train", max_size=640, device=device),
+                                  batch_size=batch_size, shuffle=True, collate_fn=collate_fn)
+        if val_loader is None:
+            val_loader = DataLoader(CellDataset(data_dir, split="val", max_size=640, device=device), batch_size=1,
+                                    shuffle=False, collate_fn=collate_fn)
     if model is None:
         model = get_model(model_name, num_classes=3, device=device, **model_kwargs).to(device)
     history = {"train_loss": [], "val_loss": [], "val_miou": [], "val_live_iou": [], "val_dead_iou": [],
@@ -227,11 +248,32 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
     return checkpoint_path
 
 
+def _numpy_safe_globals():
+    """The numpy scalar reconstructors a reference checkpoint holds: best_miou and the history
+    values are np.float64 (Evaluator.evaluate returns np.mean results, train_eval.py:1017).
+    Allow-listed for the weights-only unpickler by name, under numpy 1.x and 2.x module paths;
+    nothing else is admitted."""
+    import numpy as np
+    try:
+        from numpy._core import multiarray as ma
+    except ImportError:  # numpy < 2
+        from numpy.core import multiarray as ma
+    out = [ma.scalar, (ma.scalar, "numpy.core.multiarray.scalar"), (ma.scalar, "numpy._core.multiarray.scalar"),
+           np.dtype]
+    for nm in ("Float64DType", "Float32DType", "Float16DType", "Int64DType", "Int32DType", "BoolDType"):
+        dt = getattr(getattr(np, "dtypes", None), nm, None)
+        if dt is not None:
+            out.append(dt)
+    return out
+
+
 def load_checkpoint(model, checkpoint_path: str, map_location=None):
-    """evaluate_model's checkpoint load (train_eval.py:1186-1202), safe loader: the file holds
-    only tensors and plain containers, so weights_only=True reads reference checkpoints too.
+    """evaluate_model's checkpoint load (train_eval.py:1186-1202) with the weights-only loader:
+    tensors, plain containers and numpy scalars (_numpy_safe_globals) only, so reference
+    checkpoints (np.float64 best_miou / history) load while nothing executable is admitted.
     Also accepts a bare state_dict."""
-    ckpt = torch.load(checkpoint_path, map_location=map_location or "cpu", weights_only=True)
+    with torch.serialization.safe_globals(_numpy_safe_globals()):
+        ckpt = torch.load(checkpoint_path, map_location=map_location or "cpu", weights_only=True)
     sd = ckpt["model_state_dict"] if isinstance(ckpt, dict) and "model_state_dict" in ckpt else ckpt
     model.load_state_dict(sd)
     return ckpt

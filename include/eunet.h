@@ -153,16 +153,42 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
                    int dtype, void* ws, void* stream);
 
 /* ---- combined loss (train_eval.py:28-60, 134-197, 262-337) ----------------
- * logits [N,K,H,W] fp32 NCHW, target [N,H,W] int64; K <= 3.
- * loss = (1/N) sum_n [2.5 focal_n + 2.5 dice_n + 1.0 tversky_n].
- * sums (caller-owned, saved for backward): [N][1+3K] fp32; loss: 1 fp32 on device.
- * parts (nullable): [N][3] focal/dice/tversky per sample. */
+ * logits [N,K,H,W] fp32 NCHW, target [N,H,W] int64; K <= 3.  params (nullable = the
+ * Trainer's enhanced_unet configuration, eunet_loss_reference_params):
+ *   loss = w_focal * focal + (1/N) sum_n [w_dice dice_n + w_tversky tversky_n]
+ *   focal = sum over all pixels of alpha_t (1 - pt)^gamma ce / F_den, ce = -w_t log p_t
+ *           (F.cross_entropy weight = ce_weight, ignore_index pixels give ce = 0),
+ *           F_den = N*H*W (FocalLoss.mean(), train_eval.py:60) or, focal_norm = 1, the sum
+ *           of w_t (nn.CrossEntropyLoss(weight) mean reduction, train_eval.py:80)
+ *   dice_n / tversky_n: Trainer.dice_loss / tversky_loss (:134-181), class mean over
+ *           class_div classes (3 in _compute_combined_loss for any K, :192-193).
+ * sums (caller-owned, saved for backward): eunet_loss_sums_len floats = [N][3+3K] partial
+ * sums, then F_den, then the number of targets outside [0, K) that are not ignore_index
+ * (an error in the reference: F.cross_entropy raises; the host reports it at its next sync).
+ * loss: 1 fp32 on device.  parts (nullable): [N][3] focal/dice/tversky per sample. */
+#define EUNET_NO_IGNORE (-2147483647 - 1) /* INT32_MIN */
+typedef struct {
+  float ce_weight[3];      /* FocalLoss class_weights (F.cross_entropy weight); 1 = none */
+  float alpha[3];          /* FocalLoss alpha per class; 1 = none */
+  float gamma;             /* FocalLoss gamma */
+  int ignore_index;        /* FocalLoss ignore_index; EUNET_NO_IGNORE = none */
+  float dice_weight[3];    /* Trainer.dice_loss class weights [1, 15, 8] */
+  float tversky_weight[3]; /* Trainer.tversky_loss class weights [1, 12, 6] */
+  float tversky_alpha;     /* 0.7 */
+  float w_focal, w_dice, w_tversky;  /* term weights (2.5, 2.5, 1.0 for enhanced_unet) */
+  float class_div;         /* num_classes of dice_loss / tversky_loss */
+  int focal_norm;          /* 0 pixel mean, 1 ce-weight mean (CrossEntropyLoss) */
+} eunet_loss_params;
+int eunet_loss_reference_params(eunet_loss_params* params);
+int eunet_loss_sums_len(int n, int k, int* len);
 int eunet_loss_workspace_bytes(int n, int k, int h, int w, size_t* bytes);
 int eunet_loss_fwd(const float* logits, const int64_t* target, int n, int k, int h, int w,
-                   float* sums, float* loss, float* parts, void* ws, void* stream);
+                   const eunet_loss_params* params, float* sums, float* loss, float* parts, void* ws,
+                   void* stream);
 /* glogits = d loss / d logits * (*gloss) (gloss: device scalar) */
 int eunet_loss_bwd(const float* logits, const int64_t* target, int n, int k, int h, int w,
-                   const float* sums, const float* gloss, float* glogits, void* stream);
+                   const eunet_loss_params* params, const float* sums, const float* gloss, float* glogits,
+                   void* stream);
 
 /* ---- backward helpers ----------------------------------------------------
  * BN(+ReLU) backward (autograd of models.py:220-224): g is the gradient w.r.t.
@@ -314,6 +340,11 @@ int eunet_consistency_bwd(const float* fused, const float* br0, const float* br1
  * even-odd at the pixel centre, plus every lattice pixel on an edge. */
 int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* labels, int npoly,
                              int h, int w, int64_t* mask, void* stream);
+/* per-instance uint8 masks [npoly][h][w] (dataset.py:184-193, 'instance_masks'), same fill rule,
+ * mirrored horizontally (flip_h) / vertically (flip_v) as the training flips mirror every
+ * instance mask (dataset.py:209-222) */
+int eunet_rasterize_instances(const int* pts, const int* poly_off, int npoly, int h, int w, int flip_h,
+                              int flip_v, uint8_t* masks, void* stream);
 /* cv2.flip (dataset.py:208-222): mode 1 horizontal, 0 vertical; HWC uint8 / int64 mask */
 int eunet_flip_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, int mode, void* stream);
 int eunet_flip_mask(const int64_t* src, int64_t* dst, int h, int w, int mode, void* stream);

@@ -8,6 +8,7 @@ What is restated (all citations into /root/reference):
   * EnhancedUNet fallback   models.py:304-314 (enhance head), 334-339 (residual)
   * get_model key schema    models.py:590-624  (109 state_dict keys)
   * FocalLoss               train_eval.py:28-60  (alpha=[1,8,5], gamma=5, w=[1,20,10], :74-79)
+  * FocalLoss(alpha, gamma, ignore_index, class_weights) in general (focal_loss)
   * Trainer.dice_loss       train_eval.py:134-157 (class weights [1,15,8], eps 1e-6)
   * Trainer.tversky_loss    train_eval.py:159-181 (class weights [1,12,6], alpha 0.7)
   * _compute_combined_loss  train_eval.py:183-197 (2.5*focal + 2.5*dice + 1.0*tversky, :82-85)
@@ -165,6 +166,54 @@ def combined_loss(logits: torch.Tensor, target: torch.Tensor, parts: bool = Fals
     return total
 
 
+def focal_loss(inputs, targets, alpha=None, gamma=2.0, ignore_index=None, class_weights=None):
+    """train_eval.FocalLoss(alpha, gamma, ignore_index, class_weights).forward (train_eval.py:37-60)
+    on batched [N,K,...] inputs."""
+    if ignore_index is not None:
+        ce = F.cross_entropy(inputs, targets, ignore_index=ignore_index, reduction="none", weight=class_weights)
+    else:
+        ce = F.cross_entropy(inputs, targets, reduction="none", weight=class_weights)
+    pt = torch.exp(-ce)
+    if alpha is not None:
+        if isinstance(alpha, (list, torch.Tensor)):
+            alpha_t = torch.zeros_like(ce)
+            for i, a in enumerate(alpha):
+                if ignore_index is None or i != ignore_index:
+                    alpha_t[targets == i] = a
+            fl = alpha_t * (1 - pt) ** gamma * ce
+        else:
+            fl = alpha * (1 - pt) ** gamma * ce
+    else:
+        fl = (1 - pt) ** gamma * ce
+    return fl.mean()
+
+
+def dice_loss(pred, target, num_classes=3):
+    """Trainer.dice_loss (train_eval.py:134-157), batched [N,K,H,W] / [N,H,W]."""
+    ps = F.softmax(pred, dim=1)
+    out = []
+    for c in range(num_classes):
+        pc, tc = ps[:, c], (target == c).to(pred.dtype)
+        inter = (pc * tc).sum(dim=(1, 2))
+        union = pc.sum(dim=(1, 2)) + tc.sum(dim=(1, 2))
+        out.append(((1.0 - (2.0 * inter + 1e-6) / (union + 1e-6)) * DICE_W[c]).mean())
+    return sum(out) / len(out)
+
+
+def tversky_loss(pred, target, num_classes=3, alpha=0.7):
+    """Trainer.tversky_loss (train_eval.py:159-181), batched."""
+    ps = F.softmax(pred, dim=1)
+    out = []
+    for c in range(num_classes):
+        pc, tc = ps[:, c], (target == c).to(pred.dtype)
+        tp = (pc * tc).sum(dim=(1, 2))
+        fp = (pc * (1 - tc)).sum(dim=(1, 2))
+        fn = ((1 - pc) * tc).sum(dim=(1, 2))
+        tv = (tp + 1e-6) / (tp + alpha * fp + (1 - alpha) * fn + 1e-6)
+        out.append(((1.0 - tv) * TVERSKY_W[c]).mean())
+    return sum(out) / len(out)
+
+
 def batch_loss(out2h: torch.Tensor, target: torch.Tensor):
     """train_eval.py:262-337: per-sample resize 2H->H (bilinear) + combined loss, /B."""
     B = out2h.shape[0]
@@ -244,5 +293,6 @@ def avgpool_equals_resize(out2h: torch.Tensor) -> float:
     return float((a - b).abs().max())
 
 
-__all__ = ["state_spec", "formula_weights", "forward", "combined_loss", "batch_loss",
+__all__ = ["state_spec", "formula_weights", "forward", "combined_loss", "batch_loss", "focal_loss", "dice_loss",
+           "tversky_loss",
            "OracleTrainer", "lr_trajectory", "block_table", "flops_per_pixel", "math"]

@@ -23,6 +23,11 @@ Fixtures (all with formula weights, oracle/weights.py):
                    branch (argmax filters, background promotions, all pixel-ratio regimes)
   dual_c3k3.npz    SMP-path EnhancedUNet (attention gate, fusion head, residual, aux outputs)
                    with stand-in branches + one train_epoch with auxiliary supervision
+  loss_api.npz     the reference loss modules as API: FocalLoss(alpha, gamma, ignore_index,
+                   class_weights) over several configurations (list / scalar / short alpha,
+                   ignore_index in and out of range, non-integer gamma), Trainer.ce_loss,
+                   Trainer.dice_loss / tversky_loss with num_classes 2 and 3 -- values and
+                   d loss / d logits
   tta_c3k3.npz     Evaluator._run_model_single / _run_tta_inference (flips + 0.75/1.25
                    rescales) of the reference model (eval mode, BN stats from one train
                    forward) on a 40x56 image (reflect pad to /32 and crop exercised)
@@ -159,6 +164,44 @@ def gen_loss(ref_te, K, fname):
     np.savez_compressed(os.path.join(HERE, fname), logits=logits.detach().numpy(),
                         target=target.numpy(), total=total.item(), focal=focal.item(),
                         dice=dice.item(), tversky=tv.item(), grad=logits.grad.numpy())
+
+
+LOSS_API_FOCAL = [  # (alpha, gamma, ignore_index, class_weights)
+    ([1.0, 8.0, 5.0], 5.0, None, [1.0, 20.0, 10.0]),
+    (None, 2.0, None, None),
+    (0.25, 2.0, 1, None),
+    ([1.0, 2.0], 3.0, None, [1.0, 4.0, 2.0]),
+    ([0.5, 1.0, 2.0], 1.5, 255, [2.0, 1.0, 3.0]),
+]
+
+
+def gen_loss_api(ref_te):
+    """loss_api.npz: the reference's FocalLoss / CrossEntropyLoss / dice_loss / tversky_loss."""
+    tr = ref_te.Trainer(torch.nn.Linear(1, 1), "cpu", "enhanced_unet", total_epochs=50)
+    g = torch.Generator().manual_seed(91)
+    x = torch.randn(2, 3, 12, 10, generator=g) * 2.0
+    t = torch.randint(0, 3, (2, 12, 10), generator=g)
+    t_ign = t.clone()
+    t_ign[:, ::3, ::4] = 255
+    out = {"x": x.numpy(), "t": t.numpy(), "t_ign": t_ign.numpy()}
+
+    def run(name, fn, tt):
+        xx = x.clone().requires_grad_(True)
+        v = fn(xx, tt)
+        v.backward()
+        out[f"{name}_val"] = v.item()
+        out[f"{name}_grad"] = xx.grad.numpy()
+
+    for i, (a, gm, ii, cw) in enumerate(LOSS_API_FOCAL):
+        fl = ref_te.FocalLoss(alpha=a, gamma=gm, ignore_index=ii,
+                              class_weights=None if cw is None else torch.tensor(cw))
+        run(f"focal{i}", fl, t_ign if ii == 255 else t)
+    run("ce", tr.ce_loss, t)
+    for nc in (2, 3):
+        run(f"dice_nc{nc}", lambda xx, tt: tr.dice_loss(xx, tt, num_classes=nc), t)
+        run(f"tversky_nc{nc}", lambda xx, tt: tr.tversky_loss(xx, tt, num_classes=nc), t)
+    run("tversky_a05", lambda xx, tt: tr.tversky_loss(xx, tt, num_classes=3, alpha=0.5), t)
+    np.savez_compressed(os.path.join(HERE, "loss_api.npz"), **out)
 
 
 def gen_step(ref_models, ref_te):
@@ -376,6 +419,7 @@ def main(only=()):
         "in1_equiv": lambda: gen_in1(ref_models),
         "loss_k3": lambda: gen_loss(ref_te, 3, "loss_k3.npz"),
         "loss_k2": lambda: gen_loss(ref_te, 2, "loss_k2.npz"),
+        "loss_api": lambda: gen_loss_api(ref_te),
         "step_c3k3": lambda: gen_step(ref_models, ref_te),
         "lr_traj": lambda: gen_lr(ref_te),
         "metrics": gen_metrics,

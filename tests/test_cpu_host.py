@@ -89,15 +89,69 @@ def test_dual_branch_schema_matches_reference():
 
 def test_checkpoint_format_roundtrip_cpu(tmp_path):
     """load_checkpoint reads the reference's best_model.pth dict (and bare state_dicts) with the
-    safe loader."""
+    weights-only loader.  The reference stores best_miou and history values as np.float64
+    (Evaluator.evaluate returns np.mean results, train_eval.py:1017)."""
+    import numpy as np
     from eunet.models import EnhancedUNet
     from eunet.train_eval import load_checkpoint
     a = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16)
     b = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16)
     p = tmp_path / "ck.pth"
-    torch.save({"epoch": 1, "model_state_dict": a.state_dict(), "best_miou": 0.1, "best_loss": 2.0,
-                "history": {"train_loss": [2.0]}}, p)
-    load_checkpoint(b, str(p))
+    torch.save({"epoch": 1, "model_state_dict": a.state_dict(), "best_miou": np.float64(0.5),
+                "best_loss": np.float64(2.0),
+                "history": {"train_loss": [2.0], "val_miou": [np.float64(0.5)],
+                            "val_dice": [[np.float64(0.1), np.float64(0.2)]]}}, p)
+    ck = load_checkpoint(b, str(p))
+    assert ck["best_miou"] == 0.5 and ck["history"]["val_dice"][0][1] == 0.2
     assert all(torch.equal(x, y) for x, y in zip(a.state_dict().values(), b.state_dict().values()))
     torch.save(a.state_dict(), tmp_path / "sd.pth")
     load_checkpoint(b, str(tmp_path / "sd.pth"))
+
+
+def test_reference_loss_api_surface():
+    """train_eval.FocalLoss(alpha, gamma, ignore_index, class_weights) constructs like the
+    reference's (train_eval.py:28-35); Trainer carries focal_loss / ce_loss (:79-80) and the
+    loss methods with the reference signatures (:134, :159, :183)."""
+    import inspect
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import CrossEntropyLoss, FocalLoss, Trainer
+    fl = FocalLoss(alpha=[1.0, 8.0, 5.0], gamma=5.0, ignore_index=None, class_weights=torch.tensor([1.0, 20.0, 10.0]))
+    assert fl.gamma == 5.0 and fl.alpha == [1.0, 8.0, 5.0] and fl.ignore_index is None
+    assert FocalLoss().gamma == 2.0 and FocalLoss().alpha is None
+    tr = Trainer(EnhancedUNet(num_classes=3, base_ch=16), "cpu", "enhanced_unet")
+    assert isinstance(tr.focal_loss, FocalLoss) and isinstance(tr.ce_loss, CrossEntropyLoss)
+    assert tr.focal_loss.gamma == 5.0 and tr.focal_loss.class_weights.tolist() == [1.0, 20.0, 10.0]
+    assert list(inspect.signature(tr.dice_loss).parameters) == ["pred", "target", "num_classes"]
+    assert list(inspect.signature(tr.tversky_loss).parameters) == ["pred", "target", "num_classes", "alpha"]
+    p = tr.loss_params()
+    assert list(p.ce_weight) == [1.0, 20.0, 10.0] and list(p.alpha) == [1.0, 8.0, 5.0] and p.gamma == 5.0
+    assert (p.w_focal, p.w_dice, p.w_tversky, p.class_div) == (2.5, 2.5, 1.0, 3.0)
+    tr.focal_loss.gamma = 3.0  # _compute_combined_loss reads the module's attributes each call
+    assert tr.loss_params().gamma == 3.0
+    with pytest.raises(ValueError):
+        FocalLoss(alpha=[1.0, 2.0, 3.0, 4.0]).params()
+
+
+def test_train_model_builds_reference_loaders(tmp_path):
+    """train_model without loaders builds CellDataset train / val loaders from data_dir
+    (train_eval.py:1054-1075); zero epochs keeps it on the CPU."""
+    import json
+    from eunet import data as D
+    from eunet.train_eval import train_model
+    for i in range(10):
+        (tmp_path / f"im{i}.jpg").write_bytes(b"")
+        (tmp_path / f"im{i}.json").write_text(json.dumps({"shapes": []}))
+    built = []
+    orig = D.CellDataset.__init__
+
+    def spy(self, *a, **k):
+        orig(self, *a, **k)
+        built.append((self.split, self.max_size, len(self)))
+
+    D.CellDataset.__init__ = spy
+    try:
+        train_model("enhanced_unet", data_dir=str(tmp_path), device="cpu", num_epochs=0,
+                    save_dir=str(tmp_path / "ck"), verbose=False, base_ch=16)
+    finally:
+        D.CellDataset.__init__ = orig
+    assert built == [("train", 640, 7), ("val", 640, 1)]

@@ -81,3 +81,71 @@ def test_dp_world2_on_one_gpu():
         assert nb > 3
         assert same, "ranks must hold identical averaged gradients"
         assert err < 1e-6, err
+
+
+def _nccl_worker(port, q):
+    """world size 1 on the RCCL backend: the communicator is created, every gradient bucket is
+    all-reduced through RCCL from inside the HIP backward (BucketSink), BN buffers are broadcast
+    as one flat tensor; with one rank the averaged gradients must equal the plain run's bit for
+    bit, and the replicated training step must match as well."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "enhanced-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from oracle import eunet_ref as R
+        from eunet import synth
+        from eunet.dp import DataParallel
+        from eunet.losses import combined_loss
+        from eunet.models import EnhancedUNet
+        from eunet.train_eval import Trainer
+        sd = {k: v.float() if v.is_floating_point() else v for k, v in R.formula_weights(16, 1, 2).items()}
+        x, m = synth.batch(2, 64, 64, start_index=200, num_classes=2, in_channels=1, device="cuda")
+
+        def fresh():
+            mod = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16, dtype="bf16")
+            mod.load_state_dict(sd)
+            return mod.cuda().train()
+
+        ref = fresh()
+        combined_loss(ref.forward_lowres(x), m).backward()
+        model = fresh()
+        dp = DataParallel(model, bucket_mb=0.05)
+        buffers_are_views = all(b.untyped_storage().data_ptr() == dp.flat_buffers.untyped_storage().data_ptr()
+                                for n, b in model.named_buffers() if b.dtype.is_floating_point)
+        dp.before_forward()
+        combined_loss(model.forward_lowres(x), m).backward()
+        torch.cuda.synchronize()
+        grads_equal = all(torch.equal(p.grad, q.grad) for p, q in zip(model.parameters(), ref.parameters()))
+        # three Trainer steps with DP vs without: identical parameters and BN buffers
+        ta, tb = Trainer(fresh(), "cuda", "enhanced_unet"), Trainer(fresh(), "cuda", "enhanced_unet")
+        ta.dp = DataParallel(ta.model, bucket_mb=0.05)
+        la = [ta.step(x, m) for _ in range(3)]
+        lb = [tb.step(x, m) for _ in range(3)]
+        same_step = la == lb and all(torch.equal(p, q) for p, q in zip(ta.model.state_dict().values(),
+                                                                         tb.model.state_dict().values()))
+        q.put(dict(backend=dist.get_backend(), rccl=str(torch.cuda.nccl.version()), buckets=len(dp.buckets),
+                   views=buffers_are_views, grads_equal=grads_equal, same_step=same_step))
+    except Exception as e:  # report instead of hanging the parent on q.get
+        q.put(dict(error=repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp_nccl_world1_rccl_buckets():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=500)
+    p.join(timeout=120)
+    print("RCCL world-1 DP:", res)
+    assert "error" not in res, res
+    assert p.exitcode == 0
+    assert res["backend"] == "nccl" and res["buckets"] > 3
+    assert res["views"], "BN buffers must be views of the flat broadcast buffer"
+    assert res["grads_equal"], "RCCL-averaged gradients (world 1) must equal the plain backward"
+    assert res["same_step"], "Trainer steps with DataParallel(world 1) must equal the plain steps"

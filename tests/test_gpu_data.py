@@ -89,3 +89,48 @@ def test_cell_dataset_end_to_end(tmp_path):
     assert float(item["image"].min()) >= 0.0 and float(item["image"].max()) <= 1.0
     batch = next(iter(DataLoader(CellDataset(str(tmp_path), "val", device=DEV), batch_size=1)))
     assert batch["images"].shape == (1, 3, h, w) and batch["images"].is_cuda
+
+
+def test_instance_masks_follow_the_flips(tmp_path):
+    """'instance_masks' (dataset.py:313-321) are flipped with the image and the semantic mask
+    (dataset.py:209-222): re-painting them in order (later instances win, :197-201) gives back the
+    returned semantic mask exactly, flipped or not; an unflipped val item matches the direct fill."""
+    from PIL import Image
+    from eunet import ops
+    from eunet.data import CellDataset, load_labelme, reference_sizes
+    rng = np.random.default_rng(6)
+    shapes = [{"label": "live", "points": [[10, 10], [40, 12], [35, 40], [12, 35]]},
+              {"label": "dead", "points": [[60, 50], [95, 55], [70, 85]]},
+              {"label": "live", "points": [[30, 30], [70, 28], [66, 66]]}]  # overlaps both
+    for i in range(10):
+        Image.fromarray(rng.integers(0, 256, (100, 130, 3), dtype=np.uint8)).save(tmp_path / f"i{i:02d}.jpg")
+        (tmp_path / f"i{i:02d}.json").write_text(json.dumps({"shapes": shapes}))
+    ds = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV)
+    h, w = reference_sizes(100, 130, 640)
+    seen = set()
+    for seed in range(8):
+        random.seed(seed)
+        np.random.seed(seed)
+        r = random.Random(seed)
+        flips = (r.random() > 0.5, r.random() > 0.5)  # the dataset's first two draws
+        seen.add(flips)
+        item = ds[0]
+        inst = item["instance_masks"]
+        assert len(inst) == 3 and all(m.dtype == torch.uint8 and m.shape == (h, w) for m in inst)
+        sem = torch.zeros(h, w, dtype=torch.int64, device=DEV)
+        for m, lab in zip(inst, item["instance_labels"]):
+            sem[m > 0] = lab + 1
+        assert torch.equal(sem, item["semantic_mask"]), (seed, flips)
+        polys, labels, _ = load_labelme(str(tmp_path / "i00.json"), h / 100, w / 130)
+        direct = ops.rasterize_instances(polys, h, w, DEV)
+        want = direct
+        if flips[0]:
+            want = want.flip(2)
+        if flips[1]:
+            want = want.flip(1)
+        assert torch.equal(torch.stack(inst), want), (seed, flips)
+    assert len(seen) >= 3, seen  # flipped and unflipped cases were exercised
+    val = CellDataset(str(tmp_path), split="val", max_size=640, device=DEV)[0]
+    polys, labels, _ = load_labelme(str(tmp_path / "i07.json"), h / 100, w / 130)
+    ref = O.rasterize(polys, [l + 1 for l in labels], h, w)
+    assert np.array_equal(val["semantic_mask"].cpu().numpy(), ref)

@@ -182,3 +182,82 @@ def test_dual_bf16_vs_autocast_reference(golden_dir):
     print("dual bf16 relL2 ours", ours, "autocast", auto)
     assert torch.isfinite(out).all()
     assert ours < max(2.0 * auto, 0.02), (ours, auto)
+
+
+def _keep96(seed=7):
+    gen = torch.Generator().manual_seed(seed)
+    return ((torch.rand(2, 256, generator=gen) > 0.2).float(), (torch.rand(2, 128, generator=gen) > 0.15).float())
+
+
+def test_dual_base96_forward_fp32_vs_oracle():
+    """configs[4] width: base_ch = 96 (96/192/384/768-channel trunks; every layer runs the partial
+    co-block path, cout_pad 128 / 256 / 384 / 768).  fp32 train-mode forward at 64^2, B = 2: fused
+    and both aux outputs per pixel (floor 1e-3 of the max) within 1e-3 of the fp64 oracle, BN
+    running statistics within 1e-3."""
+    from eunet import synth
+    x, _ = synth.batch(2, 64, 64, start_index=21, num_classes=2, in_channels=1)
+    keep = _keep96()
+    S = D.dual_formula_weights(96, 1, 2, dtype=torch.float64)
+    with torch.no_grad():
+        ref, ref_aux = D.dual_forward(S, x.double(), training=True, drop_masks=keep)
+    m = _model(96, 1, 2, keep=keep).train()
+    with torch.no_grad():
+        out = m(x.to(DEV))
+    aux = m.get_aux_outputs()
+
+    def px(a, b):
+        a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+        return float(((a - b).abs() / b.abs().clamp_min(1e-3 * float(b.abs().max()))).max())
+
+    errs = (px(out, ref), px(aux["unetpp"], ref_aux["unetpp"]), px(aux["deeplab"], ref_aux["deeplab"]))
+    print("dual base96 fp32 per-pixel rel (fused, unetpp, deeplab):", errs)
+    assert max(errs) < 1e-3, errs
+    sd = m.state_dict()
+    for k, v in S.items():
+        if "running" in k:
+            assert _rel(sd[k], v) < 1e-3, k
+
+
+def test_dual_base96_train_grads_fp32_vs_oracle():
+    """Loss + every parameter gradient of one dual-branch step at base 96 (64^2, B = 2, c = 1,
+    K = 2, deep supervision) vs the fp64 oracle, tolerance as test_dual_train_grads_match_oracle."""
+    from eunet import synth
+    from eunet.train_eval import Trainer
+    x, msk = synth.batch(2, 64, 64, start_index=23, num_classes=2, in_channels=1)
+    keep = _keep96()
+    S, loss_ref = _oracle(96, 1, 2, x, msk, keep, torch.float64)
+    S32, _ = _oracle(96, 1, 2, x, msk, keep, torch.float32)
+    Sp, _ = _oracle(96, 1, 2, x, msk, keep, torch.float64, noise=1e-6, seed=1)
+    m = _model(96, 1, 2, keep=keep).train()
+    tr = Trainer(m, DEV, "enhanced_unet")
+    out = m(x.to(DEV))
+    loss = tr.aux_loss(out, m.get_aux_outputs(), msk.to(DEV))
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) < 1e-4 * abs(loss_ref.item())
+    rows = []
+    for k, p in m.named_parameters():
+        ref = S[k].grad
+        tol = max(1e-3, 3 * _rel_l2(S32[k].grad, ref), 1.5 * _rel_l2(Sp[k].grad, ref))
+        rows.append((_rel_l2(p.grad, ref) / tol, k, _rel_l2(p.grad, ref), tol))
+    for r in sorted(rows, reverse=True)[:6]:
+        print("dual base96 grad (ratio, name, err, tol):", r)
+    assert all(r[0] < 1.0 for r in rows), sorted(rows, reverse=True)[:3]
+
+
+def test_dual_base96_bf16_vs_autocast_reference():
+    """bf16 at base 96 vs the fp32 oracle, gated by what bf16 autocast of the oracle achieves."""
+    from eunet import synth
+    x, _ = synth.batch(2, 64, 64, start_index=25, num_classes=2, in_channels=1)
+    keep = _keep96()
+    with torch.no_grad():
+        ref = D.dual_forward(D.dual_formula_weights(96, 1, 2, dtype=torch.float64), x.double(), True, keep)[0]
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ac = D.dual_forward(D.dual_formula_weights(96, 1, 2, dtype=torch.float32), x, True, keep)[0].float()
+    m = _model(96, 1, 2, dtype="bf16", keep=keep).train()
+    with torch.no_grad():
+        out = m(x.to(DEV)).double().cpu()
+    ours, auto = _rel_l2(out, ref), _rel_l2(ac, ref)
+    agree = float((out.argmax(1) == ref.argmax(1)).double().mean())
+    print("dual base96 bf16 relL2 ours", ours, "autocast", auto, "argmax agreement", agree)
+    assert torch.isfinite(out).all()
+    assert ours < max(2.0 * auto, 0.02), (ours, auto)

@@ -65,6 +65,38 @@ def test_loss_matches_reference(golden_dir, fname):
     assert _rel(logits.grad.numpy(), g["grad"]) < 1e-4
 
 
+FOCAL_CFGS = [  # tests/golden/gen_golden.py LOSS_API_FOCAL
+    ([1.0, 8.0, 5.0], 5.0, None, [1.0, 20.0, 10.0]),
+    (None, 2.0, None, None),
+    (0.25, 2.0, 1, None),
+    ([1.0, 2.0], 3.0, None, [1.0, 4.0, 2.0]),
+    ([0.5, 1.0, 2.0], 1.5, 255, [2.0, 1.0, 3.0]),
+]
+
+
+def test_loss_api_restatements_match_reference(golden_dir):
+    """Generalised FocalLoss / dice_loss / tversky_loss restatements vs the reference modules."""
+    g = _load(golden_dir, "loss_api.npz")
+    x0 = torch.from_numpy(g["x"]).double()
+    t, t_ign = torch.from_numpy(g["t"]), torch.from_numpy(g["t_ign"])
+
+    def check(name, fn, tt):
+        x = x0.clone().requires_grad_(True)
+        v = fn(x, tt)
+        v.backward()
+        assert abs(v.item() - float(g[f"{name}_val"])) < 1e-5 * abs(float(g[f"{name}_val"])), name
+        assert _rel(x.grad.numpy(), g[f"{name}_grad"]) < 1e-4, name
+
+    for i, (a, gm, ii, cw) in enumerate(FOCAL_CFGS):
+        w = None if cw is None else torch.tensor(cw, dtype=torch.float64)
+        check(f"focal{i}", lambda x, tt: R.focal_loss(x, tt, a, gm, ii, w), t_ign if ii == 255 else t)
+    check("ce", lambda x, tt: torch.nn.functional.cross_entropy(x, tt, weight=torch.tensor(R.CE_WEIGHT).double()), t)
+    for nc in (2, 3):
+        check(f"dice_nc{nc}", lambda x, tt: R.dice_loss(x, tt, nc), t)
+        check(f"tversky_nc{nc}", lambda x, tt: R.tversky_loss(x, tt, nc), t)
+    check("tversky_a05", lambda x, tt: R.tversky_loss(x, tt, 3, 0.5), t)
+
+
 def test_train_step_matches_reference(golden_dir):
     g = _load(golden_dir, "step_c3k3.npz")
     S = R.formula_weights(64, 3, 3, dtype=torch.float32)
