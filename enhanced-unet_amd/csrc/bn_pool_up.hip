@@ -515,7 +515,7 @@ long long bwd_pix(long long P) {
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
-                                                           const float* gamma, const float* beta, float* part,
+                                                           const float* scale, const float* shift, float* part,
                                                            int tpix) {
   constexpr int E = Vec16<T>::N;
   __shared__ float red[2][NT][E];
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, 
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     s1[j] = 0.f; s2[j] = 0.f;
-    if (sl < slots) { mu[j] = mean[c + j]; is[j] = istd[c + j]; ga[j] = gamma[c + j]; be[j] = beta[c + j]; }
+    if (sl < slots) { mu[j] = mean[c + j]; is[j] = istd[c + j]; ga[j] = scale[c + j]; be[j] = shift[c + j]; }
   }
   const long long p0 = (long long)blockIdx.x * tpix;
   const long long p1 = min(P, p0 + tpix);
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_kernel(const T* g, int gct, 
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         const float xh = (yf[j] - mu[j]) * is[j];
-        const float gg = (fmaf(ga[j], xh, be[j]) > 0.f) ? gf[j] : 0.f;
+        const float gg = (fmaf(yf[j], ga[j], be[j]) > 0.f) ? gf[j] : 0.f;  // the forward's ReLU mask
         s1[j] += gg;
         s2[j] = fmaf(gg, xh, s2[j]);
       }
@@ -598,14 +598,16 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
   }
 }
 
-// gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [gamma xhat + beta > 0], folded per
-// channel into pre = y P + Q and gy = K1 g' + y K2 + K3.  A thread keeps one 16-byte channel
+// gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [y scale + shift > 0] (the forward's ReLU
+// mask: every BN-backward reduction and this apply use the forward affine, so the sums the apply
+// subtracts are over exactly the g' it applies), folded per channel into gy = K1 g' + y K2 + K3
+// with K1 = scale = gamma istd.  A thread keeps one 16-byte channel
 // unit with its coefficients in registers and strides over pixels; the block holds
 // floor(256 / U) pixels x U units (base_ch 96 -> U = 12, 21 pixels per step).
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
-                                                           const float* gamma, const float* beta, const float* dbeta,
+                                                           const float* scale, const float* shift, const float* dbeta,
                                                            const float* dgamma, TO* gy, int oct, int oco) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E;
@@ -614,10 +616,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   float kP[E], kQ[E], k1[E], k2[E], k3[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
-    const float is = istd[c + j], ga = gamma[c + j], off = -mean[c + j] * is;
-    kP[j] = ga * is;
-    kQ[j] = fmaf(ga, off, beta[c + j]);
-    k1[j] = ga * is;
+    const float is = istd[c + j], off = -mean[c + j] * is;
+    kP[j] = scale[c + j];
+    kQ[j] = shift[c + j];
+    k1[j] = scale[c + j];
     const float dg = dgamma[c + j] * inv_n;
     k2[j] = -k1[j] * is * dg;
     k3[j] = -k1[j] * fmaf(off, dg, dbeta[c + j] * inv_n);
@@ -639,11 +641,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
 // Fused BN-backward reduction in a gradient producer (the reduction half of bn_bwd_reduce for
 // the block whose output gradient g the kernel writes): each thread accumulates, for its 16-byte
 // channel unit, s1 += g', s2 += g' xhat over the pixels it writes (g' = stored g where
-// gamma xhat + beta > 0, xhat = (y - mean) istd); the block then sums its threads of equal unit
+// y scale + shift > 0, xhat = (y - mean) istd); the block then sums its threads of equal unit
 // in fixed order into part[block][2][C].  Requires NT % U == 0 (U = C / E channel units).
 struct BnRed {
   const void* y; int yct, yco;
-  const float* mean; const float* istd; const float* gamma; const float* beta;
+  const float* mean; const float* istd; const float* scale; const float* shift;  // scale / shift: the forward affine
   float* part;
 };
 
@@ -657,7 +659,7 @@ __device__ __forceinline__ void bnred_acc(const BnRed& r, long long pix, int c, 
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     const float xh = (yv[j] - r.mean[c + j]) * r.istd[c + j];
-    const float gp = fmaf(r.gamma[c + j], xh, r.beta[c + j]) > 0.f ? gr[j] : 0.f;
+    const float gp = fmaf(yv[j], r.scale[c + j], r.shift[c + j]) > 0.f ? gr[j] : 0.f;  // the forward's ReLU mask
     s1[j] += gp;
     s2[j] = fmaf(gp, xh, s2[j]);
   }
@@ -1243,8 +1245,8 @@ int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles) {
 }
 
 int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
-                        const float* gamma, const float* beta, float* part, void* stream) {
-  EUNET_REQUIRE(act_ok(g) && act_ok(y) && vec_ok(g) && vec_ok(y) && mean && invstd && gamma && beta && part,
+                        const float* scale, const float* shift, float* part, void* stream) {
+  EUNET_REQUIRE(act_ok(g) && act_ok(y) && vec_ok(g) && vec_ok(y) && mean && invstd && scale && shift && part,
                 "bn_bwd_reduce: bad args");
   EUNET_REQUIRE(g->dtype == y->dtype && g->c == y->c && g->n == y->n && g->h == y->h && g->w == y->w,
                 "bn_bwd_reduce: shape mismatch");
@@ -1255,11 +1257,11 @@ int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mea
   if (y->dtype == EUNET_BF16)
     bn_bwd_reduce_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, part, tpix);
+        scale, shift, part, tpix);
   else
     bn_bwd_reduce_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>(
         (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, part, tpix);
+        scale, shift, part, tpix);
   EUNET_LAUNCH_CHECK("bn_bwd_reduce");
   return EUNET_OK;
 }
@@ -1281,11 +1283,11 @@ int eunet_colsum_split(const float* part, int rows, int cols, int split, float* 
 }
 
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
-                       const float* gamma, const float* beta, const float* dbeta, const float* dgamma,
+                       const float* scale, const float* shift, const float* dbeta, const float* dgamma,
                        const eunet_act* gy, void* stream) {
   EUNET_REQUIRE(act_ok(g) && act_ok(y) && act_ok(gy) && vec_ok(g) && vec_ok(y) && vec_ok(gy),
                 "bn_bwd_apply: bad tensors");
-  EUNET_REQUIRE(mean && invstd && gamma && beta && dbeta && dgamma, "bn_bwd_apply: null stats");
+  EUNET_REQUIRE(mean && invstd && scale && shift && dbeta && dgamma, "bn_bwd_apply: null stats");
   EUNET_REQUIRE(g->dtype == y->dtype && gy->dtype == y->dtype && g->c == y->c && gy->c == y->c,
                 "bn_bwd_apply: mismatch");
   const long long P = (long long)y->n * y->h * y->w;
@@ -1297,11 +1299,11 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
   if (y->dtype == EUNET_BF16)
     bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff);
+        scale, shift, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff);
   else
     bn_bwd_apply_kernel<float, float><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        gamma, beta, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff);
+        scale, shift, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff);
   EUNET_LAUNCH_CHECK("bn_bwd_apply");
   return EUNET_OK;
 }
@@ -1387,16 +1389,16 @@ int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows) {
 
 int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
                            const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
-                           const float* gamma, const float* beta, float* part, void* stream) {
+                           const float* scale, const float* shift, float* part, void* stream) {
   EUNET_REQUIRE(act_ok(act) && act_ok(gpool) && act_ok(gout) && vec_ok(act) && vec_ok(gpool) && vec_ok(gout),
                 "pool_bwd_add_bnr: bad tensors");
   if (gskip) EUNET_REQUIRE(act_ok(gskip) && vec_ok(gskip) && gskip->c == act->c, "pool_bwd_add_bnr: gskip");
   EUNET_REQUIRE(gpool->h * 2 == act->h && gpool->w * 2 == act->w && gout->h == act->h && gout->w == act->w &&
                     gpool->c == act->c && gout->c == act->c,
                 "pool_bwd_add_bnr: shapes");
-  EUNET_REQUIRE(bnr_ok(gout, y) && mean && invstd && gamma && beta && part,
+  EUNET_REQUIRE(bnr_ok(gout, y) && mean && invstd && scale && shift && part,
                 "pool_bwd_add_bnr: y / BN args (and 256 %% channel units == 0)");
-  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, gamma, beta, part};
+  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, part};
   const unsigned gr = (unsigned)bnr_grid(pool_threads(gout), 2048);
 #define PBA(T)                                                                                                  \
   pool_bwd_add_kernel<T, true><<<gr, NT, 0, (hipStream_t)stream>>>(                                             \
@@ -1417,14 +1419,14 @@ int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows) {
 }
 
 int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eunet_act* y, const float* mean,
-                           const float* invstd, const float* gamma, const float* beta, float* part, void* stream) {
+                           const float* invstd, const float* scale, const float* shift, float* part, void* stream) {
   EUNET_REQUIRE(act_ok(ghi) && act_ok(glo) && vec_ok(ghi) && vec_ok(glo) && ghi->dtype == glo->dtype,
                 "upsample_bwd_bnr: bad tensors");
   EUNET_REQUIRE(ghi->h == 2 * glo->h && ghi->w == 2 * glo->w && ghi->c == glo->c && ghi->n == glo->n,
                 "upsample_bwd_bnr: shapes");
-  EUNET_REQUIRE(bnr_ok(glo, y) && mean && invstd && gamma && beta && part,
+  EUNET_REQUIRE(bnr_ok(glo, y) && mean && invstd && scale && shift && part,
                 "upsample_bwd_bnr: y / BN args (and 256 %% channel units == 0)");
-  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, gamma, beta, part};
+  const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, part};
   const unsigned gr = (unsigned)bnr_grid(up_threads(glo), 8192);
   if (ghi->dtype == EUNET_BF16)
     up_bwd2x2_kernel<bf16_t, bf16_t, true><<<gr, NT, 0, (hipStream_t)stream>>>(

@@ -55,10 +55,10 @@ struct FwdArgs {
   void* y; int yct, yco, cout;
   float* stats; int tx, ty, ntiles;
   // optional fused BN-backward reduction over the produced gradient (dgrad only):
-  // part[tile][2][cout] = (sum g', sum g' xhat), g' = g [gamma xhat + beta > 0],
-  // xhat = (by - mean) istd, g = the stored (rounded) output
+  // part[tile][2][cout] = (sum g', sum g' xhat), g' = g [by bsc + bsh > 0] (the forward's ReLU
+  // mask, bsc / bsh = its BN affine), xhat = (by - mean) istd, g = the stored (rounded) output
   const void* by; int byct, byco;
-  const float* bmean; const float* bistd; const float* bgam; const float* bbet;
+  const float* bmean; const float* bistd; const float* bsc; const float* bsh;
   float* bpart;
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
   int pro1;          // 1 (always, set by the launcher): the first K-chunk is staged in one round trip.
@@ -373,8 +373,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     const bool ok = co0 + tid < a.cout;
     bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
     bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
-    bprm[2 * BN + tid] = ok ? a.bgam[co0 + tid] : 0.f;
-    bprm[3 * BN + tid] = ok ? a.bbet[co0 + tid] : 0.f;
+    bprm[2 * BN + tid] = ok ? a.bsc[co0 + tid] : 0.f;
+    bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
   }
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           for (int e = 0; e < E; ++e) {
             const int cc = ucol * E + e;
             const float xh = (yv[e] - bprm[cc]) * bprm[BN + cc];
-            const float gp = fmaf(bprm[2 * BN + cc], xh, bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
+            const float gp = fmaf(yv[e], bprm[2 * BN + cc], bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
             bs1[e] += gp;
             bs2[e] = fmaf(gp, xh, bs2[e]);
           }
@@ -898,7 +898,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
-  a.bmean = a.bistd = a.bgam = a.bbet = nullptr; a.bpart = nullptr; a.gsc = nullptr;
+  a.bmean = a.bistd = a.bsc = a.bsh = nullptr; a.bpart = nullptr; a.gsc = nullptr;
   a.pro1 = 1;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
@@ -906,9 +906,9 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
 }
 
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const eunet_act* y,
-                              const float* mean, const float* invstd, const float* gamma, const float* beta,
+                              const float* mean, const float* invstd, const float* scale, const float* shift,
                               const float* gscale, float* part, void* stream) {
-  EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && act_ok(y) && wp_t && mean && invstd && gamma && beta && part,
+  EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && act_ok(y) && wp_t && mean && invstd && scale && shift && part,
                 "conv3x3_dgrad_bnbwd: bad args");
   EUNET_REQUIRE(dy->dtype == gx->dtype && y->dtype == gx->dtype, "conv3x3_dgrad_bnbwd: dtype mismatch");
   EUNET_REQUIRE(dy->n == gx->n && dy->h == gx->h && dy->w == gx->w && y->n == gx->n && y->h == gx->h &&
@@ -926,7 +926,7 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.y = gx->ptr; a.yct = gx->ctot; a.yco = gx->coff; a.cout = gx->c;
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
-  a.bmean = mean; a.bistd = invstd; a.bgam = gamma; a.bbet = beta; a.bpart = part; a.gsc = gscale;
+  a.bmean = mean; a.bistd = invstd; a.bsc = scale; a.bsh = shift; a.bpart = part; a.gsc = gscale;
   a.pro1 = 1;
   return launch_fwd(a, dy->dtype, stream);
 }

@@ -126,13 +126,13 @@ class DualEngine:
         if part is None:
             tiles = ops.bn_bwd_tiles(ops.act(y))
             part = _e(tiles * 2 * C, torch.float32, dev)
-            ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                              P[prefix + ".bias"], part)
+            ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                              bn["shift"], part)
         dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
         ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
         gy = torch.empty_like(y)
-        ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                         P[prefix + ".bias"], dbeta, dgamma, ops.act(gy))
+        ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                         bn["shift"], dbeta, dgamma, ops.act(gy))
         return gy
 
     def _wgrad(self, name, xa: ops.Act, gy, sink, d=None):
@@ -192,8 +192,8 @@ class DualEngine:
         ct = ops.conv3x3_tiles(ops.act(gg2))
         cpart = _e(ct * 2 * HEAD_CH[1], torch.float32, dev)
         ops.conv3x3_dgrad_bnbwd(ops.act(gy3), ops.conv3x3_pack(P["fusion_head.8.weight"], dt, flip=True),
-                                ops.act(gg2), ops.act(y2), h2["mean"], h2["invstd"], P["fusion_head.5.weight"],
-                                P["fusion_head.5.bias"], cpart, gscale=d2["gscale"])
+                                ops.act(gg2), ops.act(y2), h2["mean"], h2["invstd"], h2["scale"],
+                                h2["shift"], cpart, gscale=d2["gscale"])
         del gy3
         sink.ready(["fusion_head.9.weight", "fusion_head.9.bias", "fusion_head.8.weight"])
         # ---- conv 256->128 (fusion_head.4/.5)
@@ -204,8 +204,8 @@ class DualEngine:
         ct = ops.conv3x3_tiles(ops.act(gg1))
         cpart = _e(ct * 2 * HEAD_CH[0], torch.float32, dev)
         ops.conv3x3_dgrad_bnbwd(ops.act(gy2), ops.conv3x3_pack(P["fusion_head.4.weight"], dt, flip=True),
-                                ops.act(gg1), ops.act(y1), h1["mean"], h1["invstd"], P["fusion_head.1.weight"],
-                                P["fusion_head.1.bias"], cpart, gscale=d1["gscale"])
+                                ops.act(gg1), ops.act(y1), h1["mean"], h1["invstd"], h1["scale"],
+                                h1["shift"], cpart, gscale=d1["gscale"])
         del gy2
         sink.ready(["fusion_head.5.weight", "fusion_head.5.bias", "fusion_head.4.weight"])
         # ---- conv 2K->256 (fusion_head.0/.1)

@@ -219,13 +219,13 @@ class UNetEngine:
             if part is None:  # reduction not fused into the producer of g
                 tiles = ops.bn_bwd_tiles(ops.act(y))
                 part = _e(tiles * 2 * C, torch.float32, dev)
-                ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                                  P[prefix + ".bias"], part)
+                ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                                  bn["shift"], part)
             dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
             ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
             gy = torch.empty_like(y)
-            ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], P[prefix + ".weight"],
-                             P[prefix + ".bias"], dbeta, dgamma, ops.act(gy))
+            ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                             bn["shift"], dbeta, dgamma, ops.act(gy))
             return gy
 
         def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False):
@@ -255,7 +255,7 @@ class UNetEngine:
         ctiles = ops.conv3x3_tiles(ops.act(gaa))
         cpart = _e(ctiles * 2 * C, torch.float32, dev)
         ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
-                                P[p + ".1.weight"], P[p + ".1.bias"], cpart)
+                                bna["scale"], bna["shift"], cpart)
         del gyb
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
         del gaa
@@ -303,8 +303,7 @@ class UNetEngine:
 
         def bnr_args(nm):
             s = S[nm]
-            return (ops.act(s["yb"]), s["bnb"]["mean"], s["bnb"]["invstd"], P[f"{pre}{nm}.4.weight"],
-                    P[f"{pre}{nm}.4.bias"])
+            return (ops.act(s["yb"]), s["bnb"]["mean"], s["bnb"]["invstd"], s["bnb"]["scale"], s["bnb"]["shift"])
 
         def up_bwd(ghi: ops.Act, glo: torch.Tensor, nm):
             """g w.r.t. block nm's output from the upsample adjoint, its BN-b reduction fused."""

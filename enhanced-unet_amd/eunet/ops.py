@@ -80,14 +80,14 @@ def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=Non
              ctypes.byref(y), _ptr(stats), _stream())
 
 
-def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, gamma, beta, part, gscale=None):
+def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, scale, shift, part, gscale=None):
     """dgrad + the BN-backward partial sums of the layer it feeds (see eunet.h)."""
     flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
     esz = 2 if dy.dtype == _lib.EUNET_BF16 else 4
     nbytes = float(esz * dy.n * dy.h * dy.w * (dy.c + 2 * gx.c) + wp_t.numel() * wp_t.element_size())
     with kprof.timed("conv3x3_fwd", flops, nbytes):
         call("eunet_conv3x3_dgrad_bnbwd", ctypes.byref(dy), _ptr(wp_t), ctypes.byref(gx), ctypes.byref(y), _ptr(mean),
-             _ptr(invstd), _ptr(gamma), _ptr(beta), _ptr(gscale), _ptr(part), _stream())
+             _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(gscale), _ptr(part), _stream())
 
 
 def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
@@ -211,9 +211,9 @@ def bn_bwd_tiles(y: Act) -> int:
     return t.value
 
 
-def bn_bwd_reduce(g: Act, y: Act, mean, invstd, gamma, beta, part):
-    call("eunet_bn_bwd_reduce", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma),
-         _ptr(beta), _ptr(part), _stream())
+def bn_bwd_reduce(g: Act, y: Act, mean, invstd, scale, shift, part):
+    call("eunet_bn_bwd_reduce", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale),
+         _ptr(shift), _ptr(part), _stream())
 
 
 def colsum(part, rows, cols, out, split=None, out_hi=None):
@@ -227,9 +227,10 @@ def colsum(part, rows, cols, out, split=None, out_hi=None):
         call("eunet_colsum_split", _ptr(part), rows, cols, int(split), _ptr(out), _ptr(out_hi), _ptr(ws), _stream())
 
 
-def bn_bwd_apply(g: Act, y: Act, mean, invstd, gamma, beta, dbeta, dgamma, gy: Act):
-    call("eunet_bn_bwd_apply", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma),
-         _ptr(beta), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
+def bn_bwd_apply(g: Act, y: Act, mean, invstd, scale, shift, dbeta, dgamma, gy: Act):
+    """scale / shift: the BN's forward affine (they define the ReLU mask, see eunet.h)."""
+    call("eunet_bn_bwd_apply", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale),
+         _ptr(shift), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
 
 
 def pool_bwd_add(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act):
@@ -247,11 +248,11 @@ def pool_bwd_add_bnr_rows(gout: Act) -> int:
     return r.value
 
 
-def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act, y: Act, mean, invstd, gamma, beta,
+def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act, y: Act, mean, invstd, scale, shift,
                      part):
     """pool_bwd_add + the BN-backward partial sums of the block whose output gradient gout is."""
     call("eunet_pool_bwd_add_bnr", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), ctypes.byref(gout),
-         ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(gamma), _ptr(beta), _ptr(part), _stream())
+         ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(part), _stream())
 
 
 def upsample_bwd_bnr_rows(glo: Act) -> int:
@@ -260,10 +261,10 @@ def upsample_bwd_bnr_rows(glo: Act) -> int:
     return r.value
 
 
-def upsample_bwd_bnr(ghi: Act, glo: Act, y: Act, mean, invstd, gamma, beta, part):
+def upsample_bwd_bnr(ghi: Act, glo: Act, y: Act, mean, invstd, scale, shift, part):
     """upsample_bwd + the BN-backward partial sums of the block whose output gradient glo is."""
     call("eunet_upsample_bwd_bnr", ctypes.byref(ghi), ctypes.byref(glo), ctypes.byref(y), _ptr(mean), _ptr(invstd),
-         _ptr(gamma), _ptr(beta), _ptr(part), _stream())
+         _ptr(scale), _ptr(shift), _ptr(part), _stream())
 
 
 def conv1x1_bwd_tiles(y: Act) -> int:

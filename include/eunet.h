@@ -71,14 +71,16 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
 /* dgrad (wp_t packed with transpose_flip) fused with the reduction half of the
  * BatchNorm backward of the layer whose output gradient it produces (autograd of
  * models.py:220-221, BN+ReLU after the conv): y = that layer's pre-BN output,
- * part [tiles][2][gx.c] = per-tile (sum g', sum g' xhat), g' = gx [gamma xhat +
- * beta > 0], xhat = (y - mean) invstd, gx as stored (rounded).  Replaces
- * conv3x3_fwd(dgrad) + bn_bwd_reduce; colsum(part, tiles, 2C) -> (dbeta, dgamma).
+ * part [tiles][2][gx.c] = per-tile (sum g', sum g' xhat), g' = gx [y scale + shift > 0],
+ * xhat = (y - mean) invstd, gx as stored (rounded); scale / shift = the BN's forward
+ * affine (eunet_bn_finalize), so the ReLU mask is bit-identical to the forward's and to
+ * every other BN-backward kernel's.  Replaces conv3x3_fwd(dgrad) + bn_bwd_reduce;
+ * colsum(part, tiles, 2C) -> (dbeta, dgamma).
  * gscale (nullable) [N][gx.c]: gx is scaled per sample and channel before the store
  * and the reduction (the backward of a Dropout2d between the BN+ReLU and this conv). */
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx,
                               const eunet_act* y, const float* mean, const float* invstd,
-                              const float* gamma, const float* beta, const float* gscale,
+                              const float* scale, const float* shift, const float* gscale,
                               float* part, void* stream);
 /* wgrad (split over pixel tiles): dw_part [nsplit][cout][9][cin] and
  * db_part [nsplit][cout] (db only when db_part != NULL) */
@@ -192,11 +194,16 @@ int eunet_loss_bwd(const float* logits, const int64_t* target, int n, int k, int
 
 /* ---- backward helpers ----------------------------------------------------
  * BN(+ReLU) backward (autograd of models.py:220-224): g is the gradient w.r.t.
- * the ReLU output, y the pre-BN conv output.  reduce -> part [tiles][2][c]
- * (sum g', sum g'*xhat); colsum -> (dbeta, dgamma); apply -> gy. */
+ * the ReLU output, y the pre-BN conv output, mean / invstd the batch statistics and
+ * scale / shift the forward affine (scale = gamma invstd, shift = beta - mean scale, as
+ * eunet_bn_finalize emits them).  The ReLU mask g' = g [y scale + shift > 0] is the
+ * forward's, bit for bit, in every BN-backward kernel (reduce, apply, and the fused
+ * reductions below), so the apply subtracts sums over exactly the g' it applies.
+ * reduce -> part [tiles][2][c] (sum g', sum g'*xhat); colsum -> (dbeta, dgamma);
+ * apply -> gy = scale (g' - dbeta/n - xhat dgamma/n). */
 int eunet_bn_bwd_tiles(const eunet_act* y, int* tiles);
 int eunet_bn_bwd_reduce(const eunet_act* g, const eunet_act* y, const float* mean,
-                        const float* invstd, const float* gamma, const float* beta, float* part,
+                        const float* invstd, const float* scale, const float* shift, float* part,
                         void* stream);
 /* deterministic column sum of a [rows][cols] fp32 partial matrix (fp64 two-stage) */
 int eunet_colsum_ws_bytes(int rows, int cols, size_t* bytes);
@@ -206,7 +213,7 @@ int eunet_colsum(const float* part, int rows, int cols, float* out, void* ws, vo
 int eunet_colsum_split(const float* part, int rows, int cols, int split, float* out_lo,
                        float* out_hi, void* ws, void* stream);
 int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean,
-                       const float* invstd, const float* gamma, const float* beta,
+                       const float* invstd, const float* scale, const float* shift,
                        const float* dbeta, const float* dgamma, const eunet_act* gy,
                        void* stream);
 /* MaxPool2d backward (first max in row-major order wins, recomputed from the
@@ -222,10 +229,10 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
 int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows);
 int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
                            const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
-                           const float* gamma, const float* beta, float* part, void* stream);
+                           const float* scale, const float* shift, float* part, void* stream);
 int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows);
 int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eunet_act* y, const float* mean,
-                           const float* invstd, const float* gamma, const float* beta, float* part, void* stream);
+                           const float* invstd, const float* scale, const float* shift, float* part, void* stream);
 /* dec1 1x1 backward: gact = W^T gz (w.r.t. relu(bn(y))), part [tiles][K*C + K]
  * = per-tile (gW, gb) partials */
 int eunet_conv1x1_bwd_tiles(const eunet_act* y, int* tiles);

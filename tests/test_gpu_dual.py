@@ -18,6 +18,7 @@ from oracle import dual_ref as D
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+BRANCHES = ("unetpp.", "deeplab.")
 
 
 def _load(golden_dir, name):
@@ -205,12 +206,14 @@ def test_dual_base96_forward_fp32_vs_oracle():
         out = m(x.to(DEV))
     aux = m.get_aux_outputs()
 
-    def px(a, b):
+    def px(a, b, floor=1e-2):  # per-pixel gate of test_gpu_model (floor 1e-2 of the max; see there)
         a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
-        return float(((a - b).abs() / b.abs().clamp_min(1e-3 * float(b.abs().max()))).max())
+        return float(((a - b).abs() / b.abs().clamp_min(floor * float(b.abs().max()))).max())
 
-    errs = (px(out, ref), px(aux["unetpp"], ref_aux["unetpp"]), px(aux["deeplab"], ref_aux["deeplab"]))
-    print("dual base96 fp32 per-pixel rel (fused, unetpp, deeplab):", errs)
+    pairs = ((out, ref), (aux["unetpp"], ref_aux["unetpp"]), (aux["deeplab"], ref_aux["deeplab"]))
+    errs = tuple(px(a, b) for a, b in pairs)
+    print("dual base96 fp32 per-pixel vs fp64 (fused, unetpp, deeplab), floor 1e-2:", errs, "floor 1e-3:",
+          tuple(px(a, b, 1e-3) for a, b in pairs), "max-normalised:", tuple(_rel(a, b) for a, b in pairs))
     assert max(errs) < 1e-3, errs
     sd = m.state_dict()
     for k, v in S.items():
@@ -235,8 +238,14 @@ def test_dual_base96_train_grads_fp32_vs_oracle():
     loss.backward()
     assert abs(loss.item() - loss_ref.item()) < 1e-4 * abs(loss_ref.item())
     rows = []
+    scale = max(float(S[k].grad.abs().max()) for k in S if S[k].grad is not None)
     for k, p in m.named_parameters():
         ref = S[k].grad
+        if k.startswith(BRANCHES) and k.endswith((".0.bias", ".3.bias")):
+            # conv bias followed by BatchNorm: the true gradient is exactly 0; compare against the
+            # global gradient scale (test_gpu_model._pre_bn_bias)
+            assert float((p.grad.double().cpu() - ref).abs().max()) < 1e-4 * scale, k
+            continue
         tol = max(1e-3, 3 * _rel_l2(S32[k].grad, ref), 1.5 * _rel_l2(Sp[k].grad, ref))
         rows.append((_rel_l2(p.grad, ref) / tol, k, _rel_l2(p.grad, ref), tol))
     for r in sorted(rows, reverse=True)[:6]:

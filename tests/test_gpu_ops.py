@@ -210,11 +210,12 @@ def test_backward_helpers(dt):
     f = lambda t: t.float().to(DEV)
     tiles = ops.bn_bwd_tiles(ops.act(yd))
     part = torch.empty(tiles * 2 * C, device=DEV)
-    ops.bn_bwd_reduce(ops.act(gd), ops.act(yd), f(mean), f(inv), f(gamma), f(beta), part)
+    sc, sh = f(gamma * inv), f(beta - mean * gamma * inv)  # the forward affine (defines the ReLU mask)
+    ops.bn_bwd_reduce(ops.act(gd), ops.act(yd), f(mean), f(inv), sc, sh, part)
     red = torch.empty(2 * C, device=DEV)
     ops.colsum(part, tiles, 2 * C, red)
     gy = torch.empty_like(yd)
-    ops.bn_bwd_apply(ops.act(gd), ops.act(yd), f(mean), f(inv), f(gamma), f(beta), red[:C], red[C:], ops.act(gy))
+    ops.bn_bwd_apply(ops.act(gd), ops.act(yd), f(mean), f(inv), sc, sh, red[:C], red[C:], ops.act(gy))
     torch.cuda.synchronize()
     assert rel(red[:C], bt.grad) < 1e-4
     assert rel(red[C:], gt.grad) < 1e-4
@@ -298,7 +299,7 @@ def test_conv1x1_bwd_fused_bn_reduce(dt, C, K):
     ops.colsum(bp, tiles, 2 * C, red)
     bt = ops.bn_bwd_tiles(ops.act(yd))
     bp2 = torch.empty(bt * 2 * C, device=DEV)
-    ops.bn_bwd_reduce(ops.act(ga1), ops.act(yd), mean, istd, gamma, beta, bp2)
+    ops.bn_bwd_reduce(ops.act(ga1), ops.act(yd), mean, istd, sc, sh, bp2)
     red2 = torch.empty(2 * C, device=DEV)
     ops.colsum(bp2, bt, 2 * C, red2)
     torch.cuda.synchronize()
@@ -415,7 +416,8 @@ def test_conv3x3_dgrad_bnbwd_fused(dt):
     gx = torch.empty_like(gx_ref)
     tiles = ops.conv3x3_tiles(ops.act(gx))
     part = torch.empty(tiles * 2 * Cout, device=DEV)
-    ops.conv3x3_dgrad_bnbwd(ops.act(gy), wpt, ops.act(gx), ops.act(ybuf, YO, Cout), mean, istd, gamma, beta, part)
+    sc, sh = gamma * istd, beta - mean * gamma * istd  # the forward affine (defines the ReLU mask)
+    ops.conv3x3_dgrad_bnbwd(ops.act(gy), wpt, ops.act(gx), ops.act(ybuf, YO, Cout), mean, istd, sc, sh, part)
     red = torch.empty(2 * Cout, device=DEV)
     ops.colsum(part, tiles, 2 * Cout, red)
     torch.cuda.synchronize()
@@ -524,8 +526,8 @@ def test_conv3x3_k64_persistent():
     wpt = ops.conv3x3_pack(w2.float().to(DEV), dt, flip=True)
     gx = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     part = torch.empty(tiles * 2 * Cout, device=DEV)
-    ops.conv3x3_dgrad_bnbwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx), ops.act(yb), bm, bi, bgam, bbet, part,
-                            gscale=gs.float().to(DEV))
+    ops.conv3x3_dgrad_bnbwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx), ops.act(yb), bm, bi, bgam * bi,
+                            bbet - bm * bgam * bi, part, gscale=gs.float().to(DEV))
     red = torch.empty(2 * Cout, device=DEV)
     ops.colsum(part, tiles, 2 * Cout, red)
     torch.cuda.synchronize()
@@ -601,6 +603,7 @@ def test_fused_bn_reduce_in_gradient_producers(dt, kind):
     istd = (torch.rand(C, generator=g) + 0.5).to(DEV)
     gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
     beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
+    sc, sh = gamma * istd, beta - mean * gamma * istd  # the forward affine (defines the ReLU mask)
     if kind == "pool":
         act = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
         gp = torch.randn(N, h // 2, w // 2, C, generator=g).to(DEV, dt)
@@ -608,20 +611,20 @@ def test_fused_bn_reduce_in_gradient_producers(dt, kind):
         ops.pool_bwd_add(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gref))
         rows = ops.pool_bwd_add_bnr_rows(ops.act(gout))
         part = torch.empty(rows * 2 * C, device=DEV)
-        ops.pool_bwd_add_bnr(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gout), ops.act(y), mean, istd, gamma,
-                             beta, part)
+        ops.pool_bwd_add_bnr(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gout), ops.act(y), mean, istd, sc,
+                             sh, part)
     else:
         gh = torch.randn(N, 2 * h, 2 * w, C, generator=g).to(DEV, dt)
         ops.upsample_bwd(ops.act(gh), ops.act(gref))
         rows = ops.upsample_bwd_bnr_rows(ops.act(gout))
         part = torch.empty(rows * 2 * C, device=DEV)
-        ops.upsample_bwd_bnr(ops.act(gh), ops.act(gout), ops.act(y), mean, istd, gamma, beta, part)
+        ops.upsample_bwd_bnr(ops.act(gh), ops.act(gout), ops.act(y), mean, istd, sc, sh, part)
     assert rows > 0
     red = torch.empty(2 * C, device=DEV)
     ops.colsum(part, rows, 2 * C, red)
     tiles = ops.bn_bwd_tiles(ops.act(y))
     p2 = torch.empty(tiles * 2 * C, device=DEV)
-    ops.bn_bwd_reduce(ops.act(gref), ops.act(y), mean, istd, gamma, beta, p2)
+    ops.bn_bwd_reduce(ops.act(gref), ops.act(y), mean, istd, sc, sh, p2)
     red2 = torch.empty(2 * C, device=DEV)
     ops.colsum(p2, tiles, 2 * C, red2)
     torch.cuda.synchronize()
