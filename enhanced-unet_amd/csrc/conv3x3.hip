@@ -376,8 +376,29 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     bprm[2 * BN + tid] = ok ? a.bsc[co0 + tid] : 0.f;
     bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
   }
+  constexpr int SJ = PASS_PX * UPX / NTH;      // output units per thread per pass
+  constexpr bool PRE = sizeof(T) == 2;         // bf16: prefetch the pass's y (BN-backward input)
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
+    // the fused BN-backward reduction reads y at every output unit: issue those loads before the
+    // staging barrier so their latency overlaps it (the stores below would otherwise serialise
+    // each load behind the previous unit's store)
+    uint4 ryb[PRE ? SJ : 1];
+    if constexpr (PRE) {
+      if (bnb) {
+#pragma unroll
+        for (int j = 0; j < SJ; ++j) {
+          const int id = tid + j * NTH;
+          const int px = id / UPX, u = id - px * UPX;
+          const int r = pass * PROWS + px / FTW, c = px % FTW;
+          const int co = co0 + u * E;
+          ryb[j] = make_uint4(0, 0, 0, 0);
+          if (r < vh && c < vw && co < a.cout)
+            ryb[j] = *(const uint4*)((const T*)a.by + ((long long)(n * a.H + y0 + r) * a.W + x0 + c) * a.byct +
+                                     a.byco + co);
+        }
+      }
+    }
     if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -390,7 +411,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PASS_PX * UPX / NTH; ++j) {
+    for (int j = 0; j < SJ; ++j) {
       const int id = tid + j * NTH;
       const int px = id / UPX, u = id - px * UPX;
       const int r = pass * PROWS + px / FTW, c = px % FTW;
@@ -406,7 +427,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         if (bnb) {
           float gr[E], yv[E];
           Vec16<T>::unpack(packed, gr);
-          Vec16<T>::unpack(*(const uint4*)((const T*)a.by + pix * a.byct + a.byco + co), yv);
+          if constexpr (PRE) Vec16<T>::unpack(ryb[j], yv);
+          else Vec16<T>::unpack(*(const uint4*)((const T*)a.by + pix * a.byct + a.byco + co), yv);
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             const int cc = ucol * E + e;

@@ -498,9 +498,10 @@ __global__ __launch_bounds__(NT) void head_bwd_gh_kernel(HeadArgs a) {
   }
 }
 
-// g_u[q][k] = g_o[q][k] + sum_t v[q - d_t][k*9+t]   (d_t = (ky-1, kx-1))
-template <int K>
+// g_u[q][k] = g_o[q][k] + sum_t v[q - d_t][k*9+t]   (d_t = (ky-1, kx-1)); v fp32 or bf16
+template <int K, typename TV>
 __global__ void head_bwd_gu_kernel(HeadArgs a) {
+  const TV* vp = (const TV*)a.v;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= (long long)a.N * H2 * W2) return;
@@ -517,7 +518,7 @@ __global__ void head_bwd_gu_kernel(HeadArgs a) {
     if (py < 0 || py >= H2 || px < 0 || px >= W2) continue;
     const long long P2 = (long long)a.N * H2 * W2, pix = ((long long)n * H2 + py) * W2 + px;
 #pragma unroll
-    for (int k = 0; k < K; ++k) acc[k] += a.v[(long long)(k * 9 + t) * P2 + pix];
+    for (int k = 0; k < K; ++k) acc[k] += Elem<TV>::ld(vp + (long long)(k * 9 + t) * P2 + pix);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) a.gu[id * K + k] = acc[k];
@@ -886,6 +887,21 @@ __device__ __forceinline__ void bwd_params(const HeadArgs& a, int c, float& is, 
   Q = fmaf(a.gamma[c], off, a.beta[c]);
 }
 
+// g_o (the loss gradient w.r.t. the 2H output) over a tile's 16x16 pixels, K x 256 values,
+// <= 3 per thread, held in registers one tile ahead and staged in LDS per tile: the per-row
+// MFMA -> VALU chains of head_bwd1 / head_gh no longer wait on global loads.
+template <int K>
+__device__ __forceinline__ void goload(const HeadArgs& a, int tile, float (&gv)[3]) {
+  if (tile >= a.ntiles) return;
+  int n, oy0, ox0;
+  tile_coords(a, tile, n, oy0, ox0);
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int p = threadIdx.x, oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+    gv[j] = (oy < 2 * a.h && ox < 2 * a.w) ? g_out(a, K, n, j, oy, ox) : 0.f;
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = (K + 2) * MID + K;
@@ -893,6 +909,7 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID];
   __shared__ float red[STRIDE];
+  __shared__ float gos[K * T2 * T2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   if (tid < MID) bwd_params(a, tid, pis[tid], poff[tid], pP[tid], pQ[tid]);
   for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
@@ -920,13 +937,17 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   for (int k = 0; k < K; ++k) ab2[k] = 0.f;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  float zv[2] = {0.f, 0.f};
+  float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
   zload(a, blockIdx.x, zv);
+  goload<K>(a, blockIdx.x, gv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    stage_u(a, su, zs, zv, tile, oy0, ox0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
+    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
+    goload<K>(a, tile + gridDim.x, gv);
     __syncthreads();
 #pragma unroll 1
     for (int rr = 0; rr < 4; ++rr) {
@@ -942,7 +963,7 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
       }
       float go[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
+      for (int k = 0; k < K; ++k) go[k] = gos[k * T2 * T2 + r * T2 + x];  // 0 outside the image
       const bf16x8 gb = go_frag<K>(q, go);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
@@ -1015,8 +1036,10 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
   __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
   __shared__ float red[STRIDE];
+  __shared__ float gos[K * T2 * T2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
+  bf16_t* vb = (bf16_t*)a.v;
   if (tid < MID) {
     float is, of, P, Q;
     bwd_params(a, tid, is, of, P, Q);
@@ -1071,13 +1094,17 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
-  float zv[2] = {0.f, 0.f};
+  float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
   zload(a, blockIdx.x, zv);
+  goload<K>(a, blockIdx.x, gv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    stage_u(a, su, zs, zv, tile, oy0, ox0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
+    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
+    goload<K>(a, tile + gridDim.x, gv);
     __syncthreads();
 #pragma unroll 1
     for (int rp = 0; rp < 2; ++rp) {
@@ -1095,7 +1122,7 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
         }
         float go[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) go[k] = pv ? g_out(a, K, n, k, oy, ox) : 0.f;
+        for (int k = 0; k < K; ++k) go[k] = gos[k * T2 * T2 + r * T2 + x];  // 0 outside the image
         const bf16x8 gb = go_frag<K>(q, go);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
@@ -1117,12 +1144,12 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
         v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
         f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
         v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
-        if (pv) {  // planar v[j][pixel]: for each j the 16 lanes of a row write 64 contiguous bytes
+        if (pv) {  // planar bf16 v[j][pixel]: for each j the 16 lanes of a row write 32 contiguous bytes
           const long long P2 = (long long)a.N * H2 * W2, pix = ((long long)n * H2 + oy) * W2 + ox;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            if (4 * q + i < KJ) a.v[(long long)(4 * q + i) * P2 + pix] = v0[i];
-            if (16 + 4 * q + i < KJ) a.v[(long long)(16 + 4 * q + i) * P2 + pix] = v1[i];
+            if (4 * q + i < KJ) vb[(long long)(4 * q + i) * P2 + pix] = f2bf(v0[i]);
+            if (16 + 4 * q + i < KJ) vb[(long long)(16 + 4 * q + i) * P2 + pix] = f2bf(v1[i]);
           }
         }
         // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
@@ -1199,7 +1226,9 @@ WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   L.part1 = take((size_t)grid * ((K + 2) * MID + K));
   L.partw = take((size_t)grid * (MID * K * 9 + MID));
   L.gh = take(dtype == EUNET_F32 ? P2 * MID : 0);  // the bf16 path never stores g_h
-  L.v = take(P2 * ((K * 9 + 3) & ~3));
+  // per-tap products v[j][pixel]: fp32 (fp32 path) / bf16 (bf16 path, the dgrad operand precision
+  // of the reference's autocast)
+  L.v = take(dtype == EUNET_F32 ? P2 * ((K * 9 + 3) & ~3) : (P2 * ((K * 9 + 3) & ~3) + 1) / 2);
   L.gu = take(P2 * K);
   L.scale = take(MID);
   L.shift = take(MID);
@@ -1304,24 +1333,25 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   if ((rc = eunet_colsum_ld(a.part + (k + 2) * MID, L.grid, k, ld1, gb2, cws, s))) return rc;
   a.dbeta = gbeta; a.dgamma = ggamma;
   const long long P2 = (long long)n * 4 * h * w;
+  const int gridw = L.grid;
   if (mf) {
-    a.part = wsf + L.partw;  // g_h, v and the W1/b1 partials in one pass
+    a.part = wsf + L.partw;  // g_h, v (bf16) and the W1/b1 partials in one pass
     HEAD_DISPATCH(head_gh_mfma_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_gh_mfma");
-    HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
+    HEAD_DISPATCH_T(head_bwd_gu_kernel, bf16_t, (unsigned)((P2 + 255) / 256), 256, 0, s);
     EUNET_LAUNCH_CHECK("head_bwd_gu");
   } else {
     HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_bwd_gh");
-    HEAD_DISPATCH(head_bwd_gu_kernel, (unsigned)((P2 + 255) / 256), 256, 0, s);
+    HEAD_DISPATCH_T(head_bwd_gu_kernel, float, (unsigned)((P2 + 255) / 256), 256, 0, s);
     EUNET_LAUNCH_CHECK("head_bwd_gu");
     a.part = wsf + L.partw;
     HEAD_DISPATCH_T(head_wgrad_kernel, float, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_wgrad");
   }
   const int ldw = MID * k * 9 + MID;
-  if ((rc = eunet_colsum_ld(a.part, L.grid, MID * k * 9, ldw, gw1, cws, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + MID * k * 9, L.grid, MID, ldw, gb1, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part, gridw, MID * k * 9, ldw, gw1, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part + MID * k * 9, gridw, MID, ldw, gb1, cws, s))) return rc;
   eunet_act ghi = {a.gu, n, 2 * h, 2 * w, k, k, 0, EUNET_F32};
   eunet_act glo = {gz, n, h, w, k, k, 0, EUNET_F32};
   return eunet_upsample_bwd(&ghi, &glo, stream);

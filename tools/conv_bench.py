@@ -44,7 +44,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--only", default="")
-    ap.add_argument("--no-transform", action="store_true", help="forward without the BN+ReLU operand transform")
+    ap.add_argument("--transform", action="store_true",
+                    help="forward / wgrad with the BN+ReLU operand transform (the bench path materialises it)")
     ap.add_argument("--no-stats", action="store_true", help="forward without BN partials")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
@@ -69,16 +70,20 @@ def main():
         st = torch.empty(tiles * (2 * cout + 1), device=dev)
         flops = 2.0 * 9 * cin * cout * a.batch * H * H
         xa, ya, gya, gxa = ops.act(x), ops.act(y), ops.act(gy), ops.act(gx)
-        tsc, tsh = (None, None) if a.no_transform else (sc, sh)
+        tsc, tsh = (sc, sh) if a.transform else (None, None)
         tst = None if a.no_stats else st
         t_f = timeit(lambda: ops.conv3x3_fwd(xa, wp, ya, bias=bias, scale=tsc, shift=tsh, stats=tst), a.reps)
-        t_d = timeit(lambda: ops.conv3x3_fwd(gya, wpt, gxa), a.reps)
+        # dgrad as the engine runs it: fused with the BN-backward reduction of the layer it feeds
+        yb = torch.randn(a.batch, H, H, cin, device=dev).to(dt)
+        one, zero = torch.ones(cin, device=dev), torch.zeros(cin, device=dev)
+        cpart = torch.empty(ops.conv3x3_tiles(gxa) * 2 * cin, device=dev)
+        t_d = timeit(lambda: ops.conv3x3_dgrad_bnbwd(gya, wpt, gxa, ops.act(yb), zero, one, one, zero, cpart), a.reps)
         ns = ops.conv3x3_wgrad_splits(gya, cin, dt)
         dwp = torch.empty(ns * cout * 9 * cin, device=dev)
         dbp = torch.empty(ns * cout, device=dev)
         dw = torch.empty(cout, cin, 3, 3, device=dev)
         db = torch.empty(cout, device=dev)
-        t_w = timeit(lambda: ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=sc, shift=sh), a.reps)
+        t_w = timeit(lambda: ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=tsc, shift=tsh), a.reps)
         t_r = timeit(lambda: ops.wgrad_reduce(dwp, dbp, ns, cout, cin, 9, dw, db), a.reps)
         for k, t in (("fwd", t_f), ("dgrad", t_d), ("wgrad", t_w)):
             tot[k] += t
