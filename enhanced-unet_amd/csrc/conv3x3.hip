@@ -39,10 +39,7 @@ constexpr int HPX = HH_ * HW_;            // 340 halo pixels
 constexpr int HPXP = 352;                 // padded plane (multiple of 16)
 constexpr int BN = 64;                    // output channels per block
 constexpr int NTHR = 256;
-constexpr int A_UNITS = 4 * HPX;          // 16-B units in one halo chunk
-constexpr int A_ITERS = (A_UNITS + NTHR - 1) / NTHR;  // 6
 constexpr int B_UNITS = 4 * BN * 9;       // 2304
-constexpr int A_LDS_BYTES = 4 * HPXP * 16;  // 22528
 constexpr int B_LDS_BYTES = B_UNITS * 16;   // 36864
 
 template <typename T> struct KCh { static constexpr int v = 4 * Vec16<T>::N; };  // 16 (f32) / 32 (bf16)
@@ -66,38 +63,6 @@ struct FwdArgs {
                      // register allocator fits the kernel in 256 VGPRs without spills (a compile-time
                      // constant here produces SGPR / VGPR spills).
 };
-
-// stage one halo unit (pixel hp, quarter q) of chunk kc into registers (f32 wgrad)
-template <typename T>
-__device__ __forceinline__ uint4 load_halo_unit(const FwdArgs& a, int n, int y0, int x0, int id, int kc,
-                                                bool& ok) {
-  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-  const int hp = id >> 2, q = id & 3;
-  const int hy = hp / HW_, hx = hp - hy * HW_;
-  const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-  const int c = kc * KC + q * E;
-  ok = (id < A_UNITS) && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin;
-  if (!ok) return make_uint4(0, 0, 0, 0);
-  const T* p = (const T*)a.x + (((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
-  return *(const uint4*)p;
-}
-
-template <typename T>
-__device__ __forceinline__ void store_halo_unit(const FwdArgs& a, char* lds, int n, int id, int kc, uint4 v,
-                                                bool ok) {
-  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-  if (id >= A_UNITS) return;
-  const int hp = id >> 2, q = id & 3;
-  if (ok && a.isc != nullptr) {
-    const int c = kc * KC + q * E + n * a.iss;
-    float f[E];
-    Vec16<T>::unpack(v, f);
-#pragma unroll
-    for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], a.isc[c + j], a.ish[c + j]), 0.f);
-    v = Vec16<T>::pack(f);
-  }
-  *(uint4*)(lds + (q * HPXP + hp) * 16) = v;
-}
 
 // Forward: 256 threads = 4 waves (one per SIMD), output tile 16 x 32 px x 64 co;
 // wave w computes rows 4w..4w+3 (128 px = 8 m-tiles) x 64 co = 32 accumulators,
@@ -167,7 +132,9 @@ __device__ __forceinline__ void fwd_store_unit(const FwdArgs& a, char* lds, int 
   *(u32x4*)(lds + (q * FHPXP + hp) * 16) = v;
 }
 
-template <typename T>
+// DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
+// rocprofv3 and the bench report forward and data-gradient launches separately.
+template <typename T, bool DG>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -501,127 +468,6 @@ struct WgArgs {
   int tx, ty, ntiles, per_split, nsplit;
 };
 
-template <typename T>
-__global__ __launch_bounds__(NTHR, 1) void conv3x3_wgrad_kernel(WgArgs a) {  // f32 path
-  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-  constexpr int DY_UNITS_PX = 64 / E;                 // 16-B units per pixel row of dY tile
-  constexpr int DY_UNITS = TH * TW * DY_UNITS_PX;     // 2048 (bf16) / 4096 (f32)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* As = smem;                      // X halo [4][HPXP][16B]
-  char* Ds = smem + A_LDS_BYTES;        // dY tile [256 px][64 co] T
-  float* dbred = (float*)(Ds + TH * TW * 64 * sizeof(T));  // [4][64]
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int split = blockIdx.x, co0 = blockIdx.y * 64, kc = blockIdx.z;
-  const int t_begin = split * a.per_split;
-  const int t_end = min(a.ntiles, t_begin + a.per_split);
-  const int tpi = a.tx * a.ty;
-
-  FwdArgs fa;
-  fa.x = a.x; fa.N = a.N; fa.H = a.H; fa.W = a.W; fa.xct = a.xct; fa.xco = a.xco; fa.cin = a.cin;
-  fa.isc = a.isc; fa.ish = a.ish; fa.iss = a.iss;
-
-  constexpr int NACC = (sizeof(T) == 2) ? 18 : 9;
-  f32x4 acc[NACC];
-#pragma unroll
-  for (int i = 0; i < NACC; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbacc = 0.f;
-
-  for (int tile = t_begin; tile < t_end; ++tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-    __syncthreads();
-    // stage X halo
-#pragma unroll
-    for (int i = 0; i < A_ITERS; ++i) {
-      bool ok;
-      const int id = tid + i * NTHR;
-      uint4 v = load_halo_unit<T>(fa, n, y0, x0, id, kc, ok);
-      store_halo_unit<T>(fa, As, n, id, kc, v, ok);
-    }
-    // stage dY tile
-    for (int id = tid; id < DY_UNITS; id += NTHR) {
-      const int px = id / DY_UNITS_PX, u = id - px * DY_UNITS_PX;
-      const int r = px / TW, c = px - r * TW;
-      const int yy = y0 + r, xx = x0 + c, co = co0 + u * E;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (yy < a.H && xx < a.W && co < a.cout)
-        v = *(const uint4*)((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
-      *(uint4*)(Ds + id * 16) = v;
-    }
-    __syncthreads();
-    if (a.db != nullptr && kc == 0) {
-      const T* d = (const T*)Ds;
-      for (int px = wv; px < TH * TW; px += 4) dbacc += Elem<T>::ld(d + px * 64 + lane);
-    }
-    if constexpr (sizeof(T) == 2) {
-      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
-      const int cw = wv * 16;
-      for (int ks = 0; ks < TH; ++ks) {  // one output row = 32 pixels per k-step
-        const int pxa = ks * TW + 8 * g + q4;
-        const s16x4 alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, Ds + (pxa * 64 + cw + 4 * p4) * 2));
-        const s16x4 ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, Ds + ((pxa + 4) * 64 + cw + 4 * p4) * 2));
-        const bf16x8 af = cat_bf16x4(alo, ahi);
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int ky = t / 3, kx = t - ky * 3;
-          const int hp = (ks + ky) * HW_ + 8 * g + q4 + kx;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int qq = 2 * j + (p4 >> 1);
-            const char* base = As + (qq * HPXP + hp) * 16 + (p4 & 1) * 8;
-            const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base));
-            const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
-            const bf16x8 bf = cat_bf16x4(blo, bhi);
-            acc[t * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t * 2 + j], 0, 0, 0);
-          }
-        }
-      }
-    } else {
-      const int kq = lane >> 4, i = lane & 15;
-      const int cw = wv * 16;
-      const float* d = (const float*)Ds;
-      for (int ks = 0; ks < TH * TW / 4; ++ks) {
-        const int px = ks * 4 + kq;
-        const int r = px / TW, c = px - r * TW;
-        const float av = d[px * 64 + cw + i];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int ky = t / 3, kx = t - ky * 3;
-          const int hp = (r + ky) * HW_ + c + kx;
-          const float bv = *(const float*)(As + ((i >> 2) * HPXP + hp) * 16 + (i & 3) * 4);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  // ---- write partials: dw[split][co][t][ci] -------------------------------
-  const int g = lane >> 4, li = lane & 15;
-  float* out = a.dw + (long long)split * a.cout * 9 * a.cin;
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-#pragma unroll
-    for (int j = 0; j < NACC / 9; ++j) {
-      const int ci = kc * KC + j * 16 + li;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wv * 16 + g * 4 + e;
-        if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[t * (NACC / 9) + j][e];
-      }
-    }
-  }
-  if (a.db != nullptr && kc == 0) {
-    __syncthreads();
-    dbred[wv * 64 + lane] = dbacc;
-    __syncthreads();
-    if (tid < 64 && co0 + tid < a.cout)
-      a.db[(long long)split * a.cout + co0 + tid] = dbred[tid] + dbred[64 + tid] + dbred[128 + tid] + dbred[192 + tid];
-  }
-}
-
 __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised): LDS-DMA source of padding
 
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
@@ -817,6 +663,148 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   }
 }
 
+
+// fp32 wgrad (exact fp32: v_mfma_f32_16x16x4_f32, 64 FLOP/clk/SIMD).  Pixels are the GEMM K.
+// Block = (pixel split, 64 co, 32 ci) over 4 x 32 pixel tiles; wave w owns ci tile w & 1 and
+// co tiles 2 (w >> 1) .. +1 for all 9 taps (18 accumulators).  One k-step = 4 pixels: 2 A
+// (dY^T) + 9 B (X) single-dword LDS reads feed 18 MFMAs (576 clk), so the loop is MFMA-bound.
+// LDS images are channel-tile-major ([tile][pixel][16 ch] floats): the 4 pixel rows a fragment
+// read touches fall in 4 distinct 16-bank groups (conflict-free).  58 KB per block, two blocks
+// per CU; the next tile is loaded into registers while the current one is computed
+// (one LDS stage, register double buffer).
+constexpr int WF_TH = 4, WF_TW = 32;                 // pixel tile
+constexpr int WF_HW = WF_TW + 2;                     // 34
+constexpr int WF_HP = (WF_TH + 2) * WF_HW;           // 204 halo pixels
+constexpr int WF_CI = 32, WF_CO = 64;                // channels per block
+constexpr int WF_XU = WF_HP * WF_CI / 4;             // 1632 16-B halo units
+constexpr int WF_DU = WF_TH * WF_TW * WF_CO / 4;     // 2048 16-B dY units
+constexpr int WF_XI = (WF_XU + NTHR - 1) / NTHR;     // 7
+constexpr int WF_DI = WF_DU / NTHR;                  // 8
+constexpr int WF_XS = (WF_CI / 16) * WF_HP * 16;     // floats of the X image
+constexpr int WF_LDS = (WF_XS + (WF_CO / 16) * WF_TH * WF_TW * 16 + 4 * 64) * 4;  // 59 392 B
+static_assert(2 * WF_LDS <= 160 * 1024, "fp32 wgrad: two blocks per CU");
+
+__global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_f32_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Xs = (float*)smem;               // [2 ci tiles][204 px][16]
+  float* Ds = Xs + WF_XS;                 // [4 co tiles][128 px][16]
+  float* dbs = Ds + (WF_CO / 16) * WF_TH * WF_TW * 16;  // [4][64]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int split, cob, cib;
+  wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, WF_CO), cdiv(a.cin, WF_CI), split, cob, cib);
+  const int co0 = cob * WF_CO, ci0 = cib * WF_CI;
+  const int t_begin = split * a.per_split;
+  const int t_end = min(a.ntiles, t_begin + a.per_split);
+  const int tpi = a.tx * a.ty;
+  const int kq = lane >> 4, li = lane & 15;
+  const int ct0 = 2 * (wv >> 1), cit = wv & 1;
+  const bool do_db = a.db != nullptr && cib == 0;
+
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;  // co = co0 + (tid & 63), pixels (tid >> 6) + 4 i
+
+  uint4 rx[WF_XI], rd[WF_DI];
+  unsigned rok = 0;  // bit i: halo unit i is inside the image (BN+ReLU applies; padding stays 0)
+  auto gload = [&](int tile) {
+    const int n = tile / tpi, trem = tile - n * tpi;
+    const int y0 = (trem / a.tx) * WF_TH, x0 = (trem % a.tx) * WF_TW;
+    rok = 0;
+#pragma unroll
+    for (int i = 0; i < WF_XI; ++i) {
+      const int u = tid + i * NTHR;  // unit = (ci tile, halo pixel, quad m)
+      const int m = u & 3, hp = (u >> 2) % WF_HP, tl = (u >> 2) / WF_HP;
+      const int hy = hp / WF_HW, hx = hp - hy * WF_HW;
+      const int yy = y0 + hy - 1, xx = x0 + hx - 1, c = ci0 + tl * 16 + 4 * m;
+      rx[i] = make_uint4(0, 0, 0, 0);
+      if (u < WF_XU && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
+        rx[i] = *(const uint4*)((const float*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c);
+        rok |= 1u << i;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WF_DI; ++i) {
+      const int u = tid + i * NTHR;  // unit = (co tile, pixel, quad m)
+      const int m = u & 3, px = (u >> 2) % (WF_TH * WF_TW), tl = (u >> 2) / (WF_TH * WF_TW);
+      const int yy = y0 + px / WF_TW, xx = x0 + px % WF_TW, co = co0 + tl * 16 + 4 * m;
+      rd[i] = make_uint4(0, 0, 0, 0);
+      if (yy < a.H && xx < a.W && co < a.cout)
+        rd[i] = *(const uint4*)((const float*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
+    }
+  };
+  auto lwrite = [&](int tile) {
+    const int n = tile / tpi;
+#pragma unroll
+    for (int i = 0; i < WF_XI; ++i) {
+      const int u = tid + i * NTHR;
+      if (u >= WF_XU) continue;
+      uint4 v = rx[i];
+      if (a.isc != nullptr && ((rok >> i) & 1u)) {
+        const int m = u & 3, tl = (u >> 2) / WF_HP, c = ci0 + tl * 16 + 4 * m + n * a.iss;
+        float f[4];
+        Vec16<float>::unpack(v, f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f[e] = fmaxf(fmaf(f[e], a.isc[c + e], a.ish[c + e]), 0.f);
+        v = Vec16<float>::pack(f);
+      }
+      *(uint4*)(Xs + 4 * u) = v;  // unit order == [tile][pixel][16] layout
+    }
+#pragma unroll
+    for (int i = 0; i < WF_DI; ++i) *(uint4*)(Ds + 4 * (tid + i * NTHR)) = rd[i];
+  };
+
+  if (t_begin < t_end) gload(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();  // the previous tile's fragment reads are done
+    lwrite(tile);
+    __syncthreads();
+    if (tile + 1 < t_end) gload(tile + 1);  // in flight during this tile's MFMAs
+    if (do_db) {
+#pragma unroll 4
+      for (int i = 0; i < WF_TH * WF_TW / 4; ++i) {
+        const int px = (tid >> 6) + 4 * i, co = tid & 63;
+        dbacc += Ds[((co >> 4) * WF_TH * WF_TW + px) * 16 + (co & 15)];
+      }
+    }
+    const float* xb = Xs + cit * WF_HP * 16 + li;
+    const float* d0 = Ds + (ct0 * WF_TH * WF_TW) * 16 + li;
+    const float* d1 = d0 + WF_TH * WF_TW * 16;
+#pragma unroll 2
+    for (int ks = 0; ks < WF_TH * WF_TW / 4; ++ks) {
+      const int px = 4 * ks + kq, r = px / WF_TW, c = px - r * WF_TW;
+      const float a0 = d0[px * 16], a1 = d1[px * 16];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t - 3 * ky;
+        const float bv = xb[((r + ky) * WF_HW + c + kx) * 16];
+        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc[1][t], 0, 0, 0);
+      }
+    }
+  }
+  // D[m = co][n = ci]: lane holds co = tile base + 4 kq + i, ci = tile base + li
+  float* out = a.dw + (long long)split * a.cout * 9 * a.cin;
+  const int ci = ci0 + cit * 16 + li;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + (ct0 + j) * 16 + 4 * kq + i;
+        if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[j][t][i];
+      }
+  if (do_db) {
+    dbs[wv * 64 + lane] = dbacc;
+    __syncthreads();
+    if (tid < 64 && co0 + tid < a.cout)
+      a.db[(long long)split * a.cout + co0 + tid] = dbs[tid] + dbs[64 + tid] + dbs[128 + tid] + dbs[192 + tid];
+  }
+}
+
 // Deterministic split reduction: 64 consecutive elements x 4 split groups per block
 // (fixed-order fp64 sums); blocks past the dW range reduce the bias partials.
 constexpr int RSG = 4;
@@ -858,14 +846,15 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
+template <bool DG>
 int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
   dim3 grid(a.ntiles * (a.cout_pad / BN));
   if (dtype == EUNET_BF16) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    allow_lds(conv3x3_fwd_kernel<bf16_t, DG>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
   } else {
-    allow_lds(conv3x3_fwd_kernel<float>, FWD_LDS);
-    conv3x3_fwd_kernel<float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    allow_lds(conv3x3_fwd_kernel<float, DG>, FWD_LDS);
+    conv3x3_fwd_kernel<float, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
   }
   EUNET_LAUNCH_CHECK("conv3x3_fwd");
   return EUNET_OK;
@@ -924,7 +913,29 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.pro1 = 1;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
-  return launch_fwd(a, x->dtype, stream);
+  return launch_fwd<false>(a, x->dtype, stream);
+}
+
+int eunet_conv3x3_dgrad(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const float* gscale,
+                        void* stream) {
+  EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && wp_t, "conv3x3_dgrad: bad args");
+  EUNET_REQUIRE(dy->dtype == gx->dtype, "conv3x3_dgrad: dtype mismatch");
+  EUNET_REQUIRE(dy->n == gx->n && dy->h == gx->h && dy->w == gx->w, "conv3x3_dgrad: spatial mismatch");
+  const int E = elems16(dy->dtype);
+  EUNET_REQUIRE(dy->c % E == 0 && dy->ctot % E == 0 && dy->coff % E == 0 && gx->c % E == 0 && gx->ctot % E == 0 &&
+                    gx->coff % E == 0,
+                "conv3x3_dgrad: channels/strides must be multiples of %d", E);
+  FwdArgs a;
+  a.x = dy->ptr; a.N = dy->n; a.H = dy->h; a.W = dy->w; a.xct = dy->ctot; a.xco = dy->coff; a.cin = dy->c;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0;
+  a.wp = wp_t; a.cout_pad = cdiv(gx->c, BN) * BN; a.nkc = cdiv(dy->c, kchunk(dy->dtype));
+  a.bias = nullptr;
+  a.y = gx->ptr; a.yct = gx->ctot; a.yco = gx->coff; a.cout = gx->c;
+  a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
+  a.by = nullptr; a.byct = 0; a.byco = 0;
+  a.bmean = a.bistd = a.bsc = a.bsh = nullptr; a.bpart = nullptr; a.gsc = gscale;
+  a.pro1 = 1;
+  return launch_fwd<true>(a, dy->dtype, stream);
 }
 
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const eunet_act* y,
@@ -950,15 +961,16 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
   a.bmean = mean; a.bistd = invstd; a.bsc = scale; a.bsh = shift; a.bpart = part; a.gsc = gscale;
   a.pro1 = 1;
-  return launch_fwd(a, dy->dtype, stream);
+  return launch_fwd<true>(a, dy->dtype, stream);
 }
 
 
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
-  const int ntiles = dy->n * cdiv(dy->h, TH) * cdiv(dy->w, TW);
-  const int blocks = cdiv(dy->c, 64) * cdiv(cin, dtype == EUNET_BF16 ? KCW : kchunk(dtype));
-  int s = cdiv(dtype == EUNET_BF16 ? 512 : 2048, blocks);
+  const bool bf = dtype == EUNET_BF16;
+  const int ntiles = dy->n * cdiv(dy->h, bf ? TH : WF_TH) * cdiv(dy->w, bf ? TW : WF_TW);
+  const int blocks = cdiv(dy->c, 64) * cdiv(cin, bf ? KCW : WF_CI);
+  int s = cdiv(512, blocks);  // two resident blocks per CU
   s = s < 1 ? 1 : s;
   s = s > ntiles ? ntiles : s;
   // keep partials <= 256 MiB
@@ -984,7 +996,8 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.isc = in_scale; a.ish = in_shift; a.iss = in_nstride;
   a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
   a.dw = dw_part; a.db = db_part;
-  a.tx = cdiv(x->w, TW); a.ty = cdiv(x->h, TH); a.ntiles = x->n * a.tx * a.ty;
+  const bool bf = x->dtype == EUNET_BF16;
+  a.tx = cdiv(x->w, bf ? TW : WF_TW); a.ty = cdiv(x->h, bf ? TH : WF_TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
@@ -993,10 +1006,9 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
     allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
     conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
   } else {
-    dim3 grid(nsplit, cdiv(dy->c, 64), cdiv(x->c, kchunk(x->dtype)));
-    const size_t lds = A_LDS_BYTES + TH * TW * 64 * 4 + 4 * 64 * 4;
-    allow_lds(conv3x3_wgrad_kernel<float>, lds);
-    conv3x3_wgrad_kernel<float><<<grid, NTHR, lds, (hipStream_t)stream>>>(a);
+    dim3 grid(nsplit * cdiv(dy->c, WF_CO) * cdiv(x->c, WF_CI));
+    allow_lds(conv3x3_wgrad_f32_kernel, WF_LDS);
+    conv3x3_wgrad_f32_kernel<<<grid, NTHR, WF_LDS, (hipStream_t)stream>>>(a);
   }
   EUNET_LAUNCH_CHECK("conv3x3_wgrad");
   return EUNET_OK;

@@ -41,6 +41,7 @@ SIGNATURES = {
     "eunet_conv3x3_tiles": [_P, POINTER(c_int)],
     "eunet_conv3x3_fwd": [_P, _f, _f, c_int, _f, _f, _P, _f, c_void_p],
     "eunet_conv3x3_dgrad_bnbwd": [_P, _f, _P, _P, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_conv3x3_dgrad": [_P, _f, _P, _f, c_void_p],
     "eunet_conv3x3_wgrad_splits": [_P, c_int, c_int, POINTER(c_int)],
     "eunet_conv3x3_wgrad": [_P, _f, _f, c_int, _P, _f, _f, c_int, c_void_p],
     "eunet_wgrad_reduce": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, c_void_p],

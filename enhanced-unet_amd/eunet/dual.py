@@ -218,7 +218,7 @@ class DualEngine:
         ops.wgrad_reduce(dwp, None, ns, HEAD_CH[0], 2 * K, 9, sink.slot("fusion_head.0.weight", (HEAD_CH[0], 2 * K, 3, 3)),
                          None)
         gf2c = _e((N, H, W, 8), dt, dev)
-        ops.conv3x3_fwd(ops.act(gy1), ops.conv3x3_pack(P["fusion_head.0.weight"], dt, flip=True), ops.act(gf2c))
+        ops.conv3x3_dgrad(ops.act(gy1), ops.conv3x3_pack(P["fusion_head.0.weight"], dt, flip=True), ops.act(gf2c))
         del gy1
         sink.ready(["fusion_head.1.weight", "fusion_head.1.bias", "fusion_head.0.weight"])
         # ---- attention gate backward

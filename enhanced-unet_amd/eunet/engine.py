@@ -64,10 +64,28 @@ def _e(shape, dtype, device):
     return torch.empty(shape, dtype=dtype, device=device)
 
 
+_SIDE = {}
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """The per-device side stream the weight gradients run on (see UNetEngine.overlap_wgrad)."""
+    key = torch.device(device).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
+
+
 class UNetEngine:
     """One BasicUNet trunk (+ the enhance head for the single-branch model).  prefix names the
     trunk's parameters in the owning module ('model.' for EnhancedUNet, 'unetpp.' / 'deeplab.'
-    for the branches of the dual-branch model)."""
+    for the branches of the dual-branch model).
+
+    overlap_wgrad: the weight gradients of each DoubleConv (wgrad + split reduction) run on a
+    side stream, concurrently with the data-gradient chain (dgrad, BN backward) on the launch
+    stream; the two meet again before the gradients are handed out.  Same kernels and operands,
+    so the results are bit-identical either way."""
+
+    overlap_wgrad = True
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -228,7 +246,22 @@ class UNetEngine:
                              bn["shift"], dbeta, dgamma, ops.act(gy))
             return gy
 
+        main = torch.cuda.current_stream(dev)
+        side = side_stream(dev) if self.overlap_wgrad else None
+
         def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False):
+            # the gradient slots are allocated on the launch stream (their consumers run there)
+            dw = sink.slot(conv + ".weight", (C, xa.c, 3, 3))
+            db = sink.slot(conv + ".bias", (C,))
+            if side is None:
+                return wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
+            side.wait_stream(main)  # gy (and everything before it) is ready
+            with torch.cuda.stream(side):
+                wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
+            for t in (gy, xa._keep, dw, db):  # the caching allocator must not hand these out early
+                t.record_stream(side)
+
+        def wgrad_on_stream(xa: ops.Act, gy, dw, db, scale=None, shift=None, small_conv=False):
             cin = xa.c
             gya = ops.act(gy)
             if small_conv:
@@ -241,8 +274,6 @@ class UNetEngine:
                 ops.conv_small_wgrad(xa, gya, dwp, dbp, ns)
             else:
                 ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=scale, shift=shift)
-            dw = sink.slot(conv + ".weight", (C, cin, 3, 3))
-            db = sink.slot(conv + ".bias", (C,))
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
         gyb = bn_back(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
@@ -260,12 +291,18 @@ class UNetEngine:
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
         del gaa
         wgrad(p + ".0", X, gya, small_conv=small)
-        sink.ready([f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")])
+        names = [f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")]
+        if side is None:
+            sink.ready(names)
+        else:  # a bucket all-reduce launched here orders after both streams' work, without stalling main
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                sink.ready(names)
         if not need_gx:
             return None
         wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
         gx = _e((N, H, W, X.c), dt, dev)
-        ops.conv3x3_fwd(ops.act(gya), wpt, ops.act(gx))
+        ops.conv3x3_dgrad(ops.act(gya), wpt, ops.act(gx))
         return gx
 
     def backward(self, S, g_out: torch.Tensor, sink: Optional[GradSink] = None):
@@ -375,6 +412,8 @@ class UNetEngine:
         red = pool_bwd(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]), g_e1, "enc1")
         del g_p1, g_cat2
         self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True, gred=red)
+        if self.overlap_wgrad:
+            torch.cuda.current_stream(dev).wait_stream(side_stream(dev))
         return sink.finish()
 
 

@@ -80,12 +80,21 @@ def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=Non
              ctypes.byref(y), _ptr(stats), _stream())
 
 
+def conv3x3_dgrad(dy: Act, wp_t, gx: Act, gscale=None):
+    """plain dgrad (the block-input gradient): gx = conv(dy, W'), wp_t packed with flip=True."""
+    flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
+    esz = 2 if dy.dtype == _lib.EUNET_BF16 else 4
+    nbytes = float(esz * dy.n * dy.h * dy.w * (dy.c + gx.c) + wp_t.numel() * wp_t.element_size())
+    with kprof.timed("conv3x3_dgrad", flops, nbytes):
+        call("eunet_conv3x3_dgrad", ctypes.byref(dy), _ptr(wp_t), ctypes.byref(gx), _ptr(gscale), _stream())
+
+
 def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, scale, shift, part, gscale=None):
     """dgrad + the BN-backward partial sums of the layer it feeds (see eunet.h)."""
     flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
     esz = 2 if dy.dtype == _lib.EUNET_BF16 else 4
     nbytes = float(esz * dy.n * dy.h * dy.w * (dy.c + 2 * gx.c) + wp_t.numel() * wp_t.element_size())
-    with kprof.timed("conv3x3_fwd", flops, nbytes):
+    with kprof.timed("conv3x3_dgrad", flops, nbytes):
         call("eunet_conv3x3_dgrad_bnbwd", ctypes.byref(dy), _ptr(wp_t), ctypes.byref(gx), ctypes.byref(y), _ptr(mean),
              _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(gscale), _ptr(part), _stream())
 

@@ -82,6 +82,10 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
                               const eunet_act* y, const float* mean, const float* invstd,
                               const float* scale, const float* shift, const float* gscale,
                               float* part, void* stream);
+/* plain dgrad (autograd of models.py:219,222 w.r.t. the conv input): gx = conv(dy, W') with
+ * wp_t packed transpose_flip; gscale (nullable) [N][gx.c] scales gx per sample and channel */
+int eunet_conv3x3_dgrad(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const float* gscale,
+                        void* stream);
 /* wgrad (split over pixel tiles): dw_part [nsplit][cout][9][cin] and
  * db_part [nsplit][cout] (db only when db_part != NULL) */
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit);

@@ -102,6 +102,8 @@ def test_conv3x3_dgrad_wgrad(dt):
     gxd = torch.empty(N, H, W, Cin, dtype=dt, device=DEV)
     wpt = ops.conv3x3_pack(w.float().to(DEV), dt, flip=True)
     ops.conv3x3_fwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gxd))
+    gxd2 = torch.empty_like(gxd)  # the dgrad entry point runs the same kernel (own symbol)
+    ops.conv3x3_dgrad(ops.act(gy.to(DEV, dt)), wpt, ops.act(gxd2))
     # wgrad with fused transform
     dyd = gy.to(DEV, dt)
     ns = ops.conv3x3_wgrad_splits(ops.act(dyd), Cin, dt)
@@ -113,6 +115,7 @@ def test_conv3x3_dgrad_wgrad(dt):
     db = torch.empty(Cout, device=DEV)
     ops.wgrad_reduce(dwp, dbp, ns, Cout, Cin, 9, dw, db)
     torch.cuda.synchronize()
+    assert torch.equal(gxd, gxd2)
     assert rel(gxd, gx_ref) < TOL[dt]
     assert rel(dw, wt.grad) < TOL[dt]
     assert rel(db, gy.sum(dim=(0, 1, 2))) < TOL[dt]

@@ -18,7 +18,10 @@ from collections import defaultdict
 
 def short(name):
     m = re.search(r"(\w+_kernel|colsum_stage\d|\w+Kernel|multi_tensor_apply_kernel|copyBuffer\w*)", name)
-    return m.group(1) if m else name[:60]
+    k = m.group(1) if m else name[:60]
+    if k == "conv3x3_fwd_kernel" and re.search(r"conv3x3_fwd_kernel<[^>]*true>", name):
+        k += ".dgrad"  # the data-gradient launches of the same kernel (template tag DG)
+    return k
 
 
 def load(d, counter):
