@@ -650,22 +650,6 @@ struct BnRed {
 };
 
 template <typename T>
-__device__ __forceinline__ void bnred_acc(const BnRed& r, long long pix, int c, const uint4& packed, float* s1,
-                                          float* s2) {
-  constexpr int E = Vec16<T>::N;
-  float gr[E], yv[E];
-  Vec16<T>::unpack(packed, gr);
-  Vec16<T>::unpack(*(const uint4*)((const T*)r.y + pix * r.yct + r.yco + c), yv);
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    const float xh = (yv[j] - r.mean[c + j]) * r.istd[c + j];
-    const float gp = fmaf(yv[j], r.scale[c + j], r.shift[c + j]) > 0.f ? gr[j] : 0.f;  // the forward's ReLU mask
-    s1[j] += gp;
-    s2[j] = fmaf(gp, xh, s2[j]);
-  }
-}
-
-template <typename T>
 __device__ __forceinline__ void bnred_block(const BnRed& r, int C, const float* s1, const float* s2) {
   constexpr int E = Vec16<T>::N;
   __shared__ float red[2][NT][E];
@@ -688,6 +672,36 @@ __device__ __forceinline__ void bnred_block(const BnRed& r, int C, const float* 
   }
 }
 
+// Per-thread BN-backward constants of one 16-byte channel unit (the thread's unit is fixed across
+// the grid-stride loops below: the stride is a multiple of U).
+template <int E>
+struct BnUnit {
+  float mu[E], is[E], sc[E], sh[E];
+  __device__ __forceinline__ void load(const BnRed& r, int c) {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      mu[j] = r.mean[c + j];
+      is[j] = r.istd[c + j];
+      sc[j] = r.scale[c + j];
+      sh[j] = r.shift[c + j];
+    }
+  }
+  // s1 += g', s2 += g' xhat with g' = g [y scale + shift > 0], xhat = (y - mean) istd
+  __device__ __forceinline__ void acc(const float* g, const float* y, float* s1, float* s2) const {
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float gp = fmaf(y[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+      s1[j] += gp;
+      s2[j] = fmaf(gp, (y[j] - mu[j]) * is[j], s2[j]);
+    }
+  }
+};
+
+// MaxPool2d(2) adjoint (+ the skip gradient gs): every load of a unit is issued before its first
+// store (the stores may alias the loads for the compiler, so loads placed after a store would wait
+// for it).  RED: the pooled activation is not read -- bnrelu_pool stored it as
+// round(relu(y scale + shift)), recomputed here bit for bit from the y the BN-backward reduction
+// reads anyway, so the argmax (first maximum, NaN wins, as max_pool2d) is the same.
 template <typename T, bool RED = false>
 __global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
                                                           int gpco, const T* gs, int gsct, int gsco, T* go, int goct,
@@ -697,49 +711,60 @@ __global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_
   float s1[E], s2[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  // grid-stride (the fused reduction runs on a capped grid: fewer partial rows); the stride is a
-  // multiple of U, so a thread keeps its channel unit
-  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < (long long)N * Ho * Wo * U;
-       id += (long long)gridDim.x * blockDim.x) {
-  const int u = (int)(id % U);
-  long long p = id / U;
-  const int xo = (int)(p % Wo); p /= Wo;
-  const int yo = (int)(p % Ho);
-  const int n = (int)(p / Ho);
-  const int c = u * E;
-  float a[4][E], best[E], gpv[E];
-  int arg[E];
+  BnUnit<E> bu;
+  const long long id0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (RED) bu.load(br, (int)(id0 % U) * E);
+  const T* src = RED ? (const T*)br.y : act;
+  const int sct = RED ? br.yct : act_ct, sco = RED ? br.yco : act_co;
+  for (long long id = id0; id < (long long)N * Ho * Wo * U; id += (long long)gridDim.x * blockDim.x) {
+    const int u = (int)(id % U);
+    long long p = id / U;
+    const int xo = (int)(p % Wo); p /= Wo;
+    const int yo = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const int c = u * E;
+    long long pix[4];
+    uint4 ra[4], rs[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const long long pix = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-    Vec16<T>::unpack(*(const uint4*)(act + pix * act_ct + act_co + c), a[k]);
-  }
-#pragma unroll
-  for (int j = 0; j < E; ++j) {
-    best[j] = a[0][j];
-    arg[j] = 0;
-  }
-#pragma unroll
-  for (int k = 1; k < 4; ++k)
-#pragma unroll
-    for (int j = 0; j < E; ++j)
-      if (a[k][j] > best[j] || (a[k][j] != a[k][j])) { best[j] = a[k][j]; arg[j] = k; }
-  Vec16<T>::unpack(*(const uint4*)(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c), gpv);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const long long pix = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-    float o[E];
-    if (gs != nullptr) Vec16<T>::unpack(*(const uint4*)(gs + pix * gsct + gsco + c), o);
-    else {
-#pragma unroll
-      for (int j = 0; j < E; ++j) o[j] = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      pix[k] = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+      ra[k] = *(const uint4*)(src + pix[k] * sct + sco + c);
     }
+    const uint4 rg = *(const uint4*)(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c);
 #pragma unroll
-    for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
-    const uint4 packed = Vec16<T>::pack(o);
-    *(uint4*)(go + pix * goct + goco + c) = packed;
-    if constexpr (RED) bnred_acc<T>(br, pix, c, packed, s1, s2);
-  }
+    for (int k = 0; k < 4; ++k)
+      rs[k] = gs != nullptr ? *(const uint4*)(gs + pix[k] * gsct + gsco + c) : make_uint4(0, 0, 0, 0);
+    float best[E], gpv[E];
+    int arg[E];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // argmax over the activation, unpacked from the loads on the fly
+      float a[E];
+      Vec16<T>::unpack(ra[k], a);
+      if constexpr (RED) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) a[j] = fmaxf(fmaf(a[j], bu.sc[j], bu.sh[j]), 0.f);
+        Vec16<T>::unpack(Vec16<T>::pack(a), a);  // the stored (rounded) activation
+      }
+#pragma unroll
+      for (int j = 0; j < E; ++j)
+        if (k == 0 || a[j] > best[j] || (a[j] != a[j])) { best[j] = a[j]; arg[j] = k; }
+    }
+    Vec16<T>::unpack(rg, gpv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[E];
+      Vec16<T>::unpack(rs[k], o);
+#pragma unroll
+      for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
+      const uint4 packed = Vec16<T>::pack(o);
+      *(uint4*)(go + pix[k] * goct + goco + c) = packed;
+      if constexpr (RED) {
+        float gr[E], yv[E];
+        Vec16<T>::unpack(packed, gr);
+        Vec16<T>::unpack(ra[k], yv);
+        bu.acc(gr, yv, s1, s2);
+      }
+    }
   }
   if constexpr (RED) bnred_block<T>(br, C, s1, s2);
 }
@@ -786,70 +811,125 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
   *(uint4*)(o + ((long long)(n * h + y) * w + x) * oct + oco + c) = Vec16<TO>::pack(acc);
 }
 
-// 2x2 low-res outputs per thread: the 6x6 high-res window they share is read once (36 vector
-// loads instead of 4 x 16), separable adjoint weights per row / column
+// Upsample x2 adjoint, separable, as a row sweep: a thread owns low-res columns x0, x0+1 of one
+// 16-byte channel unit over UP_R low-res rows.  Each high-res row r of its 6-column window is
+// reduced horizontally once (H_b[r] = sum_dx wx_b(dx) g[r][2 x0 - 1 + dx]) and weighted into the
+// (at most two) output rows it feeds (rows 2y-1 .. 2y+2 feed y): per output row two new high-res
+// rows are read (6 loads per output instead of 9 for a 2x2 block).  RED: the BN-backward sums of
+// the produced gradient, with the outputs' y loaded with the window rows (a load placed after a
+// store that may alias it would wait for the store).
+constexpr int UP_R = 8;
 template <typename T, typename TO, bool RED = false>
-__global__ __launch_bounds__(256) void up_bwd2x2_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
-                                                        int h, int w, int C, BnRed br) {
+__global__ __launch_bounds__(256) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
+                                                          int h, int w, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
-  const int U = C / E, H2 = 2 * h, W2 = 2 * w, hb = (h + 1) / 2, wb = (w + 1) / 2;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w, hr = (h + UP_R - 1) / UP_R, wb = (w + 1) / 2;
   float s1[E], s2[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < (long long)N * hb * wb * U;
+  for (long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x; id < (long long)N * hr * wb * U;
        id += (long long)gridDim.x * blockDim.x) {
-  const int u = (int)(id % U);
-  long long p = id / U;
-  const int xb = (int)(p % wb); p /= wb;
-  const int yb = (int)(p % hb);
-  const int n = (int)(p / hb);
-  const int c = u * E, y0 = 2 * yb, x0 = 2 * xb;
-  float acc[2][2][E];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int j = 0; j < E; ++j) acc[a][b][j] = 0.f;
-  float wxs[6][2];
-#pragma unroll
-  for (int dx = 0; dx < 6; ++dx) {
-    const int ox = 2 * x0 - 1 + dx;
-    const bool ok = ox >= 0 && ox < W2;
-    wxs[dx][0] = ok ? up2_adj_w(ox, w, x0) : 0.f;
-    wxs[dx][1] = ok && x0 + 1 < w ? up2_adj_w(ox, w, x0 + 1) : 0.f;
-  }
-#pragma unroll
-  for (int dy = 0; dy < 6; ++dy) {
-    const int oy = 2 * y0 - 1 + dy;
-    if (oy < 0 || oy >= H2) continue;
-    const float wy0 = up2_adj_w(oy, h, y0), wy1 = y0 + 1 < h ? up2_adj_w(oy, h, y0 + 1) : 0.f;
+    const int u = (int)(id % U);
+    long long p = id / U;
+    const int xb = (int)(p % wb); p /= wb;
+    const int yr = (int)(p % hr);
+    const int n = (int)(p / hr);
+    const int c = u * E, x0 = 2 * xb, ys = yr * UP_R, ye = min(h, ys + UP_R);
+    float wxs[6][2];
 #pragma unroll
     for (int dx = 0; dx < 6; ++dx) {
       const int ox = 2 * x0 - 1 + dx;
-      if (ox < 0 || ox >= W2) continue;
-      float f[E];
-      Vec16<T>::unpack(*(const uint4*)(g + ((long long)(n * H2 + oy) * W2 + ox) * gct + gco + c), f);
-      const float w00 = wy0 * wxs[dx][0], w01 = wy0 * wxs[dx][1], w10 = wy1 * wxs[dx][0], w11 = wy1 * wxs[dx][1];
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        acc[0][0][j] = fmaf(w00, f[j], acc[0][0][j]);
-        acc[0][1][j] = fmaf(w01, f[j], acc[0][1][j]);
-        acc[1][0][j] = fmaf(w10, f[j], acc[1][0][j]);
-        acc[1][1][j] = fmaf(w11, f[j], acc[1][1][j]);
-      }
+      const bool ok = ox >= 0 && ox < W2;
+      wxs[dx][0] = ok ? up2_adj_w(ox, w, x0) : 0.f;
+      wxs[dx][1] = ok && x0 + 1 < w ? up2_adj_w(ox, w, x0 + 1) : 0.f;
     }
-  }
+    const T* gn = g + (long long)n * H2 * W2 * gct + gco + c;
+    // horizontal partials of high-res row r (zero outside the image)
+    auto hrow = [&](int r, float (*hv)[E]) {
+      uint4 v[6];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-      if (y0 + a < h && x0 + b < w) {
-        const long long pix = (long long)(n * h + y0 + a) * w + x0 + b;
-        const uint4 packed = Vec16<TO>::pack(acc[a][b]);
-        *(uint4*)(o + pix * oct + oco + c) = packed;
-        if constexpr (RED) bnred_acc<TO>(br, pix, c, packed, s1, s2);
+      for (int dx = 0; dx < 6; ++dx) {
+        const int ox = 2 * x0 - 1 + dx;
+        v[dx] = (r >= 0 && r < H2 && ox >= 0 && ox < W2) ? *(const uint4*)(gn + ((long long)r * W2 + ox) * gct)
+                                                          : make_uint4(0, 0, 0, 0);
       }
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < E; ++j) hv[b][j] = 0.f;
+#pragma unroll
+      for (int dx = 0; dx < 6; ++dx) {
+        float f[E];
+        Vec16<T>::unpack(v[dx], f);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          hv[0][j] = fmaf(wxs[dx][0], f[j], hv[0][j]);
+          hv[1][j] = fmaf(wxs[dx][1], f[j], hv[1][j]);
+        }
+      }
+    };
+    // row r feeds the outputs y with 2y-1 <= r <= 2y+2: carry the next output row's partial sums
+    auto wrow = [&](int r, int y) { return (r >= 0 && r < H2 && y < h) ? up2_adj_w(r, h, y) : 0.f; };
+    float acur[2][E], anext[2][E], hv[2][E];
+    hrow(2 * ys - 1, hv);
+    {
+      const float wa = wrow(2 * ys - 1, ys);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < E; ++j) acur[b][j] = wa * hv[b][j];
+    }
+    hrow(2 * ys, hv);
+    {
+      const float wa = wrow(2 * ys, ys);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < E; ++j) acur[b][j] = fmaf(wa, hv[b][j], acur[b][j]);
+    }
+#pragma unroll 1
+    for (int y = ys; y < ye; ++y) {
+      uint4 ryv[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        ryv[b] = (RED && x0 + b < w)
+                     ? *(const uint4*)((const TO*)br.y + ((long long)(n * h + y) * w + x0 + b) * br.yct + br.yco + c)
+                     : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 1; k <= 2; ++k) {
+        hrow(2 * y + k, hv);
+        const float wc = wrow(2 * y + k, y), wn = wrow(2 * y + k, y + 1);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int j = 0; j < E; ++j) {
+            acur[b][j] = fmaf(wc, hv[b][j], acur[b][j]);
+            anext[b][j] = k == 1 ? wn * hv[b][j] : fmaf(wn, hv[b][j], anext[b][j]);
+          }
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (x0 + b >= w) continue;
+        const long long pix = (long long)(n * h + y) * w + x0 + b;
+        const uint4 packed = Vec16<TO>::pack(acur[b]);
+        *(uint4*)(o + pix * oct + oco + c) = packed;
+        if constexpr (RED) {
+          float gr[E], yv[E];
+          Vec16<TO>::unpack(packed, gr);
+          Vec16<TO>::unpack(ryv[b], yv);
+#pragma unroll
+          for (int j = 0; j < E; ++j) {  // (the BN constants from L1: registers would cost occupancy)
+            const float gp = fmaf(yv[j], br.scale[c + j], br.shift[c + j]) > 0.f ? gr[j] : 0.f;
+            s1[j] += gp;
+            s2[j] = fmaf(gp, (yv[j] - br.mean[c + j]) * br.istd[c + j], s2[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < E; ++j) acur[b][j] = anext[b][j];
+    }
   }
   if constexpr (RED) bnred_block<TO>(br, C, s1, s2);
 }
@@ -915,6 +995,13 @@ __global__ __launch_bounds__(256) void up_bwd_k2_kernel(const float2* g, float2*
 // 8 lanes per pixel, lane group g owns channels 8g+64j (C <= 128); partial
 // sums stay in registers over the block's C1X_PIX pixels.
 constexpr int C1X_PIX = 1024;
+// J = 1 (C <= 64) or 2 (C <= 128): the per-lane state (BN constants, 1x1 weights, partial sums)
+// is sized by it, so the 64-channel dec2 output runs at twice the occupancy
+#define C1X_LAUNCH(kern, T, BNR, ARGS)                                                       \
+  do {                                                                                       \
+    if (y->c <= 64) kern<T, 1, BNR><<<tiles, NT, 0, (hipStream_t)stream>>> ARGS;             \
+    else kern<T, 2, BNR><<<tiles, NT, 0, (hipStream_t)stream>>> ARGS;                        \
+  } while (0)
 // sum over the 8 pixel slots of a wave (lanes l, l^8, l^16, l^32, ...): DPP row rotate by 8 within
 // each 16-lane row, then the gfx950 permlane16 / permlane32 swaps (no ds_bpermute round trips)
 __device__ __forceinline__ float sum_slots8(float v) {
@@ -924,7 +1011,7 @@ __device__ __forceinline__ float sum_slots8(float v) {
 
 // BNR: also the BN-backward reduction (sum g', sum g' xhat) of y's BatchNorm over the produced
 // gradient (g' = the stored gradient where relu(bn(y)) > 0), per block into bpart[block][2][C]
-template <typename T, bool BNR = false>
+template <typename T, int J, bool BNR>  // J = ceil(C / 64) channel halves per lane group
 __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P, int C, int yct, int yco,
                                                          const float* sc, const float* sh, const float* w, int K,
                                                          const float* gz, T* ga, int gct, int gco, float* part,
@@ -933,17 +1020,17 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
   __shared__ float red[4][3 * 128 + 3 + (BNR ? 2 * 128 : 0)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = lane & 7, ps = tid >> 3;
   const int stride = K * C + K;
-  float aw[2][3][8], ab[3] = {0.f, 0.f, 0.f};
+  float aw[J][3][8], ab[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < J; ++j)
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) aw[j][k][e] = 0.f;
-  float s8[2][8], t8[2][8], w8[2][3][8];  // this lane's channels 64j + 8g + e
-  float mu8[2][8], is8[2][8], bs1[2][8], bs2[2][8];
+  float s8[J][8], t8[J][8], w8[J][3][8];  // this lane's channels 64j + 8g + e
+  float mu8[J][8], is8[J][8], bs1[J][8], bs2[J][8];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < J; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int c = 64 * j + 8 * g + e;
@@ -961,54 +1048,76 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
     }
   const long long p0 = (long long)blockIdx.x * C1X_PIX;
   const long long p1 = min(P, p0 + C1X_PIX);
-  for (long long p = p0 + ps; p < p1; p += 32) {
-    float gk[3] = {0.f, 0.f, 0.f};
-    for (int k = 0; k < K; ++k) gk[k] = gz[p * K + k];
-    if (g == 0)
+  // PPI pixels per iteration (2 when the state fits), every load issued before the first store
+  // (a load placed after a store that may alias it waits for the store)
+  constexpr int PPI = J == 1 ? 2 : 1;
+  for (long long pa = p0 + ps; pa < p1; pa += 32 * PPI) {
+    float gk[PPI][3];
+    uint4 ry[PPI][J][2];  // [pixel][j][half]
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ab[k] += gk[k];
+    for (int i = 0; i < PPI; ++i) {
+      const long long p = pa + 32 * i;
+      const bool pv = p < p1;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = 64 * j + 8 * g;
-      if (c >= C) continue;
-      float f[8], go[8];
-      Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), f);
-      if constexpr (E == 4) Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c + 4), f + 4);
+      for (int k = 0; k < 3; ++k) gk[i][k] = (pv && k < K) ? gz[p * K + k] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float act = fmaxf(fmaf(f[e], s8[j][e], t8[j][e]), 0.f);
-        float s = 0.f;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          s = fmaf(w8[j][k][e], gk[k], s);
-          aw[j][k][e] = fmaf(gk[k], act, aw[j][k][e]);
-        }
-        go[e] = s;
+      for (int j = 0; j < J; ++j) {
+        const int c = 64 * j + 8 * g;
+        const bool ok = pv && c < C;
+        ry[i][j][0] = ok ? *(const uint4*)(y + p * yct + yco + c) : make_uint4(0, 0, 0, 0);
+        ry[i][j][1] = (ok && E == 4) ? *(const uint4*)(y + p * yct + yco + c + 4) : make_uint4(0, 0, 0, 0);
       }
-      const uint4 pk0 = Vec16<T>::pack(go);
-      *(uint4*)(ga + p * gct + gco + c) = pk0;
-      uint4 pk1 = pk0;
-      if constexpr (E == 4) {
-        pk1 = Vec16<T>::pack(go + 4);
-        *(uint4*)(ga + p * gct + gco + c + 4) = pk1;
-      }
-      if constexpr (BNR) {  // the stored (rounded) gradient, as bn_bwd_reduce would read it
-        float gr[8];
-        Vec16<T>::unpack(pk0, gr);
-        if constexpr (E == 4) Vec16<T>::unpack(pk1, gr + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < PPI; ++i) {
+      const long long p = pa + 32 * i;
+      if (p >= p1) continue;
+      if (g == 0)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ab[k] += gk[i][k];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int c = 64 * j + 8 * g;
+        if (c >= C) continue;
+        float f[8], go[8];
+        Vec16<T>::unpack(ry[i][j][0], f);
+        if constexpr (E == 4) Vec16<T>::unpack(ry[i][j][1], f + 4);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float xh = (f[e] - mu8[j][e]) * is8[j][e];
-          const float gp = fmaf(f[e], s8[j][e], t8[j][e]) > 0.f ? gr[e] : 0.f;
-          bs1[j][e] += gp;
-          bs2[j][e] = fmaf(gp, xh, bs2[j][e]);
+          const float act = fmaxf(fmaf(f[e], s8[j][e], t8[j][e]), 0.f);
+          float sv = 0.f;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            sv = fmaf(w8[j][k][e], gk[i][k], sv);
+            aw[j][k][e] = fmaf(gk[i][k], act, aw[j][k][e]);
+          }
+          go[e] = sv;
+        }
+        const uint4 pk0 = Vec16<T>::pack(go);
+        *(uint4*)(ga + p * gct + gco + c) = pk0;
+        uint4 pk1 = pk0;
+        if constexpr (E == 4) {
+          pk1 = Vec16<T>::pack(go + 4);
+          *(uint4*)(ga + p * gct + gco + c + 4) = pk1;
+        }
+        if constexpr (BNR) {  // the stored (rounded) gradient, as bn_bwd_reduce would read it
+          float gr[8];
+          Vec16<T>::unpack(pk0, gr);
+          if constexpr (E == 4) Vec16<T>::unpack(pk1, gr + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float xh = (f[e] - mu8[j][e]) * is8[j][e];
+            const float gp = fmaf(f[e], s8[j][e], t8[j][e]) > 0.f ? gr[e] : 0.f;
+            bs1[j][e] += gp;
+            bs2[j][e] = fmaf(gp, xh, bs2[j][e]);
+          }
         }
       }
     }
   }
   // reduce over the 8 pixel slots of each wave (xor 8, 16, 32), then across waves
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < J; ++j)
 #pragma unroll
     for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -1017,7 +1126,7 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
   for (int k = 0; k < 3; ++k) ab[k] = k < K ? sum_slots8(ab[k]) : 0.f;
   if constexpr (BNR)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < J; ++j)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         bs1[j][e] = sum_slots8(bs1[j][e]);
@@ -1025,7 +1134,7 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
       }
   if (lane < 8) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < J; ++j)
 #pragma unroll
       for (int k = 0; k < 3; ++k)
 #pragma unroll
@@ -1037,7 +1146,7 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
       for (int k = 0; k < K; ++k) red[wv][K * C + k] = ab[k];
     if constexpr (BNR)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < J; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 64 * j + 8 * g + e;
@@ -1349,14 +1458,14 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
   }
   EUNET_REQUIRE(vec_ok(ghi) && vec_ok(glo) && ghi->dtype == glo->dtype, "upsample_bwd: vector layout");
   const int E = e16(ghi->dtype);
-  const long long total = (long long)glo->n * ((glo->h + 1) / 2) * ((glo->w + 1) / 2) * (glo->c / E);
+  const long long total = (long long)glo->n * ((glo->h + UP_R - 1) / UP_R) * ((glo->w + 1) / 2) * (glo->c / E);
   const unsigned gr = (unsigned)((total + 255) / 256);
   if (ghi->dtype == EUNET_BF16)
-    up_bwd2x2_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<bf16_t, bf16_t><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, BnRed{});
   else
-    up_bwd2x2_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<float, float><<<gr, 256, 0, (hipStream_t)stream>>>(
         (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, BnRed{});
   EUNET_LAUNCH_CHECK("upsample_bwd");
@@ -1377,7 +1486,7 @@ long long pool_threads(const eunet_act* gout) {
 // and sum), the upsample adjoint, with more work per output, 8192 (more loads in flight).
 int bnr_grid(long long threads, int cap) { return (int)std::min<long long>((threads + NT - 1) / NT, cap); }
 long long up_threads(const eunet_act* glo) {
-  return (long long)glo->n * ((glo->h + 1) / 2) * ((glo->w + 1) / 2) * (glo->c / e16(glo->dtype));
+  return (long long)glo->n * ((glo->h + UP_R - 1) / UP_R) * ((glo->w + 1) / 2) * (glo->c / e16(glo->dtype));
 }
 }  // namespace
 
@@ -1429,11 +1538,11 @@ int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eun
   const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, part};
   const unsigned gr = (unsigned)bnr_grid(up_threads(glo), 8192);
   if (ghi->dtype == EUNET_BF16)
-    up_bwd2x2_kernel<bf16_t, bf16_t, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<bf16_t, bf16_t, true><<<gr, NT, 0, (hipStream_t)stream>>>(
         (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, br);
   else
-    up_bwd2x2_kernel<float, float, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<float, float, true><<<gr, NT, 0, (hipStream_t)stream>>>(
         (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, br);
   EUNET_LAUNCH_CHECK("upsample_bwd_bnr");
@@ -1455,15 +1564,15 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
   const long long P = (long long)y->n * y->h * y->w;
   const unsigned tiles = (unsigned)((P + C1X_PIX - 1) / C1X_PIX);
   if (y->dtype == EUNET_BF16)
-    conv1x1_bwd_kernel<bf16_t><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
+    C1X_LAUNCH(conv1x1_bwd_kernel, bf16_t, false, ((const bf16_t*)y->ptr, P, y->c, y->ctot,
                                                                         y->coff, scale, shift, w, k, gz,
                                                                         (bf16_t*)gact->ptr, gact->ctot, gact->coff,
-                                                                        part, nullptr, nullptr, nullptr);
+                                                                        part, nullptr, nullptr, nullptr));
   else
-    conv1x1_bwd_kernel<float><<<tiles, NT, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
+    C1X_LAUNCH(conv1x1_bwd_kernel, float, false, ((const float*)y->ptr, P, y->c, y->ctot,
                                                                        y->coff, scale, shift, w, k, gz,
                                                                        (float*)gact->ptr, gact->ctot, gact->coff,
-                                                                       part, nullptr, nullptr, nullptr);
+                                                                       part, nullptr, nullptr, nullptr));
   EUNET_LAUNCH_CHECK("conv1x1_bwd");
   return EUNET_OK;
 }
@@ -1479,15 +1588,15 @@ int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* s
   const long long P = (long long)y->n * y->h * y->w;
   const unsigned tiles = (unsigned)((P + C1X_PIX - 1) / C1X_PIX);
   if (y->dtype == EUNET_BF16)
-    conv1x1_bwd_kernel<bf16_t, true><<<tiles, NT, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, P, y->c, y->ctot,
+    C1X_LAUNCH(conv1x1_bwd_kernel, bf16_t, true, ((const bf16_t*)y->ptr, P, y->c, y->ctot,
                                                                         y->coff, scale, shift, w, k, gz,
                                                                         (bf16_t*)gact->ptr, gact->ctot, gact->coff,
-                                                                        part, mean, invstd, bn_part);
+                                                                        part, mean, invstd, bn_part));
   else
-    conv1x1_bwd_kernel<float, true><<<tiles, NT, 0, (hipStream_t)stream>>>((const float*)y->ptr, P, y->c, y->ctot,
+    C1X_LAUNCH(conv1x1_bwd_kernel, float, true, ((const float*)y->ptr, P, y->c, y->ctot,
                                                                        y->coff, scale, shift, w, k, gz,
                                                                        (float*)gact->ptr, gact->ctot, gact->coff,
-                                                                       part, mean, invstd, bn_part);
+                                                                       part, mean, invstd, bn_part));
   EUNET_LAUNCH_CHECK("conv1x1_bwd_bnr");
   return EUNET_OK;
 }

@@ -229,7 +229,9 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
 /* The two producers above with the reduction half of eunet_bn_bwd_reduce fused in: gout / glo is
  * the gradient w.r.t. relu(bn(y)) of the DoubleConv output y (models.py:222-223), and
  * part[rows][2][C] receives (sum g', sum g' xhat) per block, rows from the *_rows query (0: the
- * channel count does not allow the fused form -- use the separate reduce). */
+ * channel count does not allow the fused form -- use the separate reduce).  The fused max-pool
+ * adjoint does not read act (only its shape): it recomputes the activation from y as
+ * eunet_bnrelu_pool stored it, round(relu(y scale + shift)), so act must be that tensor. */
 int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows);
 int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
                            const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,

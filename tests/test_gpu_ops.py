@@ -594,7 +594,9 @@ def test_bnrelu(dt):
 @pytest.mark.parametrize("kind", ["pool", "up"])
 def test_fused_bn_reduce_in_gradient_producers(dt, kind):
     """pool_bwd_add / upsample_bwd with the BN-backward reduction fused in: the gradient equals
-    the plain kernel's bit for bit, the partial sums equal bn_bwd_reduce on that gradient."""
+    the plain kernel's bit for bit, the partial sums equal bn_bwd_reduce on that gradient.  The
+    fused max-pool adjoint takes its argmax from relu(y scale + shift) recomputed from y, so the
+    saved activation here is the one bnrelu_pool stores for that y (the engine's contract)."""
     ops = _ops()
     g = torch.Generator().manual_seed(17)
     N, C = 2, 64
@@ -608,7 +610,9 @@ def test_fused_bn_reduce_in_gradient_producers(dt, kind):
     beta = (torch.randn(C, generator=g) * 0.2).to(DEV)
     sc, sh = gamma * istd, beta - mean * gamma * istd  # the forward affine (defines the ReLU mask)
     if kind == "pool":
-        act = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
+        act = torch.empty(N, h, w, C, dtype=dt, device=DEV)
+        ops.bnrelu_pool(ops.act(y), sc, sh, ops.act(act), ops.act(torch.empty(N, h // 2, w // 2, C, dtype=dt,
+                                                                              device=DEV)))
         gp = torch.randn(N, h // 2, w // 2, C, generator=g).to(DEV, dt)
         gs = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
         ops.pool_bwd_add(ops.act(act), ops.act(gp), ops.act(gs), ops.act(gref))
