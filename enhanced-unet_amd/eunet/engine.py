@@ -33,9 +33,12 @@ BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 # DoubleConv's first BN+ReLU, za = relu(bn1(ya)), for the second conv (EUNET_MATERIALIZE_ZA):
-#   1 (default) one elementwise pass; conv .3's forward and weight gradient read za as is
-#   0 applied inside both operand stagings instead (nothing stored; A/B: profiles/r01_ab_za.txt)
-MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "1") != "0"
+#   0 (default since round 2) applied inside both operand stagings (nothing stored): the forward's
+#     halo staging loads the BN constants once per K-chunk with the halo, so the transform is free
+#     there, and the weight gradient pays it on the side stream; A/B +0.9 / +2.1 % img/s
+#     (profiles/r02_ab_za.txt; round 1's opposite result: profiles/r01_ab_za.txt)
+#   1 one elementwise pass on the main stream; conv .3's forward and weight gradient read za as is
+MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "0") != "0"
 # the BN-b backward reduction of a block fused into the kernel producing its output gradient
 # (upsample / max-pool adjoints) instead of a separate bn_bwd_reduce pass (EUNET_FUSE_BN_REDUCE=0)
 FUSE_BN_REDUCE = os.environ.get("EUNET_FUSE_BN_REDUCE", "1") != "0"

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--transform", action="store_true",
                     help="forward / wgrad with the BN+ReLU operand transform (the bench path materialises it)")
     ap.add_argument("--no-stats", action="store_true", help="forward without BN partials")
+    ap.add_argument("--plain-dgrad", action="store_true", help="dgrad without the fused BN-backward reduction")
     a = ap.parse_args()
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
     dev = "cuda"
@@ -77,7 +78,11 @@ def main():
         yb = torch.randn(a.batch, H, H, cin, device=dev).to(dt)
         one, zero = torch.ones(cin, device=dev), torch.zeros(cin, device=dev)
         cpart = torch.empty(ops.conv3x3_tiles(gxa) * 2 * cin, device=dev)
-        t_d = timeit(lambda: ops.conv3x3_dgrad_bnbwd(gya, wpt, gxa, ops.act(yb), zero, one, one, zero, cpart), a.reps)
+        if a.plain_dgrad:
+            t_d = timeit(lambda: ops.conv3x3_dgrad(gya, wpt, gxa), a.reps)
+        else:
+            t_d = timeit(lambda: ops.conv3x3_dgrad_bnbwd(gya, wpt, gxa, ops.act(yb), zero, one, one, zero, cpart),
+                         a.reps)
         ns = ops.conv3x3_wgrad_splits(gya, cin, dt)
         dwp = torch.empty(ns * cout * 9 * cin, device=dev)
         dbp = torch.empty(ns * cout, device=dev)
