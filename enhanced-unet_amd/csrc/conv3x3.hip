@@ -843,36 +843,55 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_f32_kernel(WgArgs a) {
   }
 }
 
-// Deterministic split reduction: 64 consecutive elements x 4 split groups per block
-// (fixed-order fp64 sums); blocks past the dW range reduce the bias partials.
-constexpr int RSG = 4;
+// Deterministic split reduction: a block reduces 64 consecutive elements; thread (sg, tq) sums
+// splits sg, sg + 16, ... of elements 4tq..4tq+3 (16-byte loads, 8 in flight, fp64), then the 16
+// split groups are added in a fixed pairwise order.  Blocks past the dW range reduce the bias
+// partials.
+constexpr int RSG = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* part, const float* dbp, int nsplit, int cout,
                                                            int cin, int taps, float* dw, float* db) {
   __shared__ double red[RSG][64];
-  const int tx = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int tq = threadIdx.x & 15, sg = threadIdx.x >> 4;
   const long long per = (long long)cout * taps * cin;
   const long long nbw = (per + 63) / 64;
   const bool isdw = blockIdx.x < nbw;
-  const long long e = (isdw ? (long long)blockIdx.x : (long long)blockIdx.x - nbw) * 64 + tx;
+  const long long e0 = (isdw ? (long long)blockIdx.x : (long long)blockIdx.x - nbw) * 64 + 4 * tq;
   const long long cnt = isdw ? per : cout;
   const float* src = isdw ? part : dbp;
-  double s = 0.0;
-  if (e < cnt) {
-#pragma unroll 4
-    for (int k = sg; k < nsplit; k += RSG) s += (double)src[(long long)k * cnt + e];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  if (cnt % 4 == 0 && e0 < cnt) {
+#pragma unroll 8
+    for (int k = sg; k < nsplit; k += RSG) {
+      const float4 v = *(const float4*)(src + (long long)k * cnt + e0);
+      s[0] += (double)v.x;
+      s[1] += (double)v.y;
+      s[2] += (double)v.z;
+      s[3] += (double)v.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (e0 + i < cnt)
+        for (int k = sg; k < nsplit; k += RSG) s[i] += (double)src[(long long)k * cnt + e0 + i];
   }
-  red[sg][tx] = s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[sg][4 * tq + i] = s[i];
   __syncthreads();
-  if (sg != 0 || e >= cnt) return;
-  const double t = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+  const int tx = threadIdx.x;
+  const long long e = e0 - 4 * tq + tx;
+  if (tx >= 64 || e >= cnt) return;
+  double t[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t[g] = red[2 * g][tx] + red[2 * g + 1][tx];
+  const double u = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
   if (isdw) {
     const int ci = (int)(e % cin);
     const long long r = e / cin;
     const int tp = (int)(r % taps);
     const int co = (int)(r / taps);
-    dw[((long long)co * cin + ci) * taps + tp] = (float)t;
+    dw[((long long)co * cin + ci) * taps + tp] = (float)u;
   } else {
-    db[e] = (float)t;
+    db[e] = (float)u;
   }
 }
 
