@@ -178,28 +178,54 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   float dbv[8];  // bias gradient: channels 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i
 #pragma unroll
   for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  // The next tile's x halo and dY tile are loaded into registers while this tile's MFMAs run
+  // (one exposed global round trip per block instead of one per tile).
+  constexpr int XI = ((STH + 2) * (STW + 2) * SCI + NT - 1) / NT, DI = STH * STW * 64 / E / NT;
+  static_assert(STH * STW * 64 / E % NT == 0, "dY units per thread");
+  float rx[XI];
+  uint4 rd[DI];
+  auto load_tile = [&](int tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
-    __syncthreads();
-    for (int i = tid; i < (STH + 2) * (STW + 2) * cin; i += NT) {
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * NT;
       const int hp = i / cin, ci = i - hp * cin;
       const int hy = hp / (STW + 2), hx = hp - hy * (STW + 2);
       const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      float v = 0.f;
-      if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-        v = Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci);
-      xs[hp * SCI + ci] = v;
+      rx[k] = (i < (STH + 2) * (STW + 2) * cin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+                  ? Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci)
+                  : 0.f;
     }
-    for (int id = tid; id < STH * STW * 64 / E; id += NT) {
+#pragma unroll
+    for (int k = 0; k < DI; ++k) {
+      const int id = tid + k * NT;
       const int px = id / (64 / E), u = id - px * (64 / E);
       const int r = px / STW, c = px - r * STW;
       const int yy = y0 + r, xx = x0 + c, co = co0 + u * E;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (yy < a.H && xx < a.W && co < a.cout)
-        v = *(const uint4*)((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co);
-      *(uint4*)(gs + px * 64 + u * E) = v;
+      rd[k] = (yy < a.H && xx < a.W && co < a.cout)
+                  ? *(const uint4*)((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co)
+                  : make_uint4(0, 0, 0, 0);
     }
+  };
+  if (t_begin < t_end) load_tile(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < XI; ++k) {
+      const int i = tid + k * NT;
+      if (i < (STH + 2) * (STW + 2) * cin) {
+        const int hp = i / cin, ci = i - hp * cin;
+        xs[hp * SCI + ci] = rx[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < DI; ++k) {
+      const int id = tid + k * NT;
+      const int px = id / (64 / E), u = id - px * (64 / E);
+      *(uint4*)(gs + px * 64 + u * E) = rd[k];
+    }
+    if (tile + 1 < t_end) load_tile(tile + 1);
     __syncthreads();
 #pragma unroll 4
     for (int id = tid; id < STH * STW * icw; id += NT) {
