@@ -795,14 +795,6 @@ __global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_
   if constexpr (RED) bnred_block<T>(br, C, s1, s2);
 }
 
-// adjoint of the x2 bilinear taps; per low-res row y the contributing
-// high-res rows are 2y-1 .. 2y+2
-__device__ __forceinline__ float up2_adj_w(int o, int in, int i) {
-  int i0, i1;
-  float l1;
-  up2_src(o, in, i0, i1, l1);
-  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
-}
 
 template <typename T, typename TO>
 __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N, int h, int w, int C) {

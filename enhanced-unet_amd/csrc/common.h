@@ -139,6 +139,15 @@ __device__ __forceinline__ void up2_src(int o, int in, int& i0, int& i1, float& 
   l1 = s - (float)i0;
 }
 
+// adjoint of the x2 bilinear taps: the weight of low-res index i in high-res output o; per
+// low-res row y the contributing high-res rows are 2y-1 .. 2y+2
+__device__ __forceinline__ float up2_adj_w(int o, int in, int i) {
+  int i0, i1;
+  float l1;
+  up2_src(o, in, i0, i1, l1);
+  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
 // deterministic fp64 column sum of a [rows][ld] partial matrix (bn_pool_up.hip); columns
 // >= split go to out_hi[col - split] when out_hi != nullptr
 int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s,

@@ -34,6 +34,7 @@ struct HeadArgs {
   const float* dbeta; const float* dgamma;  // bwd gh
   float* stats; float* out2h; float* logits; float* part;
   void* gh; float* v; float* gu;
+  float* patch;  // bf16 path: per-tile low-res adjoint patches [tile][10][10][K] (head_gh_mfma_kernel)
   int tx, ty, ntiles;
 };
 
@@ -1019,14 +1020,18 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
 }
 
-// g_h (never stored), the per-tap products v = g_h * W1 (stored, fp32) and the
-// W1/b1 gradients (MFMA over pixels from a wave-private bf16 g_h tile in LDS).
+// g_h (never stored), the per-tap products v = g_h * W1 and the W1/b1 gradients (MFMA over
+// pixels from a wave-private bf16 g_h tile in LDS).  v stays in LDS: per tile the kernel forms
+// g_u = g_o + sum_t v[q - d_t][t] over the 18x18 region the tile's pixels reach and applies the
+// x2 upsample adjoint to it, writing the tile's 10x10 low-res patch of g_z; head_patch_gather
+// adds the (at most four) patches covering each low-res pixel in a fixed order.  No v / g_u
+// round trip through HBM (it was 0.6 GB written and read per step at 1024^2 x 4).
 // Register budget (<= 128 VGPRs -> 4 waves/SIMD to overlap the dependent MFMA -> VALU
 // chains): the BN-backward algebra is folded into 4 per-channel constants,
 //   pre = h P + Q,   g_h = P gbn + h D + E   (D = -P c2 is, E = -P (c2 off + c1)),
 // and the constant A fragments (W1 for h, W2^T for s, W1^T for v) are read from LDS.
 template <int K>
-__global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadArgs a) {  // (K = 3: LDS allows 2)
   constexpr int STRIDE = MID * K * 9 + MID;
   constexpr int KJ = K * 9;
   __shared__ float su[18 * 18 * 3];
@@ -1035,11 +1040,13 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   __shared__ __attribute__((aligned(16))) bf16x8 fr[12][64];  // Ah[4], As[4], Av[jb][ch] per lane
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
   __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
-  __shared__ float red[STRIDE];
+  static_assert(STRIDE * 4 <= (int)sizeof(gsw), "red aliases gsw");
+  float* red = (float*)&gsw[0][0];  // (used after the tile loop only)
   __shared__ float gos[K * T2 * T2];
+  __shared__ bf16_t vt[KJ][T2 * T2];    // the tile's per-tap products
+  __shared__ float hxs[18 * 10 * 3];    // horizontal upsample adjoint of g_u [18 rows][10 cols][K]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
-  bf16_t* vb = (bf16_t*)a.v;
   if (tid < MID) {
     float is, of, P, Q;
     bwd_params(a, tid, is, of, P, Q);
@@ -1049,7 +1056,6 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
     pD[tid] = -P * c2 * is;
     pE[tid] = -P * fmaf(c2, of, c1);
   }
-  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
   if (wv == 0) {
     bf16x8 A4[4];
     load_a_w1<K>(a.w1, lane, A4);
@@ -1144,13 +1150,11 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
         v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
         f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
         v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
-        if (pv) {  // planar bf16 v[j][pixel]: for each j the 16 lanes of a row write 32 contiguous bytes
-          const long long P2 = (long long)a.N * H2 * W2, pix = ((long long)n * H2 + oy) * W2 + ox;
+        // v[j][pixel] of the tile (zero where the pixel is outside the image: g is)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (4 * q + i < KJ) vb[(long long)(4 * q + i) * P2 + pix] = f2bf(v0[i]);
-            if (16 + 4 * q + i < KJ) vb[(long long)(16 + 4 * q + i) * P2 + pix] = f2bf(v1[i]);
-          }
+        for (int i = 0; i < 4; ++i) {
+          if (4 * q + i < KJ) vt[4 * q + i][r * T2 + x] = f2bf(v0[i]);
+          if (16 + 4 * q + i < KJ) vt[16 + 4 * q + i][r * T2 + x] = f2bf(v1[i]);
         }
         // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
@@ -1179,9 +1183,71 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
       }
       __syncthreads();
     }
+    // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image
+    for (int i = tid; i < 18 * 18; i += NT) {
+      const int rr = i / 18, cc = i - rr * 18;
+      const int oy = oy0 - 1 + rr, ox = ox0 - 1 + cc;
+      float g[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[k] = 0.f;
+      if (oy >= 0 && oy < H2 && ox >= 0 && ox < W2) {
+        if (rr >= 1 && rr <= T2 && cc >= 1 && cc <= T2)
+#pragma unroll
+          for (int k = 0; k < K; ++k) g[k] = gos[k * T2 * T2 + (rr - 1) * T2 + cc - 1];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int ky = t / 3, kx = t - ky * 3, pr = rr - ky, pc = cc - kx;  // source pixel q - d_t
+          if (pr < 0 || pr >= T2 || pc < 0 || pc >= T2) continue;
+#pragma unroll
+          for (int k = 0; k < K; ++k) g[k] += bf2f(vt[k * 9 + t][pr * T2 + pc]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) su[i * 3 + k] = g[k];
+    }
+    __syncthreads();
+    const int Y0 = oy0 / 2, X0 = ox0 / 2;
+    // x2 upsample adjoint, columns first: hxs[rr][px] = sum_cc wx(ox, X) g_u[rr][cc], X = X0-1+px
+    for (int i = tid; i < 18 * 10; i += NT) {
+      const int rr = i / 10, px = i - rr * 10, X = X0 - 1 + px;
+      float hv[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) hv[k] = 0.f;
+      if (X >= 0 && X < a.w)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int cc = 2 * px - 2 + d, ox = ox0 - 1 + cc;
+          if (cc < 0 || cc >= 18 || ox < 0 || ox >= W2) continue;
+          const float wxv = up2_adj_w(ox, a.w, X);
+#pragma unroll
+          for (int k = 0; k < K; ++k) hv[k] = fmaf(wxv, su[(rr * 18 + cc) * 3 + k], hv[k]);
+        }
+#pragma unroll
+      for (int k = 0; k < K; ++k) hxs[i * 3 + k] = hv[k];
+    }
+    __syncthreads();
+    if (tid < 100) {  // rows: patch[py][px] = sum_rr wy(oy, Y) hxs[rr][px], Y = Y0-1+py
+      const int py = tid / 10, px = tid - py * 10, Y = Y0 - 1 + py;
+      float pv[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) pv[k] = 0.f;
+      if (Y >= 0 && Y < a.h)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int rr = 2 * py - 2 + d, oy = oy0 - 1 + rr;
+          if (rr < 0 || rr >= 18 || oy < 0 || oy >= H2) continue;
+          const float wyv = up2_adj_w(oy, a.h, Y);
+#pragma unroll
+          for (int k = 0; k < K; ++k) pv[k] = fmaf(wyv, hxs[(rr * 10 + px) * 3 + k], pv[k]);
+        }
+#pragma unroll
+      for (int k = 0; k < K; ++k) a.patch[((long long)tile * 100 + tid) * K + k] = pv[k];
+    }
   }
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = sum_x16(agb1[e]);
+  __syncthreads();
+  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
   for (int w = 0; w < 4; ++w) {
     __syncthreads();
     if (wv == w) {
@@ -1206,8 +1272,39 @@ __global__ __launch_bounds__(NT, 3) void head_gh_mfma_kernel(HeadArgs a) {
   for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
 }
 
+// g_z[n][y][x][k] = sum of the (at most four) tile patches covering low-res pixel (y, x), in a
+// fixed order: tile rows y/8 - 1 .. y/8 + 1, then columns (a 16x16 tile at 2H covers low-res
+// rows 8ty - 1 .. 8ty + 8)
+template <int K>
+__global__ __launch_bounds__(256) void head_patch_gather_kernel(const float* patch, float* gz, int N, int h, int w,
+                                                                int tx, int ty) {
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long long)N * h * w) return;
+  const int x = (int)(id % w);
+  const int y = (int)((id / w) % h);
+  const int n = (int)(id / ((long long)w * h));
+  float acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int tr = y / 8 + dy, py = y - 8 * tr + 1;
+    if (tr < 0 || tr >= ty || py < 0 || py >= 10) continue;
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int tc = x / 8 + dx, px = x - 8 * tc + 1;
+      if (tc < 0 || tc >= tx || px < 0 || px >= 10) continue;
+      const float* pp = patch + ((((long long)n * ty + tr) * tx + tc) * 100 + py * 10 + px) * K;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[k] += pp[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) gz[id * K + k] = acc[k];
+}
+
 struct WsLayout {
-  size_t stats, part1, partw, gh, v, gu, scale, shift, cws, total;
+  size_t stats, part1, partw, gh, v, gu, patch, scale, shift, cws, total;
   int grid;
 };
 WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
@@ -1228,8 +1325,11 @@ WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   L.gh = take(dtype == EUNET_F32 ? P2 * MID : 0);  // the bf16 path never stores g_h
   // per-tap products v[j][pixel]: fp32 (fp32 path) / bf16 (bf16 path, the dgrad operand precision
   // of the reference's autocast)
-  L.v = take(dtype == EUNET_F32 ? P2 * ((K * 9 + 3) & ~3) : (P2 * ((K * 9 + 3) & ~3) + 1) / 2);
-  L.gu = take(P2 * K);
+  // fp32 path: per-tap products v[j][pixel] and g_u at 2H; the bf16 path keeps both on chip and
+  // writes 10x10 low-res patches per tile instead
+  L.v = take(dtype == EUNET_F32 ? P2 * ((K * 9 + 3) & ~3) : 0);
+  L.gu = take(dtype == EUNET_F32 ? P2 * K : 0);
+  L.patch = take(dtype == EUNET_F32 ? 0 : (size_t)tiles * 100 * K);
   L.scale = take(MID);
   L.shift = take(MID);
   L.cws = take((size_t)2 * 16 * (MID * K * 9 + MID));  // fp64 colsum stage-1 rows (<= 16 for <= 1024 rows)
@@ -1319,7 +1419,7 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   a.w1 = w1; a.b1 = b1; a.gamma = gamma; a.beta = beta; a.w2 = w2;
   a.mean = mean; a.istd = invstd; a.glog = g_logits; a.gout2h = g_out2h;
   a.tx = cdiv(2 * w, T2); a.ty = cdiv(2 * h, T2); a.ntiles = n * a.tx * a.ty;
-  a.gh = wsf + L.gh; a.v = wsf + L.v; a.gu = wsf + L.gu;
+  a.gh = wsf + L.gh; a.v = wsf + L.v; a.gu = wsf + L.gu; a.patch = wsf + L.patch;
   hipStream_t s = (hipStream_t)stream;
   int rc;
   a.part = wsf + L.part1;
@@ -1335,11 +1435,9 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   const long long P2 = (long long)n * 4 * h * w;
   const int gridw = L.grid;
   if (mf) {
-    a.part = wsf + L.partw;  // g_h, v (bf16) and the W1/b1 partials in one pass
+    a.part = wsf + L.partw;  // g_h, v, the g_z patches and the W1/b1 partials in one pass
     HEAD_DISPATCH(head_gh_mfma_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_gh_mfma");
-    HEAD_DISPATCH_T(head_bwd_gu_kernel, bf16_t, (unsigned)((P2 + 255) / 256), 256, 0, s);
-    EUNET_LAUNCH_CHECK("head_bwd_gu");
   } else {
     HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_bwd_gh");
@@ -1352,6 +1450,14 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   const int ldw = MID * k * 9 + MID;
   if ((rc = eunet_colsum_ld(a.part, gridw, MID * k * 9, ldw, gw1, cws, s))) return rc;
   if ((rc = eunet_colsum_ld(a.part + MID * k * 9, gridw, MID, ldw, gb1, cws, s))) return rc;
+  if (mf) {
+    const unsigned gg = (unsigned)(((long long)n * h * w + 255) / 256);
+    if (k == 1) head_patch_gather_kernel<1><<<gg, 256, 0, s>>>(a.patch, gz, n, h, w, a.tx, a.ty);
+    else if (k == 2) head_patch_gather_kernel<2><<<gg, 256, 0, s>>>(a.patch, gz, n, h, w, a.tx, a.ty);
+    else head_patch_gather_kernel<3><<<gg, 256, 0, s>>>(a.patch, gz, n, h, w, a.tx, a.ty);
+    EUNET_LAUNCH_CHECK("head_patch_gather");
+    return EUNET_OK;
+  }
   eunet_act ghi = {a.gu, n, 2 * h, 2 * w, k, k, 0, EUNET_F32};
   eunet_act glo = {gz, n, h, w, k, k, 0, EUNET_F32};
   return eunet_upsample_bwd(&ghi, &glo, stream);
