@@ -39,7 +39,9 @@ struct SmallArgs {
 // 8 lanes per pixel (lane group g = lane & 7 owns output channels co0+8g..+7),
 // 32 pixels per pass = one output row of the 16x32 tile; per-thread Welford over
 // its 8 pixels, Chan-combined across lanes and waves (no transposes)
-template <typename T>
+// C1: one input channel (enc1.0 of the 1-channel configurations) -- the lane's 9 x 8 weights
+// live in registers instead of being re-read from LDS for every pixel.
+template <typename T, bool C1>
 __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
   __shared__ float xs[(SFH + 2) * (STW + 2) * SCI];
   __shared__ __attribute__((aligned(16))) float wsm[SCI * 9 * 64];  // [ci*9+t][64 co]
@@ -64,6 +66,12 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
     wsm[r * 64 + co] = (co0 + co < a.cout) ? a.w[(long long)(co0 + co) * cin * 9 + r] : 0.f;
   }
   __syncthreads();
+  float wr[C1 ? 9 : 1][8];
+  if constexpr (C1)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wr[t][e] = wsm[t * 64 + 8 * g + e];
   float bias[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias[e] = (a.b != nullptr && co0 + 8 * g + e < a.cout) ? a.b[co0 + 8 * g + e] : 0.f;
@@ -80,7 +88,16 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = bias[e];
-    for (int ci = 0; ci < cin; ++ci) {
+    if constexpr (C1) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t - ky * 3;
+        const float v = xs[((r + ky) * (STW + 2) + c + kx) * SCI];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(wr[t][e], v, acc[e]);
+      }
+    }
+    for (int ci = 0; ci < (C1 ? 0 : cin); ++ci) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
@@ -1219,10 +1236,14 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, 
   a.y = y->ptr; a.yct = y->ctot; a.yco = y->coff; a.cout = y->c;
   a.stats = stats; a.tx = cdiv(x->w, STW); a.ty = cdiv(x->h, SFH); a.ntiles = x->n * a.tx * a.ty;
   dim3 grid(a.ntiles, cdiv(y->c, 64));
-  if (x->dtype == EUNET_BF16)
-    conv_small_fwd_kernel<bf16_t><<<grid, NT, 0, (hipStream_t)stream>>>(a);
-  else
-    conv_small_fwd_kernel<float><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  const bool c1 = x->c == 1;
+  if (x->dtype == EUNET_BF16) {
+    if (c1) conv_small_fwd_kernel<bf16_t, true><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    else conv_small_fwd_kernel<bf16_t, false><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  } else {
+    if (c1) conv_small_fwd_kernel<float, true><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+    else conv_small_fwd_kernel<float, false><<<grid, NT, 0, (hipStream_t)stream>>>(a);
+  }
   EUNET_LAUNCH_CHECK("conv_small_fwd");
   return EUNET_OK;
 }
