@@ -447,49 +447,63 @@ __global__ __launch_bounds__(256) void bnrelu_kernel(const T* y, long long P, in
 template <typename T>
 __global__ __launch_bounds__(256) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
                                                         const float* sc, const float* sh, T* out, int oct, int oco) {
+  // two horizontally adjacent low-res pixels (j0, j0 + 1) per thread: 3 x 4 neighbourhood loads
+  // and transforms for 2 x 4 outputs each (9 per pixel before); rows are swept one at a time
   constexpr int E = Vec16<T>::N;
-  const int U = C / E, H2 = 2 * h, W2 = 2 * w;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w, wb = (w + 1) / 2;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)N * h * w * U;
+  const long long total = (long long)N * h * wb * U;
   if (id >= total) return;
   const int u = (int)(id % U);
   long long p = id / U;
-  const int j = (int)(p % w); p /= w;
+  const int jb = (int)(p % wb); p /= wb;
   const int i = (int)(p % h);
   const int n = (int)(p / h);
-  const int c = u * E;
+  const int c = u * E, j0 = 2 * jb;
+  const bool two = j0 + 1 < w;
   float s[E], t[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) { s[e] = sc[c + e]; t[e] = sh[c + e]; }
-  const int rs[3] = {max(i - 1, 0), i, min(i + 1, h - 1)}, cs[3] = {max(j - 1, 0), j, min(j + 1, w - 1)};
-  float v[3][3][E];
+  const int rs[3] = {max(i - 1, 0), i, min(i + 1, h - 1)};
+  const int cs[4] = {max(j0 - 1, 0), j0, min(j0 + 1, w - 1), min(j0 + 2, w - 1)};
+  uint4 raw[3][4];
 #pragma unroll
   for (int a = 0; a < 3; ++a)
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const long long pix = (long long)(n * h + rs[a]) * w + cs[b];
-      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), v[a][b]);
-#pragma unroll
-      for (int e = 0; e < E; ++e) v[a][b][e] = fmaxf(fmaf(v[a][b][e], s[e], t[e]), 0.f);
-    }
+    for (int b = 0; b < 4; ++b)
+      raw[a][b] = *(const uint4*)(y + ((long long)(n * h + rs[a]) * w + cs[b]) * yct + yco + c);
   // output 2i: rows (i-1, i) weights (0.25, 0.75), or row i with weights (1, 0) at i = 0;
   // output 2i+1: rows (i, i+1) weights (0.75, 0.25) (i+1 clamped).  Same along x; x first.
   const float wya = i > 0 ? 0.25f : 1.f, wyb = i > 0 ? 0.75f : 0.f;
-  const float wxa = j > 0 ? 0.25f : 1.f, wxb = j > 0 ? 0.75f : 0.f;
+  const float wxa = j0 > 0 ? 0.25f : 1.f, wxb = j0 > 0 ? 0.75f : 0.f;
+  float xr[3][4][E];  // x-interpolated rows: output columns 2j0 .. 2j0 + 3
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
+  for (int a = 0; a < 3; ++a) {
+    float v[4][E];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      Vec16<T>::unpack(raw[a][b], v[b]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[b][e] = fmaxf(fmaf(v[b][e], s[e], t[e]), 0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      xr[a][0][e] = fmaf(wxb, v[1][e], wxa * (j0 > 0 ? v[0][e] : v[1][e]));
+      xr[a][1][e] = fmaf(0.25f, v[2][e], 0.75f * v[1][e]);
+      xr[a][2][e] = fmaf(0.75f, v[2][e], 0.25f * v[1][e]);  // column 2(j0+1): j0 + 1 > 0
+      xr[a][3][e] = fmaf(0.25f, v[3][e], 0.75f * v[2][e]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    if (b >= 2 && !two) break;
     float o0[E], o1[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      float x[3];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-        x[r] = b == 0 ? fmaf(wxb, v[r][1][e], wxa * (j > 0 ? v[r][0][e] : v[r][1][e]))
-                      : fmaf(0.25f, v[r][2][e], 0.75f * v[r][1][e]);
-      o0[e] = fmaf(wyb, x[1], wya * (i > 0 ? x[0] : x[1]));
-      o1[e] = fmaf(0.25f, x[2], 0.75f * x[1]);
+      o0[e] = fmaf(wyb, xr[1][b][e], wya * (i > 0 ? xr[0][b][e] : xr[1][b][e]));
+      o1[e] = fmaf(0.25f, xr[2][b][e], 0.75f * xr[1][b][e]);
     }
-    const long long po = (long long)(n * H2 + 2 * i) * W2 + 2 * j + b;
+    const long long po = (long long)(n * H2 + 2 * i) * W2 + 2 * j0 + b;
     *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(o0);
     *(uint4*)(out + (po + W2) * oct + oco + c) = Vec16<T>::pack(o1);
   }
@@ -1353,7 +1367,7 @@ int eunet_bnrelu_upsample(const eunet_act* y, const float* scale, const float* s
                     out->dtype == y->dtype,
                 "bnrelu_upsample: shape");
   const int E = e16(y->dtype);
-  const long long total = (long long)y->n * y->h * y->w * (y->c / E);
+  const long long total = (long long)y->n * y->h * ((y->w + 1) / 2) * (y->c / E);
   const unsigned g = (unsigned)((total + 255) / 256);
   if (y->dtype == EUNET_BF16)
     bnrelu_up_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, y->n, y->h, y->w, y->c,
