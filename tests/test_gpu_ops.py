@@ -542,6 +542,68 @@ def test_conv3x3_k64_persistent():
     assert rel(red[Cout:], (gp * xh).sum(dim=(0, 1, 2))) < 1e-5
 
 
+def test_conv3x3_deep_layer_shapes():
+    """A deep-layer shape in bf16: Cin 272 (a partial last 32-channel K-chunk), Cout 256 (four
+    co-blocks), ragged tiles, a channel-slice input with the per-sample BN+ReLU transform, bias
+    and BN partials; then the fused dgrad epilogue (BN-backward reduction + Dropout2d scale) of
+    a 288 -> 256 conv, against fp64 references."""
+    ops = _ops()
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(15)
+    N, H, W, Cin, Cout, CT, CO = 2, 20, 44, 272, 256, 304, 16
+    buf = torch.randn(N, H, W, CT, generator=g).to(DEV, dt)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 50
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    sc = torch.rand(N, Cin, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(N, Cin, generator=g, dtype=torch.float64) * 0.3
+    x = buf.double().cpu()[..., CO:CO + Cin]
+    xt = torch.relu(x * sc[:, None, None, :] + sh[:, None, None, :]).to(dt).double()
+    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), b, padding=1))
+    y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
+    tiles = ops.conv3x3_tiles(ops.act(y))
+    st = torch.empty(tiles * (2 * Cout + 1), dtype=torch.float32, device=DEV)
+    ops.conv3x3_fwd(ops.act(buf, CO, Cin), wp, ops.act(y), bias=b.float().to(DEV), scale=sc.float().to(DEV),
+                    shift=sh.float().to(DEV), nstride=Cin, stats=st)
+    gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mean, inv = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    s1, s2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, rm, rv, mean, inv, s1, s2)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < TOL[dt]
+    yr = y.double().cpu()  # the stored outputs (stats are taken from the fp32 accumulators)
+    assert rel(mean, yr.mean(dim=(0, 1, 2))) < 1e-2
+    assert rel(1.0 / inv ** 2 - 1e-5, yr.var(dim=(0, 1, 2), unbiased=False)) < 2e-2
+    # dgrad of a 256 -> 288 conv: gx [.., 256] = conv_transpose(gy [.., 288]) * gs, fused BN-bwd sums
+    Cd = 288
+    w2 = torch.randn(Cd, Cout, 3, 3, generator=g, dtype=torch.float64) / 50  # conv weight [288 out][256 in]
+    gy = torch.randn(N, H, W, Cd, generator=g).to(dt).double()
+    gs = ((torch.rand(N, Cout, generator=g) > 0.3).double() / 0.7)
+    yb = torch.randn(N, H, W, Cout, generator=g).to(DEV, dt)
+    bm = (torch.randn(Cout, generator=g) * 0.1).to(DEV)
+    bi = (torch.rand(Cout, generator=g) + 0.5).to(DEV)
+    bgam = (torch.rand(Cout, generator=g) + 0.5).to(DEV)
+    bbet = (torch.randn(Cout, generator=g) * 0.2).to(DEV)
+    wpt = ops.conv3x3_pack(w2.float().to(DEV), dt, flip=True)
+    gx = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    part = torch.empty(tiles * 2 * Cout, device=DEV)
+    ops.conv3x3_dgrad_bnbwd(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx), ops.act(yb), bm, bi, bgam * bi,
+                            bbet - bm * bgam * bi, part, gscale=gs.float().to(DEV))
+    gx_plain = torch.empty_like(gx)
+    ops.conv3x3_dgrad(ops.act(gy.to(DEV, dt)), wpt, ops.act(gx_plain))
+    red = torch.empty(2 * Cout, device=DEV)
+    ops.colsum(part, tiles, 2 * Cout, red)
+    torch.cuda.synchronize()
+    gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w2.to(dt).double(), padding=1))
+    assert rel(gx_plain, gx_ref) < TOL[dt]
+    assert rel(gx, gx_ref * gs[:, None, None, :]) < TOL[dt]
+    xh = (yb.double() - bm.double()) * bi.double()
+    gp = torch.where(bgam.double() * xh + bbet.double() > 0, gx.double(), torch.zeros_like(xh))
+    assert rel(red[:Cout], gp.sum(dim=(0, 1, 2))) < 1e-5
+    assert rel(red[Cout:], (gp * xh).sum(dim=(0, 1, 2))) < 1e-5
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("h,w", [(7, 9), (8, 16), (1, 3)])
 def test_upsample_bwd_odd_sizes(dt, h, w):
