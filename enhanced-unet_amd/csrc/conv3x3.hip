@@ -1026,12 +1026,15 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
 }
 
 
+// weight-gradient blocks per launch: two resident per CU (1024 / 2048 measured equal / slower in
+// the bench, where the wgrad shares the chip with the data-gradient stream: profiles/r02_ab_conv.txt)
+constexpr int WG_BLOCKS = 512;
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
   const bool bf = dtype == EUNET_BF16;
   const int ntiles = dy->n * cdiv(dy->h, bf ? TH : WF_TH) * cdiv(dy->w, bf ? TW : WF_TW);
   const int blocks = cdiv(dy->c, 64) * cdiv(cin, bf ? KCW : WF_CI);
-  int s = cdiv(512, blocks);  // two resident blocks per CU
+  int s = cdiv(WG_BLOCKS, blocks);
   s = s < 1 ? 1 : s;
   s = s > ntiles ? ntiles : s;
   // keep partials <= 256 MiB
