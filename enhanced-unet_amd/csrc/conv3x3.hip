@@ -471,11 +471,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 // transpose_flip: pack W'[o=ci][i=co][t] = W[co][ci][8-t] (dgrad operand)
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ void pack_kernel(const float* w, int cout, int cin, int flip, T* wp, int cout_p, int cin_p) {
+__device__ __forceinline__ void pack_elem(const float* w, int cout, int cin, int flip, T* wp, int cout_p, int cin_p,
+                                          long long id) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-  const long long total = (long long)cin_p * cout_p * 9;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= total) return;
   // id enumerates output elements in packed order
   const int e = (int)(id % E);
   long long r = id / E;
@@ -493,6 +491,25 @@ __global__ void pack_kernel(const float* w, int cout, int cin, int flip, T* wp, 
     if (o < cin && i < cout) v = w[((long long)i * cin + o) * 9 + (8 - t)];
   }
   Elem<T>::st(wp + id, v);
+}
+
+template <typename T>
+__global__ void pack_kernel(const float* w, int cout, int cin, int flip, T* wp, int cout_p, int cin_p) {
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id < (long long)cin_p * cout_p * 9) pack_elem<T>(w, cout, cin, flip, wp, cout_p, cin_p, id);
+}
+
+// every weight tensor of a step packed in one launch: blockIdx.y = tensor
+struct PackBatch {
+  eunet_pack_desc d[EUNET_PACK_MAX];
+  int cout_p[EUNET_PACK_MAX], cin_p[EUNET_PACK_MAX];
+};
+template <typename T>
+__global__ void pack_many_kernel(PackBatch b) {
+  const eunet_pack_desc& d = b.d[blockIdx.y];
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id < (long long)b.cin_p[blockIdx.y] * b.cout_p[blockIdx.y] * 9)
+    pack_elem<T>(d.w, d.cout, d.cin, d.flip, (T*)d.wp, b.cout_p[blockIdx.y], b.cin_p[blockIdx.y], id);
 }
 
 // ---------------------------------------------------------------------------
@@ -943,6 +960,26 @@ int eunet_conv3x3_pack(const float* w, int cout, int cin, int flip, void* wp, in
   else
     pack_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(w, cout, cin, flip, (float*)wp, cp, kp);
   EUNET_LAUNCH_CHECK("conv3x3_pack");
+  return EUNET_OK;
+}
+
+int eunet_conv3x3_pack_many(const eunet_pack_desc* descs, int n, int dtype, void* stream) {
+  EUNET_REQUIRE(descs && n > 0 && n <= EUNET_PACK_MAX, "conv3x3_pack_many: 1..%d tensors", EUNET_PACK_MAX);
+  PackBatch b;
+  long long most = 0;
+  for (int i = 0; i < n; ++i) {
+    const eunet_pack_desc& d = descs[i];
+    EUNET_REQUIRE(d.w && d.wp && d.cout > 0 && d.cin > 0, "conv3x3_pack_many: bad descriptor %d", i);
+    b.d[i] = d;
+    const int go = d.flip ? d.cin : d.cout, gi = d.flip ? d.cout : d.cin;
+    b.cout_p[i] = cdiv(go, BN) * BN;
+    b.cin_p[i] = cdiv(gi, kchunk(dtype)) * kchunk(dtype);
+    most = std::max(most, (long long)b.cout_p[i] * b.cin_p[i] * 9);
+  }
+  dim3 grid((unsigned)((most + 255) / 256), (unsigned)n);
+  if (dtype == EUNET_BF16) pack_many_kernel<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(b);
+  else pack_many_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(b);
+  EUNET_LAUNCH_CHECK("conv3x3_pack_many");
   return EUNET_OK;
 }
 

@@ -22,6 +22,14 @@ class Act(ctypes.Structure):
                 ("ctot", c_int), ("coff", c_int), ("dtype", c_int)]
 
 
+class PackDesc(ctypes.Structure):
+    """eunet_pack_desc (include/eunet.h)."""
+    _fields_ = [("w", c_void_p), ("cout", c_int), ("cin", c_int), ("flip", c_int), ("wp", c_void_p)]
+
+
+PACK_MAX = 32  # EUNET_PACK_MAX
+
+
 class LossParams(ctypes.Structure):
     """eunet_loss_params (include/eunet.h): the loss configuration of one combined-loss call."""
     _fields_ = [("ce_weight", c_float * 3), ("alpha", c_float * 3), ("gamma", c_float), ("ignore_index", c_int),
@@ -38,6 +46,7 @@ SIGNATURES = {
     "eunet_nchw_to_nhwc": [_f, _P, c_void_p],
     "eunet_conv3x3_packed_bytes": [c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_conv3x3_pack": [_f, c_int, c_int, c_int, _f, c_int, c_void_p],
+    "eunet_conv3x3_pack_many": [c_void_p, c_int, c_int, c_void_p],
     "eunet_conv3x3_tiles": [_P, POINTER(c_int)],
     "eunet_conv3x3_fwd": [_P, _f, _f, c_int, _f, _f, _P, _f, c_void_p],
     "eunet_conv3x3_dgrad_bnbwd": [_P, _f, _P, _P, _f, _f, _f, _f, _f, _f, c_void_p],

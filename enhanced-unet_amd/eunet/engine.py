@@ -123,7 +123,23 @@ class UNetEngine:
         C = y.shape[3]
         return _e(tiles * (2 * C + 1), torch.float32, y.device), tiles
 
-    def _block_fwd(self, nm, X: ops.Act, training, P, B, small: bool):
+    def _pack_all(self, P, training: bool):
+        """Every 3x3 weight of the trunk packed in one launch: the forward operands and, when
+        training, the dgrad (transposed + flipped) operands -- the weights do not change between
+        this forward and its backward.  name -> packed tensor; flipped ones under name + "^T"."""
+        items, names = [], []
+        for nm in BLOCKS:
+            p = f"{self.prefix}{nm}"
+            for i in ((3,) if nm == "enc1" else (0, 3)):  # enc1.0 runs on the direct small-Cin kernel
+                items.append((P[f"{p}.{i}.weight"], False))
+                names.append(f"{p}.{i}.weight")
+            if training:
+                for i in ((3,) if nm == "enc1" else (3, 0)):
+                    items.append((P[f"{p}.{i}.weight"], True))
+                    names.append(f"{p}.{i}.weight^T")
+        return dict(zip(names, ops.conv3x3_pack_many(items, self.dtype)))
+
+    def _block_fwd(self, nm, X: ops.Act, training, P, B, small: bool, wps=None):
         p = f"{self.prefix}{nm}"
         N, H, W = X.n, X.h, X.w
         C = P[p + ".0.weight"].shape[0]
@@ -135,10 +151,10 @@ class UNetEngine:
         if small:
             ops.conv_small_fwd(X, P[p + ".0.weight"], P[p + ".0.bias"], ops.act(ya), st)
         else:
-            wp = ops.conv3x3_pack(P[p + ".0.weight"], self.dtype, flip=False)
+            wp = wps[p + ".0.weight"] if wps else ops.conv3x3_pack(P[p + ".0.weight"], self.dtype, flip=False)
             ops.conv3x3_fwd(X, wp, ops.act(ya), bias=P[p + ".0.bias"], stats=st, sub=enc)
         bna = self._bn(p + ".1", st, tiles, C, training, P, B)
-        wp = ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
+        wp = wps[p + ".3.weight"] if wps else ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
         za = None
         if MATERIALIZE_ZA:  # one BN+ReLU pass; conv .3 forward and weight gradient read za as is
             za = _e((N, H, W, C), self.dtype, dev)
@@ -187,6 +203,8 @@ class UNetEngine:
         ch = [b, 2 * b, 4 * b, 8 * b]
         lv = [(H >> i, W >> i) for i in range(4)]
         S = {}
+        wps = self._pack_all(P, training)
+        S["wp"] = wps
         xin = _e((N, H, W, Cin), dt, dev)
         ops.nchw_to_nhwc(x.contiguous().float(), xin)
         cat4 = _e((N, *lv[2], ch[3] + ch[2]), dt, dev)
@@ -207,19 +225,19 @@ class UNetEngine:
             ops.bnrelu_upsample(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
                                 ops.act(cat, 0, s["yb"].shape[3]))
 
-        S["enc1"] = self._block_fwd("enc1", ops.act(xin), training, P, B, small=True)
+        S["enc1"] = self._block_fwd("enc1", ops.act(xin), training, P, B, small=True, wps=wps)
         consume_pool("enc1", cat2, ch[1], p1)
-        S["enc2"] = self._block_fwd("enc2", ops.act(p1), training, P, B, small=False)
+        S["enc2"] = self._block_fwd("enc2", ops.act(p1), training, P, B, small=False, wps=wps)
         consume_pool("enc2", cat3, ch[2], p2)
-        S["enc3"] = self._block_fwd("enc3", ops.act(p2), training, P, B, small=False)
+        S["enc3"] = self._block_fwd("enc3", ops.act(p2), training, P, B, small=False, wps=wps)
         consume_pool("enc3", cat4, ch[3], p3)
-        S["enc4"] = self._block_fwd("enc4", ops.act(p3), training, P, B, small=False)
+        S["enc4"] = self._block_fwd("enc4", ops.act(p3), training, P, B, small=False, wps=wps)
         consume_up("enc4", cat4)
-        S["dec4"] = self._block_fwd("dec4", ops.act(cat4), training, P, B, small=False)
+        S["dec4"] = self._block_fwd("dec4", ops.act(cat4), training, P, B, small=False, wps=wps)
         consume_up("dec4", cat3)
-        S["dec3"] = self._block_fwd("dec3", ops.act(cat3), training, P, B, small=False)
+        S["dec3"] = self._block_fwd("dec3", ops.act(cat3), training, P, B, small=False, wps=wps)
         consume_up("dec3", cat2)
-        S["dec2"] = self._block_fwd("dec2", ops.act(cat2), training, P, B, small=False)
+        S["dec2"] = self._block_fwd("dec2", ops.act(cat2), training, P, B, small=False, wps=wps)
         s = S["dec2"]
         z = _e((N, H, W, K), torch.float32, dev)
         ops.bnrelu_conv1x1(ops.act(s["yb"]), s["bnb"]["scale"], s["bnb"]["shift"],
@@ -284,7 +302,9 @@ class UNetEngine:
             wgrad(p + ".3", ops.act(s["za"]), gyb)
         else:
             wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
-        wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
+        wpt = S["wp"].get(p + ".3.weight^T") if S.get("wp") else None
+        if wpt is None:
+            wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
         gaa = torch.empty_like(ya)
         ctiles = ops.conv3x3_tiles(ops.act(gaa))
         cpart = _e(ctiles * 2 * C, torch.float32, dev)
@@ -303,7 +323,9 @@ class UNetEngine:
                 sink.ready(names)
         if not need_gx:
             return None
-        wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
+        wpt = S["wp"].get(p + ".0.weight^T") if S.get("wp") else None
+        if wpt is None:
+            wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
         gx = _e((N, H, W, X.c), dt, dev)
         ops.conv3x3_dgrad(ops.act(gya), wpt, ops.act(gx))
         return gx

@@ -62,6 +62,25 @@ def conv3x3_pack(w: torch.Tensor, dtype, flip: bool) -> torch.Tensor:
     return wp
 
 
+def conv3x3_pack_many(items, dtype):
+    """[(w, flip), ...] -> packed tensors, one launch per PACK_MAX tensors (eunet_conv3x3_pack_many)."""
+    out = []
+    for lo in range(0, len(items), _lib.PACK_MAX):
+        chunk = items[lo:lo + _lib.PACK_MAX]
+        descs = (_lib.PackDesc * len(chunk))()
+        keep = []
+        for d, (w, flip) in zip(descs, chunk):
+            cout, cin = w.shape[0], w.shape[1]
+            nbytes = conv3x3_packed_bytes(cin if flip else cout, cout if flip else cin, dtype)
+            wp = torch.empty(nbytes // (2 if dtype == torch.bfloat16 else 4), dtype=dtype, device=w.device)
+            wc = w.contiguous()
+            keep.append(wc)
+            d.w, d.cout, d.cin, d.flip, d.wp = wc.data_ptr(), cout, cin, int(flip), wp.data_ptr()
+            out.append(wp)
+        call("eunet_conv3x3_pack_many", ctypes.cast(descs, ctypes.c_void_p), len(chunk), DTYPES[dtype], _stream())
+    return out
+
+
 def conv3x3_tiles(y_act: Act) -> int:
     t = c_int()
     call("eunet_conv3x3_tiles", ctypes.byref(y_act), ctypes.byref(t))

@@ -57,6 +57,15 @@ int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
 int eunet_conv3x3_packed_bytes(int cout, int cin, int dtype, size_t* bytes);
 int eunet_conv3x3_pack(const float* w, int cout, int cin, int transpose_flip, void* wp, int dtype,
                        void* stream);
+/* up to EUNET_PACK_MAX packs in one launch (a step's forward and dgrad operands: the weights do
+ * not change between the forward and the backward); each wp sized by eunet_conv3x3_packed_bytes */
+#define EUNET_PACK_MAX 32
+typedef struct {
+  const float* w;  /* torch [cout][cin][3][3] fp32 */
+  int cout, cin, flip;
+  void* wp;
+} eunet_pack_desc;
+int eunet_conv3x3_pack_many(const eunet_pack_desc* descs, int n, int dtype, void* stream);
 /* number of pixel tiles = rows of the BatchNorm statistics partial buffer */
 int eunet_conv3x3_tiles(const eunet_act* y, int* tiles);
 /* y = conv(t(x)) + bias, t = relu(x*in_scale+in_shift) per input channel when
