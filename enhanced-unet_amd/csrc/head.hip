@@ -23,6 +23,7 @@ constexpr int NT = 256;
 constexpr int T2 = 16;  // tile side at 2H
 constexpr int MID = 64;
 constexpr int HEAD_BLOCKS = 768;  // persistent grid: 3 resident blocks x 256 CUs (no second round)
+constexpr int HEAD_BLOCKS4 = 1024;  // the bf16 stats / out kernels: 4 resident blocks per CU
 
 struct HeadArgs {
   const float* z; int N, h, w, K;
@@ -727,7 +728,7 @@ __device__ __forceinline__ float sum_x16(float v) {
 }
 
 template <int K>
-__global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_stats_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
   __shared__ float zs[ZR * ZR * 3];
   __shared__ float wn_s[4], wm_s[4][MID], wq_s[4][MID];
@@ -811,7 +812,7 @@ __global__ __launch_bounds__(NT) void head_stats_mfma_kernel(HeadArgs a) {
 }
 
 template <int K>
-__global__ __launch_bounds__(NT) void head_out_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_out_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
   __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float scs[MID], shs[MID];
@@ -1305,7 +1306,7 @@ __global__ __launch_bounds__(256) void head_patch_gather_kernel(const float* pat
 
 struct WsLayout {
   size_t stats, part1, partw, gh, v, gu, patch, scale, shift, cws, total;
-  int grid;
+  int grid, grid4;  // grid4: the bf16 forward kernels' grid (also the rows of the stats partials)
 };
 WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   const int tiles = N * cdiv(2 * w, T2) * cdiv(2 * h, T2);
@@ -1313,13 +1314,14 @@ WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   const size_t P2 = (size_t)N * 4 * h * w;
   WsLayout L;
   L.grid = grid;
+  L.grid4 = dtype == EUNET_BF16 ? (tiles < HEAD_BLOCKS4 ? tiles : HEAD_BLOCKS4) : grid;
   size_t off = 0;
   auto take = [&](size_t floats) {
     size_t o = off;
     off += (floats + 63) / 64 * 64;
     return o;
   };
-  L.stats = take((size_t)grid * (2 * MID + 1));
+  L.stats = take((size_t)L.grid4 * (2 * MID + 1));
   L.part1 = take((size_t)grid * ((K + 2) * MID + K));
   L.partw = take((size_t)grid * (MID * K * 9 + MID));
   L.gh = take(dtype == EUNET_F32 ? P2 * MID : 0);  // the bf16 path never stores g_h
@@ -1384,10 +1386,10 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
   a.scale = wsf + L.scale; a.shift = wsf + L.shift;
   hipStream_t s = (hipStream_t)stream;
   if (training) {
-    if (mf) HEAD_DISPATCH(head_stats_mfma_kernel, L.grid, NT, 0, s);
+    if (mf) HEAD_DISPATCH(head_stats_mfma_kernel, L.grid4, NT, 0, s);
     else HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_stats");
-    int rc = eunet_bn_finalize(a.stats, L.grid, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
+    int rc = eunet_bn_finalize(a.stats, L.grid4, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
                                wsf + L.scale, wsf + L.shift, nullptr, stream);
     if (rc) return rc;
   } else {
@@ -1395,7 +1397,7 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     int rc = eunet_bn_eval_affine(MID, gamma, beta, run_mean, run_var, eps, wsf + L.scale, wsf + L.shift, stream);
     if (rc) return rc;
   }
-  if (mf) HEAD_DISPATCH(head_out_mfma_kernel, L.grid, NT, 0, s);
+  if (mf) HEAD_DISPATCH(head_out_mfma_kernel, L.grid4, NT, 0, s);
   else HEAD_DISPATCH(head_out_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_out");
   return EUNET_OK;
