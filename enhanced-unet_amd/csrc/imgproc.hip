@@ -1,0 +1,537 @@
+// cv2 image operations of the reference's data path, as HIP kernels.
+//
+// Reference call sites:
+//   dataset.py:58-131   CellDataset._apply_cell_specific_preprocessing (every split, :204):
+//                       RGB->LAB, CLAHE(2.5, 8x8) on L, LAB->RGB; Sobel / Laplacian edge features of
+//                       the gray image; live-cell brightening; CLAHE(3.0) of the gray image on dead
+//                       cells; edge blend; 0.85 / 0.15 mix with the input; GaussianBlur(3x3, 1.0)
+//                       unsharp mask (addWeighted 1.3 / -0.3)
+//   dataset.py:255-294  augmentations: HSV saturation, CLAHE(U(1.5, 3)), filter2D sharpen, HSV jitter
+//   train_eval.py:365-395  Evaluator._prepare_image_tensor: CLAHE(2.0) on L + filter2D sharpen 0.15
+//
+// cv2 is not importable in this image, so these follow OpenCV's documented algorithms and are
+// pinned to the numpy restatement in oracle/imgproc_ref.py, not to cv2 (parity unpinned):
+//   RGB2GRAY 8U    Y = (4899 R + 9617 G + 1868 B + 2^13) >> 14
+//   RGB<->Lab 8U   sRGB gamma, D65 XYZ, L*255/100, a+128, b+128 -- evaluated in fp32 and rounded
+//                  (cv2's fixed-point tables are not reproduced: +-1 level)
+//   RGB<->HSV 8U   H in [0, 180): cv2's hsv_shift = 12 integer division tables; HSV2RGB in fp32
+//   CLAHE          OpenCV CLAHE_Impl: tiles of the image padded to a multiple of the grid by
+//                  BORDER_REFLECT_101, clip = max(int(clipLimit * tileArea / 256), 1), excess
+//                  redistributed (batch + residual stepping), LUT = round(cdf * 255 / tileArea),
+//                  bilinear blend of the four neighbouring tile LUTs (txf = x / tileW - 0.5)
+//   filter2D 8U    fp32 sum over the 3x3 taps in row-major order, BORDER_REFLECT_101, round + saturate
+//   GaussianBlur   3x3, sigma 1, 8U: separable fixed-point weights (70, 116, 70) / 256
+//   Sobel / Laplacian (CV_64F, ksize 3 / 1), BORDER_REFLECT_101
+// One thread per pixel except the CLAHE histograms (one block per tile, integer LDS counts) and
+// the edge-feature maximum (per-block maxima, reduced in a second pass).
+#include "common.h"
+
+// every fp32 / fp64 expression below rounds per operation, as the reference's numpy arrays do
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int NT = 256;
+
+unsigned grid1(long long n) {
+  long long b = (n + NT - 1) / NT;
+  return (unsigned)(b > 65535 ? 65535 : (b < 1 ? 1 : b));
+}
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * (n - 1) - i;
+  return i;
+}
+
+__device__ __forceinline__ uint8_t sat_u8(float v) {  // saturate_cast<uchar>(v): round half to even, clamp
+  const float r = rintf(v);
+  return (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+}
+
+__device__ __forceinline__ uint8_t gray_u8(int r, int g, int b) { return (uint8_t)((4899 * r + 9617 * g + 1868 * b + (1 << 13)) >> 14); }
+
+// ---- Lab (fp32 formulas of cv2's documentation, D65, sRGB gamma) ----
+__device__ __forceinline__ float srgb_lin(float c) { return c <= 0.04045f ? c / 12.92f : powf((c + 0.055f) / 1.055f, 2.4f); }
+__device__ __forceinline__ float srgb_enc(float c) { return c <= 0.0031308f ? 12.92f * c : 1.055f * powf(c, 1.f / 2.4f) - 0.055f; }
+__device__ __forceinline__ float lab_f(float t) { return t > 0.008856f ? cbrtf(t) : 7.787f * t + 16.f / 116.f; }
+__device__ __forceinline__ float lab_finv(float f) { return f > 0.206893f ? f * f * f : (f - 16.f / 116.f) / 7.787f; }
+
+__device__ __forceinline__ void rgb2lab(int R, int G, int B, uint8_t& L8, uint8_t& a8, uint8_t& b8) {
+  const float r = srgb_lin(R / 255.f), g = srgb_lin(G / 255.f), b = srgb_lin(B / 255.f);
+  const float X = (0.412453f * r + 0.357580f * g + 0.180423f * b) / 0.950456f;
+  const float Y = 0.212671f * r + 0.715160f * g + 0.072169f * b;
+  const float Z = (0.019334f * r + 0.119193f * g + 0.950227f * b) / 1.088754f;
+  const float fx = lab_f(X), fy = lab_f(Y), fz = lab_f(Z);
+  const float L = Y > 0.008856f ? 116.f * fy - 16.f : 903.3f * Y;
+  L8 = sat_u8(L * 255.f / 100.f);
+  a8 = sat_u8(500.f * (fx - fy) + 128.f);
+  b8 = sat_u8(200.f * (fy - fz) + 128.f);
+}
+
+__device__ __forceinline__ void lab2rgb(int L8, int a8, int b8, uint8_t& R, uint8_t& G, uint8_t& B) {
+  const float L = L8 * 100.f / 255.f, a = a8 - 128.f, b = b8 - 128.f;
+  float Y, fy;
+  if (L <= 7.9996f) {  // OpenCV Lab2RGB: linear segment below L = 903.3 * 0.008856
+    Y = L / 903.3f;
+    fy = 7.787f * Y + 16.f / 116.f;
+  } else {
+    fy = (L + 16.f) / 116.f;
+    Y = fy * fy * fy;
+  }
+  const float fx = fy + a / 500.f, fz = fy - b / 200.f;
+  const float X = lab_finv(fx) * 0.950456f, Z = lab_finv(fz) * 1.088754f;
+  const float r = 3.240479f * X - 1.53715f * Y - 0.498535f * Z;
+  const float g = -0.969256f * X + 1.875991f * Y + 0.041556f * Z;
+  const float bb = 0.055648f * X - 0.204043f * Y + 1.057311f * Z;
+  R = sat_u8(255.f * srgb_enc(fminf(fmaxf(r, 0.f), 1.f)));
+  G = sat_u8(255.f * srgb_enc(fminf(fmaxf(g, 0.f), 1.f)));
+  B = sat_u8(255.f * srgb_enc(fminf(fmaxf(bb, 0.f), 1.f)));
+}
+
+// ---- HSV (8U: H in [0, 180)) ----
+__device__ __forceinline__ void rgb2hsv(int r, int g, int b, int& h, int& s, int& v) {
+  constexpr int SH = 12;
+  int vmin = min(r, min(g, b));
+  v = max(r, max(g, b));
+  const int diff = v - vmin;
+  const int vr = v == r ? -1 : 0, vg = v == g ? -1 : 0;
+  // sdiv_table[i] = round((255 << 12) / i), hdiv_table[i] = round((180 << 12) / (6 i))
+  const int sdiv = v == 0 ? 0 : (int)rint((double)(255 << SH) / v);
+  const int hdiv = diff == 0 ? 0 : (int)rint((double)(180 << SH) / (6.0 * diff));
+  s = (diff * sdiv + (1 << (SH - 1))) >> SH;
+  int hh = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))));
+  hh = (hh * hdiv + (1 << (SH - 1))) >> SH;
+  h = hh + (hh < 0 ? 180 : 0);
+}
+
+__device__ __forceinline__ void hsv2rgb(int h8, int s8, int v8, uint8_t& R, uint8_t& G, uint8_t& B) {
+  float h = h8 * (6.f / 180.f), s = s8 * (1.f / 255.f), v = v8 * (1.f / 255.f);
+  float r, g, b;
+  if (s == 0.f) {
+    r = g = b = v;
+  } else {
+    if (h < 0.f) h += 6.f;
+    if (h >= 6.f) h -= 6.f;
+    const int sector = (int)floorf(h);
+    h -= (float)sector;
+    const float t0 = v, t1 = v * (1.f - s), t2 = v * (1.f - s * h), t3 = v * (1.f - s * (1.f - h));
+    switch (sector) {
+      case 0: r = t0; g = t3; b = t1; break;
+      case 1: r = t2; g = t0; b = t1; break;
+      case 2: r = t1; g = t0; b = t3; break;
+      case 3: r = t1; g = t2; b = t0; break;
+      case 4: r = t3; g = t1; b = t0; break;
+      default: r = t0; g = t1; b = t2; break;
+    }
+  }
+  R = sat_u8(r * 255.f);
+  G = sat_u8(g * 255.f);
+  B = sat_u8(b * 255.f);
+}
+
+// ---- kernels ----
+__global__ __launch_bounds__(NT) void rgb2lab_kernel(const uint8_t* rgb, uint8_t* lab, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    uint8_t L, a, b;
+    rgb2lab(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], L, a, b);
+    lab[3 * i] = L;
+    lab[3 * i + 1] = a;
+    lab[3 * i + 2] = b;
+  }
+}
+
+__global__ __launch_bounds__(NT) void lab2rgb_kernel(const uint8_t* lab, uint8_t* rgb, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    uint8_t R, G, B;
+    lab2rgb(lab[3 * i], lab[3 * i + 1], lab[3 * i + 2], R, G, B);
+    rgb[3 * i] = R;
+    rgb[3 * i + 1] = G;
+    rgb[3 * i + 2] = B;
+  }
+}
+
+__global__ __launch_bounds__(NT) void rgb2gray_kernel(const uint8_t* rgb, uint8_t* gray, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    gray[i] = gray_u8(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2]);
+}
+
+// mode bit 0: S = trunc(clip(S * sat_mul, 0, 255))      (dataset.py:257-261)
+// mode bit 1: H = trunc((H + hue_add) mod 180), V = trunc(clip(V * val_mul, 0, 255))  (:288-292)
+// all in fp32 as the reference's float32 HSV arrays
+__global__ __launch_bounds__(NT) void hsv_adjust_kernel(uint8_t* rgb, long long n, float sat_mul, float hue_add,
+                                                        float val_mul, int mode) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    int h, s, v;
+    rgb2hsv(rgb[3 * i], rgb[3 * i + 1], rgb[3 * i + 2], h, s, v);
+    if (mode & 1) s = (int)fminf(fmaxf((float)s * sat_mul, 0.f), 255.f);
+    if (mode & 2) {
+      float hf = fmodf((float)h + hue_add, 180.f);  // numpy %: result takes the divisor's sign
+      if (hf < 0.f) hf += 180.f;
+      h = (int)hf;
+      v = (int)fminf(fmaxf((float)v * val_mul, 0.f), 255.f);
+    }
+    uint8_t R, G, B;
+    hsv2rgb(h, s, v, R, G, B);
+    rgb[3 * i] = R;
+    rgb[3 * i + 1] = G;
+    rgb[3 * i + 2] = B;
+  }
+}
+
+// CLAHE tile LUTs: one block per tile of the REFLECT_101-padded image; src channel ch of a
+// pixel-stride-ps image
+__global__ __launch_bounds__(NT) void clahe_lut_kernel(const uint8_t* src, int ps, int h, int w, int tw, int th,
+                                                       int tiles_x, int clip, float lut_scale, uint8_t* luts) {
+  __shared__ unsigned hist[256];
+  const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+  for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0u;
+  __syncthreads();
+  for (int p = threadIdx.x; p < tw * th; p += NT) {
+    const int y = reflect101(ty * th + p / tw, h), x = reflect101(tx * tw + p % tw, w);
+    atomicAdd(&hist[src[((long long)y * w + x) * ps]], 1u);  // LDS integer counts: order-free
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // clip + redistribute + cumulate, serially as OpenCV (256 steps)
+    int excess = 0;
+    for (int i = 0; i < 256; ++i) {
+      const int c = (int)hist[i];
+      if (c > clip) {
+        excess += c - clip;
+        hist[i] = (unsigned)clip;
+      }
+    }
+    const int batch = excess / 256, residual = excess - batch * 256;
+    for (int i = 0; i < 256; ++i) hist[i] += (unsigned)batch;
+    if (residual != 0) {
+      const int step = max(256 / residual, 1);
+      int r = residual;
+      for (int i = 0; i < 256 && r > 0; i += step, --r) hist[i] += 1u;
+    }
+    unsigned sum = 0;
+    uint8_t* lut = luts + (long long)blockIdx.x * 256;
+    for (int i = 0; i < 256; ++i) {
+      sum += hist[i];
+      lut[i] = sat_u8((float)sum * lut_scale);
+    }
+  }
+}
+
+// bilinear blend of the four neighbouring tile LUTs (OpenCV CLAHE_Interpolation_Body)
+__device__ __forceinline__ uint8_t clahe_px(const uint8_t* luts, int tiles_x, int tiles_y, float inv_tw, float inv_th,
+                                            int x, int y, int v) {
+  const float txf = x * inv_tw - 0.5f, tyf = y * inv_th - 0.5f;
+  int tx1 = (int)floorf(txf), ty1 = (int)floorf(tyf);
+  const float xa = txf - tx1, ya = tyf - ty1;
+  int tx2 = tx1 + 1, ty2 = ty1 + 1;
+  tx1 = max(tx1, 0);
+  ty1 = max(ty1, 0);
+  tx2 = min(tx2, tiles_x - 1);
+  ty2 = min(ty2, tiles_y - 1);
+  const uint8_t* l11 = luts + ((long long)ty1 * tiles_x + tx1) * 256;
+  const uint8_t* l12 = luts + ((long long)ty1 * tiles_x + tx2) * 256;
+  const uint8_t* l21 = luts + ((long long)ty2 * tiles_x + tx1) * 256;
+  const uint8_t* l22 = luts + ((long long)ty2 * tiles_x + tx2) * 256;
+  const float res = (l11[v] * (1.f - xa) + l12[v] * xa) * (1.f - ya) + (l21[v] * (1.f - xa) + l22[v] * xa) * ya;
+  return sat_u8(res);
+}
+
+// mode 0: gray -> gray; mode 1: Lab image, L replaced, converted back to RGB (dst 3 channels)
+__global__ __launch_bounds__(NT) void clahe_apply_kernel(const uint8_t* src, int ps, int h, int w, const uint8_t* luts,
+                                                         int tiles_x, int tiles_y, float inv_tw, float inv_th,
+                                                         uint8_t* dst, int mode) {
+  const long long n = (long long)h * w;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const int y = (int)(i / w), x = (int)(i - (long long)y * w);
+    const uint8_t L = clahe_px(luts, tiles_x, tiles_y, inv_tw, inv_th, x, y, src[i * ps]);
+    if (mode == 0) {
+      dst[i] = L;
+    } else {
+      uint8_t R, G, B;
+      lab2rgb(L, src[i * ps + 1], src[i * ps + 2], R, G, B);
+      dst[3 * i] = R;
+      dst[3 * i + 1] = G;
+      dst[3 * i + 2] = B;
+    }
+  }
+}
+
+// cv2.filter2D(src, -1, k) 8U, 3x3, anchor centre, BORDER_REFLECT_101: fp32 taps in row-major order
+struct K9 { float k[9]; };
+__global__ __launch_bounds__(NT) void filter3x3_kernel(const uint8_t* src, uint8_t* dst, int h, int w, int c, K9 k) {
+  const long long n = (long long)h * w * c;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const long long p = i / c;
+    const int ch = (int)(i - p * c), y = (int)(p / w), x = (int)(p - (long long)y * w);
+    float s = 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int yy = reflect101(y + dy, h), xx = reflect101(x + dx, w);
+        s += k.k[(dy + 1) * 3 + dx + 1] * (float)src[((long long)yy * w + xx) * c + ch];
+      }
+    dst[i] = sat_u8(s);
+  }
+}
+
+// GaussianBlur(3x3, sigma 1) 8U fixed point (70, 116, 70) / 256 rows then columns, then
+// addWeighted(src, 1.3, blur, -0.3, 0) (dataset.py:126-128)
+__global__ __launch_bounds__(NT) void unsharp_kernel(const uint8_t* src, uint8_t* dst, int h, int w, int c) {
+  const long long n = (long long)h * w * c;
+  const int wk[3] = {70, 116, 70};
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const long long p = i / c;
+    const int ch = (int)(i - p * c), y = (int)(p / w), x = (int)(p - (long long)y * w);
+    unsigned col = 0;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = reflect101(y + dy, h);
+      unsigned row = 0;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) row += wk[dx + 1] * src[((long long)yy * w + reflect101(x + dx, w)) * c + ch];
+      col += wk[dy + 1] * row;
+    }
+    const int g = (int)((col + (1u << 15)) >> 16);
+    dst[i] = sat_u8((float)src[i] * 1.3f + (float)g * -0.3f);
+  }
+}
+
+// Sobel magnitude and |Laplacian| of a gray image in fp64 (CV_64F), per-block maxima
+__global__ __launch_bounds__(NT) void edge_raw_kernel(const uint8_t* gray, int h, int w, double* mag, double* lap,
+                                                      double* bmax) {
+  __shared__ double sm[2][NT];
+  const long long n = (long long)h * w;
+  double m1 = 0.0, m2 = 0.0;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const int y = (int)(i / w), x = (int)(i - (long long)y * w);
+    int v[3][3];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) v[dy][dx] = gray[(long long)reflect101(y + dy - 1, h) * w + reflect101(x + dx - 1, w)];
+    const double sx = (double)((v[0][2] - v[0][0]) + 2 * (v[1][2] - v[1][0]) + (v[2][2] - v[2][0]));
+    const double sy = (double)((v[2][0] - v[0][0]) + 2 * (v[2][1] - v[0][1]) + (v[2][2] - v[0][2]));
+    const double mg = sqrt(sx * sx + sy * sy);
+    const double lp = fabs((double)(v[0][1] + v[1][0] - 4 * v[1][1] + v[1][2] + v[2][1]));
+    mag[i] = mg;
+    lap[i] = lp;
+    m1 = fmax(m1, mg);
+    m2 = fmax(m2, lp);
+  }
+  sm[0][threadIdx.x] = m1;
+  sm[1][threadIdx.x] = m2;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sm[0][threadIdx.x] = fmax(sm[0][threadIdx.x], sm[0][threadIdx.x + s]);
+      sm[1][threadIdx.x] = fmax(sm[1][threadIdx.x], sm[1][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bmax[2 * blockIdx.x] = sm[0][0];
+    bmax[2 * blockIdx.x + 1] = sm[1][0];
+  }
+}
+
+// edges = trunc(trunc(clip(mag / (max + 1e-6) * 255)) * 0.7 + trunc(clip(|lap| / (max + 1e-6) * 255)) * 0.3)
+// (dataset.py:81-91: fp64 normalisation, fp32 blend, astype(uint8) truncations)
+__global__ __launch_bounds__(NT) void edge_combine_kernel(const double* mag, const double* lap, const double* bmax,
+                                                          int nb, long long n, uint8_t* edges) {
+  __shared__ double mx[2];
+  if (threadIdx.x < 2) {
+    double m = 0.0;
+    for (int b = 0; b < nb; ++b) m = fmax(m, bmax[2 * b + threadIdx.x]);
+    mx[threadIdx.x] = m;
+  }
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const double e = fmin(fmax(mag[i] / (mx[0] + 1e-6) * 255.0, 0.0), 255.0);
+    const double l = fmin(fmax(lap[i] / (mx[1] + 1e-6) * 255.0, 0.0), 255.0);
+    const float c = (float)(uint8_t)e * 0.7f + (float)(uint8_t)l * 0.3f;
+    edges[i] = (uint8_t)c;
+  }
+}
+
+// live-cell brightening (dataset.py:103-107): img = trunc(clip(img * 1.1)) where live
+__global__ __launch_bounds__(NT) void live_boost_kernel(uint8_t* img, const int64_t* live, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    if (live[i] > 0)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) img[3 * i + c] = (uint8_t)fminf((float)img[3 * i + c] * 1.1f, 255.f);
+}
+
+// dataset.py:109-124: dead-cell CLAHE gray where dead (dead_gray may be null: no dead pixels), edge
+// blend trunc(clip(img * 0.9 + edges * 0.1)), then trunc(that * 0.85 + original * 0.15)
+__global__ __launch_bounds__(NT) void cell_mix_kernel(const uint8_t* orig, const uint8_t* clahe_img,
+                                                      const uint8_t* edges, const int64_t* dead,
+                                                      const uint8_t* dead_gray, long long n, uint8_t* out) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const bool dd = dead_gray != nullptr && dead[i] > 0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v = dd ? (float)dead_gray[i] : (float)clahe_img[3 * i + c];
+      const float we = fminf(fmaxf(v * 0.9f + (float)edges[i] * 0.1f, 0.f), 255.f);
+      const float fin = (float)(uint8_t)we * 0.85f + (float)orig[3 * i + c] * 0.15f;
+      out[3 * i + c] = (uint8_t)fin;
+    }
+  }
+}
+
+// Evaluator input (train_eval.py:367-377): per-block maxima of the CHW float image ...
+__global__ __launch_bounds__(NT) void max_partial_kernel(const float* x, long long n, float* bmax) {
+  __shared__ float sm[NT];
+  float m = -INFINITY;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) m = fmaxf(m, x[i]);
+  sm[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) sm[threadIdx.x] = fmaxf(sm[threadIdx.x], sm[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bmax[blockIdx.x] = sm[0];
+}
+
+// ... then HWC uint8 = astype(uint8) of (max <= 1 ? x * 255 : x): fp32, truncation (C cast through int)
+__global__ __launch_bounds__(NT) void chw_to_u8_kernel(const float* x, int c, int h, int w, const float* bmax, int nb,
+                                                       uint8_t* out) {
+  __shared__ float mx;
+  if (threadIdx.x == 0) {
+    float m = -INFINITY;
+    for (int b = 0; b < nb; ++b) m = fmaxf(m, bmax[b]);
+    mx = m;
+  }
+  __syncthreads();
+  const bool unit = mx <= 1.f;
+  const long long hw = (long long)h * w, n = hw * c;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const long long p = i / c;
+    const int ch = (int)(i - p * c);
+    const float v = x[(long long)ch * hw + p];
+    out[i] = (uint8_t)(int)(unit ? v * 255.f : v);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int eunet_chw_to_u8_workspace_bytes(int c, int h, int w, size_t* bytes) {
+  EUNET_REQUIRE(c > 0 && h > 0 && w > 0 && bytes, "chw_to_u8_workspace_bytes: bad args");
+  *bytes = (size_t)grid1((long long)c * h * w) * sizeof(float);
+  return EUNET_OK;
+}
+
+int eunet_chw_to_u8(const float* x, int c, int h, int w, void* ws, uint8_t* out, void* stream) {
+  EUNET_REQUIRE(x && ws && out && c > 0 && h > 0 && w > 0, "chw_to_u8: bad args");
+  const long long n = (long long)c * h * w;
+  const unsigned nb = grid1(n);
+  max_partial_kernel<<<nb, NT, 0, (hipStream_t)stream>>>(x, n, (float*)ws);
+  EUNET_LAUNCH_CHECK("max_partial");
+  chw_to_u8_kernel<<<nb, NT, 0, (hipStream_t)stream>>>(x, c, h, w, (const float*)ws, (int)nb, out);
+  EUNET_LAUNCH_CHECK("chw_to_u8");
+  return EUNET_OK;
+}
+
+int eunet_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, long long npix, void* stream) {
+  EUNET_REQUIRE(rgb && lab && npix > 0, "rgb2lab_u8: bad args");
+  rgb2lab_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(rgb, lab, npix);
+  EUNET_LAUNCH_CHECK("rgb2lab_u8");
+  return EUNET_OK;
+}
+
+int eunet_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, long long npix, void* stream) {
+  EUNET_REQUIRE(rgb && lab && npix > 0, "lab2rgb_u8: bad args");
+  lab2rgb_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(lab, rgb, npix);
+  EUNET_LAUNCH_CHECK("lab2rgb_u8");
+  return EUNET_OK;
+}
+
+int eunet_rgb2gray_u8(const uint8_t* rgb, uint8_t* gray, long long npix, void* stream) {
+  EUNET_REQUIRE(rgb && gray && npix > 0, "rgb2gray_u8: bad args");
+  rgb2gray_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(rgb, gray, npix);
+  EUNET_LAUNCH_CHECK("rgb2gray_u8");
+  return EUNET_OK;
+}
+
+int eunet_hsv_adjust_u8(uint8_t* rgb, long long npix, float sat_mul, float hue_add, float val_mul, int mode,
+                        void* stream) {
+  EUNET_REQUIRE(rgb && npix > 0 && (mode & ~3) == 0, "hsv_adjust_u8: bad args");
+  hsv_adjust_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(rgb, npix, sat_mul, hue_add, val_mul, mode);
+  EUNET_LAUNCH_CHECK("hsv_adjust_u8");
+  return EUNET_OK;
+}
+
+int eunet_clahe_u8(const uint8_t* src, int mode, int h, int w, double clip_limit, int tiles_x, int tiles_y,
+                   uint8_t* luts, uint8_t* dst, void* stream) {
+  EUNET_REQUIRE(src && dst && luts && h > 0 && w > 0 && tiles_x > 0 && tiles_y > 0 && (mode == 0 || mode == 1),
+                "clahe_u8: bad args");
+  const int ps = mode == 0 ? 1 : 3;
+  // OpenCV pads to a multiple of the grid (BORDER_REFLECT_101); tile = padded size / grid
+  const int tw = (w + tiles_x - 1) / tiles_x, th = (h + tiles_y - 1) / tiles_y;
+  const int area = tw * th;
+  const int clip = clip_limit > 0.0 ? std::max((int)(clip_limit * area / 256), 1) : (1 << 30);
+  clahe_lut_kernel<<<tiles_x * tiles_y, NT, 0, (hipStream_t)stream>>>(src, ps, h, w, tw, th, tiles_x, clip,
+                                                                     255.f / (float)area, luts);
+  EUNET_LAUNCH_CHECK("clahe_lut");
+  clahe_apply_kernel<<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(src, ps, h, w, luts, tiles_x, tiles_y,
+                                                                              1.f / tw, 1.f / th, dst, mode);
+  EUNET_LAUNCH_CHECK("clahe_apply");
+  return EUNET_OK;
+}
+
+int eunet_filter3x3_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, const float* k9, void* stream) {
+  EUNET_REQUIRE(src && dst && k9 && h > 0 && w > 0 && c > 0 && src != dst, "filter3x3_u8: bad args");
+  K9 k;
+  for (int i = 0; i < 9; ++i) k.k[i] = k9[i];
+  filter3x3_kernel<<<grid1((long long)h * w * c), NT, 0, (hipStream_t)stream>>>(src, dst, h, w, c, k);
+  EUNET_LAUNCH_CHECK("filter3x3_u8");
+  return EUNET_OK;
+}
+
+int eunet_unsharp_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, void* stream) {
+  EUNET_REQUIRE(src && dst && h > 0 && w > 0 && c > 0 && src != dst, "unsharp_u8: bad args");
+  unsharp_kernel<<<grid1((long long)h * w * c), NT, 0, (hipStream_t)stream>>>(src, dst, h, w, c);
+  EUNET_LAUNCH_CHECK("unsharp_u8");
+  return EUNET_OK;
+}
+
+int eunet_edge_features_workspace_bytes(int h, int w, size_t* bytes) {
+  EUNET_REQUIRE(h > 0 && w > 0 && bytes, "edge_features_workspace_bytes: bad args");
+  *bytes = (size_t)h * w * 2 * sizeof(double) + (size_t)grid1((long long)h * w) * 2 * sizeof(double);
+  return EUNET_OK;
+}
+
+int eunet_edge_features_u8(const uint8_t* gray, int h, int w, void* ws, uint8_t* edges, void* stream) {
+  EUNET_REQUIRE(gray && ws && edges && h > 0 && w > 0, "edge_features_u8: bad args");
+  const long long n = (long long)h * w;
+  double* mag = (double*)ws;
+  double* lap = mag + n;
+  double* bmax = lap + n;
+  const unsigned nb = grid1(n);
+  edge_raw_kernel<<<nb, NT, 0, (hipStream_t)stream>>>(gray, h, w, mag, lap, bmax);
+  EUNET_LAUNCH_CHECK("edge_raw");
+  edge_combine_kernel<<<nb, NT, 0, (hipStream_t)stream>>>(mag, lap, bmax, (int)nb, n, edges);
+  EUNET_LAUNCH_CHECK("edge_combine");
+  return EUNET_OK;
+}
+
+int eunet_live_boost_u8(uint8_t* img, const int64_t* live_mask, long long npix, void* stream) {
+  EUNET_REQUIRE(img && live_mask && npix > 0, "live_boost_u8: bad args");
+  live_boost_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(img, live_mask, npix);
+  EUNET_LAUNCH_CHECK("live_boost_u8");
+  return EUNET_OK;
+}
+
+int eunet_cell_mix_u8(const uint8_t* orig, const uint8_t* clahe_img, const uint8_t* edges, const int64_t* dead_mask,
+                      const uint8_t* dead_gray, long long npix, uint8_t* out, void* stream) {
+  EUNET_REQUIRE(orig && clahe_img && edges && out && npix > 0 && (dead_gray == nullptr || dead_mask != nullptr),
+                "cell_mix_u8: bad args");
+  cell_mix_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(orig, clahe_img, edges, dead_mask, dead_gray, npix,
+                                                               out);
+  EUNET_LAUNCH_CHECK("cell_mix_u8");
+  return EUNET_OK;
+}
+
+}  // extern "C"

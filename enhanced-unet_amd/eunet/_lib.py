@@ -114,6 +114,19 @@ SIGNATURES = {
     "eunet_augment_u8": [_f, c_int64, c_int, ctypes.c_double, ctypes.c_double, _f, _f, c_void_p],
     "eunet_to_tensor": [_f, c_int, c_int, c_int, _f, c_void_p],
     "eunet_resize_u8": [_f, c_int, c_int, c_int, _f, c_int, c_int, c_void_p],
+    "eunet_rgb2lab_u8": [_f, _f, c_int64, c_void_p],
+    "eunet_lab2rgb_u8": [_f, _f, c_int64, c_void_p],
+    "eunet_rgb2gray_u8": [_f, _f, c_int64, c_void_p],
+    "eunet_hsv_adjust_u8": [_f, c_int64, c_float, c_float, c_float, c_int, c_void_p],
+    "eunet_clahe_u8": [_f, c_int, c_int, c_int, ctypes.c_double, c_int, c_int, _f, _f, c_void_p],
+    "eunet_filter3x3_u8": [_f, _f, c_int, c_int, c_int, _f, c_void_p],
+    "eunet_unsharp_u8": [_f, _f, c_int, c_int, c_int, c_void_p],
+    "eunet_edge_features_workspace_bytes": [c_int, c_int, POINTER(ctypes.c_size_t)],
+    "eunet_edge_features_u8": [_f, c_int, c_int, _f, _f, c_void_p],
+    "eunet_live_boost_u8": [_f, _f, c_int64, c_void_p],
+    "eunet_cell_mix_u8": [_f, _f, _f, _f, _f, c_int64, _f, c_void_p],
+    "eunet_chw_to_u8_workspace_bytes": [c_int, c_int, c_int, POINTER(ctypes.c_size_t)],
+    "eunet_chw_to_u8": [_f, c_int, c_int, c_int, _f, _f, c_void_p],
     "eunet_consistency_tiles": [c_int, c_int, POINTER(c_int)],
     "eunet_consistency_fwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, c_void_p],
     "eunet_consistency_bwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, _f, _f,

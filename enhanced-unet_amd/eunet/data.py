@@ -6,17 +6,18 @@
 Same file split (sorted *.jpg, 70/15/15, dataset.py:37-51), the same resize-to-/32
 sizes (:141-157), LabelMe 'live'/'dead' polygons scaled and truncated to int32 as the
 reference does (:173-188), the semantic mask with later instances overwriting earlier
-ones (:197-201), per-instance uint8 masks flipped with the image (:184-193, 209-222), and the training augmentations drawn from Python's `random` in the
-reference's order, so a seeded run takes the same decisions (:204-294).  Per pixel
-everything runs in HIP (datapath.hip): polygon rasterisation, flips, the numpy pixel
-ops (brightness, contrast, noise, gamma LUT -- bit-exact with the reference's numpy
-lines), ToTensor.  Image decode stays PIL on the host (I/O).
+ones (:197-201), per-instance uint8 masks flipped with the image (:184-193, 209-222), the
+cell-specific preprocessing of every split (:58-131, :204), and the training augmentations
+drawn from Python's `random` in the reference's order, so a seeded run takes the same
+decisions (:204-300).  Per pixel everything runs in HIP: polygon rasterisation, flips, the
+numpy pixel ops (brightness, contrast, noise, gamma LUT -- bit-exact with the reference's
+numpy lines), ToTensor (datapath.hip); LAB/HSV conversions, CLAHE, Sobel/Laplacian edge
+features, GaussianBlur unsharp mask, filter2D sharpening (imgproc.hip).  Image decode stays
+PIL on the host (I/O).
 
-Not built (cv2 is absent, so their parity cannot be pinned): the cell-specific
-preprocessing (:58-131, LAB/CLAHE/Sobel/Laplacian/GaussianBlur), the HSV saturation,
-CLAHE, sharpening and HSV jitter augmentations (:255-294).  Their random draws are
-still consumed so the remaining decisions stay aligned with the reference's stream.
-cv2.fillPoly and cv2.resize are replaced by the kernels' documented rules (unpinned).
+cv2 is absent from this image: cv2.fillPoly, cv2.resize and the cv2 colour / CLAHE / filter
+calls are replaced by kernels that follow OpenCV's documented algorithms, pinned to the
+numpy restatement in oracle/imgproc_ref.py, not to cv2 (parity unpinned).
 """
 from __future__ import annotations
 
@@ -68,9 +69,10 @@ def load_labelme(json_path: str, scale_h: float, scale_w: float):
 
 class CellDataset:
     def __init__(self, data_dir: str, split: str = "train", transform=None, max_size: int = 1024,
-                 device: str = "cuda"):
+                 device: str = "cuda", cell_preprocess: bool = True):
         self.data_dir, self.split, self.transform, self.max_size = data_dir, split, transform, max_size
         self.device = device
+        self.cell_preprocess = cell_preprocess  # dataset.py:204 (always on in the reference)
         all_files = sorted(f for f in os.listdir(data_dir) if f.endswith(".jpg"))
         n_total = len(all_files)
         n_train, n_val = int(n_total * 0.7), int(n_total * 0.15)
@@ -83,6 +85,17 @@ class CellDataset:
 
     def __len__(self):
         return len(self.files)
+
+    @staticmethod
+    def _apply_cell_specific_preprocessing(img, polys, labels):
+        """dataset.py:58-131.  The live / dead unions of the instance masks (:93-100) are filled
+        straight from the polygons (same fill rule as the instance masks)."""
+        h, w, _ = img.shape
+        live = [p for p, l in zip(polys, labels) if l == 0]
+        dead = [p for p, l in zip(polys, labels) if l != 0]
+        live_mask = ops.rasterize_polygons(live, [1] * len(live), h, w, img.device) if live else None
+        dead_mask = ops.rasterize_polygons(dead, [1] * len(dead), h, w, img.device) if dead else None
+        return ops.cell_preprocess_u8(img, live_mask, dead_mask)
 
     def _augment(self, img, mask):
         """dataset.py:204-294 in order; img HWC uint8 and mask int64 on the device.  Returns
@@ -109,10 +122,10 @@ class CellDataset:
         if random.random() > 0.3:
             beta = random.uniform(-20, 40) if live_ratio < 0.4 else random.uniform(-30, 30)
             ops.augment_u8(img, beta=beta)
-        if random.random() > 0.5:  # HSV saturation (cv2): not built, draw consumed
-            random.uniform(0.8, 1.3)
-        if random.random() > 0.4:  # CLAHE (cv2): not built, draw consumed
-            random.uniform(1.5, 3.0)
+        if random.random() > 0.5:  # HSV saturation (:259-264)
+            ops.hsv_adjust_u8(img, sat=random.uniform(0.8, 1.3))
+        if random.random() > 0.4:  # CLAHE on L (:267-272)
+            img = ops.clahe_rgb_u8(img, random.uniform(1.5, 3.0))
         if random.random() > 0.5:
             sigma = random.uniform(3, 10)
             noise = np.random.normal(0, sigma, tuple(img.shape)).astype(np.float32)
@@ -120,11 +133,11 @@ class CellDataset:
         if random.random() > 0.5:
             lut = torch.from_numpy(gamma_lut(random.uniform(0.7, 1.3))).to(img.device)
             ops.augment_u8(img, lut=lut)
-        if random.random() > 0.6:  # sharpening (cv2.filter2D): not built, draw consumed
-            random.uniform(0.1, 0.3)
-        if random.random() > 0.6:  # HSV jitter (cv2): not built, draws consumed
-            random.uniform(-10, 10)
-            random.uniform(0.9, 1.1)
+        if random.random() > 0.6:  # sharpening (:287-292)
+            img = ops.sharpen_u8(img, random.uniform(0.1, 0.3))
+        if random.random() > 0.6:  # HSV jitter (:295-300): hue drawn before value
+            hue = random.uniform(-10, 10)
+            ops.hsv_adjust_u8(img, hue=hue, val=random.uniform(0.9, 1.1))
         return img, mask, (flip_h, flip_v)
 
     def __getitem__(self, idx):
@@ -139,6 +152,8 @@ class CellDataset:
         polys, labels, bboxes = load_labelme(os.path.join(self.data_dir, name.replace(".jpg", ".json")),
                                              h / original_size[0], w / original_size[1])
         mask = ops.rasterize_polygons(polys, [l + 1 for l in labels], h, w, img.device)
+        if self.cell_preprocess:
+            img = self._apply_cell_specific_preprocessing(img.contiguous(), polys, labels)
         flips = (False, False)
         if self.split == "train":
             img, mask, flips = self._augment(img.contiguous(), mask)

@@ -13,16 +13,19 @@ thresholded mask conversion (two passes; the pixel-ratio refinement reads the
 pass-1 counts on the device).  The network is the fused forward_lowres (the
 2H->H bilinear resize of train_eval.py:413 is the exact 2x2 mean it computes).
 
-Not built: the CLAHE + sharpening preprocessing of
-_prepare_image_tensor (train_eval.py:365-395) needs cv2's uint8 LAB/CLAHE,
-which is absent from this image -- preprocess=None skips it (documented
-difference; parity of that step is unpinned); instance splitting / COCO
-metrics (cv2, skimage, pycocotools).
+_prepare_image_tensor (train_eval.py:365-395) runs in HIP too (imgproc.hip):
+CHW float -> uint8 (x255 when max <= 1), RGB -> Lab, CLAHE(2.0, 8x8) on L,
+Lab -> RGB, filter2D sharpening x0.15, /255.  cv2 is absent, so those kernels
+follow OpenCV's documented algorithms (parity unpinned, oracle/imgproc_ref.py).
+preprocess=None skips the step, a callable replaces it.
+
+Not built: instance splitting / COCO metrics (cv2, skimage,
+pycocotools).
 """
 from __future__ import annotations
 
 import math
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, Optional, Union
 
 import numpy as np
 import torch
@@ -34,8 +37,16 @@ from .metrics import calculate_semantic_metrics
 TTA_SCALES = (0.75, 1.25)
 
 
+def reference_preprocess(image: torch.Tensor) -> torch.Tensor:
+    """train_eval.py:365-395 on the device: [3,h,w] float -> CLAHE(2.0) + sharpen(0.15) -> [3,h,w] / 255."""
+    if image.dim() != 3 or image.shape[0] != 3:
+        raise ValueError("the reference preprocessing converts RGB -> Lab: image must be [3, h, w]")
+    u8 = ops.chw_to_u8(image)
+    return ops.to_tensor(ops.sharpen_u8(ops.clahe_rgb_u8(u8, 2.0), 0.15))
+
+
 class Evaluator:
-    def __init__(self, model, device, model_name, preprocess: Optional[Callable] = None):
+    def __init__(self, model, device, model_name, preprocess: Union[str, Callable, None] = "reference"):
         self.model = model
         self.device = device
         self.model_name = model_name
@@ -45,7 +56,13 @@ class Evaluator:
     # ---- train_eval.py:365-395 -------------------------------------------------
     def _prepare_image_tensor(self, image: torch.Tensor) -> torch.Tensor:
         image = image.to(self.device).float()
-        return self.preprocess(image) if self.preprocess is not None else image
+        if self.preprocess is None:
+            return image
+        if callable(self.preprocess):
+            return self.preprocess(image)
+        if self.preprocess != "reference":
+            raise ValueError(f"preprocess must be 'reference', None or a callable, not {self.preprocess!r}")
+        return reference_preprocess(image)
 
     def _logits(self, image_padded: torch.Tensor) -> torch.Tensor:
         m = self.model

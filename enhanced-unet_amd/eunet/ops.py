@@ -507,3 +507,116 @@ def resize_u8(img, ho, wo):
     out = torch.empty(ho, wo, c, dtype=torch.uint8, device=img.device)
     call("eunet_resize_u8", _ptr(img.contiguous()), hi, wi, c, _ptr(out), ho, wo, _stream())
     return out
+
+
+# ---- cv2 image operations (imgproc.hip) -------------------------------------------------
+SHARPEN_3X3 = (-1.0, -1.0, -1.0, -1.0, 9.0, -1.0, -1.0, -1.0, -1.0)  # dataset.py:288-290, train_eval.py:388-390
+
+
+def _size_out(fn, *args):
+    n = ctypes.c_size_t(0)
+    call(fn, *args, ctypes.byref(n))
+    return int(n.value)
+
+
+def rgb2lab_u8(img):
+    out = torch.empty_like(img)
+    call("eunet_rgb2lab_u8", _ptr(img.contiguous()), _ptr(out), img.shape[0] * img.shape[1], _stream())
+    return out
+
+
+def lab2rgb_u8(lab):
+    out = torch.empty_like(lab)
+    call("eunet_lab2rgb_u8", _ptr(lab.contiguous()), _ptr(out), lab.shape[0] * lab.shape[1], _stream())
+    return out
+
+
+def rgb2gray_u8(img):
+    h, w, _ = img.shape
+    out = torch.empty(h, w, dtype=torch.uint8, device=img.device)
+    call("eunet_rgb2gray_u8", _ptr(img.contiguous()), _ptr(out), h * w, _stream())
+    return out
+
+
+def hsv_adjust_u8(img, sat=None, hue=None, val=None):
+    """In place: S *= sat (dataset.py:259-264) or H += hue mod 180, V *= val (:295-300)."""
+    mode = (1 if sat is not None else 0) | (2 if hue is not None else 0)
+    if mode & 2 and val is None:
+        raise ValueError("hsv_adjust_u8: hue and val go together")
+    call("eunet_hsv_adjust_u8", _ptr(img), img.shape[0] * img.shape[1], float(sat or 1.0), float(hue or 0.0),
+         float(val or 1.0), mode, _stream())
+    return img
+
+
+def clahe_u8(src, clip_limit, grid=(8, 8), lab_to_rgb=False):
+    """cv2.createCLAHE(clip_limit, grid).apply.  lab_to_rgb: src is a Lab image, its L channel is
+    equalised and the RGB image is returned (the merge + LAB2RGB of dataset.py:70-71)."""
+    h, w = src.shape[:2]
+    luts = torch.empty(grid[0] * grid[1] * 256, dtype=torch.uint8, device=src.device)
+    out = torch.empty(h, w, 3, dtype=torch.uint8, device=src.device) if lab_to_rgb else torch.empty_like(src)
+    call("eunet_clahe_u8", _ptr(src.contiguous()), int(lab_to_rgb), h, w, float(clip_limit), grid[0], grid[1],
+         _ptr(luts), _ptr(out), _stream())
+    return out
+
+
+def clahe_rgb_u8(img, clip_limit, grid=(8, 8)):
+    """RGB -> Lab, CLAHE on L, -> RGB (dataset.py:63-71, 268-272; train_eval.py:380-385)."""
+    return clahe_u8(rgb2lab_u8(img), clip_limit, grid, lab_to_rgb=True)
+
+
+def filter3x3_u8(img, k9):
+    h, w = img.shape[:2]
+    c = img.shape[2] if img.dim() == 3 else 1
+    kk = (ctypes.c_float * 9)(*[float(v) for v in k9])
+    out = torch.empty_like(img)
+    call("eunet_filter3x3_u8", _ptr(img.contiguous()), _ptr(out), h, w, c, ctypes.addressof(kk), _stream())
+    return out
+
+
+def sharpen_u8(img, strength):
+    """cv2.filter2D(img, -1, [[-1,-1,-1],[-1,9,-1],[-1,-1,-1]] * strength)."""
+    return filter3x3_u8(img, [v * strength for v in SHARPEN_3X3])
+
+
+def unsharp_u8(img):
+    h, w = img.shape[:2]
+    c = img.shape[2] if img.dim() == 3 else 1
+    out = torch.empty_like(img)
+    call("eunet_unsharp_u8", _ptr(img.contiguous()), _ptr(out), h, w, c, _stream())
+    return out
+
+
+def edge_features_u8(gray):
+    h, w = gray.shape
+    ws = torch.empty(_size_out("eunet_edge_features_workspace_bytes", h, w), dtype=torch.uint8, device=gray.device)
+    out = torch.empty_like(gray)
+    call("eunet_edge_features_u8", _ptr(gray.contiguous()), h, w, _ptr(ws), _ptr(out), _stream())
+    return out
+
+
+def cell_preprocess_u8(img, live_mask, dead_mask=None):
+    """dataset.py:58-131 (_apply_cell_specific_preprocessing) on an HWC uint8 device image.
+    live_mask / dead_mask: int64 [h, w], nonzero where any live / dead instance covers the
+    pixel (the np.maximum unions of :96-100); dead_mask None = no dead instance."""
+    h, w, _ = img.shape
+    img = img.contiguous()
+    clahe = clahe_rgb_u8(img, 2.5)
+    edges = edge_features_u8(rgb2gray_u8(img))
+    if live_mask is not None:
+        call("eunet_live_boost_u8", _ptr(clahe), _ptr(live_mask.contiguous()), h * w, _stream())
+    dead_gray = clahe_u8(rgb2gray_u8(clahe), 3.0) if dead_mask is not None else None
+    mixed = torch.empty_like(img)
+    call("eunet_cell_mix_u8", _ptr(img), _ptr(clahe), _ptr(edges),
+         _ptr(dead_mask.contiguous() if dead_mask is not None else None), _ptr(dead_gray), h * w, _ptr(mixed),
+         _stream())
+    return unsharp_u8(mixed)
+
+
+def chw_to_u8(x):
+    """train_eval.py:367-377: CHW float -> HWC uint8 (x * 255 if max(x) <= 1), on the device."""
+    c, h, w = x.shape
+    x = x.contiguous().float()
+    ws = torch.empty(_size_out("eunet_chw_to_u8_workspace_bytes", c, h, w), dtype=torch.uint8, device=x.device)
+    out = torch.empty(h, w, c, dtype=torch.uint8, device=x.device)
+    call("eunet_chw_to_u8", _ptr(x), c, h, w, _ptr(ws), _ptr(out), _stream())
+    return out

@@ -382,6 +382,46 @@ int eunet_to_tensor(const uint8_t* img, int h, int w, int c, float* out, void* s
 int eunet_resize_u8(const uint8_t* src, int hi, int wi, int c, uint8_t* dst, int ho, int wo,
                     void* stream);
 
+/* ---- cv2 image operations of the data / evaluation paths (imgproc.hip) -------------------------
+ * Replace the cv2 calls of dataset.py:58-131 (cell-specific preprocessing), dataset.py:255-294
+ * (HSV / CLAHE / sharpen augmentations) and train_eval.py:365-395 (Evaluator preprocessing).
+ * All images HWC uint8 RGB, npix = h * w.  cv2 is absent from this image: the formulas follow
+ * OpenCV's documented algorithms (parity unpinned). */
+int eunet_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, long long npix, void* stream);
+int eunet_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, long long npix, void* stream);
+/* cv2.COLOR_RGB2GRAY: (4899 R + 9617 G + 1868 B + 8192) >> 14 */
+int eunet_rgb2gray_u8(const uint8_t* rgb, uint8_t* gray, long long npix, void* stream);
+/* in place RGB -> HSV (8U, H in [0, 180)) -> adjust -> RGB.  mode bit0: S *= sat_mul
+ * (dataset.py:257-261); bit1: H = (H + hue_add) mod 180, V *= val_mul (:288-292); fp32 with
+ * clip and astype(uint8) truncation as the reference's float32 arrays */
+int eunet_hsv_adjust_u8(uint8_t* rgb, long long npix, float sat_mul, float hue_add, float val_mul,
+                        int mode, void* stream);
+/* cv2.createCLAHE(clip_limit, (tiles_x, tiles_y)).apply.  mode 0: src/dst gray [h][w];
+ * mode 1: src is a Lab image, its L channel is equalised and dst receives the RGB image
+ * (LAB2RGB fused, dataset.py:65-71 / train_eval.py:375-381).  luts: tiles_x*tiles_y*256 bytes */
+int eunet_clahe_u8(const uint8_t* src, int mode, int h, int w, double clip_limit, int tiles_x,
+                   int tiles_y, uint8_t* luts, uint8_t* dst, void* stream);
+/* cv2.filter2D(src, -1, k9) with a 3x3 kernel (row-major), BORDER_REFLECT_101; src != dst */
+int eunet_filter3x3_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, const float* k9,
+                       void* stream);
+/* GaussianBlur(3x3, 1.0) + addWeighted(src, 1.3, blur, -0.3, 0) (dataset.py:126-128); src != dst */
+int eunet_unsharp_u8(const uint8_t* src, uint8_t* dst, int h, int w, int c, void* stream);
+/* Sobel magnitude / |Laplacian| (CV_64F) of a gray image, each max-normalised to uint8 and
+ * blended 0.7 / 0.3 (dataset.py:78-91).  ws: eunet_edge_features_workspace_bytes */
+int eunet_edge_features_workspace_bytes(int h, int w, size_t* bytes);
+int eunet_edge_features_u8(const uint8_t* gray, int h, int w, void* ws, uint8_t* edges, void* stream);
+/* in place img *= 1.1 where live_mask > 0 (dataset.py:103-107) */
+int eunet_live_boost_u8(uint8_t* img, const int64_t* live_mask, long long npix, void* stream);
+/* dataset.py:109-124: where dead_mask > 0 the CLAHE'd gray dead_gray replaces clahe_img (dead_gray
+ * null = no dead pixels), then edge blend 0.9 / 0.1 and 0.85 / 0.15 mix with orig */
+int eunet_cell_mix_u8(const uint8_t* orig, const uint8_t* clahe_img, const uint8_t* edges,
+                      const int64_t* dead_mask, const uint8_t* dead_gray, long long npix,
+                      uint8_t* out, void* stream);
+/* Evaluator input (train_eval.py:367-377): CHW float -> HWC uint8, x * 255 when max(x) <= 1
+ * (max reduced on the device), astype(uint8) truncation.  ws: eunet_chw_to_u8_workspace_bytes */
+int eunet_chw_to_u8_workspace_bytes(int c, int h, int w, size_t* bytes);
+int eunet_chw_to_u8(const float* x, int c, int h, int w, void* ws, uint8_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

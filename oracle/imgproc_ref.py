@@ -1,0 +1,268 @@
+"""CPU restatement of the cv2 operations on the reference's data / evaluation paths
+(TEST INFRASTRUCTURE -- only tests/ import it).
+
+Call sites (citations into /root/reference):
+  dataset.py:58-131    _apply_cell_specific_preprocessing     -> cell_preprocess
+  dataset.py:259-264   HSV saturation augmentation             -> hsv_adjust(sat=)
+  dataset.py:267-272   CLAHE(U(1.5, 3)) augmentation           -> clahe_rgb
+  dataset.py:287-292   filter2D sharpen augmentation           -> filter3x3
+  dataset.py:295-300   HSV jitter augmentation                 -> hsv_adjust(hue=, val=)
+  train_eval.py:365-395  Evaluator._prepare_image_tensor       -> chw_to_u8, clahe_rgb, filter3x3
+
+PARITY UNPINNED: cv2 is not importable in this image and the reference holds no cv2
+fixtures, so this file restates OpenCV's published algorithms (imgproc color_lab / color_hsv
+/ clahe / filter / smooth modules) rather than being checked against cv2 itself.  The
+numpy steps around the cv2 calls (the 1.1 / 0.9 / 0.1 / 0.85 / 0.15 fp32 blends, the
+fp64 edge normalisation, astype(uint8) truncations) are the reference's own expressions.
+Known deviation from cv2: RGB<->Lab is evaluated with the float formulas, not cv2's 8U
+fixed-point tables (cv2 may differ by one level).  Every fp32 step rounds per operation
+(np.float32 arithmetic), matching the kernels, which are compiled without FMA contraction.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+f32 = np.float32
+
+
+def reflect101(i, n):
+    i = np.asarray(i)
+    if n == 1:
+        return np.zeros_like(i)
+    while np.any((i < 0) | (i >= n)):
+        i = np.where(i < 0, -i, np.where(i >= n, 2 * (n - 1) - i, i))
+    return i
+
+
+def sat_u8(v):
+    return np.clip(np.rint(v), 0, 255).astype(np.uint8)
+
+
+def rgb2gray(img):
+    """cv2 RGB2GRAY 8U fixed point."""
+    r, g, b = (img[..., k].astype(np.int32) for k in range(3))
+    return ((4899 * r + 9617 * g + 1868 * b + (1 << 13)) >> 14).astype(np.uint8)
+
+
+# ---- Lab (float formulas, D65, sRGB gamma) ----
+def _srgb_lin(c):
+    return np.where(c <= f32(0.04045), c / f32(12.92), ((c + f32(0.055)) / f32(1.055)) ** f32(2.4)).astype(f32)
+
+
+def _srgb_enc(c):
+    return np.where(c <= f32(0.0031308), f32(12.92) * c,
+                    f32(1.055) * c ** (f32(1.0) / f32(2.4)) - f32(0.055)).astype(f32)
+
+
+def _lab_f(t):
+    return np.where(t > f32(0.008856), np.cbrt(t), f32(7.787) * t + f32(16.0) / f32(116.0)).astype(f32)
+
+
+def _lab_finv(f):
+    return np.where(f > f32(0.206893), f * f * f, (f - f32(16.0) / f32(116.0)) / f32(7.787)).astype(f32)
+
+
+def rgb2lab(img):
+    c = img.astype(f32) / f32(255.0)
+    r, g, b = _srgb_lin(c[..., 0]), _srgb_lin(c[..., 1]), _srgb_lin(c[..., 2])
+    X = (f32(0.412453) * r + f32(0.357580) * g + f32(0.180423) * b) / f32(0.950456)
+    Y = f32(0.212671) * r + f32(0.715160) * g + f32(0.072169) * b
+    Z = (f32(0.019334) * r + f32(0.119193) * g + f32(0.950227) * b) / f32(1.088754)
+    fx, fy, fz = _lab_f(X), _lab_f(Y), _lab_f(Z)
+    L = np.where(Y > f32(0.008856), f32(116.0) * fy - f32(16.0), f32(903.3) * Y).astype(f32)
+    return np.stack([sat_u8(L * f32(255.0) / f32(100.0)), sat_u8(f32(500.0) * (fx - fy) + f32(128.0)),
+                     sat_u8(f32(200.0) * (fy - fz) + f32(128.0))], -1)
+
+
+def lab2rgb(lab):
+    L = lab[..., 0].astype(f32) * f32(100.0) / f32(255.0)
+    a = lab[..., 1].astype(f32) - f32(128.0)
+    b = lab[..., 2].astype(f32) - f32(128.0)
+    lin = L <= f32(7.9996)
+    Y_lin = L / f32(903.3)
+    fy = np.where(lin, f32(7.787) * Y_lin + f32(16.0) / f32(116.0), (L + f32(16.0)) / f32(116.0)).astype(f32)
+    Y = np.where(lin, Y_lin, fy * fy * fy).astype(f32)
+    fx, fz = fy + a / f32(500.0), fy - b / f32(200.0)
+    X, Z = _lab_finv(fx) * f32(0.950456), _lab_finv(fz) * f32(1.088754)
+    r = f32(3.240479) * X - f32(1.53715) * Y - f32(0.498535) * Z
+    g = f32(-0.969256) * X + f32(1.875991) * Y + f32(0.041556) * Z
+    bb = f32(0.055648) * X - f32(0.204043) * Y + f32(1.057311) * Z
+    out = [sat_u8(f32(255.0) * _srgb_enc(np.clip(v, f32(0), f32(1)).astype(f32))) for v in (r, g, bb)]
+    return np.stack(out, -1)
+
+
+# ---- HSV 8U (H in [0, 180)) ----
+def rgb2hsv(img):
+    SH = 12
+    r, g, b = (img[..., k].astype(np.int64) for k in range(3))
+    v = np.maximum(r, np.maximum(g, b))
+    vmin = np.minimum(r, np.minimum(g, b))
+    diff = v - vmin
+    vr = np.where(v == r, -1, 0)
+    vg = np.where(v == g, -1, 0)
+    idx = np.arange(256, dtype=np.float64)
+    with np.errstate(divide="ignore"):
+        sdiv = np.where(idx == 0, 0, np.rint((255 << SH) / idx)).astype(np.int64)
+        hdiv = np.where(idx == 0, 0, np.rint((180 << SH) / (6.0 * idx))).astype(np.int64)
+    s = (diff * sdiv[v] + (1 << (SH - 1))) >> SH
+    h = (vr & (g - b)) + (~vr & ((vg & (b - r + 2 * diff)) + ((~vg) & (r - g + 4 * diff))))
+    h = (h * hdiv[diff] + (1 << (SH - 1))) >> SH
+    h = h + np.where(h < 0, 180, 0)
+    return h, s, v
+
+
+def hsv2rgb(h8, s8, v8):
+    h = np.asarray(h8).astype(f32) * (f32(6.0) / f32(180.0))
+    s = np.asarray(s8).astype(f32) * (f32(1.0) / f32(255.0))
+    v = np.asarray(v8).astype(f32) * (f32(1.0) / f32(255.0))
+    h = np.where(h < 0, h + f32(6.0), h).astype(f32)
+    h = np.where(h >= 6, h - f32(6.0), h).astype(f32)
+    sector = np.floor(h).astype(np.int64)
+    hf = (h - sector.astype(f32)).astype(f32)
+    t0 = v
+    t1 = v * (f32(1.0) - s)
+    t2 = v * (f32(1.0) - s * hf)
+    t3 = v * (f32(1.0) - s * (f32(1.0) - hf))
+    tab = np.stack([t0, t1, t2, t3], 0)
+    rsel = np.array([0, 2, 1, 1, 3, 0])[sector]
+    gsel = np.array([3, 0, 0, 2, 1, 1])[sector]
+    bsel = np.array([1, 1, 3, 0, 0, 2])[sector]
+    pick = lambda sel: np.take_along_axis(tab, sel[None], 0)[0]
+    r, g, b = pick(rsel), pick(gsel), pick(bsel)
+    gray = s == 0
+    r, g, b = (np.where(gray, v, c).astype(f32) for c in (r, g, b))
+    return np.stack([sat_u8(r * f32(255.0)), sat_u8(g * f32(255.0)), sat_u8(b * f32(255.0))], -1)
+
+
+def hsv_adjust(img, sat=None, hue=None, val=None):
+    """dataset.py:261-264 (sat) and :297-300 (hue, val): fp32 arrays, astype(uint8)."""
+    h, s, v = rgb2hsv(img)
+    if sat is not None:
+        s = np.clip(s.astype(f32) * f32(sat), 0, 255).astype(np.uint8).astype(np.int64)
+    if hue is not None:
+        h = ((h.astype(f32) + f32(hue)) % f32(180.0)).astype(np.uint8).astype(np.int64)
+        v = np.clip(v.astype(f32) * f32(val), 0, 255).astype(np.uint8).astype(np.int64)
+    return hsv2rgb(h, s, v)
+
+
+# ---- CLAHE (OpenCV CLAHE_Impl) ----
+def clahe(src, clip_limit, grid=(8, 8)):
+    """src uint8 [h, w] -> uint8 [h, w]; grid = (tiles_x, tiles_y)."""
+    h, w = src.shape
+    tx_n, ty_n = grid
+    tw, th = -(-w // tx_n), -(-h // ty_n)
+    ys = reflect101(np.arange(th * ty_n), h)
+    xs = reflect101(np.arange(tw * tx_n), w)
+    ext = src[ys][:, xs]
+    area = tw * th
+    clip = max(int(clip_limit * area / 256), 1) if clip_limit > 0 else 1 << 30
+    scale = f32(255.0) / f32(area)
+    luts = np.zeros((ty_n, tx_n, 256), np.uint8)
+    for ty in range(ty_n):
+        for tx in range(tx_n):
+            hist = np.bincount(ext[ty * th:(ty + 1) * th, tx * tw:(tx + 1) * tw].ravel(), minlength=256)
+            excess = int(np.maximum(hist - clip, 0).sum())
+            hist = np.minimum(hist, clip)
+            batch, residual = excess // 256, excess % 256
+            hist = hist + batch
+            if residual:
+                step = max(256 // residual, 1)
+                for i in range(0, 256, step):
+                    if residual == 0:
+                        break
+                    hist[i] += 1
+                    residual -= 1
+            luts[ty, tx] = sat_u8(np.cumsum(hist).astype(f32) * scale)
+    inv_tw, inv_th = f32(1.0) / f32(tw), f32(1.0) / f32(th)
+    txf = np.arange(w).astype(f32) * inv_tw - f32(0.5)
+    tyf = np.arange(h).astype(f32) * inv_th - f32(0.5)
+    tx1, ty1 = np.floor(txf).astype(np.int64), np.floor(tyf).astype(np.int64)
+    xa, ya = (txf - tx1.astype(f32)).astype(f32), (tyf - ty1.astype(f32)).astype(f32)
+    tx2, ty2 = np.minimum(tx1 + 1, tx_n - 1), np.minimum(ty1 + 1, ty_n - 1)
+    tx1, ty1 = np.maximum(tx1, 0), np.maximum(ty1, 0)
+    v = src.astype(np.int64)
+    Y1, Y2, X1, X2 = ty1[:, None], ty2[:, None], tx1[None, :], tx2[None, :]
+    l11, l12 = luts[Y1, X1, v].astype(f32), luts[Y1, X2, v].astype(f32)
+    l21, l22 = luts[Y2, X1, v].astype(f32), luts[Y2, X2, v].astype(f32)
+    XA, YA = xa[None, :], ya[:, None]
+    res = (l11 * (f32(1.0) - XA) + l12 * XA) * (f32(1.0) - YA) + (l21 * (f32(1.0) - XA) + l22 * XA) * YA
+    return sat_u8(res.astype(f32))
+
+
+def clahe_rgb(img, clip_limit, grid=(8, 8)):
+    lab = rgb2lab(img)
+    lab2 = lab.copy()
+    lab2[..., 0] = clahe(lab[..., 0], clip_limit, grid)
+    return lab2rgb(lab2)
+
+
+# ---- filters (BORDER_REFLECT_101) ----
+def _taps(img):
+    h, w = img.shape[:2]
+    ys, xs = np.arange(h), np.arange(w)
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            yield dy, dx, img[reflect101(ys + dy, h)][:, reflect101(xs + dx, w)]
+
+
+def filter3x3(img, k9):
+    """cv2.filter2D(img, -1, k) with a 3x3 kernel: fp32 taps in row-major order."""
+    k = np.asarray(k9, np.float64).astype(f32).reshape(3, 3)
+    s = np.zeros(img.shape, f32)
+    for dy, dx, t in _taps(img):
+        s = s + k[dy + 1, dx + 1] * t.astype(f32)
+    return sat_u8(s)
+
+
+def sharpen(img, strength):
+    return filter3x3(img, np.array([[-1, -1, -1], [-1, 9, -1], [-1, -1, -1]]) * strength)
+
+
+def unsharp(img):
+    """GaussianBlur(3x3, 1.0) 8U fixed point (70, 116, 70)/256 + addWeighted(1.3, -0.3)."""
+    wk = (70, 116, 70)
+    h, w = img.shape[:2]
+    ys, xs = np.arange(h), np.arange(w)
+    col = np.zeros(img.shape, np.int64)
+    for dy in (-1, 0, 1):
+        rows = img[reflect101(ys + dy, h)].astype(np.int64)
+        row = sum(wk[dx + 1] * rows[:, reflect101(xs + dx, w)] for dx in (-1, 0, 1))
+        col += wk[dy + 1] * row
+    g = ((col + (1 << 15)) >> 16).astype(f32)
+    return sat_u8(img.astype(f32) * f32(1.3) + g * f32(-0.3))
+
+
+def edge_features(gray):
+    """dataset.py:77-88: Sobel magnitude and |Laplacian| (CV_64F), normalised, 0.7 / 0.3."""
+    t = {(dy, dx): v.astype(np.float64) for dy, dx, v in _taps(gray)}
+    sx = (t[-1, 1] - t[-1, -1]) + 2 * (t[0, 1] - t[0, -1]) + (t[1, 1] - t[1, -1])
+    sy = (t[1, -1] - t[-1, -1]) + 2 * (t[1, 0] - t[-1, 0]) + (t[1, 1] - t[-1, 1])
+    mag = np.sqrt(sx ** 2 + sy ** 2)
+    e = np.clip(mag / (mag.max() + 1e-6) * 255, 0, 255).astype(np.uint8)
+    lap = np.abs(t[-1, 0] + t[0, -1] - 4 * t[0, 0] + t[0, 1] + t[1, 0])
+    l = np.clip(lap / (lap.max() + 1e-6) * 255, 0, 255).astype(np.uint8)
+    return (e.astype(f32) * f32(0.7) + l.astype(f32) * f32(0.3)).astype(np.uint8)
+
+
+def cell_preprocess(image, live_mask, dead_mask):
+    """dataset.py:58-131 with the masks already reduced to (h, w) unions (:93-100)."""
+    image_clahe = clahe_rgb(image, 2.5)
+    edges = edge_features(rgb2gray(image))
+    edges_rgb = np.repeat(edges[..., None], 3, -1)
+    if live_mask.sum() > 0:
+        live_enh = np.clip(image_clahe.astype(f32) * f32(1.1), 0, 255).astype(np.uint8)
+        image_clahe = np.where(live_mask[..., None] > 0, live_enh, image_clahe)
+    if dead_mask.sum() > 0:
+        dead_clahe = clahe(rgb2gray(image_clahe), 3.0)
+        image_clahe = np.where(dead_mask[..., None] > 0, dead_clahe[..., None], image_clahe)
+    iwe = np.clip(image_clahe.astype(f32) * f32(0.9) + edges_rgb.astype(f32) * f32(0.1), 0, 255).astype(np.uint8)
+    fin = (iwe.astype(f32) * f32(0.85) + image.astype(f32) * f32(0.15)).astype(np.uint8)
+    return unsharp(fin)
+
+
+def chw_to_u8(x):
+    """train_eval.py:367-377."""
+    x = np.asarray(x, f32)
+    hwc = x.transpose(1, 2, 0)
+    v = hwc * f32(255.0) if x.max() <= 1.0 else hwc
+    return v.astype(np.int64).astype(np.uint8)

@@ -1,0 +1,100 @@
+"""CPU checks of the cv2 restatement (oracle/imgproc_ref.py) -- parity unpinned (cv2 absent).
+
+Pins what can be pinned without cv2: textbook colour values (white / black / primaries in
+8U Lab and HSV as OpenCV defines the 8U ranges), round trips, CLAHE invariants (a flat
+image stays flat, one-tile LUTs are monotone), filter identities.
+"""
+import numpy as np
+import pytest
+
+from oracle import imgproc_ref as O
+
+
+def _img(seed, h=37, w=53):
+    return np.random.default_rng(seed).integers(0, 256, (h, w, 3), dtype=np.uint8)
+
+
+def test_gray_weights():
+    px = np.array([[[255, 255, 255], [0, 0, 0], [255, 0, 0], [0, 255, 0], [0, 0, 255]]], np.uint8)
+    # 0.299 / 0.587 / 0.114 in 14-bit fixed point
+    assert O.rgb2gray(px).tolist() == [[255, 0, 76, 150, 29]]
+
+
+def test_lab_textbook_values():
+    px = np.array([[[255, 255, 255], [0, 0, 0], [255, 0, 0], [0, 255, 0], [0, 0, 255]]], np.uint8)
+    lab = O.rgb2lab(px)[0].tolist()
+    assert lab[0] == [255, 128, 128] and lab[1] == [0, 128, 128]
+    # L*, a*, b* of sRGB red / green / blue (53.2, 80.1, 67.2), (87.7, -86.2, 83.2), (32.3, 79.2, -107.9)
+    assert lab[2] == [136, 208, 195] and lab[3] == [224, 42, 211] and lab[4] == [82, 207, 20]
+
+
+def test_lab_round_trip():
+    img = _img(1, 64, 64)
+    back = O.lab2rgb(O.rgb2lab(img))
+    # 8-bit Lab quantises L to 100/255 and a, b to 1: a few levels on dark saturated colours
+    assert np.abs(back.astype(int) - img).max() <= 24  # near-zero channels: steep sRGB curve
+    assert np.abs(back.astype(int) - img).mean() < 1.0
+
+
+def test_hsv_textbook_values_and_round_trip():
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [128, 64, 0]]], np.uint8)
+    h, s, v = O.rgb2hsv(px)
+    assert h.tolist() == [[0, 60, 120, 0, 15]] and s.tolist() == [[255, 255, 255, 0, 255]]
+    assert v.tolist() == [[255, 255, 255, 255, 128]]
+    img = _img(2, 48, 48)
+    back = O.hsv2rgb(*O.rgb2hsv(img))
+    assert np.abs(back.astype(int) - img).max() <= 6  # H quantised to 2 degrees
+
+
+def test_hsv_adjust_identity_and_hue_wrap():
+    img = _img(3)
+    assert np.array_equal(O.hsv_adjust(img, sat=1.0), O.hsv2rgb(*O.rgb2hsv(img)))
+    h0, _, _ = O.rgb2hsv(img)
+    h1, _, _ = O.rgb2hsv(O.hsv_adjust(img, hue=-10.0, val=1.0))
+    assert h1.min() >= 0 and h1.max() < 180
+
+
+@pytest.mark.parametrize("h,w", [(64, 64), (37, 53), (8, 8), (100, 9)])
+def test_clahe_invariants(h, w):
+    flat = np.full((h, w), 97, np.uint8)
+    out = O.clahe(flat, 2.0)
+    assert (out == out[0, 0]).all()
+    g = np.random.default_rng(4).integers(0, 256, (h, w)).astype(np.uint8)
+    a, b = O.clahe(g, 2.0), O.clahe(g, 0.0)
+    assert a.shape == g.shape and b.shape == g.shape
+    # one tile: the transfer function (a clipped CDF) is monotone
+    ramp = np.tile(np.arange(256, dtype=np.uint8), (16, 1))[:, :w if w <= 256 else 256]
+    r = O.clahe(ramp, 3.0, (1, 1))
+    assert (np.diff(r[0].astype(int)) >= 0).all()
+
+
+def test_filters_identities():
+    img = _img(5)
+    ident = [0, 0, 0, 0, 1, 0, 0, 0, 0]
+    assert np.array_equal(O.filter3x3(img, ident), img)
+    flat = np.full((20, 30, 3), 77, np.uint8)
+    # the reference's kernel sums to 1 * strength, so on a flat image it scales brightness:
+    # 77 * 0.15 = 11.55 -> 12 (train_eval.py:388-391 darkens as written)
+    assert (O.sharpen(flat, 0.15) == 12).all()
+    assert np.array_equal(O.unsharp(flat), flat)
+    assert (O.edge_features(flat[..., 0]) == 0).all()
+
+
+def test_cell_preprocess_shapes_and_masks():
+    img = _img(6, 64, 80)
+    live = np.zeros((64, 80), np.int64)
+    live[10:30, 10:40] = 1
+    dead = np.zeros((64, 80), np.int64)
+    dead[40:60, 50:75] = 1
+    out = O.cell_preprocess(img, live, dead)
+    assert out.shape == img.shape and out.dtype == np.uint8
+    none = O.cell_preprocess(img, np.zeros_like(live), np.zeros_like(dead))
+    assert not np.array_equal(out[10:30, 10:40], none[10:30, 10:40])
+    assert np.array_equal(out[0:5, 0:5], none[0:5, 0:5])  # far from both masks nothing changes
+
+
+def test_chw_to_u8_branches():
+    x = np.random.default_rng(7).random((3, 5, 6)).astype(np.float32)
+    assert np.array_equal(O.chw_to_u8(x), (x.transpose(1, 2, 0) * np.float32(255)).astype(np.uint8))
+    y = x * 200
+    assert np.array_equal(O.chw_to_u8(y), y.transpose(1, 2, 0).astype(np.uint8))
