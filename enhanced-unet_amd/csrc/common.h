@@ -12,7 +12,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t bf16_t;  // storage type for bf16 activations
 
 __device__ __forceinline__ bf16x8 cat_bf16x4(s16x4 lo, s16x4 hi) {
@@ -161,14 +160,6 @@ inline void allow_lds(K* kernel, size_t bytes) {
 }
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
-
-// compute units of the current device (grid size of the one-block-per-CU kernels)
-inline int device_cus() {
-  int dev = 0, n = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  return n;
-}
 
 // activation view accessors
 __host__ __device__ inline long long act_pix(const eunet_act& a, int n, int y, int x) {

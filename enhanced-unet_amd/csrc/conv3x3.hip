@@ -24,9 +24,9 @@
 //
 // The library takes no configuration from the environment: the alternatives measured
 // against these kernels (double buffering, 8 waves, producer/consumer waves, LDS-DMA
-// staging, weight fragments from L2, tap pipelining, a persistent Cin=64 kernel, other
-// block orders) are recorded in DESIGN.md §4 and profiles/r01_*; their code lives in the
-// git history (round 1), not in this file.
+// staging, weight fragments from L2, tap pipelining, persistent Cin=64 kernels (round 1, and a
+// wave-group-skewed one in round 2), other block orders) are recorded in DESIGN.md §4 and
+// profiles/r0*_ab_*; their code lives in the git history, not in this file.
 #include <algorithm>
 
 #include "common.h"
@@ -465,316 +465,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Forward for 33..64 input channels (bf16, two K-chunks): enc1.3, dec2.3, enc2.0.
-// conv3x3_fwd_kernel spends most of these layers outside the MFMAs: two K-chunks
-// per 16x32 tile leave the per-block staging round trips and the epilogue
-// unamortised, and they sit at the machine balance point (288 FLOP/B).  Here one
-// 8-wave block per CU keeps all 64 x 9 x 64 weights of its co-block resident in
-// LDS and walks a contiguous run of tiles, with the halo in two 32-channel chunk
-// slots.  Waves w and w + 4 share a SIMD; the two wave groups run the same tile
-// with a skewed schedule so that one group's halo writes and epilogue overlap
-// the other group's MFMAs (three barriers per tile):
-//   seg1   G0: C1(t)                        G1: C0(t)        (both: next halo loads issued)
-//   seg2   G0: write c0(t+1), epilogue(t)   G1: C1(t)
-//   seg3   G0: C0(t+1)                      G1: write c1(t+1), epilogue(t)
-// G0 (waves 0-3) stages chunk 0 of every tile, G1 chunk 1.  The MFMA operands are
-// swapped (D^T = W^T X^T), so a lane holds 4 consecutive output channels of one
-// pixel and stores them as one 8-byte bf16 vector without LDS.  BN partials: each
-// wave reduces its two rows (sum, M2 about the wave mean) in registers; one G0
-// thread per channel Chan-combines the 8 waves of the previous tile (two-tile
-// LDS ring), so the stats keep the 16x32-tile layout of conv3x3_fwd_kernel.
-constexpr int KP_T = 512;
-constexpr int KP_ASTR = 624;                    // halo plane stride in px (multiple of 16: conflict-free)
-constexpr int KP_ABYTES = 4 * KP_ASTR * 16;     // 39936: one chunk's halo [4 quarters][624 px][16 B]
-constexpr int KP_W = 2 * B_LDS_BYTES;           // 73728: both chunks' weights
-constexpr int KP_RED = 2 * 8 * 2 * 64;          // floats: [2 tiles][8 waves][sum, M2][64]
-constexpr int KP_LDS = KP_W + 2 * KP_ABYTES + KP_RED * 4 + 64 * 4;
-constexpr int KP_UNITS = ((FHPX + 7) / 8) * 32; // 2464 halo unit ids per chunk
-constexpr int KP_IT = (KP_UNITS + 255) / 256;   // 10 per thread of a group
-static_assert(KP_LDS <= 160 * 1024, "k64p LDS");
-
-// sum over the 16 lanes of a DPP row (every lane gets it)
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror 4
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror 8
-  return v;
-}
-
-#ifndef KP_ABL
-#define KP_ABL 0  // diagnostic builds only (tools/abl_build.sh): 1 no epilogue, 2 halo staged once, 4 no MFMAs
-#endif
-__global__ __launch_bounds__(KP_T, 1) void conv3x3_k64p_kernel(FwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const Ws = smem;
-  char* const As = smem + KP_W;
-  float* const red = (float*)(smem + KP_W + 2 * KP_ABYTES);
-  float* const lbias = red + KP_RED;
-  constexpr int E = 8, MT = 4;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int q = lane >> 4, li = lane & 15;
-  const bool g0 = wv < 4;
-  const int gt = tid & 255, myc = g0 ? 0 : 1;  // thread within its group; the chunk it stages
-  const int sq = (gt >> 3) & 3;                // its halo quarter (fixed: 256 units per iteration)
-
-  // work: XCD-aware logical block -> (co-block, contiguous tile run); the launcher makes the grid
-  // a multiple of the co-block count
-  const int ncob = a.cout_pad / BN, G = gridDim.x;
-  const int L = (G & 7) == 0 ? (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-  const int cob = L % ncob, j = L / ncob, per = cdiv(a.ntiles, G / ncob);
-  const int tbeg = j * per, tend = min(a.ntiles, tbeg + per);
-  if (tbeg >= tend) return;
-  const int co0 = cob * BN, tpi = a.tx * a.ty;
-
-  {
-    const u32x4* wp = (const u32x4*)a.wp;
-    for (int id = tid; id < 2 * B_UNITS; id += KP_T) {
-      const int kc = id / B_UNITS, u = id - kc * B_UNITS;
-      *(u32x4*)(Ws + id * 16) = wp[((long long)(kc * 4 + u / (BN * 9)) * a.cout_pad + co0) * 9 + u % (BN * 9)];
-    }
-    if (tid < BN) lbias[tid] = (a.bias != nullptr && co0 + tid < a.cout) ? a.bias[co0 + tid] : 0.f;
-  }
-
-  u32x4 ra[KP_IT];
-  uint32_t rok = 0;  // bit i: unit i is inside the image (the BN+ReLU transform applies)
-  f32x4 asc[2], ash[2];
-  const bool cok = myc * 32 + sq * E < a.cin;
-  const bool tr = a.isc != nullptr;
-  // per unit: halo (row << 8 | column), 0xFFFF past the halo; the thread's quarter is sq for all
-  uint32_t upk[KP_IT];
-#pragma unroll
-  for (int i = 0; i < KP_IT; ++i) {
-    int hp, qq;
-    fwd_unit(gt + i * 256, hp, qq);
-    upk[i] = hp < FHPX ? (uint32_t)(((hp / FHW) << 8) | (hp % FHW)) : 0xFFFFu;
-  }
-  auto gload = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * FTH - 1, x0 = (trem % a.tx) * FTW - 1;
-    const int ns = __builtin_amdgcn_readfirstlane(n);
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const bf16_t*)a.x + (long long)ns * a.H * a.W * a.xct), 0, a.H * a.W * a.xct * 2, 0x00020000);
-    const int cadd = a.xco + myc * 32 + sq * E;
-    rok = 0;
-    // interior tile (halo inside the image): no per-unit bounds, only the past-the-halo units
-    const bool inner = y0 >= 0 && x0 >= 0 && y0 + FTH + 2 <= a.H && x0 + FHW <= a.W;
-    const int tb = (y0 * a.W + x0) * a.xct + cadd;
-#pragma unroll
-    for (int i = 0; i < KP_IT; ++i) {
-      uint32_t u = upk[i];
-      asm volatile("" : "+v"(u));  // derived values stay per tile (not hoisted into live registers)
-      const int hy = (int)(u >> 8), hx = (int)(u & 0xFFu);
-      const int yy = y0 + hy, xx = x0 + hx;
-      const bool ok = cok && u != 0xFFFFu && (inner || (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W));
-      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (uint32_t)((tb + (hy * a.W + hx) * a.xct) * 2) : FWD_OOB,
-                                                    0, 0);
-      rok |= (uint32_t)ok << i;
-    }
-    const int nbytes = tr ? a.cin * 4 : 0;
-    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(tr ? a.isc + (long long)ns * a.iss : nullptr), 0, nbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(tr ? a.ish + (long long)ns * a.iss : nullptr), 0, nbytes, 0x00020000);
-    const uint32_t aoff = (uint32_t)((myc * 32 + sq * E) * 4);
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      asc[jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(sr, aoff + 16 * jj, 0, 0));
-      ash[jj] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, aoff + 16 * jj, 0, 0));
-    }
-  };
-  auto lwrite = [&]() {
-    char* const A_ = As + myc * KP_ABYTES;
-#pragma unroll
-    for (int i = 0; i < KP_IT; ++i) {
-      uint32_t u = upk[i];
-      asm volatile("" : "+v"(u));
-      if (u == 0xFFFFu) continue;
-      const int hp = (int)(u >> 8) * FHW + (int)(u & 0xFFu);
-      u32x4 v = ra[i];
-      if (tr) {  // BN + ReLU of the producing layer; padding stays zero
-        float f[E];
-        Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, v), f);
-        const bool ok = (rok >> i) & 1u;
-#pragma unroll
-        for (int e = 0; e < E; ++e) f[e] = ok ? fmaxf(fmaf(f[e], asc[e >> 2][e & 3], ash[e >> 2][e & 3]), 0.f) : 0.f;
-        v = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
-      }
-      *(u32x4*)(A_ + (sq * KP_ASTR + hp) * 16) = v;
-    }
-  };
-
-  f32x4 acc[MT][4];
-  auto zero = [&]() {  // accumulators start at the bias (lane: channels nt*16 + 4q + 0..3)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const f32x4 bv = *(const f32x4*)(lbias + nt * 16 + 4 * q);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = bv;
-    }
-  };
-  auto compute = [&](int kc) {  // this wave's rows 2w, 2w+1 x 64 co over one K-chunk
-    int abase = (q * KP_ASTR + 2 * wv * FHW + li) * 16, bbase = (q * (BN * 9) + li * 9) * 16;
-    asm volatile("" : "+v"(abase), "+v"(bbase));
-    const char* A_ = As + kc * KP_ABYTES + abase;
-    const char* B_ = Ws + kc * B_LDS_BYTES + bbase;
-#pragma unroll 1
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int t = ky * 3 + kx;
-        uint4 fb[4];
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(B_ + (nt * 16 * 9 + t) * 16);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const uint4 fa = *(const uint4*)(A_ + (((mt >> 1) + ky) * FHW + (mt & 1) * 16 + kx) * 16);
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            if constexpr ((KP_ABL & 4) != 0)
-              acc[mt][nt][0] += __uint_as_float((fa.x ^ fb[nt].x) & 0x3f000000u);
-            else
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[nt]),
-                                                                    __builtin_bit_cast(bf16x8, fa), acc[mt][nt], 0, 0, 0);
-          }
-        }
-      }
-  };
-  // lane (q, li) of acc[mt][nt] holds output channels nt*16 + 4q + (0..3) of pixel li of m-tile mt
-  auto epilogue = [&](int tile, int k) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
-    const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
-    const int nrow = max(0, min(2, vh - 2 * wv)), nw = nrow * vw;
-    if ((KP_ABL & 16) == 0 && a.stats != nullptr) {
-      float* rr = red + (k & 1) * (KP_RED / 2);
-      const float rn = nw > 0 ? 1.f / (float)nw : 0.f;
-      // m-tile validity of this lane (a wave-uniform 'full' skips the selects on whole tiles)
-      const bool full = nrow == 2 && vw == FTW;
-      bool mv[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) mv[mt] = full || ((mt >> 1) < nrow && (mt & 1) * 16 + li < vw);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        f32x4 sv = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) sv += mv[mt] ? acc[mt][nt] : (f32x4){0.f, 0.f, 0.f, 0.f};
-        float sr[4], m2r[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sr[r] = row16_sum(sv[r]);
-        const f32x4 mw = (f32x4){sr[0], sr[1], sr[2], sr[3]} * rn;
-        f32x4 m2 = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const f32x4 d = acc[mt][nt] - mw;
-          m2 += mv[mt] ? d * d : (f32x4){0.f, 0.f, 0.f, 0.f};
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) m2r[r] = row16_sum(m2[r]);
-        if (li == 0) {
-          *(f32x4*)(rr + wv * 64 + nt * 16 + 4 * q) = (f32x4){sr[0], sr[1], sr[2], sr[3]};
-          *(f32x4*)(rr + 8 * 64 + wv * 64 + nt * 16 + 4 * q) = (f32x4){m2r[0], m2r[1], m2r[2], m2r[3]};
-        }
-      }
-    }
-    // stores through a descriptor of this sample's output slice (32-bit offsets; the launcher
-    // checks the slice is < 2 GiB); out-of-tile pixels and padded channels get offset FWD_OOB
-    const int ns = __builtin_amdgcn_readfirstlane(n);
-    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((bf16_t*)a.y + (long long)ns * a.H * a.W * a.yct), 0, a.H * a.W * a.yct * 2, 0x00020000);
-    int lb = li;
-    asm volatile("" : "+v"(lb));
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int r = 2 * wv + (mt >> 1), c = (mt & 1) * 16 + lb;
-      const bool pok = r < vh && c < vw;
-      const int pbase = ((y0 + r) * a.W + x0 + c) * a.yct + a.yco + co0 + 4 * q;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const bool ok = pok && co0 + nt * 16 + 4 * q < a.cout;
-        const uint32_t lo = (uint32_t)f2bf(acc[mt][nt][0]) | ((uint32_t)f2bf(acc[mt][nt][1]) << 16);
-        const uint32_t hi = (uint32_t)f2bf(acc[mt][nt][2]) | ((uint32_t)f2bf(acc[mt][nt][3]) << 16);
-        if constexpr ((KP_ABL & 8) == 0)
-          __builtin_amdgcn_raw_buffer_store_b64((u32x2){lo, hi}, yr, ok ? (uint32_t)((pbase + nt * 16) * 2) : FWD_OOB, 0, 0);
-        else if (lo == 0x12345u && hi == 7u) a.stats[0] = 1.f;
-      }
-    }
-  };
-  auto combine = [&](int tile, int k) {  // G0 threads 0..63, one channel each
-    if ((KP_ABL & 32) != 0 || a.stats == nullptr || tid >= 64 || co0 + tid >= a.cout) return;
-    const float* rr = red + (k & 1) * (KP_RED / 2);
-    const int trem = tile % tpi;
-    const int vh = min(FTH, a.H - (trem / a.tx) * FTH), vw = min(FTW, a.W - (trem % a.tx) * FTW);
-    const float cnt = (float)(vh * vw);
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) sum += rr[w * 64 + tid];
-    const float mean = sum / cnt;
-    float m2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const int nwv = max(0, min(2, vh - 2 * w)) * vw;
-      const float d = nwv > 0 ? rr[w * 64 + tid] / (float)nwv - mean : 0.f;
-      m2 += rr[8 * 64 + w * 64 + tid] + (float)nwv * d * d;
-    }
-    a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
-    a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
-    if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
-  };
-
-  // diagnostic builds (KP_ABL & 32): per-wave clock stamps of block 0's first 8 tiles into a.stats
-  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)a.stats, 0, (KP_ABL & 32) ? 8 * 8 * 8 * 8 : 0,
-                                                                      0x00020000);
-  auto stamp = [&](int k, int slot) {
-    if constexpr ((KP_ABL & 32) != 0) {
-      if (blockIdx.x == 0 && lane == 0 && k < 8) {
-        const unsigned long long c = clock64();
-        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)c, (uint32_t)(c >> 32)}, dr,
-                                              (uint32_t)(((wv * 8 + k) * 8 + slot) * 8 + lane), 0, 0);
-      }
-    }
-  };
-  gload(tbeg);
-  lwrite();
-  __syncthreads();
-  zero();
-  if (g0) compute(0);
-  int k = 0;
-  for (int t = tbeg; t < tend; ++t, ++k) {
-    const bool more = t + 1 < tend;
-    stamp(k, 0);
-    // seg1: G0 finishes tile t (chunk 1), G1 starts it (chunk 0); both groups' next loads in flight
-    if ((KP_ABL & 2) == 0 && more) gload(t + 1);
-    if (!g0) zero();
-    compute(g0 ? 1 : 0);
-    stamp(k, 1);
-    __syncthreads();
-    stamp(k, 2);
-    // seg2 / seg3: one group computes while the other writes its next chunk and runs the epilogue
-#pragma unroll 1
-    for (int s = 0; s < 2; ++s) {
-      if (g0 == (s == 1)) {
-        if (s == 0 || more) {
-          if (s == 1) zero();
-          compute(s == 0 ? 1 : 0);
-        }
-      } else {
-        if ((KP_ABL & 2) == 0 && more) lwrite();
-        if constexpr ((KP_ABL & 1) != 0) {
-          if (acc[0][0][0] == 1234.5f && acc[3][3][3] == 1.f) a.stats[tid] = 1.f;
-        } else {
-          epilogue(t, k);
-          if (s == 0 && k > 0) combine(t - 1, k - 1);
-        }
-      }
-      stamp(k, 3 + 2 * s);
-      __syncthreads();
-      stamp(k, 4 + 2 * s);
-    }
-  }
-  combine(tend - 1, k - 1);
-}
 
 // ---------------------------------------------------------------------------
 // weight packing: torch [Cout][Cin][3][3] fp32 -> [Cin_p/KC][4][Cout_p][9][E]
@@ -1236,18 +926,7 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
   EUNET_REQUIRE((long long)a.H * a.W * a.xct * esz < (1ll << 31),
                 "conv3x3: one sample's input (%d x %d x %d) must be < 2 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
   EUNET_REQUIRE((long long)a.nkc * kchunk(dtype) * a.cout_pad * 9 * esz < (1ll << 31), "conv3x3: packed weights >= 2 GiB");
-  const int ncob = a.cout_pad / BN;
-  if (!DG && dtype == EUNET_BF16 && a.nkc == 2 && a.bpart == nullptr && a.gsc == nullptr) {
-    const int cus = device_cus();
-    const int G = (cus / ncob) * ncob;  // one resident block per CU, whole co-block groups
-    if (G > 0 && (long long)a.ntiles * ncob >= G && (long long)a.H * a.W * a.yct * 2 < (1ll << 31)) {
-      allow_lds(conv3x3_k64p_kernel, KP_LDS);
-      conv3x3_k64p_kernel<<<dim3(G), KP_T, KP_LDS, (hipStream_t)stream>>>(a);
-      EUNET_LAUNCH_CHECK("conv3x3_fwd");
-      return EUNET_OK;
-    }
-  }
-  dim3 grid(a.ntiles * ncob);
+  dim3 grid(a.ntiles * (a.cout_pad / BN));
   if (dtype == EUNET_BF16) {
     allow_lds(conv3x3_fwd_kernel<bf16_t, DG>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
