@@ -699,3 +699,25 @@ def test_fused_bn_reduce_in_gradient_producers(dt, kind):
     torch.cuda.synchronize()
     assert torch.equal(gout, gref)
     assert rel(red, red2) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,K", [(64, 2), (64, 1), (96, 3), (128, 2), (8, 3)])
+def test_bnrelu_conv1x1_shapes(dt, C, K):
+    """dec1 (BN+ReLU -> 1x1 conv): every K, one and two 64-channel groups, a channel slice of a
+    wider buffer, and a pixel count that leaves a partial block step (4 x 32 pixels)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(40 + C + K)
+    N, H, W, CT, CO = 3, 13, 27, C + 16, 8
+    buf = torch.randn(N, H, W, CT, generator=g, dtype=torch.float64).to(dt)
+    y = buf.double()[..., CO:CO + C]
+    sc = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(C, generator=g, dtype=torch.float64) * 0.3
+    w = torch.randn(K, C, generator=g, dtype=torch.float64) / 5
+    b = torch.randn(K, generator=g, dtype=torch.float64)
+    ref = torch.einsum("nhwc,kc->nhwk", torch.relu(y * sc + sh), w) + b
+    z = torch.empty(N, H, W, K, device=DEV)
+    ops.bnrelu_conv1x1(ops.act(buf.to(DEV), CO, C), sc.float().to(DEV), sh.float().to(DEV), w.float().to(DEV),
+                       b.float().to(DEV), K, z)
+    torch.cuda.synchronize()
+    assert rel(z, ref) < 1e-5
