@@ -1,0 +1,36 @@
+"""Standalone timing of HBM-bound kernels at the 1024^2 x 4, 64-channel bf16 shape (HIP events).
+    python tools/time_memk.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "enhanced-unet_amd")]
+import torch  # noqa: E402
+from eunet import ops  # noqa: E402
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+N, H, C = 4, 1024, 64
+dev = "cuda"
+g = torch.randn(N, H, H, C, device=dev).bfloat16()
+y = torch.randn(N, H, H, C, device=dev).bfloat16()
+gy = torch.empty_like(g)
+v = [torch.rand(C, device=dev) + 0.5 for _ in range(6)]
+ms = timeit(lambda: ops.bn_bwd_apply(ops.act(g), ops.act(y), *v, ops.act(gy)))
+print(f"bn_bwd_apply        {ms * 1e3:7.1f} us  {3 * g.numel() * 2 / ms / 1e9:5.2f} TB/s")
+z = torch.empty(N, H, H, 2, device=dev)
+w, b = torch.randn(2, C, device=dev), torch.randn(2, device=dev)
+ms = timeit(lambda: ops.bnrelu_conv1x1(ops.act(y), v[0], v[1], w, b, 2, z))
+print(f"bnrelu_conv1x1      {ms * 1e3:7.1f} us  {(y.numel() * 2 + z.numel() * 4) / ms / 1e9:5.2f} TB/s")
