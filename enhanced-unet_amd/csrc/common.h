@@ -12,6 +12,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef uint16_t bf16_t;  // storage type for bf16 activations
 
 __device__ __forceinline__ bf16x8 cat_bf16x4(s16x4 lo, s16x4 hi) {

@@ -525,6 +525,21 @@ struct WgArgs {
 
 __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised): LDS-DMA source of padding
 
+// LDS bank spreading of the wgrad stages (ds_read_b64_tr_b16 serves 2 x 32 lanes; a wave's
+// fragment reads were 4-way (dY) / 2-way (X) conflicted):
+//  - dY tile [256 px][8 units of 16 B]: pixel p's channel unit u is stored at unit u ^ wd_swz(p),
+//    so the 32 lanes of a transposed read (8 pixels x 4 channel quads) hit 64 distinct banks;
+//  - X halo [8 octants][HPXP]: odd channel octants start 4 slots (64 B) later, so the two octants
+//    a read spans fall in different banks.
+#ifndef WG_SWZ_D
+#define WG_SWZ_D 1
+#endif
+#ifndef WG_SWZ_X
+#define WG_SWZ_X 1
+#endif
+__device__ __forceinline__ int wd_swz(int p) { return WG_SWZ_D ? (p & 3) ^ (((p >> 3) & 1) << 2) : 0; }
+__device__ __forceinline__ int wx_shift(int oc) { return WG_SWZ_X ? (oc & 1) * 4 : 0; }
+
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
 // w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
 // 32-pixel k-step costs 8 + 18 transposed fragment reads for 36 MFMAs.
@@ -570,6 +585,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   const int t_end = min(a.ntiles, t_begin + a.per_split);
   const int tpi = a.tx * a.ty;
   const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  // this lane's dY read offset within a pixel row, less the 2ct units: wd_swz(pxa) is q4 ^ 4 (g & 1)
+  // for every k-step (pxa = 32 ks + 8 g + q4), and XOR-ing 2ct (even) into the unit index
+  // commutes with the low bit and the byte offset of the half
+  const int sw16 = (((p4 >> 1) ^ wd_swz(8 * g + q4)) * 8 + 4 * (p4 & 1)) * 2;
 
   f32x4 acc[9][4];
 #pragma unroll
@@ -587,7 +606,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     char* Ds = smem + WX_LDS;
     for (int j = wv; j < WD_ITERS * NTHR / 64; j += NTHR / 64) {
       const int id = j * 64 + lane;
-      const int px = id >> 3, u = id & 7;
+      const int px = id >> 3, u = (id & 7) ^ wd_swz(px);  // LDS unit id & 7 holds channel unit u
       const int r = px / TW, c = px - r * TW;
       const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
       const void* src = (yy < a.H && xx < a.W && co < a.cout)
@@ -602,34 +621,49 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
     for (int j = wv; j < 8 * HPXP / 64; j += NTHR / 64) {
-      const int sl = j * 64 + lane, oc = sl / HPXP, hp = sl - oc * HPXP;
+      const int sl = j * 64 + lane, oc = sl / HPXP, hp = sl - oc * HPXP - wx_shift(oc);
       const int hy = hp / HW_, hx = hp - hy * HW_;
       const int yy = y0 + hy - 1, xx = x0 + hx - 1;
       const int c = kc * KCW + oc * 8;
-      const void* src = (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
+      const void* src = (hp >= 0 && hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
                             ? (const void*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c)
                             : (const void*)&g_conv_zero;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(smem + j * 64 * 16), 16, 0, 0);
     }
   };
-  auto bnrelu_x = [&](int tile) {  // BN+ReLU of the staged halo in place; padding stays 0
+  // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t & 7 and
+  // halo pixels (t >> 3) + 32 i (i < 11): its 8 scales / shifts are read once per tile and the
+  // pixel coordinates advance incrementally (32 < 34 columns: at most one row wrap per step).
+  const int xo = tid & 7;
+  auto bnrelu_x = [&](int tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-    for (int sl = tid; sl < 8 * HPXP; sl += NTHR) {
-      const int oc = sl / HPXP, hp = sl - oc * HPXP;
-      const int hy = hp / HW_, hx = hp - hy * HW_;
+    if (kc * KCW + xo * 8 >= a.cin) return;
+    const f32x4 s0 = *(const f32x4*)(lsc + xo * 8), s1 = *(const f32x4*)(lsc + xo * 8 + 4);
+    const f32x4 h0 = *(const f32x4*)(lsc + KCW + xo * 8), h1 = *(const f32x4*)(lsc + KCW + xo * 8 + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    char* const plane = smem + (xo * HPXP + wx_shift(xo)) * 16;
+    int hp = tid >> 3, hy = 0, hx = hp;
+#pragma unroll 1
+    for (int i = 0; i < (HPX + 31) / 32; ++i, hp += 32) {
       const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      const int c = kc * KCW + oc * 8;
-      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) {
-        u32x4* q = (u32x4*)(smem + sl * 16);
-        float f[8];
-        const float* sc = lsc + oc * 8;  // the tile's scale / shift rows, staged in LDS
-        Vec16<bf16_t>::unpack(__builtin_bit_cast(uint4, *q), f);
+      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+        u32x4* q = (u32x4*)(plane + hp * 16);
+        const u32x4 w = *q;
+        u32x4 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], sc[e], sc[KCW + e]), 0.f);
-        *q = __builtin_bit_cast(u32x4, Vec16<bf16_t>::pack(f));
+        for (int d = 0; d < 4; ++d) {  // packed fp32 FMA, round to bf16, ReLU on the bf16 pair (sign bit)
+          const f32x2 x = {__uint_as_float(w[d] << 16), __uint_as_float(w[d] & 0xFFFF0000u)};
+          const f32x2 r = __builtin_elementwise_fma(x, (f32x2){sc[2 * d], sc[2 * d + 1]}, (f32x2){sh[2 * d], sh[2 * d + 1]});
+          const s16x2 b = __builtin_bit_cast(s16x2, (uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16));
+          o[d] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
+        }
+        *q = o;
       }
+      hx += 32;
+      if (hx >= HW_) { hx -= HW_; ++hy; }
     }
   };
   for (int tile = t_begin; tile < t_end; ++tile) {
@@ -658,18 +692,21 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
 #pragma unroll
       for (int i = 0; i < TH * TW / 32; ++i) {  // independent 16-B reads, no per-read wait
         float f[8];
-        Vec16<bf16_t>::unpack(*(const uint4*)(d + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8), f);
+        const int px = (tid >> 3) + 32 * i;
+        Vec16<bf16_t>::unpack(*(const uint4*)(d + px * 64 + ((tid & 7) ^ wd_swz(px)) * 8), f);
 #pragma unroll
         for (int e = 0; e < 8; ++e) dbv[e] += f[e];
       }
     }
-    auto load_af = [&](int ks, bf16x8* f) {  // dY^T fragments of k-step ks (32 pixels x 4 co tiles)
+    // dY^T fragments of k-step ks (32 pixels x 4 co tiles); channel unit 2ct + (p4 >> 1) of pixel
+    // pxa (and pxa + 4: same wd_swz) sits at LDS unit (2ct + (p4 >> 1)) ^ wd_swz(pxa)
+    auto load_af = [&](int ks, bf16x8* f) {
       const int pxa = ks * TW + 8 * g + q4;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa * 64 + ct * 16 + 4 * p4) * 2));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            LDS_PTR(s16x4, Ds + ((pxa + 4) * 64 + ct * 16 + 4 * p4) * 2));
+        const int uo = (32 * ct) ^ sw16;  // byte offset of unit (2ct + (p4 >> 1)) ^ wd_swz(pxa), + the half
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + pxa * 128 + uo));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa + 4) * 128 + uo));
         f[ct] = cat_bf16x4(lo, hi);
       }
     };
@@ -682,7 +719,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
         const int hp = (ks + ky) * HW_ + 8 * g + q4 + kx;
-        const char* base = Xs + (oc * HPXP + hp) * 16 + (p4 & 1) * 8;
+        const char* base = Xs + (oc * HPXP + wx_shift(oc) + hp) * 16 + (p4 & 1) * 8;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
         const bf16x8 bfr = cat_bf16x4(lo, hi);
