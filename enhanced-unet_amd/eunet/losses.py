@@ -28,12 +28,30 @@ from ._lib import LossParams
 NO_IGNORE = -(2 ** 31)  # EUNET_NO_IGNORE
 
 
+_host_copies = {}  # id(tensor) -> (weakref, _version, values): no device sync per training step
+
+
+def _host_values(t: torch.Tensor):
+    """t's values as a Python list.  A device tensor is copied once and re-copied only after an
+    in-place change (t._version): the Trainer rebuilds its loss parameters every step from
+    self.focal_loss.class_weights, a cuda tensor, and a .cpu() there would drain the launch queue."""
+    import weakref
+    hit = _host_copies.get(id(t))
+    if hit is not None and hit[0]() is t and hit[1] == t._version:
+        return hit[2]
+    vals = t.detach().cpu().reshape(-1).tolist()
+    if len(_host_copies) > 64:
+        _host_copies.clear()
+    _host_copies[id(t)] = (weakref.ref(t), t._version, vals)
+    return vals
+
+
 def _triple(v, default: float, what: str):
     """A per-class table of 3 floats from None / a scalar / a list / a tensor (missing classes 0)."""
     if v is None:
         return [default] * 3
     if isinstance(v, torch.Tensor):
-        v = v.detach().cpu().reshape(-1).tolist()
+        v = _host_values(v)
     if isinstance(v, (int, float)):
         return [float(v)] * 3
     v = [float(a) for a in v]
