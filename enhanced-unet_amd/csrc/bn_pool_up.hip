@@ -173,17 +173,11 @@ struct SmallWgArgs {
   const void* dy; int dct, dco, cout;
   float* dw; float* db;
   int tx, ty, ntiles, per_split;
-  // optional BN-backward apply of dY (bn_bwd_apply_kernel's arithmetic, in the dY staging): dy is then
-  // the gradient g w.r.t. the BN+ReLU output, by the BN input y, and dY = K1 g' + y K2 + K3
-  const void* by; int byct, byco;
-  const float* mean; const float* istd; const float* scale; const float* shift; const float* dbeta;
-  const float* dgamma;
 };
 
 // direct-conv wgrad as MFMA: dW[co][ci*9+t] = sum_p dY[p][co] im2col(x)[p][ci*9+t];
 // im2col (cin*9 columns padded to njt*16 <= 80) and the dY tile are staged in LDS per 8x32 tile
-// BNB: dY = bn_bwd_apply(g, y) formed in the staging (SmallWgArgs.by / .mean ...)
-template <typename T, int CI, bool BNB = false>  // CI = max input channels of the instance (4: enc1.0, 8: fusion_head.0)
+template <typename T, int CI>  // CI = max input channels of the instance (4: enc1.0, 8: fusion_head.0)
 __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   constexpr int SCI = CI, SJT = (CI * 9 + 15) / 16;  // LDS sized per instance (occupancy)
   constexpr int E = Vec16<T>::N;
@@ -207,23 +201,6 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   static_assert(STH * STW * 64 / E % NT == 0, "dY units per thread");
   float rx[XI];
   uint4 rd[DI];
-  // fused BN-backward apply: this thread's dY channel unit is fixed (id % (64 / E) == tid % (64 / E))
-  constexpr bool bnb = BNB;
-  uint4 ry[DI];
-  // per-channel coefficients (kP, kQ: the forward affine = the ReLU mask; k1..k3 the apply) in LDS, read
-  // in the staging only (kept in registers they would stay live across the MFMA loop: occupancy 1)
-  __shared__ __attribute__((aligned(16))) float kt[5][64];
-  if (bnb && tid < 64) {
-    const int c = co0 + tid;
-    const bool ok = c < a.cout;
-    const float inv_n = 1.f / (float)((long long)a.N * a.H * a.W);
-    const float is = ok ? a.istd[c] : 0.f, off = ok ? -a.mean[c] * is : 0.f;
-    const float k1 = ok ? a.scale[c] : 0.f, dg = ok ? a.dgamma[c] * inv_n : 0.f;
-    kt[0][tid] = k1;
-    kt[1][tid] = ok ? a.shift[c] : 0.f;
-    kt[2][tid] = -k1 * is * dg;
-    kt[3][tid] = -k1 * fmaf(off, dg, (ok ? a.dbeta[c] : 0.f) * inv_n);
-  }
   auto load_tile = [&](int tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
     const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
@@ -243,31 +220,12 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       const int px = id / (64 / E), u = id - px * (64 / E);
       const int r = px / STW, c = px - r * STW;
       const int yy = y0 + r, xx = x0 + c, co = co0 + u * E;
-      const bool in = yy < a.H && xx < a.W && co < a.cout;
-      const long long pix = (long long)(n * a.H + yy) * a.W + xx;
-      rd[k] = in ? *(const uint4*)((const T*)a.dy + pix * a.dct + a.dco + co) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  // y of the fused BN-backward apply: loaded after the previous tile's MFMAs, not with the dY prefetch
-  // (held across the MFMA loop it costs the second wave per SIMD: 256+ VGPRs)
-  auto load_y = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * STH, x0 = (trem % a.tx) * STW;
-#pragma unroll
-    for (int k = 0; k < DI; ++k) {
-      const int id = tid + k * NT;
-      const int px = id / (64 / E), u = id - px * (64 / E);
-      const int r = px / STW, c = px - r * STW;
-      const int yy = y0 + r, xx = x0 + c, co = co0 + u * E;
-      ry[k] = (yy < a.H && xx < a.W && co < a.cout)
-                  ? *(const uint4*)((const T*)a.by + ((long long)(n * a.H + yy) * a.W + xx) * a.byct + a.byco + co)
+      rd[k] = (yy < a.H && xx < a.W && co < a.cout)
+                  ? *(const uint4*)((const T*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co)
                   : make_uint4(0, 0, 0, 0);
     }
   };
-  if (t_begin < t_end) {
-    load_tile(t_begin);
-    if (bnb) load_y(t_begin);
-  }
+  if (t_begin < t_end) load_tile(t_begin);
   for (int tile = t_begin; tile < t_end; ++tile) {
     __syncthreads();
 #pragma unroll
@@ -282,28 +240,9 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
     for (int k = 0; k < DI; ++k) {
       const int id = tid + k * NT;
       const int px = id / (64 / E), u = id - px * (64 / E);
-      uint4 v = rd[k];
-      if (bnb) {  // bn_bwd_apply_kernel's operations in its order (bit-identical dY); padding stays 0
-        const int r = px / STW, c = px - r * STW;
-        const int n = tile / tpi, trem = tile - n * tpi;
-        const bool in = (trem / a.tx) * STH + r < a.H && (trem % a.tx) * STW + c < a.W && co0 + u * E < a.cout;
-        float gf[E], yf[E], o[E];
-        Vec16<T>::unpack(v, gf);
-        Vec16<T>::unpack(ry[k], yf);
-#pragma unroll
-        for (int j = 0; j < E; ++j) {
-          const int cc = u * E + j;
-          const float k1 = kt[0][cc];
-          const float gg = fmaf(yf[j], k1, kt[1][cc]) > 0.f ? gf[j] : 0.f;
-          o[j] = in ? fmaf(k1, gg, fmaf(yf[j], kt[2][cc], kt[3][cc])) : 0.f;
-        }
-        v = Vec16<T>::pack(o);
-      }
-      *(uint4*)(gs + px * 64 + u * E) = v;
-      if (bnb) __builtin_amdgcn_sched_barrier(0);  // one unit at a time: the unrolled transforms
-                                                   // scheduled together need 256+ VGPRs
+      *(uint4*)(gs + px * 64 + u * E) = rd[k];
     }
-    if (!bnb && tile + 1 < t_end) load_tile(tile + 1);
+    if (tile + 1 < t_end) load_tile(tile + 1);
     __syncthreads();
 #pragma unroll 4
     for (int id = tid; id < STH * STW * icw; id += NT) {
@@ -355,10 +294,6 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
           acc[jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, ((const float*)cs)[px * icw + jt * 16 + i], acc[jt], 0, 0, 0);
         }
       }
-    }
-    if (bnb && tile + 1 < t_end) {  // the fused form loads the next tile after the MFMAs (registers)
-      load_tile(tile + 1);
-      load_y(tile + 1);
     }
   }
   float* out = a.dw + (long long)split * a.cout * 9 * cin;
@@ -1374,24 +1309,11 @@ int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
   return EUNET_OK;
 }
 
-namespace {
-int small_wgrad(const eunet_act* x, const eunet_act* dy, const eunet_act* y, const float* mean, const float* invstd,
-                const float* scale, const float* shift, const float* dbeta, const float* dgamma, float* dw_part,
-                float* db_part, int nsplit, void* stream) {
+int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
+                           void* stream) {
   EUNET_REQUIRE(act_ok(x) && act_ok(dy) && dw_part && nsplit > 0, "conv_small_wgrad: bad args");
   EUNET_REQUIRE(x->c <= SCI && x->dtype == dy->dtype, "conv_small_wgrad: Cin <= 8, equal dtypes");
   SmallWgArgs a;
-  a.by = nullptr; a.byct = a.byco = 0;
-  a.mean = a.istd = a.scale = a.shift = a.dbeta = a.dgamma = nullptr;
-  if (y != nullptr) {
-    EUNET_REQUIRE(act_ok(y) && y->dtype == dy->dtype && y->n == dy->n && y->h == dy->h && y->w == dy->w &&
-                      y->c == dy->c && mean && invstd && scale && shift && dbeta && dgamma,
-                  "conv_small_wgrad_bnbwd: bad BN-backward operands");
-    const int E = y->dtype == EUNET_BF16 ? 8 : 4;
-    EUNET_REQUIRE(y->ctot % E == 0 && y->coff % E == 0, "conv_small_wgrad_bnbwd: y stride / offset");
-    a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
-    a.mean = mean; a.istd = invstd; a.scale = scale; a.shift = shift; a.dbeta = dbeta; a.dgamma = dgamma;
-  }
   a.x = x->ptr; a.N = x->n; a.H = x->h; a.W = x->w; a.xct = x->ctot; a.xco = x->coff; a.cin = x->c;
   a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
   a.dw = dw_part; a.db = db_part;
@@ -1399,11 +1321,7 @@ int small_wgrad(const eunet_act* x, const eunet_act* dy, const eunet_act* y, con
   a.per_split = cdiv(a.ntiles, nsplit);
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv_small_wgrad: nsplit mismatch");
   dim3 grid(nsplit, cdiv(dy->c, 64));
-  if (y != nullptr) {  // fused BN-backward apply: enc1.0 (Cin <= 4)
-    EUNET_REQUIRE(x->c <= 4, "conv_small_wgrad_bnbwd: Cin <= 4");
-    if (x->dtype == EUNET_BF16) conv_small_wgrad_kernel<bf16_t, 4, true><<<grid, NT, 0, (hipStream_t)stream>>>(a);
-    else conv_small_wgrad_kernel<float, 4, true><<<grid, NT, 0, (hipStream_t)stream>>>(a);
-  } else if (x->dtype == EUNET_BF16)
+  if (x->dtype == EUNET_BF16)
     if (x->c <= 4)
       conv_small_wgrad_kernel<bf16_t, 4><<<grid, NT, 0, (hipStream_t)stream>>>(a);
     else
@@ -1415,20 +1333,6 @@ int small_wgrad(const eunet_act* x, const eunet_act* dy, const eunet_act* y, con
       conv_small_wgrad_kernel<float, 8><<<grid, NT, 0, (hipStream_t)stream>>>(a);
   EUNET_LAUNCH_CHECK("conv_small_wgrad");
   return EUNET_OK;
-}
-}  // namespace
-
-int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part, float* db_part, int nsplit,
-                           void* stream) {
-  return small_wgrad(x, dy, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, dw_part, db_part, nsplit,
-                     stream);
-}
-
-int eunet_conv_small_wgrad_bnbwd(const eunet_act* x, const eunet_act* g, const eunet_act* y, const float* mean,
-                                 const float* invstd, const float* scale, const float* shift, const float* dbeta,
-                                 const float* dgamma, float* dw_part, float* db_part, int nsplit, void* stream) {
-  EUNET_REQUIRE(y != nullptr, "conv_small_wgrad_bnbwd: y required");
-  return small_wgrad(x, g, y, mean, invstd, scale, shift, dbeta, dgamma, dw_part, db_part, nsplit, stream);
 }
 
 int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, const float* beta, float eps,

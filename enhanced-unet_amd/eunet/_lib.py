@@ -57,7 +57,6 @@ SIGNATURES = {
     "eunet_conv_small_fwd": [_P, _f, _f, _P, _f, c_void_p],
     "eunet_conv_small_wgrad_splits": [_P, POINTER(c_int)],
     "eunet_conv_small_wgrad": [_P, _P, _f, _f, c_int, c_void_p],
-    "eunet_conv_small_wgrad_bnbwd": [_P, _P, _P, _f, _f, _f, _f, _f, _f, _f, _f, c_int, c_void_p],
     "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_bn_eval_affine": [c_int, _f, _f, _f, _f, c_float, _f, _f, c_void_p],
     "eunet_bnrelu": [_P, _f, _f, _P, c_void_p],

@@ -42,9 +42,6 @@ MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "0") != "0"
 # the BN-b backward reduction of a block fused into the kernel producing its output gradient
 # (upsample / max-pool adjoints) instead of a separate bn_bwd_reduce pass (EUNET_FUSE_BN_REDUCE=0)
 FUSE_BN_REDUCE = os.environ.get("EUNET_FUSE_BN_REDUCE", "1") != "0"
-# BN-a backward apply of the first block fused into conv .0's weight gradient
-# (eunet_conv_small_wgrad_bnbwd) instead of a separate bn_bwd_apply pass (EUNET_FUSE_SMALL_BNBWD=0)
-FUSE_SMALL_BNBWD = os.environ.get("EUNET_FUSE_SMALL_BNBWD", "1") != "0"
 
 
 class GradSink:
@@ -257,7 +254,7 @@ class UNetEngine:
         N, H, W, C = yb.shape
         dev, dt = yb.device, self.dtype
 
-        def bn_back(prefix, g, y, bn, part=None, tiles=0, apply=True):
+        def bn_back(prefix, g, y, bn, part=None, tiles=0):
             if part is None:  # reduction not fused into the producer of g
                 tiles = ops.bn_bwd_tiles(ops.act(y))
                 part = _e(tiles * 2 * C, torch.float32, dev)
@@ -265,8 +262,6 @@ class UNetEngine:
                                   bn["shift"], part)
             dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
             ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
-            if not apply:  # the consumer applies it in its staging
-                return dbeta, dgamma
             gy = torch.empty_like(y)
             ops.bn_bwd_apply(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
                              bn["shift"], dbeta, dgamma, ops.act(gy))
@@ -275,19 +270,19 @@ class UNetEngine:
         main = torch.cuda.current_stream(dev)
         side = side_stream(dev) if self.overlap_wgrad else None
 
-        def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False, on_main=False, bnbwd=None):
+        def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False, on_main=False):
             # the gradient slots are allocated on the launch stream (their consumers run there)
             dw = sink.slot(conv + ".weight", (C, xa.c, 3, 3))
             db = sink.slot(conv + ".bias", (C,))
             if side is None or on_main:
-                return wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv, bnbwd)
+                return wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
             side.wait_stream(main)  # gy (and everything before it) is ready
             with torch.cuda.stream(side):
                 wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
             for t in (gy, xa._keep, dw, db):  # the caching allocator must not hand these out early
                 t.record_stream(side)
 
-        def wgrad_on_stream(xa: ops.Act, gy, dw, db, scale=None, shift=None, small_conv=False, bnbwd=None):
+        def wgrad_on_stream(xa: ops.Act, gy, dw, db, scale=None, shift=None, small_conv=False):
             cin = xa.c
             gya = ops.act(gy)
             if small_conv:
@@ -296,9 +291,7 @@ class UNetEngine:
                 ns = ops.conv3x3_wgrad_splits(gya, cin, dt)
             dwp = _e(ns * C * 9 * cin, torch.float32, dev)
             dbp = _e(ns * C, torch.float32, dev)
-            if bnbwd is not None:  # gy is the BN+ReLU-output gradient; dY = bn_bwd_apply(gy, *bnbwd)
-                ops.conv_small_wgrad_bnbwd(xa, gya, *bnbwd, dwp, dbp, ns)
-            elif small_conv:
+            if small_conv:
                 ops.conv_small_wgrad(xa, gya, dwp, dbp, ns)
             else:
                 ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=scale, shift=shift)
@@ -318,18 +311,10 @@ class UNetEngine:
         ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
                                 bna["scale"], bna["shift"], cpart)
         del gyb
-        if small and not need_gx and FUSE_SMALL_BNBWD:
-            # the trunk's first block: conv .0's weight gradient is the only consumer of BN a's input
-            # gradient, so the apply runs inside its dY staging (gya is never stored); on the main
-            # stream, which is otherwise idle here, not queued behind the side stream's conv .3 wgrad
-            dbeta, dgamma = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles, apply=False)
-            wgrad(p + ".0", X, gaa, small_conv=True, on_main=True,
-                  bnbwd=(ops.act(ya), bna["mean"], bna["invstd"], bna["scale"], bna["shift"], dbeta, dgamma))
-            gya = None
-        else:
-            gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
-            # the trunk's last weight gradient (no data gradient follows it) runs on the main stream
-            wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx)
+        gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
+        # the trunk's last weight gradient (no data gradient follows it): on the main stream, which is
+        # otherwise idle here, instead of queueing behind the side stream's conv .3 wgrad
+        wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx)
         del gaa
         names = [f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")]
         if side is None:

@@ -152,14 +152,6 @@ def conv_small_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit):
          _stream())
 
 
-def conv_small_wgrad_bnbwd(x: Act, g: Act, y: Act, mean, invstd, scale, shift, dbeta, dgamma, dw_part, db_part,
-                           nsplit):
-    """conv_small_wgrad of dY = bn_bwd_apply(g, y, ...), the apply fused into the dY staging."""
-    call("eunet_conv_small_wgrad_bnbwd", ctypes.byref(x), ctypes.byref(g), ctypes.byref(y), _ptr(mean),
-         _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(dbeta), _ptr(dgamma), _ptr(dw_part), _ptr(db_part), nsplit,
-         _stream())
-
-
 def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, scale, shift,
                 num_batches_tracked=None):
     call("eunet_bn_finalize", _ptr(stats), tiles, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),

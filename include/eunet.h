@@ -112,13 +112,6 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias,
 int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit);
 int eunet_conv_small_wgrad(const eunet_act* x, const eunet_act* dy, float* dw_part,
                            float* db_part, int nsplit, void* stream);
-/* the same with the BN-backward apply of dY fused into its staging (the enc1 block's conv .0,
- * whose dY = bn_bwd_apply(g, y, ...) has no other consumer): g, y and the statistics as for
- * eunet_bn_bwd_apply; dY is formed in registers with that kernel's arithmetic and never stored */
-int eunet_conv_small_wgrad_bnbwd(const eunet_act* x, const eunet_act* g, const eunet_act* y,
-                                 const float* mean, const float* invstd, const float* scale,
-                                 const float* shift, const float* dbeta, const float* dgamma,
-                                 float* dw_part, float* db_part, int nsplit, void* stream);
 
 /* ---- BatchNorm2d train-mode statistics (models.py:220,223; eps 1e-5, momentum 0.1)
  * combine per-tile (sum, M2, count) partials (Chan, fp64); update running

@@ -128,6 +128,12 @@ def test_reference_loss_api_surface():
     assert (p.w_focal, p.w_dice, p.w_tversky, p.class_div) == (2.5, 2.5, 1.0, 3.0)
     tr.focal_loss.gamma = 3.0  # _compute_combined_loss reads the module's attributes each call
     assert tr.loss_params().gamma == 3.0
+    # class_weights' host copy is cached per tensor version (no device sync per step), so an in-place
+    # change or a new tensor is still seen
+    tr.focal_loss.class_weights.mul_(2.0)
+    assert list(tr.loss_params().ce_weight) == [2.0, 40.0, 20.0]
+    tr.focal_loss.class_weights = torch.tensor([3.0, 1.0, 1.0])
+    assert list(tr.loss_params().ce_weight) == [3.0, 1.0, 1.0]
     with pytest.raises(ValueError):
         FocalLoss(alpha=[1.0, 2.0, 3.0, 4.0]).params()
 

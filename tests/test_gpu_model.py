@@ -316,30 +316,6 @@ def test_materialised_activation_is_exact(dtype, monkeypatch):
         assert torch.equal(g, out[False][2][k]), k
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-@pytest.mark.parametrize("H", [64, 72])
-def test_small_wgrad_fused_bn_backward_is_exact(dtype, H, monkeypatch):
-    """enc1's BN-a backward apply fused into conv .0's weight-gradient staging
-    (eunet_conv_small_wgrad_bnbwd) forms dY with bn_bwd_apply's arithmetic, so every gradient
-    equals the separate-pass path bit for bit (H = 72: partial 8x32 tiles at the edges)."""
-    from eunet import engine, synth
-    from eunet.losses import combined_loss
-    x, msk = synth.batch(2, H, H, start_index=5, num_classes=2, in_channels=1)
-    out = {}
-    for fused in (True, False):
-        monkeypatch.setattr(engine, "FUSE_SMALL_BNBWD", fused)
-        m = _model(16, 1, 2, dtype)
-        m.train()
-        logits = m.forward_lowres(x.to(DEV))
-        loss = combined_loss(logits, msk.to(DEV))
-        loss.backward()
-        torch.cuda.synchronize()
-        out[fused] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
-    for k, g in out[True].items():
-        assert torch.equal(g, out[False][k]), k
-    assert out[True]["model.enc1.0.weight"].abs().sum() > 0
-
-
 def test_train_epoch_device_loss_sum():
     """Trainer.train_epoch keeps the running loss on the device (one sync per epoch) and returns
     what the reference's per-step `total += loss.item()` loop returns (train_eval.py train_epoch),
