@@ -104,8 +104,10 @@ __device__ __forceinline__ void fwd_unit(int id, int& hp, int& q) {
 // Halo staging loads go through buffer descriptors (one per sample slice of x, one for the
 // packed weights): 32-bit per-unit offsets instead of 64-bit addresses, and no branch per
 // unit -- a unit outside the image gets offset FWD_OOB, which the descriptor's range check
-// turns into zeros.  The launcher requires each slice to be < 2 GiB.
-constexpr uint32_t FWD_OOB = 0x80000000u;
+// turns into zeros.  Offsets are unsigned 32-bit: the launcher requires each slice to be < 3 GiB
+// (FWD_OOB plus a chunk's channel offset stays above any valid offset; a 2048^2 x 288-channel bf16
+// slice, the dual-branch base-96 dec2.0 input of configs[4], is 2.4 GB).
+constexpr uint32_t FWD_OOB = 0xC0000000u;
 
 template <typename T>
 __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x0, int id) {
@@ -115,7 +117,7 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
   const int hy = hp / FHW, hx = hp - hy * FHW;
   const int yy = y0 + hy - 1, xx = x0 + hx - 1;
   const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-  return ok ? (uint32_t)(((yy * a.W + xx) * a.xct + a.xco + q * E) * (int)sizeof(T)) : FWD_OOB;
+  return ok ? (uint32_t)((yy * a.W + xx) * a.xct + a.xco + q * E) * (uint32_t)sizeof(T) : FWD_OOB;
 }
 
 // The halo quarter (16-byte channel group) of unit id depends only on tid: FT = 256 units per
@@ -156,7 +158,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   const int sq = (tid >> 3) & 3;  // this thread's halo quarter (fwd_unit), the same for every unit
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((const T*)a.x + (long long)ns * a.H * a.W * a.xct), 0, a.H * a.W * a.xct * (int)sizeof(T), 0x00020000);
+      (void*)((const T*)a.x + (long long)ns * a.H * a.W * a.xct), 0,
+      (int)((uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T)), 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wp, 0, a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T), 0x00020000);
 #pragma unroll
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       if (a.isc != nullptr) {  // BN + ReLU of the producing layer; padding stays zero
         float f[E];
         Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
-        const bool ok = cok && !(aoff[i] & FWD_OOB);
+        const bool ok = cok && aoff[i] < FWD_OOB;
 #pragma unroll
         for (int j = 0; j < E; ++j) f[j] = ok ? fmaxf(fmaf(f[j], asc[j >> 2][j & 3], ash[j >> 2][j & 3]), 0.f) : 0.f;
         v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
@@ -960,8 +963,8 @@ int kchunk(int dtype) { return 4 * elems16(dtype); }
 template <bool DG>
 int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
   const long long esz = dtype == EUNET_BF16 ? 2 : 4;
-  EUNET_REQUIRE((long long)a.H * a.W * a.xct * esz < (1ll << 31),
-                "conv3x3: one sample's input (%d x %d x %d) must be < 2 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
+  EUNET_REQUIRE((long long)a.H * a.W * a.xct * esz < (long long)FWD_OOB,
+                "conv3x3: one sample's input (%d x %d x %d) must be < 3 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
   EUNET_REQUIRE((long long)a.nkc * kchunk(dtype) * a.cout_pad * 9 * esz < (1ll << 31), "conv3x3: packed weights >= 2 GiB");
   dim3 grid(a.ntiles * (a.cout_pad / BN));
   if (dtype == EUNET_BF16) {

@@ -81,6 +81,36 @@ def test_conv3x3_fwd_stats(dt, transform):
     assert rel(rv, 0.9 + 0.1 * v_ref * n / (n - 1)) < tol * 10
 
 
+def test_conv3x3_fwd_large_sample_slice():
+    """One sample's input above 2 GiB (2048^2 x 288 bf16 = 2.4 GB: the dual-branch base-96 dec2.0
+    input of BASELINE configs[4]) through the buffer-descriptor staging (unsigned 32-bit offsets, slices
+    < 3 GiB): outputs at points whose halo lies beyond the 2 GiB mark vs fp64 dot products."""
+    ops = _ops()
+    N, H, W, Cin, Cout = 1, 2048, 2048, 288, 96
+    g = torch.Generator(device=DEV).manual_seed(21)
+    x = torch.randn(N, H, W, Cin, generator=g, device=DEV, dtype=torch.float32).to(torch.bfloat16)
+    gc = torch.Generator().manual_seed(22)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=gc, dtype=torch.float64) / 50).to(torch.bfloat16).double()
+    b = torch.randn(Cout, generator=gc, dtype=torch.float64)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device=DEV)
+    wp = ops.conv3x3_pack(w.float().to(DEV), torch.bfloat16, flip=False)
+    ops.conv3x3_fwd(ops.act(x), wp, ops.act(y), bias=b.float().to(DEV))
+    torch.cuda.synchronize()
+    pts = [(2047, 2047), (2047, 0), (1900, 1500), (1800, 2047), (0, 0), (1024, 17), (2046, 1023)]
+    for yy, xx in pts:
+        patch = torch.zeros(3, 3, Cin, dtype=torch.float64)
+        for dy in range(3):
+            for dx in range(3):
+                sy, sx = yy + dy - 1, xx + dx - 1
+                if 0 <= sy < H and 0 <= sx < W:
+                    patch[dy, dx] = x[0, sy, sx].double().cpu()
+        ref = torch.einsum("oiyx,yxi->o", w, patch) + b
+        got = y[0, yy, xx].double().cpu()
+        assert rel(got, ref) < 2e-2, (yy, xx, rel(got, ref))
+    assert (1900 * W + 1500) * Cin * 2 > 2 ** 31  # the checked halos sit beyond 2 GiB
+    del x, y
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_conv3x3_dgrad_wgrad(dt):
     ops = _ops()
