@@ -450,19 +450,33 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     }
     if (pass + 1 < NPASS) __syncthreads();
   }
-  if (bnb) {  // fixed-order block reduction of the per-thread channel sums
-    __syncthreads();
-    float* r2 = (float*)smem;  // [NTH][2E]
+  if (bnb) {  // fixed-order reduction of the per-thread channel sums: the lanes of a wave that share a
+             // channel unit (lane = ucol mod UPX) by DPP / permlane xor sums, then the 4 waves through LDS
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      r2[tid * 2 * E + e] = bs1[e];
-      r2[tid * 2 * E + E + e] = bs2[e];
+      float v1 = bs1[e], v2 = bs2[e];
+      if constexpr (UPX == 8) {  // lane bit 3: row_ror:8 within each row of 16 lanes
+        v1 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v1), 0x128, 0xF, 0xF, false));
+        v2 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v2), 0x128, 0xF, 0xF, false));
+      }
+      bs1[e] = xor32_sum(xor16_sum(v1));
+      bs2[e] = xor32_sum(xor16_sum(v2));
+    }
+    __syncthreads();
+    float* r2 = (float*)smem;  // [NW waves][UPX units][2E]
+    if (lane < UPX) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        r2[(wv * UPX + lane) * 2 * E + e] = bs1[e];
+        r2[(wv * UPX + lane) * 2 * E + E + e] = bs2[e];
+      }
     }
     __syncthreads();
     if (tid < 2 * BN) {
       const int which = tid / BN, cc = tid % BN, u = cc / E, e = cc % E;
       float t = 0.f;
-      for (int k = u; k < NTH; k += UPX) t += r2[k * 2 * E + which * E + e];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += r2[(w * UPX + u) * 2 * E + which * E + e];
       if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
     }
   }
