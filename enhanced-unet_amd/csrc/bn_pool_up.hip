@@ -736,7 +736,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
 // the block whose output gradient g the kernel writes): each thread accumulates, for its 16-byte
 // channel unit, s1 += g', s2 += g' xhat over the pixels it writes (g' = stored g where
 // y scale + shift > 0, xhat = (y - mean) istd); the block then sums its threads of equal unit
-// in fixed order into part[block][2][C].  Requires NT % U == 0 (U = C / E channel units).
+// in fixed order into part[block][2][C].  Requires blockDim.x % U == 0 (U = C / E channel units).
 struct BnRed {
   const void* y; int yct, yco;
   const float* mean; const float* istd; const float* scale; const float* shift;  // scale / shift: the forward affine
@@ -755,7 +755,7 @@ __device__ __forceinline__ void bnred_block(const BnRed& r, int C, const float* 
     float t1[E], t2[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) { t1[j] = 0.f; t2[j] = 0.f; }
-    for (int k = tid; k < NT; k += U)
+    for (int k = tid; k < (int)blockDim.x; k += U)
 #pragma unroll
       for (int j = 0; j < E; ++j) { t1[j] += red[0][k][j]; t2[j] += red[1][k][j]; }
 #pragma unroll
@@ -1564,9 +1564,16 @@ int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, void* stream)
 
 // ---- gradient producers with the BN-backward reduction of the block they feed fused in ----
 namespace {
+// block size of the fused BN-backward reductions: the block's threads must cover whole channel units
+// (a thread's unit is fixed across the grid-stride loop) -- 256 threads, or 192 for the channel counts
+// of base 96 (96 / 192 / 384 / 768 channels: 12 / 24 / 48 / 96 bf16 units); 0: not fusable
+int bnr_block(const eunet_act* g) {
+  const int U = g->c / e16(g->dtype);
+  return U > 0 && NT % U == 0 ? NT : (U > 0 && 192 % U == 0 ? 192 : 0);
+}
 bool bnr_ok(const eunet_act* g, const eunet_act* y) {
   return act_ok(y) && vec_ok(y) && y->dtype == g->dtype && y->n == g->n && y->h == g->h && y->w == g->w &&
-         y->c == g->c && NT % (g->c / e16(g->dtype)) == 0;
+         y->c == g->c && bnr_block(g) > 0;
 }
 long long pool_threads(const eunet_act* gout) {
   return (long long)gout->n * (gout->h / 2) * (gout->w / 2) * (gout->c / e16(gout->dtype));
@@ -1574,7 +1581,7 @@ long long pool_threads(const eunet_act* gout) {
 // fused-reduction grid, which is also the number of partial rows: at most cap blocks (each thread
 // then covers several outputs).  Measured: the max-pool adjoint prefers 2048 (fewer rows to write
 // and sum), the upsample adjoint, with more work per output, 8192 (more loads in flight).
-int bnr_grid(long long threads, int cap) { return (int)std::min<long long>((threads + NT - 1) / NT, cap); }
+int bnr_grid(long long threads, int cap, int block) { return (int)std::min<long long>((threads + block - 1) / block, cap); }
 long long up_threads(const eunet_act* glo) {
   return (long long)glo->n * ((glo->h + UP_R - 1) / UP_R) * ((glo->w + 1) / 2) * (glo->c / e16(glo->dtype));
 }
@@ -1582,7 +1589,8 @@ long long up_threads(const eunet_act* glo) {
 
 int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows) {
   EUNET_REQUIRE(act_ok(gout) && rows, "pool_bwd_add_bnr_rows: bad args");
-  *rows = (NT % (gout->c / e16(gout->dtype)) == 0) ? bnr_grid(pool_threads(gout), 2048) : 0;
+  const int bs = bnr_block(gout);
+  *rows = bs > 0 ? bnr_grid(pool_threads(gout), 2048, bs) : 0;
   return EUNET_OK;
 }
 
@@ -1596,11 +1604,12 @@ int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const e
                     gpool->c == act->c && gout->c == act->c,
                 "pool_bwd_add_bnr: shapes");
   EUNET_REQUIRE(bnr_ok(gout, y) && mean && invstd && scale && shift && part,
-                "pool_bwd_add_bnr: y / BN args (and 256 %% channel units == 0)");
+                "pool_bwd_add_bnr: y / BN args (and 256 or 192 %% channel units == 0)");
   const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, part};
-  const unsigned gr = (unsigned)bnr_grid(pool_threads(gout), 2048);
+  const int bs = bnr_block(gout);
+  const unsigned gr = (unsigned)bnr_grid(pool_threads(gout), 2048, bs);
 #define PBA(T)                                                                                                  \
-  pool_bwd_add_kernel<T, true><<<gr, NT, 0, (hipStream_t)stream>>>(                                             \
+  pool_bwd_add_kernel<T, true><<<gr, bs, 0, (hipStream_t)stream>>>(                                             \
       (const T*)act->ptr, act->ctot, act->coff, (const T*)gpool->ptr, gpool->ctot, gpool->coff,                 \
       gskip ? (const T*)gskip->ptr : nullptr, gskip ? gskip->ctot : 0, gskip ? gskip->coff : 0, (T*)gout->ptr, \
       gout->ctot, gout->coff, act->n, act->h, act->w, act->c, br)
@@ -1613,7 +1622,8 @@ int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const e
 
 int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows) {
   EUNET_REQUIRE(act_ok(glo) && rows, "upsample_bwd_bnr_rows: bad args");
-  *rows = (vec_ok(glo) && NT % (glo->c / e16(glo->dtype)) == 0) ? bnr_grid(up_threads(glo), 8192) : 0;
+  const int bs = vec_ok(glo) ? bnr_block(glo) : 0;
+  *rows = bs > 0 ? bnr_grid(up_threads(glo), 8192, bs) : 0;
   return EUNET_OK;
 }
 
@@ -1624,15 +1634,16 @@ int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eun
   EUNET_REQUIRE(ghi->h == 2 * glo->h && ghi->w == 2 * glo->w && ghi->c == glo->c && ghi->n == glo->n,
                 "upsample_bwd_bnr: shapes");
   EUNET_REQUIRE(bnr_ok(glo, y) && mean && invstd && scale && shift && part,
-                "upsample_bwd_bnr: y / BN args (and 256 %% channel units == 0)");
+                "upsample_bwd_bnr: y / BN args (and 256 or 192 %% channel units == 0)");
   const BnRed br{y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, part};
-  const unsigned gr = (unsigned)bnr_grid(up_threads(glo), 8192);
+  const int bs = bnr_block(glo);
+  const unsigned gr = (unsigned)bnr_grid(up_threads(glo), 8192, bs);
   if (ghi->dtype == EUNET_BF16)
-    up_bwd_rows_kernel<bf16_t, bf16_t, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<bf16_t, bf16_t, true><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const bf16_t*)ghi->ptr, ghi->ctot, ghi->coff, (bf16_t*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, br);
   else
-    up_bwd_rows_kernel<float, float, true><<<gr, NT, 0, (hipStream_t)stream>>>(
+    up_bwd_rows_kernel<float, float, true><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const float*)ghi->ptr, ghi->ctot, ghi->coff, (float*)glo->ptr, glo->ctot, glo->coff, glo->n, glo->h,
         glo->w, glo->c, br);
   EUNET_LAUNCH_CHECK("upsample_bwd_bnr");

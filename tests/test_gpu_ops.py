@@ -684,15 +684,21 @@ def test_bnrelu(dt):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("kind", ["pool", "up"])
-def test_fused_bn_reduce_in_gradient_producers(dt, kind):
+@pytest.mark.parametrize("C,big", [(64, False), (96, False), (192, False), (768, False), (96, True)])
+def test_fused_bn_reduce_in_gradient_producers(dt, kind, C, big):
     """pool_bwd_add / upsample_bwd with the BN-backward reduction fused in: the gradient equals
     the plain kernel's bit for bit, the partial sums equal bn_bwd_reduce on that gradient.  The
     fused max-pool adjoint takes its argmax from relu(y scale + shift) recomputed from y, so the
-    saved activation here is the one bnrelu_pool stores for that y (the engine's contract)."""
+    saved activation here is the one bnrelu_pool stores for that y (the engine's contract).
+    C = 96 / 192 / 768 (base 96: 12 / 24 / 96 bf16 units) run in 192-thread blocks; big: the
+    grid-stride loop wraps (more outputs than the capped grid has threads)."""
     ops = _ops()
     g = torch.Generator().manual_seed(17)
-    N, C = 2, 64
-    h, w = (10, 14) if kind == "pool" else (7, 9)   # gradient (output) spatial size
+    N = 4 if big else 2
+    if big:
+        h, w = (260, 520) if kind == "pool" else (200, 400)
+    else:
+        h, w = (10, 14) if kind == "pool" else (7, 9)   # gradient (output) spatial size
     gout = torch.empty(N, h, w, C, dtype=dt, device=DEV)
     gref = torch.empty_like(gout)
     y = torch.randn(N, h, w, C, generator=g).to(DEV, dt)
