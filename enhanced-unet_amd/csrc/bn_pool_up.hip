@@ -721,8 +721,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   const int ppb = blockDim.x / U;  // pixels per block per step (blockDim.x = ppb * U)
   for (long long p = (long long)blockIdx.x * ppb + threadIdx.x / U; p < P; p += (long long)gridDim.x * ppb) {
     float gf[E], yf[E], o[E];
-    Vec16<T>::unpack(*(const uint4*)(g + p * gct + gco + c), gf);
-    Vec16<T>::unpack(*(const uint4*)(y + p * yct + yco + c), yf);
+    // g and y are read once here: non-temporal loads, so they do not displace the L2 lines the
+    // concurrent weight-gradient kernels re-read (their X halo / dY tiles)
+    Vec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)(g + p * gct + gco + c))), gf);
+    Vec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)(y + p * yct + yco + c))), yf);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
       const float gg = fmaf(yf[j], kP[j], kQ[j]) > 0.f ? gf[j] : 0.f;
@@ -819,15 +821,18 @@ __global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_
     const int c = u * E;
     long long pix[4];
     uint4 ra[4], rs[4];
+    // every input element is read once (disjoint 2x2 windows): non-temporal loads, so they do not
+    // displace the L2 lines the concurrent weight-gradient kernels re-read
+    auto ldnt = [](const T* q) { return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)q)); };
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       pix[k] = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
-      ra[k] = *(const uint4*)(src + pix[k] * sct + sco + c);
+      ra[k] = ldnt(src + pix[k] * sct + sco + c);
     }
-    const uint4 rg = *(const uint4*)(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c);
+    const uint4 rg = ldnt(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      rs[k] = gs != nullptr ? *(const uint4*)(gs + pix[k] * gsct + gsco + c) : make_uint4(0, 0, 0, 0);
+      rs[k] = gs != nullptr ? ldnt(gs + pix[k] * gsct + gsco + c) : make_uint4(0, 0, 0, 0);
     float best[E], gpv[E];
     int arg[E];
 #pragma unroll
