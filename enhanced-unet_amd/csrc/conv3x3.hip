@@ -126,6 +126,9 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 // once per chunk, with the halo loads (not per unit after its data arrived: a dependent
 // global round trip per unit).
 
+#ifndef CONV_PRIO
+#define CONV_PRIO 1
+#endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
 template <typename T, bool DG>
@@ -291,7 +294,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       stage_halves(kc);
       __syncthreads();
     }
+    if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
     chunk();
+    if (CONV_PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
@@ -727,6 +732,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         f[ct] = cat_bf16x4(lo, hi);
       }
     };
+    if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
     for (int ks = 0; ks < TH; ++ks) {
       bf16x8 af[4];
@@ -746,6 +752,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         }
       }
     }
+    if (CONV_PRIO) __builtin_amdgcn_s_setprio(0);
   }
   float* out = a.dw + (long long)split * a.cout * 9 * a.cin;
   const int ci = kc * KCW + wv * 16 + i16;
