@@ -1133,6 +1133,21 @@ int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsp
   const int ntiles = dy->n * cdiv(dy->h, bf ? TH : WF_TH) * cdiv(dy->w, bf ? TW : WF_TW);
   const int blocks = cdiv(dy->c, 64) * cdiv(cin, bf ? KCW : WF_CI);
   int s = cdiv(WG_BLOCKS, blocks);
+#ifndef WG_FILL
+#define WG_FILL 1
+#endif
+  if (WG_FILL) {
+    // fewest launch waves per unit of work: a split count whose blocks leave a nearly empty last wave
+    // (the decoder's concat inputs: 48 / 12 / 3 block columns -> 528 / 516 / 513 blocks) runs that
+    // wave's tail alone; pick s in [s0/2, 2 s0] minimising waves / s (ties: fewer splits)
+    const int s0 = s;
+    long long bw = 1, bs = 0;  // best waves / best s as the fraction bw / bs
+    for (int c = (s0 + 1) / 2; c <= 2 * s0; ++c) {
+      const long long w = cdiv(c * blocks, WG_BLOCKS);
+      if (c >= 1 && (bs == 0 || w * bs < bw * c)) bw = w, bs = c;
+    }
+    s = (int)bs;
+  }
   s = s < 1 ? 1 : s;
   s = s > ntiles ? ntiles : s;
   // keep partials <= 256 MiB
