@@ -42,6 +42,12 @@ MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "0") != "0"
 # the BN-b backward reduction of a block fused into the kernel producing its output gradient
 # (upsample / max-pool adjoints) instead of a separate bn_bwd_reduce pass (EUNET_FUSE_BN_REDUCE=0)
 FUSE_BN_REDUCE = os.environ.get("EUNET_FUSE_BN_REDUCE", "1") != "0"
+# conv .3's weight gradient joins the side stream after the block's BN-a backward (EUNET_WG3_LATE=1,
+# default) rather than before conv .3's data gradient: the side stream's wgrad blocks hold whole CUs
+# (256 VGPRs x 8 waves), and bn_bwd_apply, on the critical launch stream, then waited for CU slots;
+# this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7 alternating
+# pairs on one box (profiles/r02_ab_conv.txt)
+WG3_LATE = os.environ.get("EUNET_WG3_LATE", "1") != "0"
 
 
 class GradSink:
@@ -298,10 +304,14 @@ class UNetEngine:
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
         gyb = bn_back(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
-        if s.get("za") is not None:
-            wgrad(p + ".3", ops.act(s["za"]), gyb)
-        else:
-            wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
+
+        def wgrad3():
+            if s.get("za") is not None:
+                wgrad(p + ".3", ops.act(s["za"]), gyb)
+            else:
+                wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
+        if not WG3_LATE:
+            wgrad3()
         wpt = S["wp"].get(p + ".3.weight^T") if S.get("wp") else None
         if wpt is None:
             wpt = ops.conv3x3_pack(P[p + ".3.weight"], dt, flip=True)
@@ -310,8 +320,10 @@ class UNetEngine:
         cpart = _e(ctiles * 2 * C, torch.float32, dev)
         ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
                                 bna["scale"], bna["shift"], cpart)
-        del gyb
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
+        if WG3_LATE:
+            wgrad3()
+        del gyb
         # the trunk's last weight gradient (no data gradient follows it): on the main stream, which is
         # otherwise idle here, instead of queueing behind the side stream's conv .3 wgrad
         wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx)
