@@ -25,6 +25,35 @@ def test_library_exports_every_header_symbol():
     assert "gfx950" in _lib.version()
 
 
+@pytest.mark.parametrize("n,hw,cout,cin,dtype", [
+    (4, 256, 256, 768, "bf16"), (4, 512, 128, 384, "bf16"), (4, 1024, 64, 192, "bf16"),
+    (4, 128, 512, 512, "bf16"), (4, 1024, 64, 64, "bf16"), (8, 128, 256, 768, "fp32"), (1, 16, 64, 64, "bf16")])
+def test_wgrad_split_count_fills_launch_waves(n, hw, cout, cin, dtype):
+    """Host-only: the weight-gradient split count (eunet_conv3x3_wgrad_splits) leaves no nearly
+    empty last wave of 512 blocks (the decoder concat layers had 528 / 516 / 513 blocks), covers
+    every tile, and keeps the fp32 partials <= 256 MiB."""
+    import ctypes
+    from eunet import _lib
+    lib = _lib.load()
+    dtc = _lib.EUNET_BF16 if dtype == "bf16" else _lib.EUNET_F32
+    dy = _lib.Act(0x1000, n, hw, hw, cout, cout, 0, dtc)  # descriptor only: nothing is dereferenced
+    s = ctypes.c_int()
+    assert lib.eunet_conv3x3_wgrad_splits(ctypes.byref(dy), cin, dtc, ctypes.byref(s)) == 0
+    ns = s.value
+    bf = dtype == "bf16"
+    th, tw, kc = (8, 32, 64) if bf else (4, 32, 32)
+    ntiles = n * -(-hw // th) * -(-hw // tw)
+    blocks = -(-cout // 64) * -(-cin // kc)
+    assert 1 <= ns <= ntiles
+    per = -(-ntiles // ns)
+    assert -(-ntiles // per) == ns  # every split non-empty
+    assert cout * 9 * cin * 4 * ns <= 256 << 20
+    total = ns * blocks
+    if total >= 512:  # the last wave is at least 90 % full
+        waves = -(-total // 512)
+        assert total / (waves * 512) >= 0.9, (ns, blocks, total)
+
+
 def test_state_dict_schema_matches_reference():
     from eunet.models import EnhancedUNet, get_model
     from oracle.eunet_ref import state_spec
