@@ -316,6 +316,29 @@ def test_materialised_activation_is_exact(dtype, monkeypatch):
         assert torch.equal(g, out[False][2][k]), k
 
 
+def test_backward_stream_schedules_are_exact(monkeypatch):
+    """The weight gradients on the side stream (conv .3's enqueued early or after the block's BN-a
+    backward, engine.WG3_LATE) or all on the launch stream run the same kernels on the same
+    operands: every gradient agrees bit for bit."""
+    from eunet import engine, synth
+    from eunet.losses import combined_loss
+    x, msk = synth.batch(2, 64, 64, start_index=5, num_classes=2, in_channels=1)
+    out = {}
+    for overlap, late in ((True, True), (True, False), (False, True)):
+        monkeypatch.setattr(engine, "WG3_LATE", late)
+        monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", overlap)
+        m = _model(16, 1, 2, "bf16")
+        m.train()
+        loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        out[(overlap, late)] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    ref = out[(True, True)]
+    for key, grads in out.items():
+        for k, g in grads.items():
+            assert torch.equal(g, ref[k]), (key, k)
+
+
 def test_train_epoch_device_loss_sum():
     """Trainer.train_epoch keeps the running loss on the device (one sync per epoch) and returns
     what the reference's per-step `total += loss.item()` loop returns (train_eval.py train_epoch),
