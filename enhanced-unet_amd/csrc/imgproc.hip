@@ -468,8 +468,12 @@ int eunet_clahe_u8(const uint8_t* src, int mode, int h, int w, double clip_limit
   EUNET_REQUIRE(src && dst && luts && h > 0 && w > 0 && tiles_x > 0 && tiles_y > 0 && (mode == 0 || mode == 1),
                 "clahe_u8: bad args");
   const int ps = mode == 0 ? 1 : 3;
-  // OpenCV pads to a multiple of the grid (BORDER_REFLECT_101); tile = padded size / grid
-  const int tw = (w + tiles_x - 1) / tiles_x, th = (h + tiles_y - 1) / tiles_y;
+  // OpenCV CLAHE_Impl::apply: when the image is a multiple of the grid on both axes the tile is
+  // size / grid; otherwise BOTH axes are padded (BORDER_REFLECT_101, bottom / right) by
+  // tiles - size % tiles, so the tile is size / tiles + 1 on each axis -- also on an axis that
+  // divides evenly
+  const bool even = w % tiles_x == 0 && h % tiles_y == 0;
+  const int tw = w / tiles_x + (even ? 0 : 1), th = h / tiles_y + (even ? 0 : 1);
   const int area = tw * th;
   const int clip = clip_limit > 0.0 ? std::max((int)(clip_limit * area / 256), 1) : (1 << 30);
   clahe_lut_kernel<<<tiles_x * tiles_y, NT, 0, (hipStream_t)stream>>>(src, ps, h, w, tw, th, tiles_x, clip,

@@ -180,8 +180,19 @@ class DataLoader:
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
     def __iter__(self):
-        idx = list(range(len(self.dataset)))
+        n = len(self.dataset)
+        # torch.utils.data.DataLoader's draws from torch's global generator, in its order: the
+        # iterator's worker base seed (drawn even with num_workers=0 and shuffle off), then
+        # RandomSampler's seed for a randperm on a private generator.  Python's `random` stream
+        # (which the augmentations draw from, dataset.py:204-300) is left untouched, as under the
+        # reference's DataLoader.
+        torch.empty((), dtype=torch.int64).random_()
         if self.shuffle:
-            random.shuffle(idx)
+            seed = int(torch.empty((), dtype=torch.int64).random_().item())
+            gen = torch.Generator()
+            gen.manual_seed(seed)
+            idx = torch.randperm(n, generator=gen).tolist()
+        else:
+            idx = list(range(n))
         for i in range(0, len(idx), self.batch_size):
             yield self.collate_fn([self.dataset[j] for j in idx[i:i + self.batch_size]])

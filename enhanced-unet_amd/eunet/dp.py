@@ -107,30 +107,42 @@ class DataParallel:
         with torch.no_grad():  # identical initial replicas
             for n in self.order:
                 dist.broadcast(params[n].data, src=0, group=group)
-        self.flat_buffers = self._flatten_buffers(model)
+        self.flat_buffers, self._buffer_views = self._flatten_buffers(model)
         self._sync_buffers()
         model.grad_sink_factory = lambda: BucketSink(self)
 
     @staticmethod
     def _flatten_buffers(model):
         """Re-point every floating-point buffer (BN running_mean / running_var) at a slice of one
-        flat tensor; returns it (None without such buffers)."""
+        flat tensor; returns (flat, [(module, name, data_ptr)]) ((None, []) without such buffers)."""
         entries = [(mod, name, b) for mod in model.modules() for name, b in mod._buffers.items()
                    if b is not None and b.dtype.is_floating_point]
         if not entries:
-            return None
+            return None, []
         dt, dev = entries[0][2].dtype, entries[0][2].device
         if any(b.dtype != dt or b.device != dev for _, _, b in entries):
             raise RuntimeError("DataParallel: floating-point buffers must share one dtype and device")
         flat = torch.empty(sum(b.numel() for _, _, b in entries), dtype=dt, device=dev)
-        off = 0
+        off, views = 0, []
         with torch.no_grad():
             for mod, name, b in entries:
                 view = flat[off:off + b.numel()].view_as(b)
                 view.copy_(b)
                 mod._buffers[name] = view
+                views.append((mod, name, view.data_ptr()))
                 off += b.numel()
-        return flat
+        return flat, views
+
+    def _check_buffer_views(self):
+        """The broadcast updates flat_buffers; a module._apply (model.to / .float / .cuda ...) after
+        construction replaces the registered buffers with tensors the broadcast no longer reaches,
+        and the replicas' running statistics would drift apart silently.  Raise instead."""
+        for mod, name, ptr in self._buffer_views:
+            b = mod._buffers.get(name)
+            if b is None or b.data_ptr() != ptr:
+                raise RuntimeError(f"DataParallel: buffer {type(mod).__name__}.{name} no longer aliases the flat "
+                                   "broadcast buffer (the model was moved or cast after DataParallel was built); "
+                                   "construct DataParallel after the last .to() / dtype change")
 
     def _sync_buffers(self):
         if self.flat_buffers is None or self.world == 1:
@@ -139,6 +151,7 @@ class DataParallel:
 
     def before_forward(self):
         if self.broadcast_buffers:
+            self._check_buffer_views()
             self._sync_buffers()
 
     def after_backward(self):

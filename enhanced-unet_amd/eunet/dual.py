@@ -172,7 +172,7 @@ class DualEngine:
         part = _e(ct * (K * C3 + K), torch.float32, dev)
         w11 = P["fusion_head.11.weight"].reshape(K, C3).contiguous()
         red3 = (None, 0)
-        if engine.FUSE_BN_REDUCE:
+        if engine.UNetEngine.fuse_bn_reduce:
             bpart = _e(ct * 2 * C3, torch.float32, dev)
             ops.conv1x1_bwd_bnr(ops.act(y3), h3["scale"], h3["shift"], w11, K, gz, ops.act(g3), part,
                                 h3["mean"], h3["invstd"], bpart)

@@ -22,8 +22,6 @@ from __future__ import annotations
 
 from typing import Dict, Optional
 
-import os
-
 import torch
 
 from . import ops
@@ -32,24 +30,6 @@ from ._lib import EunetError
 BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
-# DoubleConv's first BN+ReLU, za = relu(bn1(ya)), for the second conv (EUNET_MATERIALIZE_ZA):
-#   0 (default since round 2) applied inside both operand stagings (nothing stored): the forward's
-#     halo staging loads the BN constants once per K-chunk with the halo, so the transform is free
-#     there, and the weight gradient pays it on the side stream; A/B +0.9 / +2.1 % img/s
-#     (profiles/r02_ab_za.txt; round 1's opposite result: profiles/r01_ab_za.txt)
-#   1 one elementwise pass on the main stream; conv .3's forward and weight gradient read za as is
-MATERIALIZE_ZA = os.environ.get("EUNET_MATERIALIZE_ZA", "0") != "0"
-# the BN-b backward reduction of a block fused into the kernel producing its output gradient
-# (upsample / max-pool adjoints) instead of a separate bn_bwd_reduce pass (EUNET_FUSE_BN_REDUCE=0)
-FUSE_BN_REDUCE = os.environ.get("EUNET_FUSE_BN_REDUCE", "1") != "0"
-# conv .3's weight gradient joins the side stream after the block's BN-a backward (EUNET_WG3_LATE=1,
-# default) rather than before conv .3's data gradient: the side stream's wgrad blocks hold whole CUs
-# (256 VGPRs x 8 waves), and bn_bwd_apply, on the critical launch stream, then waited for CU slots;
-# this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7 alternating
-# pairs on one box (profiles/r02_ab_conv.txt)
-WG3_LATE = os.environ.get("EUNET_WG3_LATE", "1") != "0"
-
-
 class GradSink:
     """Default sink: a fresh fp32 tensor per parameter gradient."""
 
@@ -95,6 +75,24 @@ class UNetEngine:
     so the results are bit-identical either way."""
 
     overlap_wgrad = True
+    # Schedule choices, with their measured defaults (instance or class attributes; the library and
+    # this module read nothing from the process environment):
+    # materialize_za -- DoubleConv's first BN+ReLU, za = relu(bn1(ya)), for the second conv:
+    #   False (default since round 2): applied inside both operand stagings (nothing stored); the
+    #     forward's halo staging loads the BN constants once per K-chunk with the halo, so the
+    #     transform is free there, and the weight gradient pays it on the side stream; A/B +0.9 /
+    #     +2.1 % img/s (profiles/r02_ab_za.txt; round 1's opposite result: profiles/r01_ab_za.txt)
+    #   True: one elementwise pass on the main stream; conv .3's forward and wgrad read za as is
+    materialize_za = False
+    # fuse_bn_reduce -- a block's BN-b backward reduction fused into the kernel producing its output
+    # gradient (upsample / max-pool / 1x1 adjoints) instead of a separate bn_bwd_reduce pass
+    fuse_bn_reduce = True
+    # wg3_late -- conv .3's weight gradient joins the side stream after the block's BN-a backward
+    # rather than before conv .3's data gradient: the side stream's wgrad blocks hold whole CUs
+    # (256 VGPRs x 8 waves), and bn_bwd_apply on the critical launch stream waited for CU slots;
+    # this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7
+    # alternating pairs on one box (profiles/r02_ab_conv.txt)
+    wg3_late = True
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -162,7 +160,7 @@ class UNetEngine:
         bna = self._bn(p + ".1", st, tiles, C, training, P, B)
         wp = wps[p + ".3.weight"] if wps else ops.conv3x3_pack(P[p + ".3.weight"], self.dtype, flip=False)
         za = None
-        if MATERIALIZE_ZA:  # one BN+ReLU pass; conv .3 forward and weight gradient read za as is
+        if self.materialize_za:  # one BN+ReLU pass; conv .3 forward and weight gradient read za as is
             za = _e((N, H, W, C), self.dtype, dev)
             ops.bnrelu(ops.act(ya), bna["scale"], bna["shift"], ops.act(za))
             ops.conv3x3_fwd(ops.act(za), wp, ops.act(yb), bias=P[p + ".3.bias"], stats=st, sub=enc)
@@ -310,7 +308,7 @@ class UNetEngine:
                 wgrad(p + ".3", ops.act(s["za"]), gyb)
             else:
                 wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
-        if not WG3_LATE:
+        if not self.wg3_late:
             wgrad3()
         wpt = S["wp"].get(p + ".3.weight^T") if S.get("wp") else None
         if wpt is None:
@@ -321,7 +319,7 @@ class UNetEngine:
         ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
                                 bna["scale"], bna["shift"], cpart)
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
-        if WG3_LATE:
+        if self.wg3_late:
             wgrad3()
         del gyb
         # the trunk's last weight gradient (no data gradient follows it): on the main stream, which is
@@ -383,7 +381,7 @@ class UNetEngine:
 
         def up_bwd(ghi: ops.Act, glo: torch.Tensor, nm):
             """g w.r.t. block nm's output from the upsample adjoint, its BN-b reduction fused."""
-            rows = ops.upsample_bwd_bnr_rows(ops.act(glo)) if FUSE_BN_REDUCE else 0
+            rows = ops.upsample_bwd_bnr_rows(ops.act(glo)) if self.fuse_bn_reduce else 0
             if not rows:
                 ops.upsample_bwd(ghi, ops.act(glo))
                 return None, 0
@@ -392,7 +390,7 @@ class UNetEngine:
             return part, rows
 
         def pool_bwd(act_saved: ops.Act, gpool: ops.Act, gskip: ops.Act, gout: torch.Tensor, nm):
-            rows = ops.pool_bwd_add_bnr_rows(ops.act(gout)) if FUSE_BN_REDUCE else 0
+            rows = ops.pool_bwd_add_bnr_rows(ops.act(gout)) if self.fuse_bn_reduce else 0
             if not rows:
                 ops.pool_bwd_add(act_saved, gpool, gskip, ops.act(gout))
                 return None, 0
@@ -409,7 +407,7 @@ class UNetEngine:
         w1 = P[pre + "dec1.weight"].reshape(K, b).contiguous()
         bnb2 = s2["bnb"]
         red2 = (None, 0)
-        if FUSE_BN_REDUCE:
+        if self.fuse_bn_reduce:
             bpart = _e(tiles * 2 * b, torch.float32, dev)
             ops.conv1x1_bwd_bnr(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part,
                                 bnb2["mean"], bnb2["invstd"], bpart)

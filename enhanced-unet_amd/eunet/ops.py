@@ -543,8 +543,9 @@ def hsv_adjust_u8(img, sat=None, hue=None, val=None):
     mode = (1 if sat is not None else 0) | (2 if hue is not None else 0)
     if mode & 2 and val is None:
         raise ValueError("hsv_adjust_u8: hue and val go together")
-    call("eunet_hsv_adjust_u8", _ptr(img), img.shape[0] * img.shape[1], float(sat or 1.0), float(hue or 0.0),
-         float(val or 1.0), mode, _stream())
+    # explicit None tests: sat = 0.0 / val = 0.0 are real requests (desaturate / black), not "unset"
+    call("eunet_hsv_adjust_u8", _ptr(img), img.shape[0] * img.shape[1], 1.0 if sat is None else float(sat),
+         0.0 if hue is None else float(hue), 1.0 if val is None else float(val), mode, _stream())
     return img
 
 

@@ -136,6 +136,10 @@ class Trainer:
                 out = self.model(images)
                 logits = F.interpolate(out, size=masks.shape[-2:], mode="bilinear", align_corners=False)
             loss = combined_loss(logits, masks, params=self.loss_params())
+        if sync_loss:
+            # out-of-range targets raise here, before backward and the update, where the reference's
+            # F.cross_entropy raises (one extra host sync; the deferred path below has none)
+            check_targets()
         loss.backward()
         if self.dp is not None:
             self.dp.after_backward()
@@ -143,11 +147,13 @@ class Trainer:
         self.optimizer.step()
         if not sync_loss:
             return loss.detach()
-        value = loss.item()
-        check_targets()  # out-of-range targets surface at this sync, as the reference's device assert would
-        return value
+        return loss.item()
 
     def train_epoch(self, dataloader):
+        """Mean loss over the epoch with one host sync at its end.  Out-of-range targets are counted
+        on the device and raise ValueError at that sync -- after the epoch's updates, including the
+        offending batches' (with their bad pixels dropped from the loss).  Trainer.step(...,
+        sync_loss=True) raises before the update instead."""
         self.model.train()
         total = None  # device-side running sum: one host sync per epoch, not per step
         n = 0

@@ -150,7 +150,10 @@ def clahe(src, clip_limit, grid=(8, 8)):
     """src uint8 [h, w] -> uint8 [h, w]; grid = (tiles_x, tiles_y)."""
     h, w = src.shape
     tx_n, ty_n = grid
-    tw, th = -(-w // tx_n), -(-h // ty_n)
+    # CLAHE_Impl::apply: a grid multiple on both axes -> size / grid; otherwise both axes are padded
+    # by tiles - size % tiles (BORDER_REFLECT_101), so each tile is size // tiles + 1
+    even = w % tx_n == 0 and h % ty_n == 0
+    tw, th = w // tx_n + (0 if even else 1), h // ty_n + (0 if even else 1)
     ys = reflect101(np.arange(th * ty_n), h)
     xs = reflect101(np.arange(tw * tx_n), w)
     ext = src[ys][:, xs]

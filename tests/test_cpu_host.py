@@ -190,3 +190,37 @@ def test_train_model_builds_reference_loaders(tmp_path):
     finally:
         D.CellDataset.__init__ = orig
     assert built == [("train", 640, 7), ("val", 640, 1)]
+
+
+def test_loader_shuffle_matches_torch_random_sampler():
+    """eunet.data.DataLoader draws from torch's global generator as torch's DataLoader +
+    RandomSampler do (the reference's loaders, train_eval.py:1071-1075): the same permutation
+    under the same torch seed, the global stream left at the same position, and Python's
+    `random` stream -- the one the augmentations draw from -- untouched."""
+    import random
+
+    import torch.utils.data as tud
+
+    from eunet.data import DataLoader
+
+    class _Items:
+        def __len__(self):
+            return 23
+
+        def __getitem__(self, i):
+            return i
+
+    def ident(b):
+        return b
+
+    for shuffle in (True, False):
+        random.seed(5)
+        state = random.getstate()
+        torch.manual_seed(77)
+        ours = [i for b in DataLoader(_Items(), batch_size=4, shuffle=shuffle, collate_fn=ident) for i in b]
+        ours_next = torch.rand(1).item()
+        assert random.getstate() == state
+        torch.manual_seed(77)
+        ref = [i for b in tud.DataLoader(_Items(), batch_size=4, shuffle=shuffle, collate_fn=ident) for i in b]
+        assert ours == ref and sorted(ours) == list(range(23))
+        assert ours_next == torch.rand(1).item()

@@ -67,8 +67,15 @@ def _worker(rank, world, port, q):
         grads = sink.finish()
         err = max(float((grads[k].double() - expected[k]).abs().max() / expected[k].abs().max().clamp_min(1e-12))
                   for k in expected if not k.endswith((".0.bias", ".3.bias")))
-        q.put((rank, same, len(dp.buckets), launched_early, err,
-               float(model.enhance[1].running_mean.abs().max())))
+        rm = float(model.enhance[1].running_mean.abs().max())
+        dp.before_forward()  # buffers still alias the flat broadcast buffer: fine
+        model.double()  # module._apply replaces every buffer: the broadcast would no longer reach them
+        try:
+            dp.before_forward()
+            stale_raised = False
+        except RuntimeError:
+            stale_raised = True
+        q.put((rank, same, len(dp.buckets), launched_early, err, rm, stale_raised))
     finally:
         dist.destroy_process_group()
 
@@ -85,7 +92,8 @@ def test_dp_world2_gloo_bucketed_allreduce():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, same, nb, early, err, rm in res:
+    for rank, same, nb, early, err, rm, stale_raised in res:
+        assert stale_raised, "a buffer replaced after DataParallel was built must be reported"
         assert same, "replicas must be identical after the rank-0 broadcast"
         assert nb > 3, "expected several buckets"
         assert early >= nb - 1, "buckets must be launched as they complete, not at finish()"

@@ -13,7 +13,7 @@ from oracle import imgproc_ref as O
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-SIZES = [(37, 53), (64, 64), (256, 256), (8, 8), (100, 9)]
+SIZES = [(37, 53), (64, 64), (256, 256), (8, 8), (100, 9), (64, 60), (60, 64)]
 
 
 def _img(seed, h=37, w=53):
@@ -47,11 +47,11 @@ def test_gray_and_hsv_bit_exact(h, w):
     from eunet import ops
     img = _img(h * 1000 + w, h, w)
     assert np.array_equal(ops.rgb2gray_u8(_d(img)).cpu().numpy(), O.rgb2gray(img))
-    for sat in (0.8, 1.0, 1.27):
+    for sat in (0.0, 0.8, 1.0, 1.27):  # 0.0: fully desaturated (not read as 'unset')
         t = _d(img)
         ops.hsv_adjust_u8(t, sat=sat)
         assert np.array_equal(t.cpu().numpy(), O.hsv_adjust(img, sat=sat)), sat
-    for hue, val in ((-9.7, 0.93), (0.0, 1.0), (9.99, 1.1), (-10.0, 1.05)):
+    for hue, val in ((-9.7, 0.93), (0.0, 1.0), (9.99, 1.1), (-10.0, 1.05), (3.0, 0.0)):
         t = _d(img)
         ops.hsv_adjust_u8(t, hue=hue, val=val)
         assert np.array_equal(t.cpu().numpy(), O.hsv_adjust(img, hue=hue, val=val)), (hue, val)

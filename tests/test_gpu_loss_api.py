@@ -95,8 +95,13 @@ def test_out_of_range_target_is_reported():
         combined_loss(lg, bad, validate=True)
     combined_loss(lg, m, validate=True)  # the counter was reset by the raise; clean input passes
     tr = Trainer(EnhancedUNet(num_classes=2, in_channels=1, base_ch=16).to(DEV), DEV, "enhanced_unet")
+    before = {k: v.detach().clone() for k, v in tr.model.state_dict().items()}
     with pytest.raises(ValueError, match="15 target"):
         tr.step(x, bad)
+    # raised before backward / AdamW: the parameters are untouched (BN running stats, updated by
+    # the forward, are buffers the reference's forward updates too before its loss raises)
+    for k, v in tr.model.named_parameters():
+        assert torch.equal(v.detach(), before[k]), k
     assert np.isfinite(tr.step(x, m))
     with pytest.raises(ValueError):
         tr.train_epoch([{"images": x.cpu(), "batch_items": [{"semantic_mask": bad[i].cpu()} for i in range(2)]}])

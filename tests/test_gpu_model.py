@@ -293,15 +293,16 @@ def test_train_step_multitile_256_vs_fp64_oracle():
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_materialised_activation_is_exact(dtype, monkeypatch):
-    """The DoubleConv activation materialised once (eunet_bnrelu, default) and the BN+ReLU
-    applied inside conv .3's forward / wgrad operand staging round identically, so the
-    logits, the loss and every gradient agree bit for bit."""
+    """The BN+ReLU applied inside conv .3's forward / wgrad operand staging (the default,
+    UNetEngine.materialize_za = False) and the DoubleConv activation materialised once
+    (eunet_bnrelu, materialize_za = True) round identically, so the logits, the loss and
+    every gradient agree bit for bit."""
     from eunet import engine, synth
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 64, 64, start_index=3, num_classes=2, in_channels=1)
     out = {}
     for mat in (True, False):
-        monkeypatch.setattr(engine, "MATERIALIZE_ZA", mat)
+        monkeypatch.setattr(engine.UNetEngine, "materialize_za", mat)
         m = _model(16, 1, 2, dtype)
         m.train()
         logits = m.forward_lowres(x.to(DEV))
@@ -318,14 +319,14 @@ def test_materialised_activation_is_exact(dtype, monkeypatch):
 
 def test_backward_stream_schedules_are_exact(monkeypatch):
     """The weight gradients on the side stream (conv .3's enqueued early or after the block's BN-a
-    backward, engine.WG3_LATE) or all on the launch stream run the same kernels on the same
+    backward, UNetEngine.wg3_late) or all on the launch stream run the same kernels on the same
     operands: every gradient agrees bit for bit."""
     from eunet import engine, synth
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 64, 64, start_index=5, num_classes=2, in_channels=1)
     out = {}
     for overlap, late in ((True, True), (True, False), (False, True)):
-        monkeypatch.setattr(engine, "WG3_LATE", late)
+        monkeypatch.setattr(engine.UNetEngine, "wg3_late", late)
         monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", overlap)
         m = _model(16, 1, 2, "bf16")
         m.train()

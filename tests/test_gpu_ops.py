@@ -515,11 +515,11 @@ def test_conv3x3_per_sample_affine_and_gscale(dt):
     assert rel(gx, exp) < (1e-6 if dt == torch.float32 else 1e-2)
 
 
-def test_conv3x3_k64_persistent():
-    """Cin == 64 bf16 layers run the persistent resident-weight kernel: several tiles per block
-    (prefetched halo), ragged tiles, a partial third co-block, a channel-slice input with the
-    per-sample BN+ReLU transform, bias, BN partials, and the fused dgrad epilogue (BN-backward
-    reduction + Dropout2d scale)."""
+def test_conv3x3_cin64_ragged_slice():
+    """The Cin == 64 bf16 shape (two K-chunks per block, the enc1.3 / dec2.3 layers) through
+    conv3x3_fwd_kernel: ragged 16 x 32 tiles at both image edges, a partial third co-block, a
+    channel-slice input with the per-sample BN+ReLU transform, bias, BN partials, and the fused
+    dgrad epilogue (BN-backward reduction + Dropout2d scale)."""
     ops = _ops()
     dt = torch.bfloat16
     g = torch.Generator().manual_seed(14)

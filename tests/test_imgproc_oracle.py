@@ -68,6 +68,36 @@ def test_clahe_invariants(h, w):
     assert (np.diff(r[0].astype(int)) >= 0).all()
 
 
+def test_clahe_tile_rule_one_axis_uneven():
+    """OpenCV's CLAHE_Impl::apply pads BOTH axes by tiles - size % tiles as soon as one axis is
+    not a multiple of the grid: with h = 64 (divisible by 8) and w = 60 the tile is 9 x 8,
+    not 8 x 8, so the LUTs cover rows reflected past the bottom edge.  Pinned through the
+    result on an image whose histogram differs between rows 0..63 and the reflected rows."""
+    h, w = 64, 60
+    g = np.zeros((h, w), np.uint8)
+    g[:, :] = (np.arange(w)[None, :] * 4).astype(np.uint8)
+    g[-8:, :] = 250  # bottom band: the reflected padding rows 64..71 repeat rows 62..55
+    got = O.clahe(g, 2.0)
+    # restate the padded-tile computation directly: tile 9 x 8 -> area 72, clip int(2.0 * 72 / 256) = 0 -> 1
+    ext = g[O.reflect101(np.arange(8 * 9), h)][:, O.reflect101(np.arange(8 * 8), w)]
+    hist = np.bincount(ext[:9, :8].ravel(), minlength=256)
+    clip = 1
+    excess = int(np.maximum(hist - clip, 0).sum())
+    hist = np.minimum(hist, clip) + excess // 256
+    res = excess % 256
+    if res:
+        for i in range(0, 256, max(256 // res, 1)):
+            if res == 0:
+                break
+            hist[i] += 1
+            res -= 1
+    lut0 = O.sat_u8(np.cumsum(hist).astype(np.float32) * (np.float32(255.0) / np.float32(72)))
+    # pixel (0, 0) sits in the top-left quarter of tile (0, 0): its value is tile (0, 0)'s LUT
+    assert got[0, 0] == lut0[g[0, 0]]
+    even = O.clahe(g[:, :56].copy(), 2.0)  # 64 x 56: both multiples of 8 -> 8 x 7 tiles, no padding
+    assert even.shape == (64, 56)
+
+
 def test_filters_identities():
     img = _img(5)
     ident = [0, 0, 0, 0, 1, 0, 0, 0, 0]
