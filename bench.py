@@ -7,25 +7,30 @@ Workload (BASELINE.json configs[2], the metric's config): base_ch=64,
 1x1024x1024 synthetic bright-field tiles, 1-ch -> 2-class, batch 4 per GPU,
 bf16 activations / MFMA (fp32 params, BN stats, loss, AdamW).  A "step" is one
 full Trainer step (forward, fused loss, backward, bucketed RCCL all-reduce when
-N>1, clip_grad_norm_, AdamW, loss.item()).  Inputs are resident in HBM before
-the timed region.  value = images processed by all ranks / max-over-ranks time.
+N>1, clip_grad_norm_, AdamW; the loss stays on the device, as Trainer.train_epoch keeps
+it).  Inputs are resident in HBM before the timed region.  value = images processed by all ranks / max-over-ranks time.
 
 Also reported on the same JSON line:
-  roofline     -- the dominant kernel family (conv3x3 implicit-GEMM fwd/dgrad),
-                  algorithmic FLOPs / its summed launch time, measured with HIP
-                  events on the launch stream over the timed region, vs the
-                  gfx950 dense MFMA peak of the dtype;
-  cpu_baseline -- the oracle (PyTorch CPU restatement of the reference step)
-                  on the host cores, bounded sample (1 warm-up + 3 timed steps), rank 0 at
-                  N=1 only;
-  parity       -- after the timed region, untimed: a fresh model of the same configuration
-                  is trained for --dice-steps seeded steps on distinct synthetic batches
-                  (so it segments the cells instead of sitting in a degenerate state), then
-                  on held-out tiles its GPU logits (the bench dtype and fp32) are compared
-                  with the fp64 CPU oracle on the same weights (logits_rel_err_vs_cpu), and
-                  its GPU masks with the fp32 CPU oracle's masks (dice_vs_cpu_ref).
+  roofline      -- the dominant kernel family, the conv3x3 implicit-GEMM MFMA kernels (forward,
+                   data gradient, weight gradient): algorithmic FLOPs / the wall time any of them
+                   ran (union of HIP-event intervals on both streams of the timed region) vs the
+                   gfx950 dense MFMA peak of the dtype; per kernel the overlapped-span rate and,
+                   from the committed rocprofv3 --pmc pass, the serialised rate, MFMA-busy
+                   fraction and HBM traffic; step_frac = whole-step model FLOPs / time / peak;
+                   encoder_fwd = the north-star's "3x3 encoder convs" subset;
+  dp_world1     -- the same per-rank workload through eunet.dp.DataParallel on RCCL at world
+                   size 1 (BASELINE configs[3] per rank): ms/step and overhead vs the plain step;
+  fp32_configs1 -- BASELINE configs[1] (base 64, 512^2, batch 8, fp32) timed in this same run;
+  cpu_baseline  -- the oracle (PyTorch CPU restatement of the reference step) on the host
+                   cores, bounded sample (1 warm-up + 3 timed steps), rank 0 at N=1 only;
+  parity        -- after the timed region, untimed: a fresh model of the same configuration
+                   is trained for --dice-steps seeded steps on distinct synthetic batches
+                   (so it segments the cells instead of sitting in a degenerate state), then
+                   on held-out tiles its GPU logits (the bench dtype and fp32) are compared
+                   with the fp64 CPU oracle on the same weights (logits_rel_err_vs_cpu), and
+                   its GPU masks with the fp32 CPU oracle's masks (dice_vs_cpu_ref).
 
-    python bench.py --dtype fp32 --size 512 --batch 8     # BASELINE configs[1] (fp32 MFMA path)
+    python bench.py --dtype fp32 --size 512 --batch 8     # BASELINE configs[1] alone
 """
 from __future__ import annotations
 
@@ -70,6 +75,9 @@ def parse():
     ap.add_argument("--dice-steps", type=int, default=200, help="training steps of the parity model")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the weight gradients on the launch stream (no side-stream overlap; A/B)")
+    ap.add_argument("--no-dp-world1", action="store_true",
+                    help="skip the DataParallel-on-RCCL world-1 leg (N=1 only)")
+    ap.add_argument("--no-fp32-leg", action="store_true", help="skip the fp32 BASELINE configs[1] leg (N=1 only)")
     ap.add_argument("--dual", action="store_true",
                     help="dual-branch model + deep supervision (BASELINE configs[4]: --dual --base 96 --size 2048)")
     return ap.parse_args()
@@ -208,42 +216,50 @@ def dice_vs_cpu_ref(model, args, dev):
     return out
 
 
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
+# rocprofv3 --pmc summaries of the default bench command (tools/gpu_pmc.sh, tools/gpu_pmc_mfma.sh);
+# the newest round's file that exists is used
+def _profile(name):
+    for r in ("r03", "r02"):
+        f = os.path.join(ROOT, "profiles", f"{r}_{name}")
+        if os.path.exists(f):
+            return f
+    return None
+
+
+def _load_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError, TypeError):
+        return None
 
 
 def pmc_traffic(args, kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary
-    (tools/gpu_pmc.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes) of this same
-    bench command; None when no summary for this workload exists."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != [args.base, args.size, args.batch, args.dtype]:
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc summary (FETCH_SIZE x2 +
+    WRITE_SIZE, separate passes) of this same bench command; None for another workload."""
+    path = _profile("pmc_summary.json")
+    d = _load_json(path)
+    if not d or d.get("workload") != [args.base, args.size, args.batch, args.dtype]:
         return None
     k = d["kernels"].get(kernel)
     if not k:
         return None
-    return round(k["hbm_bytes_per_launch"]), f"profiles/{os.path.basename(PMC_SUMMARY)} ({d['correction']})"
+    return k["hbm_bytes_per_launch"], f"profiles/{os.path.basename(path)} ({d['correction']})"
 
 
-MFMA_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_mfma_summary.json")
-
-
-def pmc_mfma(kernel):
-    """MFMA-pipe busy fraction and effective clock of `kernel` from the committed
-    SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass of the default bench command
-    (tools/gpu_pmc_mfma.sh); None when absent."""
-    try:
-        with open(MFMA_SUMMARY) as f:
-            k = json.load(f)["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
+def pmc_mfma(args, kernel):
+    """MFMA-pipe busy fraction, effective clock and serialised launch time of `kernel` from the
+    committed SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass of the default bench command (the
+    counter pass serialises the streams); None for another workload."""
+    path = _profile("pmc_mfma_summary.json")
+    d = _load_json(path)
+    if not d or d.get("workload", [64, 1024, 4, "bf16"]) != [args.base, args.size, args.batch, args.dtype] \
+            or args.dual:
         return None
+    k = d["kernels"].get(kernel)
     if not k:
         return None
-    return {"mfma_busy_frac": round(k["mfma_busy_frac"], 4), "clock_ghz": round(k["clock_ghz"], 3),
-            "source": f"profiles/{os.path.basename(MFMA_SUMMARY)}"}
+    return dict(k, source=f"profiles/{os.path.basename(path)}")
 
 
 def _config_tag(args):
@@ -254,6 +270,161 @@ def _config_tag(args):
     if (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16"):
         return "(BASELINE configs[2]; configs[3] at N=8)"
     return "(custom)"
+
+
+def build_trainer(args, dev, dtype=None, base=None):
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    torch.manual_seed(0)
+    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=base or args.base, dtype=dtype or args.dtype,
+                         dual_branch=args.dual).to(dev)
+    tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
+    tr.epoch_lr_step(0)
+    return tr
+
+
+def timed_steps(tr, x, m, steps, warmup, world, dev):
+    """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; returns the
+    max-over-ranks elapsed seconds and the kernel timer of the timed region."""
+    from eunet import kprof
+    for _ in range(warmup):
+        tr.step(x, m)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    with kprof.KernelTimer() as timer:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.step(x, m, sync_loss=SYNC_LOSS)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    return float(elapsed.item()), timer
+
+
+CONV_FAMILIES = (("conv3x3_fwd", "fwd", "conv3x3_fwd_kernel"),
+                 ("conv3x3_dgrad", "dgrad", "conv3x3_fwd_kernel.dgrad"),
+                 ("conv3x3_wgrad", "wgrad", "conv3x3_wgrad_bf16_kernel"))
+
+
+def conv_roofline(args, timer, steps, step_flops, elapsed, dtype):
+    """roofline of the dominant kernel family, the conv3x3 implicit-GEMM MFMA kernels (forward, data
+    gradient, weight gradient: ~99 % of the step's FLOPs).  achieved = the family's algorithmic FLOPs
+    / the wall time during which any of its launches ran (union of the HIP-event intervals on both
+    streams: the weight gradients run on a side stream concurrently with the data gradients, so the
+    summed spans would count shared time twice).  components: each kernel's own rate over its summed
+    spans as it runs in the step (overlapped), and -- from the committed PMC pass, where the counter
+    collection serialises the streams -- its standalone launch time and MFMA-busy fraction."""
+    ks = timer.summary()
+    peak = PEAK_TFLOPS[dtype]
+    fams = [f for f, _, _ in CONV_FAMILIES if f in ks]
+    flops = sum(ks[f]["flops"] for f in fams)
+    launches = sum(ks[f]["launches"] for f in fams)
+    union = timer.union_ms(fams)
+    achieved = flops / (union * 1e-3) / 1e12 if union else None
+    roof = {"kernel": "conv3x3 implicit-GEMM MFMA family: conv3x3_fwd_kernel (forward + data-gradient launches) "
+                      "+ conv3x3_wgrad kernel", "bound": "mfma",
+            "achieved": round(achieved, 2) if achieved else None, "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
+            "launches_per_step": launches // max(1, steps),
+            "family_wall_ms_per_step": round(union / steps, 3),
+            "family_flops_per_step": flops / steps,
+            "algorithmic_bytes_per_launch": round(sum(ks[f]["bytes"] for f in fams) / max(1, launches)),
+            "step_frac": round(step_flops / (elapsed / steps) / 1e12 / peak, 4),
+            "components": {}}
+    traffic, src, have_all = 0.0, None, True
+    for fam, nm, kname in CONV_FAMILIES:
+        if fam not in ks:
+            continue
+        k = ks[fam]
+        per = k["flops"] / max(1, k["launches"])
+        comp = {"launches_per_step": k["launches"] // max(1, steps), "ms_per_step_spans": round(k["ms"] / steps, 3),
+                "frac_overlapped_spans": round(k["flops"] / (k["ms"] * 1e-3) / 1e12 / peak, 4)}
+        mf = pmc_mfma(args, kname) if dtype == args.dtype else None
+        if mf is not None:
+            comp["serialised_us_per_launch"] = round(mf["us_per_launch"], 1)
+            comp["frac_serialised"] = round(per / (mf["us_per_launch"] * 1e-6) / 1e12 / peak, 4)
+            comp["mfma_busy_frac"] = round(mf["mfma_busy_frac"], 4)
+            comp["clock_ghz"] = round(mf["clock_ghz"], 3)
+            comp["pmc_source"] = mf["source"]
+        pm = pmc_traffic(args, kname) if dtype == args.dtype else None
+        if pm is not None:
+            comp["traffic_per_launch"] = round(pm[0])
+            traffic += pm[0] * k["launches"]
+            src = pm[1]
+        else:
+            have_all = False
+        roof["components"][nm] = comp
+    if have_all and src:
+        roof["traffic"] = round(traffic / max(1, launches))
+        roof["traffic_source"] = src
+    if "conv3x3_fwd.encoder" in ks:  # BASELINE north_star's target is stated on the 3x3 encoder convs
+        en = ks["conv3x3_fwd.encoder"]
+        en_tf = en["flops"] / (en["ms"] * 1e-3) / 1e12
+        roof["encoder_fwd"] = {"achieved": round(en_tf, 2), "frac": round(en_tf / peak, 4),
+                               "ms_per_step": round(en["ms"] / steps, 3),
+                               "launches_per_step": en["launches"] // max(1, steps),
+                               "covers": "forward launches of enc1.3 and enc2-4 .0/.3 (enc1.0, Cin=1, runs on the "
+                                         "HBM-bound conv_small kernel)"}
+    return roof
+
+
+def step_flops_of(args, base, size, batch):
+    from oracle.eunet_ref import flops_per_pixel
+    from oracle.dual_ref import dual_flops_per_pixel
+    fpp = dual_flops_per_pixel(base, 1, 2) if args.dual else flops_per_pixel(base, 1, 2)
+    return fpp * size * size * batch
+
+
+def dp_world1_leg(args, tr, x, m, dev, ms_plain):
+    """The configs[3] per-rank workload through the data-parallel path on RCCL at world size 1:
+    DataParallel (flat gradient buffer in backward order, bucketed async all-reduces issued from the
+    backward, flat BN-buffer broadcast) on the nccl backend, same trainer and inputs; prices the
+    bucketing and RCCL launches against the plain step."""
+    import socket
+    from eunet.dp import DataParallel
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        tr.dp = DataParallel(tr.model)
+        el, _ = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
+        nb = len(tr.dp.buckets)
+        tr.dp = None
+    finally:
+        dist.destroy_process_group()
+    ms = 1e3 * el / args.steps
+    return {"dp_world1_ms_per_step": round(ms, 3), "overhead_pct": round(100.0 * (ms - ms_plain) / ms_plain, 2),
+            "buckets": nb, "backend": "nccl (RCCL)",
+            "note": "same per-rank workload through eunet.dp.DataParallel at world size 1 (bucketed all-reduce "
+                    "from inside the HIP backward, BN-buffer broadcast); BASELINE configs[3] per rank"}
+
+
+def fp32_configs1_leg(args, dev):
+    """BASELINE configs[1] (base 64, 1x512^2, batch 8, fp32: the 1e-3 parity path) timed in the same
+    invocation: value, ms/step and its conv roofline against the fp32 MFMA peak."""
+    from eunet import synth
+    size, batch = 512, 8
+    tr = build_trainer(args, dev, dtype="fp32", base=64)
+    x, m = synth.batch(batch, size, size, start_index=0, num_classes=2, in_channels=1, device=dev)
+    el, timer = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
+    sf = step_flops_of(args, 64, size, batch)
+    a32 = argparse.Namespace(**vars(args))
+    a32.size, a32.batch, a32.dtype, a32.base = size, batch, "fp32", 64
+    roof = conv_roofline(a32, timer, args.steps, sf, el, "fp32")
+    out = {"value": round(batch * args.steps / el, 3), "unit": "img/s", "ms_per_step": round(1e3 * el / args.steps, 3),
+           "workload": "base_ch=64, 1x512x512 1-ch->2-cls, batch 8, fp32 (BASELINE configs[1])",
+           "model_tflops": round(sf / (el / args.steps) / 1e12, 2), "roofline": roof}
+    del tr
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -268,78 +439,34 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from eunet import synth, kprof
+    from eunet import synth
     from eunet.engine import UNetEngine
-    from eunet.models import EnhancedUNet
     UNetEngine.overlap_wgrad = not args.no_overlap
-    from eunet.train_eval import Trainer
 
-    torch.manual_seed(0)
-    model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=args.base, dtype=args.dtype,
-                         dual_branch=args.dual).to(dev)
-    tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
-    tr.epoch_lr_step(0)
+    tr = build_trainer(args, dev)
     if world > 1:
         from eunet.dp import DataParallel
-        tr.dp = DataParallel(model)
+        tr.dp = DataParallel(tr.model)
     x, m = synth.batch(args.batch, args.size, args.size, start_index=rank * args.batch, num_classes=2,
                        in_channels=1, device=dev)
-    for _ in range(args.warmup):
-        tr.step(x, m)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    with kprof.KernelTimer() as timer:
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            tr.step(x, m, sync_loss=SYNC_LOSS)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-    ks = timer.summary()
+    elapsed, timer = timed_steps(tr, x, m, args.steps, args.warmup, world, dev)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
     imgs = world * args.batch * args.steps
-    fam = ks.get("conv3x3_fwd", {"ms": 0.0, "flops": 0.0, "launches": 0, "bytes": 0.0})
-    achieved = fam["flops"] / (fam["ms"] * 1e-3) / 1e12 if fam["ms"] else None
-    peak = PEAK_TFLOPS[args.dtype]
-    roof = {"kernel": "conv3x3_fwd_kernel<T, false> (implicit-GEMM MFMA, forward launches)", "bound": "mfma",
-            "achieved": round(achieved, 2) if achieved else None, "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4) if achieved else None, "traffic": None,
-            "launches_per_step": fam["launches"] // max(1, args.steps),
-            "kernel_ms_per_step": round(fam["ms"] / args.steps, 3),
-            "algorithmic_bytes_per_launch": round(fam["bytes"] / max(1, fam["launches"]))}
-    pmc = pmc_traffic(args, "conv3x3_fwd_kernel")
-    if pmc is not None:
-        roof["traffic"], roof["traffic_source"] = pmc
-    mf = pmc_mfma("conv3x3_fwd_kernel") if (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16") \
-        and not args.dual else None
-    if mf is not None:
-        roof["pmc_mfma"] = mf
-    if "conv3x3_fwd.encoder" in ks:  # BASELINE north_star's target is stated on the 3x3 encoder convs
-        en = ks["conv3x3_fwd.encoder"]
-        en_tf = en["flops"] / (en["ms"] * 1e-3) / 1e12
-        roof["encoder_fwd"] = {"achieved": round(en_tf, 2), "frac": round(en_tf / peak, 4),
-                               "ms_per_step": round(en["ms"] / args.steps, 3),
-                               "launches_per_step": en["launches"] // max(1, args.steps),
-                               "covers": "forward launches of enc1.3 and enc2-4 .0/.3 (subset of the family "
-                                         "above; enc1.0, Cin=1, runs on the HBM-bound conv_small kernel)"}
-    # backward MFMA kernels: the weight gradients run on a side stream concurrently with the data
-    # gradients (UNetEngine.overlap_wgrad), so these per-launch spans include time shared with the
-    # other stream -- lower bounds of each kernel's own rate
-    for key, nm in (("conv3x3_dgrad", "dgrad"), ("conv3x3_wgrad", "wgrad")):
-        if key in ks and ks[key]["ms"]:
-            k = ks[key]
-            roof[f"{nm}_tflops_overlapped_spans"] = round(k["flops"] / (k["ms"] * 1e-3) / 1e12, 2)
-            roof[f"{nm}_ms_per_step_spans"] = round(k["ms"] / args.steps, 3)
+    step_flops = step_flops_of(args, args.base, args.size, args.batch)
+    roof = conv_roofline(args, timer, args.steps, step_flops, elapsed, args.dtype)
+    ms_plain = 1e3 * elapsed / args.steps
+    dpw1 = None
+    if world == 1 and not args.no_dp_world1 and not args.dual:
+        dpw1 = dp_world1_leg(args, tr, x, m, dev, ms_plain)
+    del tr
+    torch.cuda.empty_cache()
+    fp32 = None
+    if world == 1 and not args.no_fp32_leg and not args.dual and \
+            (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16"):
+        fp32 = fp32_configs1_leg(args, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -348,10 +475,6 @@ def main():
         pmodel = train_parity_model(args, dev)
         logits_err = logits_rel_err_vs_cpu(pmodel, args, dev)
         dice = dice_vs_cpu_ref(pmodel, args, dev)
-    from oracle.eunet_ref import flops_per_pixel
-    from oracle.dual_ref import dual_flops_per_pixel
-    fpp = dual_flops_per_pixel(args.base, 1, 2) if args.dual else flops_per_pixel(args.base, 1, 2)
-    step_flops = fpp * args.size * args.size * args.batch
     line = {
         "metric": METRIC,
         "value": round(imgs / elapsed, 3),
@@ -359,7 +482,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "ms_per_step": round(ms_plain, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -371,6 +494,8 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.size, "parallelism": f"dp{world}"},
         "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
         "roofline": roof,
+        "dp_world1": dpw1,
+        "fp32_configs1": fp32,
         "cpu_baseline": cpu,
         "logits_rel_err_vs_cpu": logits_err,
         "dice_vs_cpu_ref": dice,

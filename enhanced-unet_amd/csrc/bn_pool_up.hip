@@ -698,11 +698,40 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
 // with K1 = scale = gamma istd.  A thread keeps one 16-byte channel
 // unit with its coefficients in registers and strides over pixels; the block holds
 // floor(256 / U) pixels x U units (base_ch 96 -> U = 12, 21 pixels per step).
+// The per-channel constants of the BN-backward apply, gy = k1 g' + k2 y + k3 (k1 = scale = gamma
+// istd, also the forward-mask slope; kq = shift).  One function for the standalone apply below and
+// the coefficient table the fused consumers read (eunet_bn_bwd_coef -> conv3x3 dgrad staging), so
+// both round identically.
+struct BnBwdCoef { float k1, kq, k2, k3; };
+__device__ __forceinline__ BnBwdCoef bn_bwd_coef(float mean, float istd, float scale, float shift, float dbeta,
+                                                 float dgamma, float inv_n) {
+  const float off = -mean * istd;
+  const float dg = dgamma * inv_n;
+  BnBwdCoef c;
+  c.k1 = scale;
+  c.kq = shift;
+  c.k2 = -scale * istd * dg;
+  c.k3 = -scale * fmaf(off, dg, dbeta * inv_n);
+  return c;
+}
+
+__global__ void bn_bwd_coef_kernel(const float* mean, const float* istd, const float* scale, const float* shift,
+                                   const float* dbeta, const float* dgamma, float inv_n, int C, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const BnBwdCoef k = bn_bwd_coef(mean[c], istd[c], scale[c], shift[c], dbeta[c], dgamma[c], inv_n);
+  coef[c] = k.k1;
+  coef[C + c] = k.kq;
+  coef[2 * C + c] = k.k2;
+  coef[3 * C + c] = k.k3;
+}
+
 template <typename T, typename TO>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
                                                            const float* scale, const float* shift, const float* dbeta,
-                                                           const float* dgamma, TO* gy, int oct, int oco) {
+                                                           const float* dgamma, TO* gy, int oct, int oco,
+                                                           const float* coef) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E;
   const int u = threadIdx.x % U, c = u * E;
@@ -710,13 +739,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   float kP[E], kQ[E], k1[E], k2[E], k3[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
-    const float is = istd[c + j], off = -mean[c + j] * is;
-    kP[j] = scale[c + j];
-    kQ[j] = shift[c + j];
-    k1[j] = scale[c + j];
-    const float dg = dgamma[c + j] * inv_n;
-    k2[j] = -k1[j] * is * dg;
-    k3[j] = -k1[j] * fmaf(off, dg, dbeta[c + j] * inv_n);
+    // coef: the table eunet_bn_bwd_coef wrote (the same bn_bwd_coef values)
+    const BnBwdCoef k = coef != nullptr
+                            ? BnBwdCoef{coef[c + j], coef[C + c + j], coef[2 * C + c + j], coef[3 * C + c + j]}
+                            : bn_bwd_coef(mean[c + j], istd[c + j], scale[c + j], shift[c + j], dbeta[c + j],
+                                          dgamma[c + j], inv_n);
+    kP[j] = k.k1;
+    kQ[j] = k.kq;
+    k1[j] = k.k1;
+    k2[j] = k.k2;
+    k3[j] = k.k3;
   }
   const int ppb = blockDim.x / U;  // pixels per block per step (blockDim.x = ppb * U)
   for (long long p = (long long)blockIdx.x * ppb + threadIdx.x / U; p < P; p += (long long)gridDim.x * ppb) {
@@ -1486,12 +1518,12 @@ int eunet_colsum_split(const float* part, int rows, int cols, int split, float* 
   return eunet_colsum_ld(part, rows, cols, cols, out_lo, ws, (hipStream_t)stream, split, out_hi);
 }
 
-int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
-                       const float* scale, const float* shift, const float* dbeta, const float* dgamma,
-                       const eunet_act* gy, void* stream) {
+static int bn_bwd_apply_launch(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
+                               const float* scale, const float* shift, const float* dbeta, const float* dgamma,
+                               const float* coef, const eunet_act* gy, void* stream) {
   EUNET_REQUIRE(act_ok(g) && act_ok(y) && act_ok(gy) && vec_ok(g) && vec_ok(y) && vec_ok(gy),
                 "bn_bwd_apply: bad tensors");
-  EUNET_REQUIRE(mean && invstd && scale && shift && dbeta && dgamma, "bn_bwd_apply: null stats");
+  EUNET_REQUIRE(coef || (mean && invstd && scale && shift && dbeta && dgamma), "bn_bwd_apply: null stats");
   EUNET_REQUIRE(g->dtype == y->dtype && gy->dtype == y->dtype && g->c == y->c && gy->c == y->c,
                 "bn_bwd_apply: mismatch");
   const long long P = (long long)y->n * y->h * y->w;
@@ -1503,12 +1535,35 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
   if (y->dtype == EUNET_BF16)
     bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        scale, shift, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff);
+        scale, shift, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff, coef);
   else
     bn_bwd_apply_kernel<float, float><<<gr, bs, 0, (hipStream_t)stream>>>(
         (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        scale, shift, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff);
+        scale, shift, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff, coef);
   EUNET_LAUNCH_CHECK("bn_bwd_apply");
+  return EUNET_OK;
+}
+
+int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean, const float* invstd,
+                       const float* scale, const float* shift, const float* dbeta, const float* dgamma,
+                       const eunet_act* gy, void* stream) {
+  EUNET_REQUIRE(mean && invstd && scale && shift && dbeta && dgamma, "bn_bwd_apply: null stats");
+  return bn_bwd_apply_launch(g, y, mean, invstd, scale, shift, dbeta, dgamma, nullptr, gy, stream);
+}
+
+int eunet_bn_bwd_apply_coef(const eunet_act* g, const eunet_act* y, const float* coef, const eunet_act* gy,
+                            void* stream) {
+  EUNET_REQUIRE(coef, "bn_bwd_apply_coef: null coef");
+  return bn_bwd_apply_launch(g, y, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, coef, gy, stream);
+}
+
+int eunet_bn_bwd_coef(const float* mean, const float* invstd, const float* scale, const float* shift,
+                      const float* dbeta, const float* dgamma, long long count, int C, float* coef, void* stream) {
+  EUNET_REQUIRE(mean && invstd && scale && shift && dbeta && dgamma && coef && count > 0 && C > 0,
+                "bn_bwd_coef: bad args");
+  bn_bwd_coef_kernel<<<(C + 255) / 256, 256, 0, (hipStream_t)stream>>>(mean, invstd, scale, shift, dbeta, dgamma,
+                                                                       1.f / (float)count, C, coef);
+  EUNET_LAUNCH_CHECK("bn_bwd_coef");
   return EUNET_OK;
 }
 

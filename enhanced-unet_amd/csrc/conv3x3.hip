@@ -58,6 +58,12 @@ struct FwdArgs {
   const float* bmean; const float* bistd; const float* bsc; const float* bsh;
   float* bpart;
   const float* gsc;  // dgrad only, nullable: output scaled by gsc[n][co] (Dropout2d keep mask / (1-p))
+  // dgrad only, nullable: BatchNorm-backward transform of the operand (the "apply" half of BN
+  // backward, fused into the halo staging).  x holds g (gradient w.r.t. the BN+ReLU output), ty the
+  // BN's input y in tyin (same layout as x); the staged operand is gy = k1 g [y k1 + kq > 0] + k2 y + k3
+  // with tcoef = [k1 | kq | k2 | k3][cin] (eunet_bn_bwd_coef).  Co-block 0 also stores the tile
+  // interior of gy to tgo (same layout, nullable) for the weight gradient.
+  const void* tyin; const float* tcoef; void* tgo;
   int pro1;          // 1 (always, set by the launcher): the first K-chunk is staged in one round trip.
                      // Kept a runtime flag: with the halved-staging prologue still compiled in, the
                      // register allocator fits the kernel in 256 VGPRs without spills (a compile-time
@@ -131,7 +137,9 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 #endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
-template <typename T, bool DG>
+// TO: the output element type -- T, or float for a bf16 data gradient whose consumer keeps fp32
+// (the dual-branch gate backward reads the 2K-channel g_f2 in fp32; no fused BN reduction then)
+template <typename T, bool DG, typename TO = T>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -168,13 +176,45 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < A_IT; ++i) aoff[i] = fwd_unit_off<T>(a, y0, x0, tid + i * FT);
 
+  // dgrad: the BN-backward transform (k1 in asc, kq in ash, k2 / k3 below) and its y operand
+  constexpr int BE = DG ? E / 4 : 1;
+  f32x4 ak2[BE], ak3[BE];
+  u32x4 ry[DG ? A_IT : 1];
+  // bf16 only: the fp32 dgrad has no registers to spare (eunet_conv3x3_dgrad_fused applies the transform
+  // in a separate pass for fp32)
+  constexpr bool BTR = DG && sizeof(T) == 2;
+  const bool btr = BTR && a.tcoef != nullptr;
+  const uint32_t slice_bytes = (uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(btr ? (const T*)a.tyin + (long long)ns * a.H * a.W * a.xct : nullptr), 0, btr ? (int)slice_bytes : 0,
+      0x00020000);
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc((void*)(btr ? a.tcoef : nullptr), 0,
+                                                                      btr ? 16 * a.cin : 0, 0x00020000);
+  // co-block 0 stores the staged gy (tile interior only: every pixel belongs to one tile)
+  const bool wgy = btr && a.tgo != nullptr && cob == 0;
+  const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(wgy ? (T*)a.tgo + (long long)ns * a.H * a.W * a.xct : nullptr), 0, wgy ? (int)slice_bytes : 0,
+      0x00020000);
+  uint32_t interior = 0;  // bit i: halo unit i is a tile-interior pixel (its gy is stored)
+  if (BTR) {
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      int hp, qq;
+      fwd_unit(tid + i * FT, hp, qq);
+      const int hy = hp / FHW, hx = hp - hy * FHW;
+      if (hp < FHPX && hy >= 1 && hy <= FTH && hx >= 1 && hx <= FTW) interior |= 1u << i;
+    }
+  }
   auto chunk_ok = [&](int kc) { return kc * KC + sq * E < a.cin; };
   auto gload_a = [&](int kc, int i0, int i1) {
     const bool cok = chunk_ok(kc);
     const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
 #pragma unroll
-    for (int i = i0; i < i1; ++i)
+    for (int i = i0; i < i1; ++i) {
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
+      if constexpr (BTR)
+        if (btr) ry[i] = __builtin_amdgcn_raw_buffer_load_b128(yr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
+    }
   };
   auto gload_b = [&](int kc, int i0, int i1) {
 #pragma unroll
@@ -195,10 +235,21 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   f32x4 asc[E / 4], ash[E / 4];
   auto gload_affine = [&](int kc) {
     const uint32_t off = (uint32_t)((kc * KC + sq * E) * 4);
+    if constexpr (BTR) {
+      const uint32_t row = (uint32_t)(4 * a.cin);
 #pragma unroll
-    for (int j = 0; j < E / 4; ++j) {
-      asc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(sr, off + 16 * j, 0, 0));
-      ash[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, off + 16 * j, 0, 0));
+      for (int j = 0; j < E / 4; ++j) {
+        asc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, off + 16 * j, 0, 0));
+        ash[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, row + off + 16 * j, 0, 0));
+        ak2[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, 2 * row + off + 16 * j, 0, 0));
+        ak3[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cr, 3 * row + off + 16 * j, 0, 0));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < E / 4; ++j) {
+        asc[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(sr, off + 16 * j, 0, 0));
+        ash[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(hr, off + 16 * j, 0, 0));
+      }
     }
   };
   auto lwrite_a = [&](int kc, int i0, int i1) {
@@ -209,7 +260,24 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       fwd_unit(tid + i * FT, hp, qq);
       if (hp >= FHPX) continue;
       u32x4 v = ra[i];
-      if (a.isc != nullptr) {  // BN + ReLU of the producing layer; padding stays zero
+      if constexpr (DG) {
+        if (BTR && btr) {  // BN backward of the layer whose input gradient this is; padding stays zero
+          float f[E], yv[E];
+          Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
+          Vec16<T>::unpack(__builtin_bit_cast(uint4, ry[i]), yv);
+          const bool ok = cok && aoff[i] < FWD_OOB;
+#pragma unroll
+          for (int j = 0; j < E; ++j) {
+            const float k1 = asc[j >> 2][j & 3];
+            const float gg = fmaf(yv[j], k1, ash[j >> 2][j & 3]) > 0.f ? f[j] : 0.f;  // the forward's ReLU mask
+            f[j] = ok ? fmaf(k1, gg, fmaf(yv[j], ak2[j >> 2][j & 3], ak3[j >> 2][j & 3])) : 0.f;
+          }
+          v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
+          if (wgy && ((interior >> i) & 1u))
+            __builtin_amdgcn_raw_buffer_store_b128(v, gr, cok ? aoff[i] + (uint32_t)(kc * KC * (int)sizeof(T)) : FWD_OOB,
+                                                   0, 0);
+        }
+      } else if (a.isc != nullptr) {  // BN + ReLU of the producing layer; padding stays zero
         float f[E];
         Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
         const bool ok = cok && aoff[i] < FWD_OOB;
@@ -265,10 +333,20 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
   auto stage_halves = [&](int kc) {
     gload_affine(kc);
-    gload_a(kc, 0, AH);
-    lwrite_a(kc, 0, AH);
-    gload_a(kc, AH, A_IT);
-    lwrite_a(kc, AH, A_IT);
+    if (DG && btr) {  // two loads per halo unit (g and y): thirds bound the staging registers
+      constexpr int A3 = (A_IT + 2) / 3;
+      gload_a(kc, 0, A3);
+      lwrite_a(kc, 0, A3);
+      gload_a(kc, A3, 2 * A3);
+      lwrite_a(kc, A3, 2 * A3);
+      gload_a(kc, 2 * A3, A_IT);
+      lwrite_a(kc, 2 * A3, A_IT);
+    } else {
+      gload_a(kc, 0, AH);
+      lwrite_a(kc, 0, AH);
+      gload_a(kc, AH, A_IT);
+      lwrite_a(kc, AH, A_IT);
+    }
     gload_b(kc, 0, BH);
     lwrite_b(0, BH);
     gload_b(kc, BH, B_IT);
@@ -436,7 +514,13 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         for (int e = 0; e < E; ++e) f[e] = sp[e];
         const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
         const uint4 packed = Vec16<T>::pack(f);
-        *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
+        if constexpr (sizeof(TO) == sizeof(T)) {
+          *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
+        } else {  // fp32 output of a bf16 kernel: E = 8 floats, two 16-byte stores
+          float* yo = (float*)a.y + pix * a.yct + a.yco + co;
+          *(float4*)yo = make_float4(f[0], f[1], f[2], f[3]);
+          *(float4*)(yo + 4) = make_float4(f[4], f[5], f[6], f[7]);
+        }
         if (bnb) {
           float gr[E], yv[E];
           Vec16<T>::unpack(packed, gr);
@@ -982,13 +1066,16 @@ int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
 template <bool DG>
-int launch_fwd(const FwdArgs& a, int dtype, void* stream) {
+int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false) {
   const long long esz = dtype == EUNET_BF16 ? 2 : 4;
   EUNET_REQUIRE((long long)a.H * a.W * a.xct * esz < (long long)FWD_OOB,
                 "conv3x3: one sample's input (%d x %d x %d) must be < 3 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
   EUNET_REQUIRE((long long)a.nkc * kchunk(dtype) * a.cout_pad * 9 * esz < (1ll << 31), "conv3x3: packed weights >= 2 GiB");
   dim3 grid(a.ntiles * (a.cout_pad / BN));
-  if (dtype == EUNET_BF16) {
+  if (dtype == EUNET_BF16 && out_f32) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t, true, float>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t, true, float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else if (dtype == EUNET_BF16) {
     allow_lds(conv3x3_fwd_kernel<bf16_t, DG>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
   } else {
@@ -1069,6 +1156,7 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
   a.stats = stats; a.tx = cdiv(x->w, FTW); a.ty = cdiv(x->h, FTH); a.ntiles = x->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
   a.bmean = a.bistd = a.bsc = a.bsh = nullptr; a.bpart = nullptr; a.gsc = nullptr;
+  a.tyin = nullptr; a.tcoef = nullptr; a.tgo = nullptr;
   a.pro1 = 1;
   EUNET_REQUIRE(y->c % E == 0 && y->ctot % E == 0 && y->coff % E == 0,
                 "conv3x3_fwd: output channels/stride/offset must be multiples of %d", E);
@@ -1078,7 +1166,9 @@ int eunet_conv3x3_fwd(const eunet_act* x, const float* in_scale, const float* in
 int eunet_conv3x3_dgrad(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const float* gscale,
                         void* stream) {
   EUNET_REQUIRE(act_ok(dy) && act_ok(gx) && wp_t, "conv3x3_dgrad: bad args");
-  EUNET_REQUIRE(dy->dtype == gx->dtype, "conv3x3_dgrad: dtype mismatch");
+  // gx is dy's dtype, or fp32 for a bf16 dy (the output rounded to fp32 instead of bf16)
+  const bool out_f32 = dy->dtype == EUNET_BF16 && gx->dtype == EUNET_F32;
+  EUNET_REQUIRE(dy->dtype == gx->dtype || out_f32, "conv3x3_dgrad: dtype mismatch");
   EUNET_REQUIRE(dy->n == gx->n && dy->h == gx->h && dy->w == gx->w, "conv3x3_dgrad: spatial mismatch");
   const int E = elems16(dy->dtype);
   EUNET_REQUIRE(dy->c % E == 0 && dy->ctot % E == 0 && dy->coff % E == 0 && gx->c % E == 0 && gx->ctot % E == 0 &&
@@ -1093,8 +1183,9 @@ int eunet_conv3x3_dgrad(const eunet_act* dy, const void* wp_t, const eunet_act* 
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = nullptr; a.byct = 0; a.byco = 0;
   a.bmean = a.bistd = a.bsc = a.bsh = nullptr; a.bpart = nullptr; a.gsc = gscale;
+  a.tyin = nullptr; a.tcoef = nullptr; a.tgo = nullptr;
   a.pro1 = 1;
-  return launch_fwd<true>(a, dy->dtype, stream);
+  return launch_fwd<true>(a, dy->dtype, stream, out_f32);
 }
 
 int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const eunet_act* y,
@@ -1119,8 +1210,57 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
   a.stats = nullptr; a.tx = cdiv(dy->w, FTW); a.ty = cdiv(dy->h, FTH); a.ntiles = dy->n * a.tx * a.ty;
   a.by = y->ptr; a.byct = y->ctot; a.byco = y->coff;
   a.bmean = mean; a.bistd = invstd; a.bsc = scale; a.bsh = shift; a.bpart = part; a.gsc = gscale;
+  a.tyin = nullptr; a.tcoef = nullptr; a.tgo = nullptr;
   a.pro1 = 1;
   return launch_fwd<true>(a, dy->dtype, stream);
+}
+
+int eunet_conv3x3_dgrad_fused(const eunet_act* g, const eunet_act* y_in, const float* coef, const eunet_act* gy_out,
+                              const void* wp_t, const eunet_act* gx, const eunet_act* y_next, const float* mean,
+                              const float* invstd, const float* scale, const float* shift, float* part,
+                              const float* gscale, void* stream) {
+  EUNET_REQUIRE(act_ok(g) && act_ok(y_in) && coef && act_ok(gx) && wp_t, "conv3x3_dgrad_fused: bad args");
+  EUNET_REQUIRE(g->dtype == gx->dtype && y_in->dtype == g->dtype, "conv3x3_dgrad_fused: dtype mismatch");
+  EUNET_REQUIRE(g->n == gx->n && g->h == gx->h && g->w == gx->w, "conv3x3_dgrad_fused: spatial mismatch");
+  // y_in (and gy_out) are addressed with g's unit offsets: the same shape and channel layout
+  EUNET_REQUIRE(y_in->n == g->n && y_in->h == g->h && y_in->w == g->w && y_in->c == g->c && y_in->ctot == g->ctot &&
+                    y_in->coff == g->coff,
+                "conv3x3_dgrad_fused: y_in must have g's shape and channel layout");
+  if (gy_out)
+    EUNET_REQUIRE(act_ok(gy_out) && gy_out->dtype == g->dtype && gy_out->n == g->n && gy_out->h == g->h &&
+                      gy_out->w == g->w && gy_out->c == g->c && gy_out->ctot == g->ctot && gy_out->coff == g->coff,
+                  "conv3x3_dgrad_fused: gy_out must have g's shape and channel layout");
+  const bool red = y_next != nullptr;
+  EUNET_REQUIRE(red == (part != nullptr) && (!red || (act_ok(y_next) && mean && invstd && scale && shift)),
+                "conv3x3_dgrad_fused: the next-BN reduction needs y_next, mean, invstd, scale, shift and part");
+  if (red)
+    EUNET_REQUIRE(y_next->dtype == gx->dtype && y_next->n == gx->n && y_next->h == gx->h && y_next->w == gx->w &&
+                      y_next->c == gx->c,
+                  "conv3x3_dgrad_fused: y_next shape mismatch");
+  const int E = elems16(g->dtype);
+  EUNET_REQUIRE(g->c % E == 0 && g->ctot % E == 0 && g->coff % E == 0 && gx->c % E == 0 && gx->ctot % E == 0 &&
+                    gx->coff % E == 0 && (!red || (y_next->ctot % E == 0 && y_next->coff % E == 0)),
+                "conv3x3_dgrad_fused: channels/strides must be multiples of %d", E);
+  FwdArgs a;
+  a.x = g->ptr; a.N = g->n; a.H = g->h; a.W = g->w; a.xct = g->ctot; a.xco = g->coff; a.cin = g->c;
+  a.isc = nullptr; a.ish = nullptr; a.iss = 0;
+  a.wp = wp_t; a.cout_pad = cdiv(gx->c, BN) * BN; a.nkc = cdiv(g->c, kchunk(g->dtype));
+  a.bias = nullptr;
+  a.y = gx->ptr; a.yct = gx->ctot; a.yco = gx->coff; a.cout = gx->c;
+  a.stats = nullptr; a.tx = cdiv(g->w, FTW); a.ty = cdiv(g->h, FTH); a.ntiles = g->n * a.tx * a.ty;
+  a.by = red ? y_next->ptr : nullptr; a.byct = red ? y_next->ctot : 0; a.byco = red ? y_next->coff : 0;
+  a.bmean = mean; a.bistd = invstd; a.bsc = scale; a.bsh = shift; a.bpart = part; a.gsc = gscale;
+  a.tyin = y_in->ptr; a.tcoef = coef; a.tgo = gy_out ? gy_out->ptr : nullptr;
+  a.pro1 = 1;
+  if (g->dtype != EUNET_BF16) {
+    // fp32: the transform runs as its own pass into gy_out (the fp32 staging has no registers for
+    // it), then the plain data gradient reads gy_out -- the same values
+    EUNET_REQUIRE(gy_out, "conv3x3_dgrad_fused: fp32 needs gy_out (the transform is materialised)");
+    const int rc = eunet_bn_bwd_apply_coef(g, y_in, coef, gy_out, stream);
+    if (rc != EUNET_OK) return rc;
+    a.x = gy_out->ptr; a.tyin = nullptr; a.tcoef = nullptr; a.tgo = nullptr;
+  }
+  return launch_fwd<true>(a, g->dtype, stream);
 }
 
 

@@ -727,19 +727,28 @@ __device__ __forceinline__ float sum_x16(float v) {
   return v;
 }
 
+// Per lane shifted sums S1 = sum (h - s), S2 = sum (h - s)^2 over its pixels, with the shift s =
+// the lane's first computed value (any finite shift is exact in real arithmetic; one near the
+// mean keeps S2 - S1^2 / n free of cancellation), then (mean, M2) per lane and Chan's combine
+// across lanes and waves.  Full tiles (every 2H tile of a multiple-of-16 image) take a branch-free
+// path with two rows' MFMAs issued ahead of their VALU work; the count is kept per lane.
 template <int K>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_stats_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
   __shared__ float zs[ZR * ZR * 3];
   __shared__ float wn_s[4], wm_s[4][MID], wq_s[4][MID];
+  __shared__ __attribute__((aligned(16))) float shs[4][MID];  // per-wave shift of each channel
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   bf16x8 Ah[4];
   load_a_w1<K>(a.w1, lane, Ah);
   int off[8];
   im2col_offsets<K>(q, off);
-  float n = 0.f, mean[16], m2[16];
+  float n = 0.f, s1[16], s2[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
+  for (int e = 0; e < 16; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  const float* shw = shs[wv];
+  bool first = true;
   float zv[2] = {0.f, 0.f};
   zload(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
@@ -748,49 +757,55 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
     __syncthreads();
     stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
+    if (first) {  // the wave's shift per channel: its first row's pixel 0 (a zero-padded 0 at an edge)
+      f32x4 acc[4];
+      conv_h_mfma(su, ((4 * wv) * 18 + x) * 3, off, Ah, acc);
+      if (x == 0)
 #pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) shs[wv][16 * cb + 4 * q + i] = acc[cb][i];
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes (wave-private row)
+      __builtin_amdgcn_wave_barrier();
+      first = false;
+    }
+    const bool full = oy0 + T2 <= H2 && ox0 + T2 <= W2;  // uniform (every tile of a multiple-of-16 image)
+#pragma unroll 1
     for (int rr = 0; rr < 4; ++rr) {
       const int r = 4 * wv + rr;
       f32x4 acc[4];
       conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
-      if (oy0 + r < 2 * a.h && ox0 + x < 2 * a.w) {
-        n += 1.f;
-        const float inv = 1.f / n;
+      const float m = (full || (oy0 + r < H2 && ox0 + x < W2)) ? 1.f : 0.f;
+      n += m;
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
+      for (int cb = 0; cb < 4; ++cb) {
+        const float4 s4 = ld4(shw + 16 * cb + 4 * q);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int e = 4 * cb + i;
-            const float d = acc[cb][i] - mean[e];
-            mean[e] = fmaf(d, inv, mean[e]);
-            m2[e] = fmaf(d, acc[cb][i] - mean[e], m2[e]);
-          }
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * cb + i;
+          const float d = (acc[cb][i] - f4(s4, i)) * m;
+          s1[e] += d;
+          s2[e] = fmaf(d, d, s2[e]);
+        }
       }
     }
   }
+  // the lanes of a row share the wave's shifts: their shifted sums add directly
 #pragma unroll
-  for (int o = 1; o <= 8; o <<= 1) {
-    const float nb = __shfl_xor(n, o, 64);
-    const float nt = n + nb;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const float mb = __shfl_xor(mean[e], o, 64), qb = __shfl_xor(m2[e], o, 64);
-      const float d = mb - mean[e];
-      if (nt > 0.f) {
-        mean[e] += d * nb / nt;
-        m2[e] += qb + d * d * n * nb / nt;
-      }
-    }
-    n = nt;
+  for (int e = 0; e < 16; ++e) {
+    s1[e] = sum_x16(s1[e]);
+    s2[e] = sum_x16(s2[e]);
   }
+  n = sum_x16(n);
   if (x == 0) {
+    const float inv = n > 0.f ? 1.f / n : 0.f;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int c = 16 * cb + 4 * q + i;
-        wm_s[wv][c] = mean[4 * cb + i] + a.b1[c];
-        wq_s[wv][c] = m2[4 * cb + i];
+        const int c = 16 * cb + 4 * q + i, e = 4 * cb + i;
+        wm_s[wv][c] = fmaf(s1[e], inv, shs[wv][c]) + a.b1[c];
+        wq_s[wv][c] = fmaxf(fmaf(-s1[e] * inv, s1[e], s2[e]), 0.f);
       }
     if (q == 0) wn_s[wv] = n;
   }

@@ -51,6 +51,7 @@ SIGNATURES = {
     "eunet_conv3x3_fwd": [_P, _f, _f, c_int, _f, _f, _P, _f, c_void_p],
     "eunet_conv3x3_dgrad_bnbwd": [_P, _f, _P, _P, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_conv3x3_dgrad": [_P, _f, _P, _f, c_void_p],
+    "eunet_conv3x3_dgrad_fused": [_P, _P, _f, _P, _f, _P, _P, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_conv3x3_wgrad_splits": [_P, c_int, c_int, POINTER(c_int)],
     "eunet_conv3x3_wgrad": [_P, _f, _f, c_int, _P, _f, _f, c_int, c_void_p],
     "eunet_wgrad_reduce": [_f, _f, c_int, c_int, c_int, c_int, _f, _f, c_void_p],
@@ -79,6 +80,8 @@ SIGNATURES = {
     "eunet_colsum": [_f, c_int, c_int, _f, _f, c_void_p],
     "eunet_colsum_split": [_f, c_int, c_int, c_int, _f, _f, _f, c_void_p],
     "eunet_bn_bwd_apply": [_P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
+    "eunet_bn_bwd_coef": [_f, _f, _f, _f, _f, _f, c_int64, c_int, _f, c_void_p],
+    "eunet_bn_bwd_apply_coef": [_P, _P, _f, _P, c_void_p],
     "eunet_pool_bwd_add": [_P, _P, _P, _P, c_void_p],
     "eunet_upsample_bwd": [_P, _P, c_void_p],
     "eunet_pool_bwd_add_bnr_rows": [_P, POINTER(c_int)],

@@ -217,7 +217,10 @@ class DualEngine:
         ops.conv_small_wgrad(f2a, ops.act(gy1), dwp, None, ns)
         ops.wgrad_reduce(dwp, None, ns, HEAD_CH[0], 2 * K, 9, sink.slot("fusion_head.0.weight", (HEAD_CH[0], 2 * K, 3, 3)),
                          None)
-        gf2c = _e((N, H, W, 8), dt, dev)
+        # g_f2 leaves the bf16 dgrad in fp32: the gate backward's BN sums cancel strongly, and a
+        # bf16-rounded g_f2 left attention_gate.1's gradient at 1.1 relative L2 vs the fp64 oracle
+        # (bf16 autocast of the reference: 0.24; tests/test_gpu_dual.py bf16 gradient parity)
+        gf2c = _e((N, H, W, 8), torch.float32, dev)
         ops.conv3x3_dgrad(ops.act(gy1), ops.conv3x3_pack(P["fusion_head.0.weight"], dt, flip=True), ops.act(gf2c))
         del gy1
         sink.ready(["fusion_head.1.weight", "fusion_head.1.bias", "fusion_head.0.weight"])

@@ -93,6 +93,10 @@ class UNetEngine:
     # this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7
     # alternating pairs on one box (profiles/r02_ab_conv.txt)
     wg3_late = True
+    # fuse_bn_apply -- the apply half of each DoubleConv BatchNorm backward (gy = k1 g' + k2 y + k3)
+    # runs inside the data gradient's operand staging (eunet_conv3x3_dgrad_fused), which also stores
+    # gy for the weight gradient; False: a separate bn_bwd_apply pass per BN (round 2).  Same values.
+    fuse_bn_apply = True
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -301,6 +305,8 @@ class UNetEngine:
                 ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=scale, shift=shift)
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
+        if self.fuse_bn_apply:
+            return self._block_bwd_fused(nm, G, S, P, sink, need_gx, small, gred, wgrad, side, main)
         gyb = bn_back(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
 
         def wgrad3():
@@ -340,6 +346,70 @@ class UNetEngine:
             wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
         gx = _e((N, H, W, X.c), dt, dev)
         ops.conv3x3_dgrad(ops.act(gya), wpt, ops.act(gx))
+        return gx
+
+    def _block_bwd_fused(self, nm, G, S, P, sink, need_gx, small, gred, wgrad, side, main):
+        """_block_bwd with each BN backward's apply fused into the data gradient that consumes it:
+        colsum -> (dbeta, dgamma) -> coefficient table; the dgrad stages gy = k1 g' + k2 y + k3 from
+        (g, y) and stores it for the weight gradient, which therefore follows its dgrad."""
+        p = f"{self.prefix}{nm}"
+        s = S[nm]
+        ya, yb, bna, bnb, X = s["ya"], s["yb"], s["bna"], s["bnb"], s["X"]
+        N, H, W, C = yb.shape
+        dev, dt = yb.device, self.dtype
+
+        def bn_coef(prefix, g, y, bn, part=None, tiles=0):
+            if part is None:  # reduction not fused into the producer of g
+                tiles = ops.bn_bwd_tiles(ops.act(y))
+                part = _e(tiles * 2 * C, torch.float32, dev)
+                ops.bn_bwd_reduce(ops.act(g), ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                                  bn["shift"], part)
+            dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
+            ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
+            coef = _e(4 * C, torch.float32, dev)
+            ops.bn_bwd_coef(bn["mean"], bn["invstd"], bn["scale"], bn["shift"], dbeta, dgamma, N * H * W, coef)
+            return coef
+
+        def packed(conv):
+            wpt = S["wp"].get(conv + ".weight^T") if S.get("wp") else None
+            return wpt if wpt is not None else ops.conv3x3_pack(P[conv + ".weight"], dt, flip=True)
+
+        coefb = bn_coef(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
+        gyb = torch.empty_like(yb)
+        gaa = torch.empty_like(ya)
+        ctiles = ops.conv3x3_tiles(ops.act(gaa))
+        cpart = _e(ctiles * 2 * C, torch.float32, dev)
+        ops.conv3x3_dgrad_fused(ops.act(G), ops.act(yb), coefb, ops.act(gyb), packed(p + ".3"), ops.act(gaa),
+                                ops.act(ya), bna["mean"], bna["invstd"], bna["scale"], bna["shift"], cpart)
+
+        def wgrad3():
+            if s.get("za") is not None:
+                wgrad(p + ".3", ops.act(s["za"]), gyb)
+            else:
+                wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
+        if not self.wg3_late:
+            wgrad3()
+        coefa = bn_coef(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
+        if self.wg3_late:
+            wgrad3()
+        del gyb
+        gya = torch.empty_like(ya)
+        gx = None
+        if need_gx:
+            gx = _e((N, H, W, X.c), dt, dev)
+            ops.conv3x3_dgrad_fused(ops.act(gaa), ops.act(ya), coefa, ops.act(gya), packed(p + ".0"), ops.act(gx))
+            wgrad(p + ".0", X, gya, small_conv=small)
+        else:  # the trunk's first conv has no data gradient: materialise gy for its weight gradient
+            ops.bn_bwd_apply_coef(ops.act(gaa), ops.act(ya), coefa, ops.act(gya))
+            wgrad(p + ".0", X, gya, small_conv=small, on_main=True)
+        del gaa, gya
+        names = [f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")]
+        if side is None:
+            sink.ready(names)
+        else:  # a bucket all-reduce launched here orders after both streams' work, without stalling main
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                sink.ready(names)
         return gx
 
     def backward(self, S, g_out: torch.Tensor, sink: Optional[GradSink] = None):

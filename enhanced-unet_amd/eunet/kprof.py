@@ -20,6 +20,8 @@ class KernelTimer:
     def __enter__(self):
         global _active
         _active = self
+        self.origin = torch.cuda.Event(enable_timing=True)  # common time origin for interval unions
+        self.origin.record()
         return self
 
     def __exit__(self, *exc):
@@ -34,6 +36,25 @@ class KernelTimer:
             out[fam] = dict(launches=len(recs), ms=ms, flops=sum(r[2] for r in recs),
                             bytes=sum(r[3] for r in recs))
         return out
+
+    def union_ms(self, families):
+        """Wall time (ms) during which at least one launch of `families` ran: the union of their
+        event intervals across streams (launches of one family on two streams overlap, so the
+        summed spans of summary() count shared time twice)."""
+        torch.cuda.synchronize()
+        iv = sorted((self.origin.elapsed_time(a), self.origin.elapsed_time(b))
+                    for fam in families for a, b, _, _ in self.records.get(fam, ()))
+        tot, cur0, cur1 = 0.0, None, None
+        for a, b in iv:
+            if cur1 is None or a > cur1:
+                if cur1 is not None:
+                    tot += cur1 - cur0
+                cur0, cur1 = a, b
+            else:
+                cur1 = max(cur1, b)
+        if cur1 is not None:
+            tot += cur1 - cur0
+        return tot
 
 
 _OFF = os.environ.get("EUNET_KPROF", "1") == "0"  # diagnostic: measure the event overhead itself

@@ -124,9 +124,28 @@ def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
     return s.value
 
 
+def conv3x3_dgrad_fused(g: Act, y_in: Act, coef, gy_out: Act | None, wp_t, gx: Act, y_next: Act | None = None,
+                        mean=None, invstd=None, scale=None, shift=None, part=None, gscale=None):
+    """Data gradient with the BN backward of the differentiated layer fused into the operand staging
+    (gy = coef-affine of (g, y_in), stored to gy_out for the weight gradient) and, optionally, the
+    reduction half of the next BN backward over gx (include/eunet.h)."""
+    flops = 2.0 * 9 * g.c * gx.c * g.n * g.h * g.w
+    esz = 2 if g.dtype == _lib.EUNET_BF16 else 4
+    # algorithmic HBM bytes: read g and y_in once, write gy_out and gx once, (read y_next), weights once
+    nbytes = float(esz * g.n * g.h * g.w * (2 * g.c + (g.c if gy_out is not None else 0) + gx.c +
+                                            (gx.c if y_next is not None else 0)) + wp_t.numel() * wp_t.element_size())
+    with kprof.timed("conv3x3_dgrad", flops, nbytes):
+        call("eunet_conv3x3_dgrad_fused", ctypes.byref(g), ctypes.byref(y_in), _ptr(coef), _ref(gy_out), _ptr(wp_t),
+             ctypes.byref(gx), _ref(y_next), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(part),
+             _ptr(gscale), _stream())
+
+
 def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=None, nstride=0):
     flops = 2.0 * 9 * x.c * dy.c * x.n * x.h * x.w
-    with kprof.timed("conv3x3_wgrad", flops):
+    esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
+    # algorithmic HBM bytes: read x and dy once, write the fp32 split partials of dW (and db) once
+    nbytes = float(esz * x.n * x.h * x.w * (x.c + dy.c) + 4 * nsplit * dy.c * (9 * x.c + 1))
+    with kprof.timed("conv3x3_wgrad", flops, nbytes):
         call("eunet_conv3x3_wgrad", ctypes.byref(x), _ptr(scale), _ptr(shift), int(nstride), ctypes.byref(dy),
              _ptr(dw_part),
              _ptr(db_part), nsplit, _stream())
@@ -259,6 +278,16 @@ def bn_bwd_apply(g: Act, y: Act, mean, invstd, scale, shift, dbeta, dgamma, gy: 
     """scale / shift: the BN's forward affine (they define the ReLU mask, see eunet.h)."""
     call("eunet_bn_bwd_apply", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale),
          _ptr(shift), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
+
+
+def bn_bwd_coef(mean, invstd, scale, shift, dbeta, dgamma, count: int, coef):
+    """coef [4][C] = (k1, kq, k2, k3) of gy = k1 g [y k1 + kq > 0] + k2 y + k3 (count = N*H*W)."""
+    call("eunet_bn_bwd_coef", _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(dbeta), _ptr(dgamma),
+         int(count), int(mean.numel()), _ptr(coef), _stream())
+
+
+def bn_bwd_apply_coef(g: Act, y: Act, coef, gy: Act):
+    call("eunet_bn_bwd_apply_coef", ctypes.byref(g), ctypes.byref(y), _ptr(coef), ctypes.byref(gy), _stream())
 
 
 def pool_bwd_add(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act):

@@ -91,6 +91,20 @@ int eunet_conv3x3_dgrad_bnbwd(const eunet_act* dy, const void* wp_t, const eunet
                               const eunet_act* y, const float* mean, const float* invstd,
                               const float* scale, const float* shift, const float* gscale,
                               float* part, void* stream);
+/* dgrad with the whole BatchNorm backward of the layer it differentiates fused in (autograd of
+ * models.py:219-224: conv -> BN -> ReLU; replaces bn_bwd_apply + dgrad).  g = gradient w.r.t. the
+ * BN+ReLU output, y_in = the BN's input (the conv output, same shape and channel layout as g),
+ * coef = eunet_bn_bwd_coef's [4][g.c] table; the operand staged for the MFMAs is
+ * gy = k1 g [y k1 + kq > 0] + k2 y + k3 (the forward's ReLU mask), rounded to the dtype exactly as
+ * eunet_bn_bwd_apply rounds it.  gy_out (nullable, g's layout) receives gy for the weight gradient
+ * (bf16: stored from the staging by the co-block-0 launches; fp32: a separate apply pass, gy_out
+ * then required).  y_next .. part (all or none): the reduction half of the NEXT BatchNorm backward
+ * over gx, as eunet_conv3x3_dgrad_bnbwd.  gscale as eunet_conv3x3_dgrad. */
+int eunet_conv3x3_dgrad_fused(const eunet_act* g, const eunet_act* y_in, const float* coef,
+                              const eunet_act* gy_out, const void* wp_t, const eunet_act* gx,
+                              const eunet_act* y_next, const float* mean, const float* invstd,
+                              const float* scale, const float* shift, float* part, const float* gscale,
+                              void* stream);
 /* plain dgrad (autograd of models.py:219,222 w.r.t. the conv input): gx = conv(dy, W') with
  * wp_t packed transpose_flip; gscale (nullable) [N][gx.c] scales gx per sample and channel */
 int eunet_conv3x3_dgrad(const eunet_act* dy, const void* wp_t, const eunet_act* gx, const float* gscale,
@@ -229,6 +243,15 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
                        const float* invstd, const float* scale, const float* shift,
                        const float* dbeta, const float* dgamma, const eunet_act* gy,
                        void* stream);
+/* BN-backward apply constants, coef [4][C] = (k1 = scale, kq = shift, k2, k3) with
+ * gy = k1 g' + k2 y + k3 (count = N*H*W, the BN's batch); the table the fused consumers
+ * (eunet_conv3x3_dgrad_fused) and eunet_bn_bwd_apply_coef read -- bit-identical to the constants
+ * eunet_bn_bwd_apply forms itself. */
+int eunet_bn_bwd_coef(const float* mean, const float* invstd, const float* scale, const float* shift,
+                      const float* dbeta, const float* dgamma, long long count, int C, float* coef,
+                      void* stream);
+int eunet_bn_bwd_apply_coef(const eunet_act* g, const eunet_act* y, const float* coef, const eunet_act* gy,
+                            void* stream);
 /* MaxPool2d backward (first max in row-major order wins, recomputed from the
  * saved activation) + the skip-path gradient: gout = gskip + scatter(gpool) */
 int eunet_pool_bwd_add(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,

@@ -149,3 +149,66 @@ def test_dp_nccl_world1_rccl_buckets():
     assert res["views"], "BN buffers must be views of the flat broadcast buffer"
     assert res["grads_equal"], "RCCL-averaged gradients (world 1) must equal the plain backward"
     assert res["same_step"], "Trainer steps with DataParallel(world 1) must equal the plain steps"
+
+
+def _nccl_cfg3_worker(port, q):
+    """BASELINE configs[3]'s per-rank workload (base 64, 1x1024^2, batch 4, bf16) through the RCCL
+    data-parallel path at world size 1: default 8 MiB buckets, weight gradients on the side stream
+    (the bench schedule), bucket all-reduces issued from the side stream inside the backward.  The
+    gradients and two Trainer steps must equal the plain (non-DP) run bit for bit."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "enhanced-unet_amd")]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        from eunet import synth
+        from eunet.dp import DataParallel
+        from eunet.engine import UNetEngine
+        from eunet.losses import combined_loss
+        from eunet.models import EnhancedUNet
+        from eunet.train_eval import Trainer
+        assert UNetEngine.overlap_wgrad, "the bench schedule runs the weight gradients on the side stream"
+        x, m = synth.batch(4, 1024, 1024, start_index=0, num_classes=2, in_channels=1, device="cuda")
+
+        def fresh():
+            torch.manual_seed(0)
+            return EnhancedUNet(num_classes=2, in_channels=1, base_ch=64, dtype="bf16").cuda().train()
+
+        ref = fresh()
+        combined_loss(ref.forward_lowres(x), m).backward()
+        model = fresh()
+        dp = DataParallel(model)  # default 8 MiB buckets
+        dp.before_forward()
+        combined_loss(model.forward_lowres(x), m).backward()
+        torch.cuda.synchronize()
+        grads_equal = all(torch.equal(p.grad, r.grad) for p, r in zip(model.parameters(), ref.parameters()))
+        ta, tb = Trainer(fresh(), "cuda", "enhanced_unet"), Trainer(fresh(), "cuda", "enhanced_unet")
+        ta.dp = DataParallel(ta.model)
+        la = [ta.step(x, m) for _ in range(2)]
+        lb = [tb.step(x, m) for _ in range(2)]
+        same_step = la == lb and all(torch.equal(a, b) for a, b in zip(ta.model.state_dict().values(),
+                                                                        tb.model.state_dict().values()))
+        q.put(dict(buckets=len(dp.buckets), mb=round(dp.flat.numel() * 4 / 2 ** 20, 2), grads_equal=grads_equal,
+                   same_step=same_step, losses=la))
+    except Exception as e:
+        q.put(dict(error=repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dp_nccl_world1_configs3_workload_bit_identical():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_cfg3_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=500)
+    p.join(timeout=120)
+    print("RCCL world-1 DP at configs[3] per-rank workload:", res)
+    assert "error" not in res, res
+    assert p.exitcode == 0
+    assert res["buckets"] == 4 and res["mb"] > 29, res  # 31 MB of gradients in 8 MiB buckets
+    assert res["grads_equal"], "DP gradients (world 1, RCCL) must equal the plain backward bit for bit"
+    assert res["same_step"], "two Trainer steps with DataParallel must equal the plain steps bit for bit"

@@ -270,3 +270,41 @@ def test_dual_base96_bf16_vs_autocast_reference():
     print("dual base96 bf16 relL2 ours", ours, "autocast", auto, "argmax agreement", agree)
     assert torch.isfinite(out).all()
     assert ours < max(2.0 * auto, 0.02), (ours, auto)
+
+
+def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
+    """bf16 whole-network gradient parity of the dual-branch model at base 96 (64^2, B 2, c 1, K 2,
+    deep supervision): every parameter gradient vs the fp64 oracle within
+    max(2 x the oracle-under-bf16-autocast error, 3e-2) relative L2
+    (test_gpu_model.test_bf16_train_grads_vs_fp64_oracle)."""
+    from eunet import synth
+    from eunet.train_eval import Trainer
+    x, msk = synth.batch(2, 64, 64, start_index=27, num_classes=2, in_channels=1)
+    keep = _keep96()
+    S, loss_ref = _oracle(96, 1, 2, x, msk, keep, torch.float64)
+    Sac = D.dual_formula_weights(96, 1, 2, dtype=torch.float32)
+    for k in Sac:
+        if Sac[k].is_floating_point() and "running" not in k:
+            Sac[k].requires_grad_(True)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        fused, aux = D.dual_forward(Sac, x, training=True, drop_masks=keep)
+    D.dual_batch_loss(fused.float(), {n: a.float() for n, a in aux.items()}, msk).backward()
+    m = _model(96, 1, 2, dtype="bf16", keep=keep).train()
+    tr = Trainer(m, DEV, "enhanced_unet")
+    out = m(x.to(DEV))
+    loss = tr.aux_loss(out, m.get_aux_outputs(), msk.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    scale = max(float(S[k].grad.abs().max()) for k in S if S[k].grad is not None)
+    rows = []
+    for k, p in m.named_parameters():
+        ref = S[k].grad
+        if k.startswith(BRANCHES) and k.endswith((".0.bias", ".3.bias")):
+            err, err_ac = float((p.grad.double().cpu() - ref).abs().max()), float((Sac[k].grad.double() - ref).abs().max())
+            assert err < max(2 * err_ac, 1e-3 * scale), (k, err, err_ac, scale)
+            continue
+        e, eac = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref)
+        rows.append((e / max(2 * eac, 3e-2), k, e, eac))
+    for r in sorted(rows, reverse=True)[:8]:
+        print("dual base96 bf16 grad (ratio, name, ours, autocast):", r)
+    assert all(r[0] < 1.0 for r in rows), sorted(rows, reverse=True)[:3]

@@ -757,3 +757,85 @@ def test_bnrelu_conv1x1_shapes(dt, C, K):
                        b.float().to(DEV), K, z)
     torch.cuda.synchronize()
     assert rel(z, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,C,Cx,nextbn,gs", [(2, 40, 70, 64, 192, False, False),  # 3 co-blocks, ragged
+                                                  (1, 64, 96, 128, 64, True, False),   # 4 K-chunks, next BN
+                                                  (2, 16, 32, 32, 96, True, True)])    # partial co-block, gscale
+def test_conv3x3_dgrad_fused_bn_apply_bit_exact(dt, N, H, W, C, Cx, nextbn, gs):
+    """eunet_conv3x3_dgrad_fused (the BN-backward apply in the dgrad's operand staging) against the
+    unfused path it replaces, bn_bwd_apply + conv3x3_dgrad(_bnbwd): the stored gy, gx and the next
+    BN's reduction rows agree bit for bit, and gy matches the fp64 formula."""
+    ops = _ops()
+    g0 = torch.Generator().manual_seed(31)
+    G = torch.randn(N, H, W, C, generator=g0).to(DEV, dt)
+    y = torch.randn(N, H, W, C, generator=g0).to(DEV, dt)
+    mean = (torch.randn(C, generator=g0) * 0.1).to(DEV)
+    invstd = (torch.rand(C, generator=g0) + 0.5).to(DEV)
+    gamma = torch.randn(C, generator=g0).to(DEV)
+    beta = torch.randn(C, generator=g0).to(DEV)
+    scale, shift = gamma * invstd, beta - mean * gamma * invstd
+    dbeta = torch.randn(C, generator=g0).to(DEV) * 100
+    dgamma = torch.randn(C, generator=g0).to(DEV) * 100
+    w = (torch.randn(C, Cx, 3, 3, generator=g0) / (3 * C ** 0.5)).to(DEV)  # conv Cx -> C (dgrad: C -> Cx)
+    wpt = ops.conv3x3_pack(w, dt, flip=True)
+    yn = torch.randn(N, H, W, Cx, generator=g0).to(DEV, dt) if nextbn else None
+    nb = [torch.randn(Cx, generator=g0).to(DEV) * 0.2 + o for o in (0.0, 1.0, 1.0, 0.0)] if nextbn else [None] * 4
+    gsc = (torch.rand(N, Cx, generator=g0) + 0.5).to(DEV) if gs else None
+    # unfused reference path
+    gy_ref = torch.empty_like(G)
+    ops.bn_bwd_apply(ops.act(G), ops.act(y), mean, invstd, scale, shift, dbeta, dgamma, ops.act(gy_ref))
+    gx_ref = torch.empty(N, H, W, Cx, dtype=dt, device=DEV)
+    tiles = ops.conv3x3_tiles(ops.act(gx_ref))
+    part_ref = torch.zeros(tiles * 2 * Cx, device=DEV) if nextbn else None
+    if nextbn:
+        ops.conv3x3_dgrad_bnbwd(ops.act(gy_ref), wpt, ops.act(gx_ref), ops.act(yn), *nb, part_ref, gscale=gsc)
+    else:
+        ops.conv3x3_dgrad(ops.act(gy_ref), wpt, ops.act(gx_ref), gscale=gsc)
+    # fused
+    coef = torch.empty(4 * C, device=DEV)
+    ops.bn_bwd_coef(mean, invstd, scale, shift, dbeta, dgamma, N * H * W, coef)
+    gy = torch.full_like(G, float("nan"))
+    gx = torch.empty_like(gx_ref)
+    part = torch.zeros_like(part_ref) if nextbn else None
+    ops.conv3x3_dgrad_fused(ops.act(G), ops.act(y), coef, ops.act(gy), wpt, ops.act(gx),
+                            ops.act(yn) if nextbn else None, *nb, part, gscale=gsc)
+    torch.cuda.synchronize()
+    assert torch.equal(gy, gy_ref), "gy stored by the fused staging must equal bn_bwd_apply's"
+    assert torch.equal(gx, gx_ref)
+    if nextbn:
+        assert torch.equal(part, part_ref)
+    # the formula itself (fp64): gy = scale (g' - dbeta/n - xhat dgamma/n)
+    gd, yd = G.double().cpu(), y.double().cpu()
+    n = N * H * W
+    mask = (yd * scale.double().cpu() + shift.double().cpu()) > 0
+    gp = torch.where(mask, gd, torch.zeros_like(gd))
+    xh = (yd - mean.double().cpu()) * invstd.double().cpu()
+    want = scale.double().cpu() * (gp - dbeta.double().cpu() / n - xh * dgamma.double().cpu() / n)
+    assert rel(gy, want) < TOL[dt]
+    # the apply with the coefficient table equals the standalone apply too
+    gy2 = torch.empty_like(G)
+    ops.bn_bwd_apply_coef(ops.act(G), ops.act(y), coef, ops.act(gy2))
+    torch.cuda.synchronize()
+    assert torch.equal(gy2, gy_ref)
+
+
+def test_conv3x3_dgrad_bf16_fp32_output():
+    """The bf16 data gradient with an fp32 output (the dual-branch gate's g_f2): the same fp32
+    accumulators stored without the bf16 rounding -- rounding them gives the bf16-output launch bit
+    for bit -- and within fp32 accuracy of the fp64 transposed convolution of the bf16 operands."""
+    ops = _ops()
+    g0 = torch.Generator().manual_seed(41)
+    N, H, W, C, Cx = 2, 40, 72, 256, 8
+    dy = torch.randn(N, H, W, C, generator=g0).to(DEV, torch.bfloat16)
+    w = (torch.randn(C, Cx, 3, 3, generator=g0) / 48).to(DEV)
+    wpt = ops.conv3x3_pack(w, torch.bfloat16, flip=True)
+    gb = torch.empty(N, H, W, Cx, dtype=torch.bfloat16, device=DEV)
+    gf = torch.empty(N, H, W, Cx, dtype=torch.float32, device=DEV)
+    ops.conv3x3_dgrad(ops.act(dy), wpt, ops.act(gb))
+    ops.conv3x3_dgrad(ops.act(dy), wpt, ops.act(gf))
+    torch.cuda.synchronize()
+    assert torch.equal(gf.to(torch.bfloat16), gb)
+    ref = nhwc(F.conv_transpose2d(nchw(dy.double().cpu()), w.to(torch.bfloat16).double().cpu(), padding=1))
+    assert rel(gf, ref) < 1e-5
