@@ -8,6 +8,8 @@
 
 #include <algorithm>
 
+EUNET_DEBUG_UNIT(bnpool)
+
 namespace {
 
 constexpr int NT = 256;
@@ -762,6 +764,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
       const float gg = fmaf(yf[j], kP[j], kQ[j]) > 0.f ? gf[j] : 0.f;
       o[j] = fmaf(k1[j], gg, fmaf(yf[j], k2[j], k3[j]));
     }
+    EUNET_DASSERT(p < P && oco + c + E <= oct && u < U);
     *(uint4*)(gy + p * oct + oco + c) = Vec16<TO>::pack(o);
   }
 }

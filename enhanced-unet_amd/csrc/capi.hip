@@ -23,7 +23,20 @@ int check_launch(const char* what) {
 }
 }  // namespace eunet
 
+EUNET_DEBUG_UNIT(capi)
+
+namespace eunet {
+#ifdef EUNET_DEBUG
+int debug_read_conv3x3(unsigned*, unsigned*, bool);
+int debug_read_bnpool(unsigned*, unsigned*, bool);
+int debug_read_head(unsigned*, unsigned*, bool);
+#endif
+}  // namespace eunet
+
 namespace {
+// a deliberately failing check (eunet_debug_selftest): proves the debug build's reporting path
+__global__ void debug_selftest_kernel(int n) { EUNET_DASSERT(threadIdx.x >= (unsigned)n); }
+
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* x, int N, int C, int H, int W, T* out, int ct, int co) {
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -43,6 +56,45 @@ extern "C" {
 const char* eunet_version(void) { return "eunet-mi355x 0.1 (gfx950)"; }
 
 const char* eunet_last_error(void) { return eunet::g_err; }
+
+int eunet_debug_enabled(void) {
+#ifdef EUNET_DEBUG
+  return 1;
+#else
+  return 0;
+#endif
+}
+
+int eunet_debug_status(unsigned* unit_line, unsigned* count, int reset) {
+  EUNET_REQUIRE(unit_line && count, "debug_status: null outputs");
+  *unit_line = 0;
+  *count = 0;
+#ifdef EUNET_DEBUG
+  if (hipDeviceSynchronize() != hipSuccess) {
+    eunet::set_error("debug_status: device synchronisation failed");
+    return EUNET_ERR_HIP;
+  }
+  int (*readers[4])(unsigned*, unsigned*, bool) = {eunet::debug_read_capi, eunet::debug_read_conv3x3,
+                                                   eunet::debug_read_bnpool, eunet::debug_read_head};
+  for (int u = 0; u < 4; ++u) {
+    unsigned line = 0, cnt = 0;
+    const int rc = readers[u](&line, &cnt, reset != 0);
+    if (rc != EUNET_OK) {
+      eunet::set_error("debug_status: reading unit %d failed", u);
+      return rc;
+    }
+    if (cnt && !*unit_line) *unit_line = (unsigned)(u + 1) * 100000u + line;
+    *count += cnt;
+  }
+#endif
+  return EUNET_OK;
+}
+
+int eunet_debug_selftest(void* stream) {
+  debug_selftest_kernel<<<1, 64, 0, (hipStream_t)stream>>>(1);
+  EUNET_LAUNCH_CHECK("debug_selftest");
+  return EUNET_OK;
+}
 
 int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream) {
   EUNET_REQUIRE(x && out && out->ptr && out->c > 0 && out->coff + out->c <= out->ctot, "nchw_to_nhwc: bad args");

@@ -46,6 +46,46 @@ int check_launch(const char* what);
   } while (0)
 
 // ---------------------------------------------------------------------------
+// bounds-checked debug build (make debug -> libeunet_hip_debug.so, -DEUNET_DEBUG).
+// EUNET_DASSERT(cond) in device code records the first failing source line of its translation
+// unit and counts failures in a per-TU device word (a vector atomic: no trap, the kernel runs on);
+// eunet_debug_status() reads every unit's words after a device synchronisation.  Release builds
+// compile the checks away.  Each .hip file that uses EUNET_DASSERT names itself once with
+// EUNET_DEBUG_UNIT(tag) at namespace scope.
+// ---------------------------------------------------------------------------
+#ifdef EUNET_DEBUG
+#define EUNET_DEBUG_UNIT(tag)                                                    \
+  __device__ unsigned g_eunet_dbg[2];                                            \
+  namespace eunet {                                                              \
+  int debug_read_##tag(unsigned* line, unsigned* count, bool reset) {            \
+    unsigned h[2] = {0u, 0u};                                                    \
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_eunet_dbg), sizeof(h)) != hipSuccess) \
+      return EUNET_ERR_HIP;                                                      \
+    *line = h[0];                                                                \
+    *count = h[1];                                                               \
+    if (reset) {                                                                 \
+      const unsigned z[2] = {0u, 0u};                                            \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(g_eunet_dbg), z, sizeof(z)) != hipSuccess) \
+        return EUNET_ERR_HIP;                                                    \
+    }                                                                            \
+    return EUNET_OK;                                                             \
+  }                                                                              \
+  }
+#define EUNET_DASSERT(cond)                                   \
+  do {                                                        \
+    if (!(cond)) {                                            \
+      atomicCAS(&g_eunet_dbg[0], 0u, (unsigned)__LINE__);     \
+      atomicAdd(&g_eunet_dbg[1], 1u);                         \
+    }                                                         \
+  } while (0)
+#else
+#define EUNET_DEBUG_UNIT(tag)
+#define EUNET_DASSERT(cond) \
+  do {                      \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------------------
 // element conversion
 // ---------------------------------------------------------------------------
 // x + x[lane ^ 16] / x + x[lane ^ 32] on every lane with the gfx950 permlane swaps (VALU, no

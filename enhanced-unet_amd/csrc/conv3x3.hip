@@ -31,6 +31,8 @@
 
 #include "common.h"
 
+EUNET_DEBUG_UNIT(conv3x3)
+
 namespace {
 
 constexpr int TH = 8, TW = 32;            // wgrad output tile (pixels)
@@ -153,6 +155,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int tile, cob;
   xcd_map(blockIdx.x, a.ntiles, a.cout_pad / BN, tile, cob);
+  EUNET_DASSERT(tile < a.ntiles && cob * BN < a.cout_pad && a.cout <= a.cout_pad);
   const int tpi = a.tx * a.ty;
   const int n = tile / tpi, trem = tile - n * tpi;
   const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
@@ -211,6 +214,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
+      // a staged unit lies inside its sample slice (or is padding, read as zeros)
+      EUNET_DASSERT(!cok || aoff[i] == FWD_OOB || aoff[i] + cadd + 16u <= slice_bytes);
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
       if constexpr (BTR)
         if (btr) ry[i] = __builtin_amdgcn_raw_buffer_load_b128(yr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
@@ -220,9 +225,11 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
       const int id = tid + i * FT;
-      if (!B_TAIL || id < B_UNITS)
-        rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
-            wr, (uint32_t)((((kc * 4 + id / (BN * 9)) * a.cout_pad + co0) * 9 + id % (BN * 9)) * 16), 0, 0);
+      if (!B_TAIL || id < B_UNITS) {
+        const uint32_t wo = (uint32_t)((((kc * 4 + id / (BN * 9)) * a.cout_pad + co0) * 9 + id % (BN * 9)) * 16);
+        EUNET_DASSERT(wo + 16u <= (uint32_t)(a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T)));
+        rb[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wo, 0, 0);
+      }
     }
   };
   // BN scale / shift of this thread's channel group, through descriptors too (no branch, so
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
             f[j] = ok ? fmaf(k1, gg, fmaf(yv[j], ak2[j >> 2][j & 3], ak3[j >> 2][j & 3])) : 0.f;
           }
           v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
+          EUNET_DASSERT(!(wgy && ((interior >> i) & 1u) && ok) || aoff[i] + (uint32_t)(kc * KC * (int)sizeof(T)) + 16u <= slice_bytes);
           if (wgy && ((interior >> i) & 1u))
             __builtin_amdgcn_raw_buffer_store_b128(v, gr, cok ? aoff[i] + (uint32_t)(kc * KC * (int)sizeof(T)) : FWD_OOB,
                                                    0, 0);
@@ -397,7 +405,12 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= FWD_LDS, "epilogue LDS");
   __syncthreads();  // all waves are done with the K loop's LDS
   if (a.stats != nullptr) {
-    float s[4];
+    // per wave: its rows' channel sums and M2 about the wave's own mean, both from the fp32
+    // accumulators (two register passes, lane sums by the permlane swaps); the 4 waves are then
+    // Chan-combined by 64 threads -- one barrier, one LDS round trip
+    const int nw = max(0, min(RPW, vh - RPW * wv)) * vw;  // valid pixels in this wave's rows
+    const float inv_nw = nw > 0 ? 1.f / (float)nw : 0.f;
+    float s1[4], s2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       float v = 0.f;
@@ -408,44 +421,42 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
           v += ok ? acc[mt][nt][i] : 0.f;
         }
-      s[nt] = xor32_sum(xor16_sum(v));
-    }
-    if (q == 0)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) red[wv * 64 + nt * 16 + li] = s[nt];
-    __syncthreads();
-    const float cnt = (float)(vh * vw);
-    float mb[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NCW; ++w) t += red[w * 64 + nt * 16 + li];
-      mb[nt] = t / cnt;
+      s1[nt] = xor32_sum(xor16_sum(v));
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
+      const float mw = s1[nt] * inv_nw;
       float v = 0.f;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
-          const float d = acc[mt][nt][i] - mb[nt];
+          const float d = acc[mt][nt][i] - mw;
           v += ok ? d * d : 0.f;
         }
-      s[nt] = xor32_sum(xor16_sum(v));
+      s2[nt] = xor32_sum(xor16_sum(v));
     }
     if (q == 0)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) red[NCW * 64 + wv * 64 + nt * 16 + li] = s[nt];
+      for (int nt = 0; nt < 4; ++nt) {
+        red[wv * 64 + nt * 16 + li] = s1[nt];
+        red[NCW * 64 + wv * 64 + nt * 16 + li] = s2[nt];
+      }
     __syncthreads();
+    const float cnt = (float)(vh * vw);
     if (tid < 64 && co0 + tid < a.cout) {
       float sum = 0.f, m2 = 0.f;
 #pragma unroll
+      for (int w = 0; w < NCW; ++w) sum += red[w * 64 + tid];
+      const float mean = sum / cnt;
+#pragma unroll
       for (int w = 0; w < NCW; ++w) {
-        sum += red[w * 64 + tid];
-        m2 += red[NCW * 64 + w * 64 + tid];
+        const int nwv = max(0, min(RPW, vh - RPW * w)) * vw;
+        if (nwv > 0) {
+          const float d = red[w * 64 + tid] / (float)nwv - mean;
+          m2 += red[NCW * 64 + w * 64 + tid] + (float)nwv * d * d;
+        }
       }
       a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
       a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
@@ -513,6 +524,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int e = 0; e < E; ++e) f[e] = sp[e];
         const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
+        EUNET_DASSERT(pix < (long long)a.N * a.H * a.W && co + E <= a.cout && a.yco + co + E <= a.yct);
         const uint4 packed = Vec16<T>::pack(f);
         if constexpr (sizeof(TO) == sizeof(T)) {
           *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
@@ -689,6 +701,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   const int co0 = cob * 64;
   const int t_begin = split * a.per_split;
   const int t_end = min(a.ntiles, t_begin + a.per_split);
+  EUNET_DASSERT(split < a.nsplit && co0 < a.cout && kc * KCW < a.cin && t_begin < a.ntiles);
   const int tpi = a.tx * a.ty;
   const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
   // this lane's dY read offset within a pixel row, less the 2ct units: wd_swz(pxa) is q4 ^ 4 (g & 1)
@@ -718,6 +731,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       const void* src = (yy < a.H && xx < a.W && co < a.cout)
                             ? (const void*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co)
                             : (const void*)&g_conv_zero;
+      EUNET_DASSERT(!(yy < a.H && xx < a.W && co < a.cout) || (n < a.N && a.dco + co + 8 <= a.dct));
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(Ds + j * 64 * 16), 16, 0, 0);
     }
@@ -734,6 +748,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       const void* src = (hp >= 0 && hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
                             ? (const void*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c)
                             : (const void*)&g_conv_zero;
+      EUNET_DASSERT(!(hp >= 0 && hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) ||
+                    (n < a.N && a.xco + c + 8 <= a.xct));
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(smem + j * 64 * 16), 16, 0, 0);
     }
@@ -847,7 +863,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int co = co0 + ct * 16 + g * 4 + e;
-        if (co < a.cout && ci < a.cin) out[((long long)co * 9 + t) * a.cin + ci] = acc[t][ct][e];
+        if (co < a.cout && ci < a.cin) {
+          EUNET_DASSERT(split < a.nsplit);
+          out[((long long)co * 9 + t) * a.cin + ci] = acc[t][ct][e];
+        }
       }
   if (a.db != nullptr && kc == 0) {
     float* dbred = (float*)smem;  // [32 pixel groups][64 co], over the finished tile stage

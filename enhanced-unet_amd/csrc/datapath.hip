@@ -118,6 +118,28 @@ __global__ __launch_bounds__(NT) void augment_kernel(uint8_t* img, long long n, 
   }
 }
 
+// dataset.py:225-257 with the live ratio read on the device: counts = eunet_semantic_counts of the
+// (flipped) mask, live_ratio = #live / (#live + #dead) (0.5 without cells, :227-229); alpha / beta =
+// random.uniform(a, b) = a + (b - a) u for the reference's ratio-dependent ranges, with u the
+// host's random.random() draw -- the same double the reference forms (its uniform() draws exactly
+// once in every branch), evaluated without FMA contraction as CPython does.  No host round trip.
+__device__ __forceinline__ double uniform_ab(double a, double b, double u) { return __dadd_rn(a, __dmul_rn(b - a, u)); }
+
+__global__ __launch_bounds__(NT) void augment_ratio_kernel(uint8_t* img, long long n, const long long* counts,
+                                                           int flags, double ua, double ub) {
+  const long long live = counts[3], dead = counts[6];  // counts[c][0] = #pixels of class c
+  const long long total = live + dead;
+  const double ratio = total > 0 ? (double)live / (double)total : 0.5;
+  const double alpha = ratio > 0.6 ? uniform_ab(0.8, 1.3, ua) : (ratio < 0.4 ? uniform_ab(0.6, 1.1, ua) : uniform_ab(0.7, 1.3, ua));
+  const double beta = ratio < 0.4 ? uniform_ab(-20.0, 40.0, ub) : uniform_ab(-30.0, 30.0, ub);
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    uint8_t v = img[i];
+    if (flags & 1) v = clip_u8((double)v * alpha);
+    if (flags & 2) v = clip_u8((double)v + beta);
+    img[i] = v;
+  }
+}
+
 // HWC uint8 -> CHW float32 / 255 (transforms.ToTensor), into out[c][h][w]
 __global__ __launch_bounds__(NT) void to_tensor_kernel(const uint8_t* img, int h, int w, int c, float* out) {
   const long long hw = (long long)h * w, total = hw * c;
@@ -195,6 +217,14 @@ int eunet_augment_u8(uint8_t* img, long long n, int flags, double alpha, double 
   EUNET_REQUIRE(img && n > 0 && (!(flags & 4) || noise) && (!(flags & 8) || lut), "augment_u8: bad args");
   augment_kernel<<<grid1(n), NT, 0, (hipStream_t)stream>>>(img, n, flags, alpha, beta, noise, lut);
   EUNET_LAUNCH_CHECK("augment_u8");
+  return EUNET_OK;
+}
+
+int eunet_augment_ratio_u8(uint8_t* img, long long n, const long long* counts, int flags, double u_alpha,
+                           double u_beta, void* stream) {
+  EUNET_REQUIRE(img && n > 0 && counts && (flags & ~3) == 0, "augment_ratio_u8: bad args");
+  augment_ratio_kernel<<<grid1(n), NT, 0, (hipStream_t)stream>>>(img, n, counts, flags, u_alpha, u_beta);
+  EUNET_LAUNCH_CHECK("augment_ratio_u8");
   return EUNET_OK;
 }
 

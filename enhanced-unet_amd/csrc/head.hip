@@ -18,6 +18,8 @@
 //         upsample adjoint g_u -> g_z.
 #include "common.h"
 
+EUNET_DEBUG_UNIT(head)
+
 namespace {
 constexpr int NT = 256;
 constexpr int T2 = 16;  // tile side at 2H
@@ -1256,6 +1258,8 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
 #pragma unroll
           for (int k = 0; k < K; ++k) pv[k] = fmaf(wyv, hxs[(rr * 10 + px) * 3 + k], pv[k]);
         }
+#pragma unroll
+      EUNET_DASSERT(tile < a.ntiles && tid < 100);
 #pragma unroll
       for (int k = 0; k < K; ++k) a.patch[((long long)tile * 100 + tid) * K + k] = pv[k];
     }

@@ -114,6 +114,7 @@ SIGNATURES = {
     "eunet_rasterize_instances": [_f, _f, c_int, c_int, c_int, c_int, c_int, _f, c_void_p],
     "eunet_flip_u8": [_f, _f, c_int, c_int, c_int, c_int, c_void_p],
     "eunet_flip_mask": [_f, _f, c_int, c_int, c_int, c_void_p],
+    "eunet_augment_ratio_u8": [_f, c_int64, _f, c_int, ctypes.c_double, ctypes.c_double, c_void_p],
     "eunet_augment_u8": [_f, c_int64, c_int, ctypes.c_double, ctypes.c_double, _f, _f, c_void_p],
     "eunet_to_tensor": [_f, c_int, c_int, c_int, _f, c_void_p],
     "eunet_resize_u8": [_f, c_int, c_int, c_int, _f, c_int, c_int, c_void_p],
@@ -130,6 +131,9 @@ SIGNATURES = {
     "eunet_cell_mix_u8": [_f, _f, _f, _f, _f, c_int64, _f, c_void_p],
     "eunet_chw_to_u8_workspace_bytes": [c_int, c_int, c_int, POINTER(ctypes.c_size_t)],
     "eunet_chw_to_u8": [_f, c_int, c_int, c_int, _f, _f, c_void_p],
+    "eunet_debug_enabled": [],
+    "eunet_debug_status": [POINTER(ctypes.c_uint), POINTER(ctypes.c_uint), c_int],
+    "eunet_debug_selftest": [c_void_p],
     "eunet_consistency_tiles": [c_int, c_int, POINTER(c_int)],
     "eunet_consistency_fwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, c_void_p],
     "eunet_consistency_bwd": [_f, _f, _f, c_int, c_int, c_int, c_int, c_float, c_float, _f, _f, _f, _f,
@@ -181,6 +185,18 @@ def exported_symbols():
 
 def version() -> str:
     return load().eunet_version().decode()
+
+
+DEBUG_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libeunet_hip_debug.so")
+
+
+def debug_status(reset: bool = False):
+    """(unit * 100000 + line of the first failed device check, failed-check count) of the loaded
+    library; (0, 0) in the release build (eunet_debug_enabled() == 0), where checks compile away."""
+    lib = load()
+    line, cnt = ctypes.c_uint(0), ctypes.c_uint(0)
+    call("eunet_debug_status", ctypes.byref(line), ctypes.byref(cnt), 1 if reset else 0)
+    return int(line.value), int(cnt.value)
 
 
 __all__ = ["Act", "LossParams", "load", "call", "EunetError", "EUNET_F32", "EUNET_BF16", "exported_symbols",

@@ -18,12 +18,24 @@ PIL on the host (I/O).
 cv2 is absent from this image: cv2.fillPoly, cv2.resize and the cv2 colour / CLAHE / filter
 calls are replaced by kernels that follow OpenCV's documented algorithms, pinned to the
 numpy restatement in oracle/imgproc_ref.py, not to cv2 (parity unpinned).
+
+Feeding the GPU (round 3): a sample makes no host round trip -- host arrays reach the device
+through pinned staging buffers (ops.upload), the live ratio that selects the brightness /
+contrast ranges is read on the device (eunet_augment_ratio_u8: the host draws the same
+random.random() values random.uniform would), and the Gaussian noise is drawn on the device
+(host_noise=True keeps the reference's numpy draw: np.random.normal, bit-exact values, one host
+sync).  DataLoader(workers=W, prefetch=P) decodes JPEG + JSON in W threads and runs the device
+part of the next P batches on a side stream while the trainer consumes the current one; the
+Python `random` draws stay in item order (one producer thread).
 """
 from __future__ import annotations
 
 import json
 import os
+import queue
 import random
+import threading
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -69,10 +81,18 @@ def load_labelme(json_path: str, scale_h: float, scale_w: float):
 
 class CellDataset:
     def __init__(self, data_dir: str, split: str = "train", transform=None, max_size: int = 1024,
-                 device: str = "cuda", cell_preprocess: bool = True):
+                 device: str = "cuda", cell_preprocess: bool = True, host_noise: bool = False,
+                 host_ratio: bool = False):
         self.data_dir, self.split, self.transform, self.max_size = data_dir, split, transform, max_size
         self.device = device
         self.cell_preprocess = cell_preprocess  # dataset.py:204 (always on in the reference)
+        # host_noise: the reference's np.random.normal noise (exact values; a host draw of 3 H W
+        # normals + one synchronising copy per noisy sample); default: drawn on the device from a
+        # generator seeded by one np.random draw (same Python `random` decisions, other noise values)
+        self.host_noise = host_noise
+        # host_ratio: read the live ratio back to the host (round 2's path; one sync per sample)
+        self.host_ratio = host_ratio
+        self._noise_gen = None
         all_files = sorted(f for f in os.listdir(data_dir) if f.endswith(".jpg"))
         n_total = len(all_files)
         n_train, n_val = int(n_total * 0.7), int(n_total * 0.15)
@@ -108,30 +128,41 @@ class CellDataset:
         if random.random() > 0.5:
             img, mask = ops.flip_u8(img, 0), ops.flip_mask(mask, 0)
             flip_v = True
-        c = ops.semantic_counts(mask.reshape(1, -1), mask.reshape(1, -1))[0, :, 0].tolist()  # #pixels per class
-        total = c[1] + c[2]
-        live_ratio = c[1] / total if total > 0 else 0.5
-        if random.random() > 0.3:
-            if live_ratio > 0.6:
-                alpha = random.uniform(0.8, 1.3)
-            elif live_ratio < 0.4:
-                alpha = random.uniform(0.6, 1.1)
-            else:
-                alpha = random.uniform(0.7, 1.3)
-            ops.augment_u8(img, alpha=alpha)
-        if random.random() > 0.3:
-            beta = random.uniform(-20, 40) if live_ratio < 0.4 else random.uniform(-30, 30)
-            ops.augment_u8(img, beta=beta)
+        counts = ops.semantic_counts(mask.reshape(1, -1), mask.reshape(1, -1))  # [1][class][0] = #pixels
+        if self.host_ratio:
+            c = counts[0, :, 0].tolist()
+            total = c[1] + c[2]
+            live_ratio = c[1] / total if total > 0 else 0.5
+            if random.random() > 0.3:
+                if live_ratio > 0.6:
+                    alpha = random.uniform(0.8, 1.3)
+                elif live_ratio < 0.4:
+                    alpha = random.uniform(0.6, 1.1)
+                else:
+                    alpha = random.uniform(0.7, 1.3)
+                ops.augment_u8(img, alpha=alpha)
+            if random.random() > 0.3:
+                beta = random.uniform(-20, 40) if live_ratio < 0.4 else random.uniform(-30, 30)
+                ops.augment_u8(img, beta=beta)
+        else:
+            # every branch of the reference draws one uniform = a + (b - a) random.random(): draw
+            # that random() here, let the device pick (a, b) from its own live ratio
+            ua = random.random() if random.random() > 0.3 else None
+            ub = random.random() if random.random() > 0.3 else None
+            ops.augment_ratio_u8(img, counts, ua, ub)
         if random.random() > 0.5:  # HSV saturation (:259-264)
             ops.hsv_adjust_u8(img, sat=random.uniform(0.8, 1.3))
         if random.random() > 0.4:  # CLAHE on L (:267-272)
             img = ops.clahe_rgb_u8(img, random.uniform(1.5, 3.0))
         if random.random() > 0.5:
             sigma = random.uniform(3, 10)
-            noise = np.random.normal(0, sigma, tuple(img.shape)).astype(np.float32)
-            ops.augment_u8(img, noise=torch.from_numpy(noise).to(img.device))
+            if self.host_noise:
+                noise = np.random.normal(0, sigma, tuple(img.shape)).astype(np.float32)
+                ops.augment_u8(img, noise=torch.from_numpy(noise).to(img.device))
+            else:
+                ops.augment_u8(img, noise=self._device_noise(sigma, tuple(img.shape), img.device))
         if random.random() > 0.5:
-            lut = torch.from_numpy(gamma_lut(random.uniform(0.7, 1.3))).to(img.device)
+            lut = ops.upload(gamma_lut(random.uniform(0.7, 1.3)), img.device)
             ops.augment_u8(img, lut=lut)
         if random.random() > 0.6:  # sharpening (:287-292)
             img = ops.sharpen_u8(img, random.uniform(0.1, 0.3))
@@ -140,17 +171,36 @@ class CellDataset:
             ops.hsv_adjust_u8(img, hue=hue, val=random.uniform(0.9, 1.1))
         return img, mask, (flip_h, flip_v)
 
-    def __getitem__(self, idx):
+    def _device_noise(self, sigma, shape, device):
+        """N(0, sigma) float32 noise drawn on the device; the generator is reseeded from one
+        np.random draw per use, so np.random.seed still makes a run reproducible."""
+        if self._noise_gen is None:
+            self._noise_gen = torch.Generator(device=device)
+        self._noise_gen.manual_seed(int(np.random.randint(0, 2 ** 62, dtype=np.int64)))
+        return torch.normal(0.0, float(sigma), shape, generator=self._noise_gen, device=device)
+
+    def load_host(self, idx):
+        """The host half of __getitem__ (thread-safe, no GPU work, no random draws): the decoded
+        image, the reference's target size and the scaled LabelMe polygons."""
         from PIL import Image
         name = self.files[idx]
         image = np.array(Image.open(os.path.join(self.data_dir, name)).convert("RGB"))
         original_size = image.shape[:2]
-        img = torch.from_numpy(image).to(self.device)
         h, w = reference_sizes(*original_size, self.max_size)
-        if (h, w) != tuple(original_size):
-            img = ops.resize_u8(img, h, w)
         polys, labels, bboxes = load_labelme(os.path.join(self.data_dir, name.replace(".jpg", ".json")),
                                              h / original_size[0], w / original_size[1])
+        return name, image, original_size, (h, w), polys, labels, bboxes
+
+    def __getitem__(self, idx):
+        return self.from_host(self.load_host(idx))
+
+    def from_host(self, host):
+        """The device half of __getitem__ (enqueued on the current stream, no host synchronisation
+        unless host_noise / host_ratio)."""
+        name, image, original_size, (h, w), polys, labels, bboxes = host
+        img = ops.upload(image, self.device)
+        if (h, w) != tuple(original_size):
+            img = ops.resize_u8(img, h, w)
         mask = ops.rasterize_polygons(polys, [l + 1 for l in labels], h, w, img.device)
         if self.cell_preprocess:
             img = self._apply_cell_specific_preprocessing(img.contiguous(), polys, labels)
@@ -170,14 +220,46 @@ def collate_fn(batch):
 
 
 class DataLoader:
-    """Minimal in-order / shuffled batch iterator over a CellDataset (num_workers=0 like the
-    reference's train_model loaders, train_eval.py:1073-1077)."""
+    """In-order / shuffled batch iterator over a CellDataset (the reference's train_model loaders,
+    train_eval.py:1071-1075, run with num_workers=0).
 
-    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, collate_fn=collate_fn):
+    workers > 0: JPEG decode + JSON parsing (CellDataset.load_host) in a thread pool, ahead of use.
+    prefetch > 0: one producer thread builds the next `prefetch` batches' device data on a side
+    stream while the caller consumes the current batch; the caller's stream waits on each batch's
+    event (no host synchronisation) and its tensors are recorded on that stream.  The augmentation
+    draws from Python's `random` stay in item order (one producer), so a seeded run takes the same
+    decisions either way.  Datasets without load_host / from_host run in the loop."""
+
+    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, collate_fn=collate_fn,
+                 workers: int = 0, prefetch: int = 0):
         self.dataset, self.batch_size, self.shuffle, self.collate_fn = dataset, batch_size, shuffle, collate_fn
+        self.workers, self.prefetch = workers, prefetch
+        self._pool = None
 
     def __len__(self):
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def _batches(self, idx):
+        ds = self.dataset
+        split = hasattr(ds, "load_host") and hasattr(ds, "from_host")
+        if self.workers > 0 and split:
+            if self._pool is None:
+                self._pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="eunet-decode")
+            ahead = max(2 * self.workers, self.batch_size * (self.prefetch + 1))
+            futs = [self._pool.submit(ds.load_host, j) for j in idx[:ahead]]
+            nxt = len(futs)
+            for i in range(0, len(idx), self.batch_size):
+                items = []
+                for k in range(i, min(i + self.batch_size, len(idx))):
+                    items.append(ds.from_host(futs[k].result()))
+                    futs[k] = None
+                    if nxt < len(idx):
+                        futs.append(self._pool.submit(ds.load_host, idx[nxt]))
+                        nxt += 1
+                yield self.collate_fn(items)
+        else:
+            for i in range(0, len(idx), self.batch_size):
+                yield self.collate_fn([ds[j] for j in idx[i:i + self.batch_size]])
 
     def __iter__(self):
         n = len(self.dataset)
@@ -194,5 +276,62 @@ class DataLoader:
             idx = torch.randperm(n, generator=gen).tolist()
         else:
             idx = list(range(n))
-        for i in range(0, len(idx), self.batch_size):
-            yield self.collate_fn([self.dataset[j] for j in idx[i:i + self.batch_size]])
+        if self.prefetch <= 0 or not torch.cuda.is_available():
+            yield from self._batches(idx)
+            return
+        yield from self._prefetched(idx)
+
+    def _prefetched(self, idx):
+        consumer = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=consumer.device)
+        q = queue.Queue(maxsize=self.prefetch)
+        stop = threading.Event()
+
+        def produce():
+            try:
+                with torch.cuda.stream(side):
+                    for b in self._batches(idx):
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                        while not stop.is_set():
+                            try:
+                                q.put((b, ev), timeout=0.1)
+                                break
+                            except queue.Full:
+                                continue
+                        if stop.is_set():
+                            return
+                q.put(None)
+            except BaseException as e:  # surfaced in the consumer
+                q.put(e)
+
+        th = threading.Thread(target=produce, name="eunet-prefetch", daemon=True)
+        th.start()
+        try:
+            while True:
+                got = q.get()
+                if got is None:
+                    break
+                if isinstance(got, BaseException):
+                    raise got
+                b, ev = got
+                consumer.wait_event(ev)
+                _record(b, consumer)
+                yield b
+        finally:
+            stop.set()
+            th.join()
+
+
+def _record(obj, stream):
+    """record_stream every device tensor of a batch on the consuming stream (the caching allocator
+    must not reuse their blocks while that stream still reads them)."""
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            obj.record_stream(stream)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _record(v, stream)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _record(v, stream)

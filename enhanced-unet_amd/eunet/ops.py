@@ -474,6 +474,24 @@ def consistency_bwd(fused, b0, b1, c0, c1, gloss, gfused, g0, g1):
 
 
 # ---- device-side data path (datapath.hip) ---------------------------------------------
+def upload(a, device):
+    """Host numpy array -> device tensor without a host synchronisation: staged through the
+    caching pinned-memory allocator and copied asynchronously on the current stream (a pageable
+    copy would wait for the stream to drain first)."""
+    import numpy as np
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if torch.device(device).type != "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
+def _poly_arrays(polys):
+    import numpy as np
+    pts = np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in polys])
+    off = np.concatenate([[0], np.cumsum([len(p) for p in polys])]).astype(np.int32)
+    return pts, off
+
+
 def rasterize_polygons(polys, labels, h, w, device):
     """polys: list of int32 [n_i, 2] (x, y) arrays; labels: ints (1 live, 2 dead) -> int64 [h, w]."""
     mask = torch.empty(h, w, dtype=torch.int64, device=device)
@@ -481,9 +499,8 @@ def rasterize_polygons(polys, labels, h, w, device):
         call("eunet_rasterize_polygons", None, None, None, 0, h, w, _ptr(mask), _stream())
         return mask
     import numpy as np
-    pts = torch.from_numpy(np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in polys])).to(device)
-    off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in polys])]).astype(np.int32), device=device)
-    lab = torch.tensor(np.asarray(labels, np.int32), device=device)
+    pts_h, off_h = _poly_arrays(polys)
+    pts, off, lab = upload(pts_h, device), upload(off_h, device), upload(np.asarray(labels, np.int32), device)
     call("eunet_rasterize_polygons", _ptr(pts), _ptr(off), _ptr(lab), len(polys), h, w, _ptr(mask), _stream())
     return mask
 
@@ -492,9 +509,8 @@ def rasterize_instances(polys, h, w, device, flip_h: bool = False, flip_v: bool 
     """One uint8 [h, w] mask per polygon (stacked [n, h, w]), mirrored by the training flips."""
     if not polys:
         return torch.zeros(0, h, w, dtype=torch.uint8, device=device)
-    import numpy as np
-    pts = torch.from_numpy(np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in polys])).to(device)
-    off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in polys])]).astype(np.int32), device=device)
+    pts_h, off_h = _poly_arrays(polys)
+    pts, off = upload(pts_h, device), upload(off_h, device)
     masks = torch.empty(len(polys), h, w, dtype=torch.uint8, device=device)
     call("eunet_rasterize_instances", _ptr(pts), _ptr(off), len(polys), h, w, int(flip_h), int(flip_v), _ptr(masks),
          _stream())
@@ -521,6 +537,16 @@ def augment_u8(img, alpha=None, beta=None, noise=None, lut=None):
         (4 if noise is not None else 0) | (8 if lut is not None else 0)
     call("eunet_augment_u8", _ptr(img), img.numel(), flags, float(alpha or 0.0), float(beta or 0.0),
          _ptr(noise), _ptr(lut), _stream())
+    return img
+
+
+def augment_ratio_u8(img, counts, u_alpha=None, u_beta=None):
+    """In place: the reference's live-ratio-dependent brightness / contrast (dataset.py:225-257) with
+    the ratio read from device counts (semantic_counts) and u_* the host's random.random() draws."""
+    flags = (1 if u_alpha is not None else 0) | (2 if u_beta is not None else 0)
+    if flags:
+        call("eunet_augment_ratio_u8", _ptr(img), img.numel(), _ptr(counts), flags,
+             0.0 if u_alpha is None else float(u_alpha), 0.0 if u_beta is None else float(u_beta), _stream())
     return img
 
 

@@ -243,6 +243,16 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
                        const float* invstd, const float* scale, const float* shift,
                        const float* dbeta, const float* dgamma, const eunet_act* gy,
                        void* stream);
+/* Bounds-checked debug build (make -C enhanced-unet_amd debug -> libeunet_hip_debug.so, compiled with
+ * -DEUNET_DEBUG): device-side checks on staging offsets, tile / split / block indices
+ * and output addresses record the first failing check per source unit without trapping.
+ * eunet_debug_enabled: 1 in the debug build, 0 in the release library (where the checks compile away).
+ * eunet_debug_status: synchronises the device; *count = failed checks since the last reset,
+ * *unit_line = unit * 100000 + source line of the first (units: 1 capi, 2 conv3x3, 3 bn_pool_up,
+ * 4 head; 0 = none).  eunet_debug_selftest launches one deliberately failing check (capi unit). */
+int eunet_debug_enabled(void);
+int eunet_debug_status(unsigned* unit_line, unsigned* count, int reset);
+int eunet_debug_selftest(void* stream);
 /* BN-backward apply constants, coef [4][C] = (k1 = scale, kq = shift, k2, k3) with
  * gy = k1 g' + k2 y + k3 (count = N*H*W, the BN's batch); the table the fused consumers
  * (eunet_conv3x3_dgrad_fused) and eunet_bn_bwd_apply_coef read -- bit-identical to the constants
@@ -398,6 +408,12 @@ int eunet_flip_mask(const int64_t* src, int64_t* dst, int h, int w, int mode, vo
  * bit3 gamma LUT[256] (:273-276) */
 int eunet_augment_u8(uint8_t* img, long long n, int flags, double alpha, double beta,
                      const float* noise, const uint8_t* lut, void* stream);
+/* dataset.py:225-257 without the host round trip for the live ratio: counts = the [3][3]
+ * eunet_semantic_counts of the (flipped) semantic mask (device); flags bit 0 brightness, bit 1
+ * contrast; u_alpha / u_beta = the random.random() draws that random.uniform(a, b) = a + (b-a) u
+ * would have made in the reference's ratio-dependent branches (one draw in every branch). */
+int eunet_augment_ratio_u8(uint8_t* img, long long n, const long long* counts, int flags, double u_alpha,
+                           double u_beta, void* stream);
 /* transforms.ToTensor (dataset.py:302-305): HWC uint8 -> CHW float32 / 255 */
 int eunet_to_tensor(const uint8_t* img, int h, int w, int c, float* out, void* stream);
 /* bilinear uint8 resize with cv2 INTER_LINEAR's half-pixel mapping (dataset.py:145-157);

@@ -134,3 +134,62 @@ def test_instance_masks_follow_the_flips(tmp_path):
     polys, labels, _ = load_labelme(str(tmp_path / "i07.json"), h / 100, w / 130)
     ref = O.rasterize(polys, [l + 1 for l in labels], h, w)
     assert np.array_equal(val["semantic_mask"].cpu().numpy(), ref)
+
+
+def _write_cells(tmp_path, n=12, h=100, w=130, seed=7):
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    for i in range(n):
+        im = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        Image.fromarray(im).save(tmp_path / f"c{i:02d}.jpg", quality=95)
+        k = int(rng.integers(1, 4))
+        shapes = [{"label": "live", "points": [[10, 10], [40, 12], [35, 40], [12, 35]]},
+                  {"label": "dead", "points": [[60, 50], [90, 55], [70, 80]]},
+                  {"label": "live", "points": [[80, 10], [120, 14], [110, 40]]}][:k]
+        if i % 4 == 3:  # dead-dominated (live ratio < 0.4) and cell-free (ratio 0.5) items
+            shapes = [{"label": "dead", "points": [[5, 5], [120, 8], [115, 90], [8, 85]]},
+                      {"label": "live", "points": [[50, 40], [60, 40], [55, 50]]}]
+        if i % 6 == 5:
+            shapes = []
+        (tmp_path / f"c{i:02d}.json").write_text(json.dumps({"shapes": shapes}))
+
+
+def test_sync_free_augmentation_matches_host_ratio(tmp_path):
+    """The live ratio read on the device (eunet_augment_ratio_u8, the host drawing the same
+    random.random() values random.uniform would) gives the same images as round 2's host read-back
+    (dataset.py:225-257), for seeds that reach every ratio branch; the noise is the reference's
+    numpy draw here (host_noise=True), so the whole item is compared bit for bit."""
+    from eunet.data import CellDataset
+    _write_cells(tmp_path)
+    a = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV, host_noise=True, host_ratio=True)
+    b = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV, host_noise=True, host_ratio=False)
+    for seed in range(6):
+        for idx in range(len(a)):
+            out = []
+            for ds in (a, b):
+                random.seed(seed)
+                np.random.seed(seed)
+                out.append(ds[idx])
+            assert torch.equal(out[0]["image"], out[1]["image"]), (seed, idx)
+            assert torch.equal(out[0]["semantic_mask"], out[1]["semantic_mask"]), (seed, idx)
+
+
+def test_prefetching_loader_same_batches(tmp_path):
+    """DataLoader(workers=3, prefetch=2) -- host decode threads, device work of the next batches on
+    a side stream -- yields the batches the plain loop yields for the same seeds (device noise
+    included: its generator is reseeded from np.random in item order)."""
+    from eunet.data import CellDataset, DataLoader
+    _write_cells(tmp_path, n=14)
+    ds = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV)
+    runs = []
+    for workers, prefetch in ((0, 0), (3, 2)):
+        random.seed(3)
+        np.random.seed(3)
+        torch.manual_seed(3)
+        got = [(b["images"].clone(), torch.stack([it["semantic_mask"] for it in b["batch_items"]]).clone())
+               for b in DataLoader(ds, batch_size=2, shuffle=True, workers=workers, prefetch=prefetch)]
+        torch.cuda.synchronize()
+        runs.append(got)
+    assert len(runs[0]) == len(runs[1]) == 5
+    for (xa, ma), (xb, mb) in zip(*runs):
+        assert torch.equal(xa, xb) and torch.equal(ma, mb)
