@@ -728,7 +728,7 @@ __global__ void bn_bwd_coef_kernel(const float* mean, const float* istd, const f
   coef[3 * C + c] = k.k3;
 }
 
-template <typename T, typename TO>
+template <typename T, typename TO, bool COEF = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, int gco, const T* y, int yct, int yco,
                                                            long long P, int C, const float* mean, const float* istd,
                                                            const float* scale, const float* shift, const float* dbeta,
@@ -741,11 +741,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   float kP[E], kQ[E], k1[E], k2[E], k3[E];
 #pragma unroll
   for (int j = 0; j < E; ++j) {
-    // coef: the table eunet_bn_bwd_coef wrote (the same bn_bwd_coef values)
-    const BnBwdCoef k = coef != nullptr
-                            ? BnBwdCoef{coef[c + j], coef[C + c + j], coef[2 * C + c + j], coef[3 * C + c + j]}
-                            : bn_bwd_coef(mean[c + j], istd[c + j], scale[c + j], shift[c + j], dbeta[c + j],
-                                          dgamma[c + j], inv_n);
+    // COEF: the table eunet_bn_bwd_coef wrote (the same bn_bwd_coef values).  A compile-time choice:
+    // with a runtime one the kernel held both paths' registers and ran 35 % slower (2.61 vs
+    // 1.93 ms/step over its 14 launches, same-box rocprofv3)
+    BnBwdCoef k;
+    if constexpr (COEF)
+      k = BnBwdCoef{coef[c + j], coef[C + c + j], coef[2 * C + c + j], coef[3 * C + c + j]};
+    else
+      k = bn_bwd_coef(mean[c + j], istd[c + j], scale[c + j], shift[c + j], dbeta[c + j], dgamma[c + j], inv_n);
     kP[j] = k.k1;
     kQ[j] = k.kq;
     k1[j] = k.k1;
@@ -1535,14 +1538,18 @@ static int bn_bwd_apply_launch(const eunet_act* g, const eunet_act* y, const flo
   const int bs = (256 / U) * U;
   const long long nb = (P * U + bs - 1) / bs;
   const unsigned gr = (unsigned)(nb < 4096 ? nb : 4096);
-  if (y->dtype == EUNET_BF16)
-    bn_bwd_apply_kernel<bf16_t, bf16_t><<<gr, bs, 0, (hipStream_t)stream>>>(
-        (const bf16_t*)g->ptr, g->ctot, g->coff, (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        scale, shift, dbeta, dgamma, (bf16_t*)gy->ptr, gy->ctot, gy->coff, coef);
-  else
-    bn_bwd_apply_kernel<float, float><<<gr, bs, 0, (hipStream_t)stream>>>(
-        (const float*)g->ptr, g->ctot, g->coff, (const float*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd,
-        scale, shift, dbeta, dgamma, (float*)gy->ptr, gy->ctot, gy->coff, coef);
+#define EUNET_APPLY_LAUNCH(TT, CF)                                                                              \
+  bn_bwd_apply_kernel<TT, TT, CF><<<gr, bs, 0, (hipStream_t)stream>>>(                                        \
+      (const TT*)g->ptr, g->ctot, g->coff, (const TT*)y->ptr, y->ctot, y->coff, P, y->c, mean, invstd, scale, \
+      shift, dbeta, dgamma, (TT*)gy->ptr, gy->ctot, gy->coff, coef)
+  if (y->dtype == EUNET_BF16) {
+    if (coef) EUNET_APPLY_LAUNCH(bf16_t, true);
+    else EUNET_APPLY_LAUNCH(bf16_t, false);
+  } else {
+    if (coef) EUNET_APPLY_LAUNCH(float, true);
+    else EUNET_APPLY_LAUNCH(float, false);
+  }
+#undef EUNET_APPLY_LAUNCH
   EUNET_LAUNCH_CHECK("bn_bwd_apply");
   return EUNET_OK;
 }

@@ -141,7 +141,9 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 // rocprofv3 and the bench report forward and data-gradient launches separately.
 // TO: the output element type -- T, or float for a bf16 data gradient whose consumer keeps fp32
 // (the dual-branch gate backward reads the 2K-channel g_f2 in fp32; no fused BN reduction then)
-template <typename T, bool DG, typename TO = T>
+// BT: the dgrad with the BN-backward transform in its staging (eunet_conv3x3_dgrad_fused; bf16) -- its
+// own instantiation, so the plain data-gradient launches keep their register allocation.
+template <typename T, bool DG, typename TO = T, bool BT = false>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   u32x4 ry[DG ? A_IT : 1];
   // bf16 only: the fp32 dgrad has no registers to spare (eunet_conv3x3_dgrad_fused applies the transform
   // in a separate pass for fp32)
-  constexpr bool BTR = DG && sizeof(T) == 2;
+  constexpr bool BTR = DG && BT && sizeof(T) == 2;
   const bool btr = BTR && a.tcoef != nullptr;
   const uint32_t slice_bytes = (uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
@@ -198,16 +200,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(wgy ? (T*)a.tgo + (long long)ns * a.H * a.W * a.xct : nullptr), 0, wgy ? (int)slice_bytes : 0,
       0x00020000);
-  uint32_t interior = 0;  // bit i: halo unit i is a tile-interior pixel (its gy is stored)
-  if (BTR) {
-#pragma unroll
-    for (int i = 0; i < A_IT; ++i) {
-      int hp, qq;
-      fwd_unit(tid + i * FT, hp, qq);
-      const int hy = hp / FHW, hx = hp - hy * FHW;
-      if (hp < FHPX && hy >= 1 && hy <= FTH && hx >= 1 && hx <= FTW) interior |= 1u << i;
-    }
-  }
   auto chunk_ok = [&](int kc) { return kc * KC + sq * E < a.cin; };
   auto gload_a = [&](int kc, int i0, int i1) {
     const bool cok = chunk_ok(kc);
@@ -280,10 +272,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
             f[j] = ok ? fmaf(k1, gg, fmaf(yv[j], ak2[j >> 2][j & 3], ak3[j >> 2][j & 3])) : 0.f;
           }
           v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
-          EUNET_DASSERT(!(wgy && ((interior >> i) & 1u) && ok) || aoff[i] + (uint32_t)(kc * KC * (int)sizeof(T)) + 16u <= slice_bytes);
-          if (wgy && ((interior >> i) & 1u))
-            __builtin_amdgcn_raw_buffer_store_b128(v, gr, cok ? aoff[i] + (uint32_t)(kc * KC * (int)sizeof(T)) : FWD_OOB,
-                                                   0, 0);
         }
       } else if (a.isc != nullptr) {  // BN + ReLU of the producing layer; padding stays zero
         float f[E];
@@ -360,6 +348,25 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     gload_b(kc, BH, B_IT);
     lwrite_b(BH, B_IT);
   };
+  // co-block 0 of the fused BN-backward dgrad stores the tile interior of the staged gy (for the
+  // weight gradient) from LDS right before the chunk's MFMAs, so the stores drain under them instead
+  // of holding the next staging loads' vmcnt waits: 2048 units = 16 x 32 px x 4 channel quarters
+  auto store_gy = [&](int kc) {
+    if constexpr (BTR) {
+      constexpr int SU = FTH * FTW * 4 / FT;  // 8 units per thread
+#pragma unroll 1
+      for (int j = 0; j < SU; ++j) {
+        const int u = tid + j * FT;            // (pixel row, quarter, pixel column): coalesced stores
+        const int px = u & (FTW - 1), qq = (u >> 5) & 3, py = u >> 7;
+        const int yy = y0 + py, xx = x0 + px;
+        const bool ok = yy < a.H && xx < a.W && kc * KC + qq * E < a.cin;
+        const u32x4 v = *(const u32x4*)(As + (qq * FHPXP + (py + 1) * FHW + px + 1) * 16);
+        const uint32_t off = ok ? (uint32_t)(((yy * a.W + xx) * a.xct + a.xco + kc * KC + qq * E) * (int)sizeof(T)) : FWD_OOB;
+        EUNET_DASSERT(!ok || off + 16u <= slice_bytes);
+        __builtin_amdgcn_raw_buffer_store_b128(v, gr, off, 0, 0);
+      }
+    }
+  };
   if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
     gload_affine(0);
     gload_a(0, 0, A_IT);
@@ -370,6 +377,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     stage_halves(0);
   }
   __syncthreads();
+  if (wgy) store_gy(0);
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -379,6 +387,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       __syncthreads();  // every wave is done reading the stage
       stage_halves(kc);
       __syncthreads();
+      if (wgy) store_gy(kc);
     }
     if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
     chunk();
@@ -1085,7 +1094,7 @@ int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
 template <bool DG>
-int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false) {
+int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, bool bt = false) {
   const long long esz = dtype == EUNET_BF16 ? 2 : 4;
   EUNET_REQUIRE((long long)a.H * a.W * a.xct * esz < (long long)FWD_OOB,
                 "conv3x3: one sample's input (%d x %d x %d) must be < 3 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
@@ -1094,6 +1103,9 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false) 
   if (dtype == EUNET_BF16 && out_f32) {
     allow_lds(conv3x3_fwd_kernel<bf16_t, true, float>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t, true, float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  } else if (dtype == EUNET_BF16 && DG && bt) {
+    allow_lds(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true>, FWD_LDS);
+    conv3x3_fwd_kernel<bf16_t, true, bf16_t, true><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
   } else if (dtype == EUNET_BF16) {
     allow_lds(conv3x3_fwd_kernel<bf16_t, DG>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
@@ -1279,7 +1291,7 @@ int eunet_conv3x3_dgrad_fused(const eunet_act* g, const eunet_act* y_in, const f
     if (rc != EUNET_OK) return rc;
     a.x = gy_out->ptr; a.tyin = nullptr; a.tcoef = nullptr; a.tgo = nullptr;
   }
-  return launch_fwd<true>(a, g->dtype, stream);
+  return launch_fwd<true>(a, g->dtype, stream, false, a.tcoef != nullptr);
 }
 
 

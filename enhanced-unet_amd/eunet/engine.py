@@ -93,10 +93,16 @@ class UNetEngine:
     # this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7
     # alternating pairs on one box (profiles/r02_ab_conv.txt)
     wg3_late = True
-    # fuse_bn_apply -- the apply half of each DoubleConv BatchNorm backward (gy = k1 g' + k2 y + k3)
-    # runs inside the data gradient's operand staging (eunet_conv3x3_dgrad_fused), which also stores
-    # gy for the weight gradient; False: a separate bn_bwd_apply pass per BN (round 2).  Same values.
+    # fuse_bn_apply -- the apply half of the DoubleConv's second BatchNorm backward (gy = k1 g' + k2
+    # y + k3) runs inside conv .3's data-gradient operand staging (eunet_conv3x3_dgrad_fused), which
+    # also stores gy for conv .3's weight gradient (enqueued after that dgrad anyway, wg3_late);
+    # False: a separate bn_bwd_apply pass (round 2).  Same values, bit for bit.
     fuse_bn_apply = True
+    # fuse_bn_apply_a -- the same for the first BatchNorm (conv .0's data gradient).  Off: conv .0's
+    # weight gradient then has to wait for that dgrad and overlaps the next level's HBM-bound upsample
+    # / max-pool adjoints instead of the dgrad (they ran 2.7x longer: +0.85 ms/step in a same-box A/B,
+    # profiles/r03_ab.txt)
+    fuse_bn_apply_a = False
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -395,13 +401,17 @@ class UNetEngine:
         del gyb
         gya = torch.empty_like(ya)
         gx = None
-        if need_gx:
+        if need_gx and self.fuse_bn_apply_a:
             gx = _e((N, H, W, X.c), dt, dev)
             ops.conv3x3_dgrad_fused(ops.act(gaa), ops.act(ya), coefa, ops.act(gya), packed(p + ".0"), ops.act(gx))
             wgrad(p + ".0", X, gya, small_conv=small)
-        else:  # the trunk's first conv has no data gradient: materialise gy for its weight gradient
+        else:  # gy materialised; conv .0's weight gradient overlaps its data gradient (round 2's order)
             ops.bn_bwd_apply_coef(ops.act(gaa), ops.act(ya), coefa, ops.act(gya))
-            wgrad(p + ".0", X, gya, small_conv=small, on_main=True)
+            # the trunk's last weight gradient (no data gradient follows it): on the then idle main stream
+            wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx)
+            if need_gx:
+                gx = _e((N, H, W, X.c), dt, dev)
+                ops.conv3x3_dgrad(ops.act(gya), packed(p + ".0"), ops.act(gx))
         del gaa, gya
         names = [f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")]
         if side is None:

@@ -275,8 +275,13 @@ def test_dual_base96_bf16_vs_autocast_reference():
 def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
     """bf16 whole-network gradient parity of the dual-branch model at base 96 (64^2, B 2, c 1, K 2,
     deep supervision): every parameter gradient vs the fp64 oracle within
-    max(2 x the oracle-under-bf16-autocast error, 3e-2) relative L2
-    (test_gpu_model.test_bf16_train_grads_vs_fp64_oracle)."""
+    max(2 x the oracle-under-bf16-autocast error, 3e-2, 2 x spread) relative L2
+    (test_gpu_model.test_bf16_train_grads_vs_fp64_oracle).  spread = how far the fp64 oracle's own
+    gradient moves under a bf16-scale (1e-3 relative) perturbation of the weights: the attention
+    gate's parameter gradients are tiny sums with heavy cancellation (|g| ~ 3e-4 .. 7e-3 against
+    ~0.1 for the fusion head) and move by 0.2-2x under such perturbations -- autocast's own error
+    on them ranges 0.05 .. 2.1 and ours moved from 1.1 to 0.45 when the forward BN statistics were
+    re-associated (tools/diag_dual_gate.py) -- so their gate is the measured conditioning."""
     from eunet import synth
     from eunet.train_eval import Trainer
     x, msk = synth.batch(2, 64, 64, start_index=27, num_classes=2, in_channels=1)
@@ -289,6 +294,7 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
     with torch.autocast("cpu", dtype=torch.bfloat16):
         fused, aux = D.dual_forward(Sac, x, training=True, drop_masks=keep)
     D.dual_batch_loss(fused.float(), {n: a.float() for n, a in aux.items()}, msk).backward()
+    Sp, _ = _oracle(96, 1, 2, x, msk, keep, torch.float64, noise=1e-3, seed=3)
     m = _model(96, 1, 2, dtype="bf16", keep=keep).train()
     tr = Trainer(m, DEV, "enhanced_unet")
     out = m(x.to(DEV))
@@ -303,8 +309,8 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
             err, err_ac = float((p.grad.double().cpu() - ref).abs().max()), float((Sac[k].grad.double() - ref).abs().max())
             assert err < max(2 * err_ac, 1e-3 * scale), (k, err, err_ac, scale)
             continue
-        e, eac = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref)
-        rows.append((e / max(2 * eac, 3e-2), k, e, eac))
+        e, eac, sp = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref), _rel_l2(Sp[k].grad, ref)
+        rows.append((e / max(2 * eac, 3e-2, 2 * sp), k, e, eac, sp))
     for r in sorted(rows, reverse=True)[:8]:
-        print("dual base96 bf16 grad (ratio, name, ours, autocast):", r)
+        print("dual base96 bf16 grad (ratio, name, ours, autocast, spread):", r)
     assert all(r[0] < 1.0 for r in rows), sorted(rows, reverse=True)[:3]

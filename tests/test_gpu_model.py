@@ -426,16 +426,18 @@ def test_fused_bn_apply_schedule_is_exact(dtype, monkeypatch):
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 96, 64, start_index=13, num_classes=2, in_channels=1)
     out = {}
-    for fused, overlap in ((True, True), (False, True), (True, False)):
+    for fused, fused_a, overlap in ((True, False, True), (True, True, True), (False, False, True),
+                                    (True, True, False)):
         monkeypatch.setattr(engine.UNetEngine, "fuse_bn_apply", fused)
+        monkeypatch.setattr(engine.UNetEngine, "fuse_bn_apply_a", fused_a)
         monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", overlap)
         m = _model(32, 1, 2, dtype)
         m.train()
         loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
         loss.backward()
         torch.cuda.synchronize()
-        out[(fused, overlap)] = (loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
-    ref = out[(False, True)]
+        out[(fused, fused_a, overlap)] = (loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    ref = out[(False, False, True)]
     for key, (lv, grads) in out.items():
         assert lv == ref[0], key
         for k, g in grads.items():

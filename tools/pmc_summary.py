@@ -19,7 +19,7 @@ from collections import defaultdict
 def short(name):
     m = re.search(r"(\w+_kernel|colsum_stage\d|\w+Kernel|multi_tensor_apply_kernel|copyBuffer\w*)", name)
     k = m.group(1) if m else name[:60]
-    if k == "conv3x3_fwd_kernel" and re.search(r"conv3x3_fwd_kernel<[^>]*true>", name):
+    if k == "conv3x3_fwd_kernel" and re.search(r"conv3x3_fwd_kernel<[^,>]*, ?true", name):
         k += ".dgrad"  # the data-gradient launches of the same kernel (template tag DG)
     return k
 
