@@ -94,14 +94,16 @@ class UNetEngine:
     # alternating pairs on one box (profiles/r02_ab_conv.txt)
     wg3_late = True
     # fuse_bn_apply -- the apply half of the DoubleConv's second BatchNorm backward (gy = k1 g' + k2
-    # y + k3) runs inside conv .3's data-gradient operand staging (eunet_conv3x3_dgrad_fused), which
-    # also stores gy for conv .3's weight gradient (enqueued after that dgrad anyway, wg3_late);
-    # False: a separate bn_bwd_apply pass (round 2).  Same values, bit for bit.
-    fuse_bn_apply = True
-    # fuse_bn_apply_a -- the same for the first BatchNorm (conv .0's data gradient).  Off: conv .0's
-    # weight gradient then has to wait for that dgrad and overlaps the next level's HBM-bound upsample
-    # / max-pool adjoints instead of the dgrad (they ran 2.7x longer: +0.85 ms/step in a same-box A/B,
-    # profiles/r03_ab.txt)
+    # y + k3) inside conv .3's data-gradient operand staging (eunet_conv3x3_dgrad_fused), which also
+    # stores gy for conv .3's weight gradient.  Same values, bit for bit, but measured slower: the
+    # dgrad's staging carries two loads per halo unit, the transform and the gy stores while the
+    # standalone apply streams at ~4.9 TB/s beside the side stream's weight gradients -- 26.0-26.1 vs
+    # 25.3-25.5 ms/step in three alternating same-box rounds (profiles/r03_ab.txt).  Off by default.
+    fuse_bn_apply = False
+    # fuse_bn_apply_a -- the same for the first BatchNorm (conv .0's data gradient; needs
+    # fuse_bn_apply).  Off: conv .0's weight gradient then has to wait for that dgrad and overlaps the
+    # next level's HBM-bound upsample / max-pool adjoints instead of the dgrad (they ran 2.7x longer:
+    # +0.85 ms/step in a same-box A/B, profiles/r03_ab.txt)
     fuse_bn_apply_a = False
 
     def __init__(self, model, prefix: str = "model."):
