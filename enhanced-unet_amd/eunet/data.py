@@ -31,11 +31,10 @@ Python `random` draws stay in item order (one producer thread).
 from __future__ import annotations
 
 import json
+import multiprocessing
 import os
-import queue
 import random
-import threading
-from concurrent.futures import ThreadPoolExecutor
+from collections import deque
 
 import numpy as np
 import torch
@@ -77,6 +76,22 @@ def load_labelme(json_path: str, scale_h: float, scale_w: float):
         x_max, y_max = pts.max(axis=0)
         bboxes.append([x_min, y_min, x_max, y_max])
     return polys, labels, bboxes
+
+
+def host_load(data_dir, name, max_size):
+    """dataset.py:133-195 up to the pixels: JPEG decode (PIL), the /32 target size and the LabelMe
+    polygons scaled to it.  Module level, so DataLoader worker processes can run it."""
+    from PIL import Image
+    image = np.array(Image.open(os.path.join(data_dir, name)).convert("RGB"))
+    original_size = image.shape[:2]
+    h, w = reference_sizes(*original_size, max_size)
+    polys, labels, bboxes = load_labelme(os.path.join(data_dir, name.replace(".jpg", ".json")),
+                                         h / original_size[0], w / original_size[1])
+    return name, image, original_size, (h, w), polys, labels, bboxes
+
+
+def _host_load_args(args):
+    return host_load(*args)
 
 
 class CellDataset:
@@ -179,17 +194,14 @@ class CellDataset:
         self._noise_gen.manual_seed(int(np.random.randint(0, 2 ** 62, dtype=np.int64)))
         return torch.normal(0.0, float(sigma), shape, generator=self._noise_gen, device=device)
 
+    def host_args(self, idx):
+        """Picklable arguments of host_load for item idx (DataLoader worker processes)."""
+        return self.data_dir, self.files[idx], self.max_size
+
     def load_host(self, idx):
-        """The host half of __getitem__ (thread-safe, no GPU work, no random draws): the decoded
-        image, the reference's target size and the scaled LabelMe polygons."""
-        from PIL import Image
-        name = self.files[idx]
-        image = np.array(Image.open(os.path.join(self.data_dir, name)).convert("RGB"))
-        original_size = image.shape[:2]
-        h, w = reference_sizes(*original_size, self.max_size)
-        polys, labels, bboxes = load_labelme(os.path.join(self.data_dir, name.replace(".jpg", ".json")),
-                                             h / original_size[0], w / original_size[1])
-        return name, image, original_size, (h, w), polys, labels, bboxes
+        """The host half of __getitem__ (no GPU work, no random draws): the decoded image, the
+        reference's target size and the scaled LabelMe polygons."""
+        return host_load(*self.host_args(idx))
 
     def __getitem__(self, idx):
         return self.from_host(self.load_host(idx))
@@ -223,12 +235,15 @@ class DataLoader:
     """In-order / shuffled batch iterator over a CellDataset (the reference's train_model loaders,
     train_eval.py:1071-1075, run with num_workers=0).
 
-    workers > 0: JPEG decode + JSON parsing (CellDataset.load_host) in a thread pool, ahead of use.
-    prefetch > 0: one producer thread builds the next `prefetch` batches' device data on a side
-    stream while the caller consumes the current batch; the caller's stream waits on each batch's
-    event (no host synchronisation) and its tensors are recorded on that stream.  The augmentation
-    draws from Python's `random` stay in item order (one producer), so a seeded run takes the same
-    decisions either way.  Datasets without load_host / from_host run in the loop."""
+    workers > 0: JPEG decode + JSON parsing (host_load) in that many worker processes (spawned:
+    they never touch the GPU), in item order.  prefetch > 0: the device half of the next `prefetch`
+    batches is enqueued on a side stream, from the calling thread, before the current batch is
+    handed out; the caller's stream waits on each batch's event (no host synchronisation) and its
+    tensors are recorded on that stream.  One thread issues every Python `random` draw in item
+    order, so a seeded run takes the same augmentation decisions either way.  (A producer thread
+    plus decode threads was tried first: its hundreds of short GIL-releasing launches per batch
+    ping-ponged the GIL with the other threads -- slower than no prefetch, profiles/r03_loader.txt.)
+    Datasets without host_args / from_host run in the loop."""
 
     def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, collate_fn=collate_fn,
                  workers: int = 0, prefetch: int = 0):
@@ -239,27 +254,39 @@ class DataLoader:
     def __len__(self):
         return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
-    def _batches(self, idx):
+    def close(self):
+        if self._pool is not None:
+            self._pool.terminate()
+            self._pool = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _split(self):
         ds = self.dataset
-        split = hasattr(ds, "load_host") and hasattr(ds, "from_host")
-        if self.workers > 0 and split:
+        return hasattr(ds, "host_args") and hasattr(ds, "from_host")
+
+    def _host_items(self, idx):
+        ds = self.dataset
+        if self.workers > 0:
             if self._pool is None:
-                self._pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="eunet-decode")
-            ahead = max(2 * self.workers, self.batch_size * (self.prefetch + 1))
-            futs = [self._pool.submit(ds.load_host, j) for j in idx[:ahead]]
-            nxt = len(futs)
-            for i in range(0, len(idx), self.batch_size):
-                items = []
-                for k in range(i, min(i + self.batch_size, len(idx))):
-                    items.append(ds.from_host(futs[k].result()))
-                    futs[k] = None
-                    if nxt < len(idx):
-                        futs.append(self._pool.submit(ds.load_host, idx[nxt]))
-                        nxt += 1
-                yield self.collate_fn(items)
-        else:
+                self._pool = multiprocessing.get_context("spawn").Pool(self.workers)
+            return self._pool.imap(_host_load_args, [ds.host_args(j) for j in idx], chunksize=1)
+        return (ds.load_host(j) for j in idx)
+
+    def _batches(self, idx):
+        """Batches built in the calling thread on the current stream, host halves from _host_items."""
+        ds = self.dataset
+        if not self._split():
             for i in range(0, len(idx), self.batch_size):
                 yield self.collate_fn([ds[j] for j in idx[i:i + self.batch_size]])
+            return
+        host = self._host_items(idx)
+        for i in range(0, len(idx), self.batch_size):
+            yield self.collate_fn([ds.from_host(next(host)) for _ in range(min(self.batch_size, len(idx) - i))])
 
     def __iter__(self):
         n = len(self.dataset)
@@ -279,48 +306,31 @@ class DataLoader:
         if self.prefetch <= 0 or not torch.cuda.is_available():
             yield from self._batches(idx)
             return
-        yield from self._prefetched(idx)
-
-    def _prefetched(self, idx):
         consumer = torch.cuda.current_stream()
         side = torch.cuda.Stream(device=consumer.device)
-        q = queue.Queue(maxsize=self.prefetch)
-        stop = threading.Event()
+        src = self._batches(idx)
+        ready = deque()
 
-        def produce():
-            try:
-                with torch.cuda.stream(side):
-                    for b in self._batches(idx):
-                        ev = torch.cuda.Event()
-                        ev.record(side)
-                        while not stop.is_set():
-                            try:
-                                q.put((b, ev), timeout=0.1)
-                                break
-                            except queue.Full:
-                                continue
-                        if stop.is_set():
-                            return
-                q.put(None)
-            except BaseException as e:  # surfaced in the consumer
-                q.put(e)
+        def build():  # the next batch's device work, enqueued on the side stream
+            with torch.cuda.stream(side):
+                b = next(src, None)
+                if b is None:
+                    return False
+                ev = torch.cuda.Event()
+                ev.record(side)
+            ready.append((b, ev))
+            return True
 
-        th = threading.Thread(target=produce, name="eunet-prefetch", daemon=True)
-        th.start()
-        try:
-            while True:
-                got = q.get()
-                if got is None:
-                    break
-                if isinstance(got, BaseException):
-                    raise got
-                b, ev = got
-                consumer.wait_event(ev)
-                _record(b, consumer)
-                yield b
-        finally:
-            stop.set()
-            th.join()
+        more = True
+        while more and len(ready) < self.prefetch:
+            more = build()
+        while ready:
+            b, ev = ready.popleft()
+            if more:
+                more = build()
+            consumer.wait_event(ev)
+            _record(b, consumer)
+            yield b
 
 
 def _record(obj, stream):

@@ -33,7 +33,7 @@ def make_dataset(d, n, h=600, w=800, seed=0):
     rng = np.random.default_rng(seed)
     yy, xx = np.mgrid[0:h, 0:w]
     for i in range(n):
-        img = np.full((h, w, 3), 170.0) + 20 * np.sin(xx / 97.0 + i) * np.cos(yy / 131.0)
+        img = np.full((h, w, 3), 170.0) + (20 * np.sin(xx / 97.0 + i) * np.cos(yy / 131.0))[..., None]
         shapes = []
         for c in range(int(rng.integers(25, 60))):
             cy, cx = rng.uniform(20, h - 20), rng.uniform(20, w - 20)
@@ -67,23 +67,31 @@ def main():
     t0 = time.perf_counter()
     make_dataset(tmp, args.images)
     t_make = time.perf_counter() - t0
-    ds = CellDataset(tmp, split="train", max_size=640, device=dev, host_noise=args.host_noise)
-    loader = DataLoader(ds, batch_size=2, shuffle=True, collate_fn=collate_fn, workers=args.workers,
-                        prefetch=args.prefetch)
-    random.seed(0)
-    np.random.seed(0)
-    torch.manual_seed(0)
+    configs = [("round2_path", dict(host_noise=True, host_ratio=True), 0, 0),
+               ("sync_free_in_loop", dict(host_noise=args.host_noise), 0, 0),
+               ("sync_free_prefetch", dict(host_noise=args.host_noise), 0, args.prefetch),
+               ("sync_free_workers_prefetch", dict(host_noise=args.host_noise), args.workers, args.prefetch)]
+    loaders = {}
+    rates = {}
     shape = None
-    for b in loader:  # warm-up epoch (allocator, kernels, thread pool)
-        shape = tuple(b["images"].shape)
-    torch.cuda.synchronize()
-    n = 0
-    t0 = time.perf_counter()
-    for _ in range(args.epochs):
-        for b in loader:
-            n += b["images"].shape[0]
-    torch.cuda.synchronize()
-    loader_ips = n / (time.perf_counter() - t0)
+    for label, kw, workers, prefetch in configs:
+        ds = CellDataset(tmp, split="train", max_size=640, device=dev, **kw)
+        loader = DataLoader(ds, batch_size=2, shuffle=True, collate_fn=collate_fn, workers=workers, prefetch=prefetch)
+        random.seed(0)
+        np.random.seed(0)
+        torch.manual_seed(0)
+        for b in loader:  # warm-up epoch (allocator, kernels, thread pool)
+            shape = tuple(b["images"].shape)
+        torch.cuda.synchronize()
+        n = 0
+        t0 = time.perf_counter()
+        for _ in range(args.epochs):
+            for b in loader:
+                n += b["images"].shape[0]
+        torch.cuda.synchronize()
+        rates[label] = round(n / (time.perf_counter() - t0), 1)
+        loaders[label] = (ds, loader)
+    loader_ips = rates["sync_free_workers_prefetch"]
 
     model = get_model("enhanced_unet", num_classes=3, dtype="bf16").to(dev)
     tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
@@ -98,17 +106,25 @@ def main():
     torch.cuda.synchronize()
     trainer_ips = 2 * args.steps / (time.perf_counter() - t0)
 
-    tr.train_epoch(loader)  # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    n = 0
-    for _ in range(args.epochs):
-        tr.train_epoch(loader)
-        n += len(ds)
-    torch.cuda.synchronize()
-    epoch_ips = n / (time.perf_counter() - t0)
-    print(json.dumps({"loader_img_s": round(loader_ips, 1), "trainer_img_s": round(trainer_ips, 1),
-                      "train_epoch_img_s": round(epoch_ips, 1), "tile": list(shape[2:]), "batch": 2,
+    epoch_rates = {}
+    for label in ("sync_free_in_loop", "sync_free_workers_prefetch"):
+        ds, loader = loaders[label]
+        tr.train_epoch(loader)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 0
+        for _ in range(args.epochs):
+            tr.train_epoch(loader)
+            n += len(ds)
+        torch.cuda.synchronize()
+        epoch_rates[label] = round(n / (time.perf_counter() - t0), 1)
+    epoch_ips = epoch_rates["sync_free_workers_prefetch"]
+    for _, ld in loaders.values():
+        ld.close()
+    print(json.dumps({"loader_img_s": loader_ips, "loader_img_s_by_config": rates,
+                      "trainer_img_s": round(trainer_ips, 1),
+                      "train_epoch_img_s": round(epoch_ips, 1), "train_epoch_img_s_by_loader": epoch_rates,
+                      "tile": list(shape[2:]), "batch": 2,
                       "train_images": len(ds), "workers": args.workers, "prefetch": args.prefetch,
                       "host_noise": args.host_noise, "dataset_write_s": round(t_make, 1),
                       "host_cpus": os.cpu_count(), "omp_threads": os.environ.get("OMP_NUM_THREADS")}), flush=True)
