@@ -94,22 +94,41 @@ def reference_params() -> LossParams:
 
 
 # ---- out-of-range target bookkeeping (see module docstring) --------------------------------
-_bad = None  # device scalar: out-of-range targets seen since the last check
+_bad = {}  # device -> fp64 [1] accumulator of out-of-range targets since the last check
+_bad_pending = False  # a loss call (or a graph replay holding one) ran since the last check
+
+
+def bad_target_accumulator(device) -> torch.Tensor:
+    """The persistent per-device counter the loss adds its out-of-range count to, in place: a
+    captured step graph (train_eval.StepGraph) keeps accumulating into it on every replay."""
+    dev = torch.device(device)
+    acc = _bad.get(dev)
+    if acc is None:
+        acc = _bad[dev] = torch.zeros(1, dtype=torch.float64, device=dev)
+    return acc
+
+
+def mark_pending():
+    global _bad_pending
+    _bad_pending = True
 
 
 def _record_bad(sums: torch.Tensor):
-    global _bad
-    _bad = sums[-1:].clone() if _bad is None else _bad + sums[-1:]
+    bad_target_accumulator(sums.device).add_(sums[-1:])
+    mark_pending()
 
 
 def check_targets():
     """Raise ValueError if any loss call since the last check saw a target outside [0, K)
     (synchronises with the device)."""
-    global _bad
-    if _bad is None:
+    global _bad_pending
+    if not _bad_pending:
         return
-    n = int(_bad.item())
-    _bad = None
+    _bad_pending = False
+    n = 0
+    for acc in _bad.values():
+        n += int(acc.item())
+        acc.zero_()
     if n:
         raise ValueError(f"{n} target value(s) outside [0, num_classes) reached the loss "
                          f"(F.cross_entropy would raise: class index out of bounds)")

@@ -62,6 +62,13 @@ class Trainer:
         self.warmup_scheduler = torch.optim.lr_scheduler.LinearLR(
             self.optimizer, start_factor=0.001, end_factor=1.0, total_iters=self.warmup_epochs)
         self.dp = None  # eunet.dp.DataParallel when training on several GPUs
+        # step_graph: replay deferred-loss steps from a captured HIP graph (StepGraph) once
+        # graph_warmup eager steps have run; re-captured when the shapes, the learning rate or the
+        # engine schedule change
+        self.step_graph = False
+        self.graph_warmup = 2
+        self._graph = None
+        self._graph_warm = 0
 
     # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
     def loss_params(self):
@@ -115,7 +122,29 @@ class Trainer:
         return m
 
     def step(self, images: torch.Tensor, masks: torch.Tensor, sync_loss: bool = True):
-        """One optimisation step on device-resident images [B,C,H,W] / masks [B,H,W]."""
+        """One optimisation step on device-resident images [B,C,H,W] / masks [B,H,W].
+
+        With self.step_graph set, a deferred-loss step (sync_loss=False, no DataParallel) replays a
+        captured HIP graph of this same step (StepGraph): same kernels, same bits, one launch."""
+        if self.step_graph and not sync_loss and self.dp is None and images.is_cuda:
+            return self._graphed_step(images, masks)
+        return self._step(images, masks, sync_loss)
+
+    def _graphed_step(self, images, masks):
+        key = StepGraph.key(self, images, masks)
+        g = self._graph
+        if g is not None and g.key == key:
+            return g.replay(images, masks)
+        self._graph = None  # release the old graph's memory pool before capturing anew
+        if self._graph_warm < self.graph_warmup:
+            # eager warm-up steps (real steps): lazy allocations, fused-AdamW state, the loss tables'
+            # host copies, every kernel's first launch happen outside the capture
+            self._graph_warm += 1
+            return self._step(images, masks, False)
+        self._graph = StepGraph(self, images, masks, key)
+        return self._graph.replay(images, masks)
+
+    def _step(self, images, masks, sync_loss):
         self.model.train()
         _, _, h, w = images.shape
         h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
@@ -178,6 +207,72 @@ class Trainer:
             else:
                 self.scheduler.step()
         return self.optimizer.param_groups[0]["lr"]
+
+
+ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late", "fuse_bn_apply", "fuse_bn_apply_a")
+
+
+class StepGraph:
+    """One Trainer step (forward, fused loss, backward, clip_grad_norm_, fused AdamW) captured as a
+    HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch: one host launch
+    instead of several hundred, so a small tile (the reference's 640x480 batch of 2) is no longer
+    bound by Python + ctypes issue and the data loader's host work fits beside it.
+
+    A replay runs the eager step's kernels in the eager order with the same arguments: the engine
+    launches on torch's current stream (the capture stream) and forks / joins its weight-gradient
+    side stream with events; the loss adds its out-of-range target count into a persistent device
+    accumulator in place (losses.bad_target_accumulator); fused AdamW keeps its step count on the
+    device; clip_grad_norm_ and the BN running statistics never leave it.  What the graph bakes in
+    from the host is in key(): shapes, the optimizer's hyper-parameters (the learning rate changes
+    once per epoch -> one re-capture), the loss parameters, the engine schedule, and the parameter
+    / optimizer-state storage (load_state_dict replacing it -> re-capture)."""
+
+    def __init__(self, trainer, images, masks, key):
+        from . import losses as _L
+        self.key = key
+        dev = images.device
+        self.images = torch.empty_like(images)
+        self.masks = torch.empty_like(masks)
+        _L.bad_target_accumulator(dev)
+        opt = trainer.optimizer
+        caps = [g.get("capturable", False) for g in opt.param_groups]
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            for g in opt.param_groups:  # fused AdamW: the flag only gates torch's capture check
+                g["capturable"] = True
+            with torch.cuda.graph(self.graph):
+                self.loss = trainer._step(self.images, self.masks, False)
+        finally:
+            for g, c in zip(opt.param_groups, caps):
+                g["capturable"] = c
+
+    def replay(self, images, masks):
+        from . import losses as _L
+        self.images.copy_(images, non_blocking=True)
+        self.masks.copy_(masks, non_blocking=True)
+        self.graph.replay()
+        _L.mark_pending()
+        return self.loss.clone()
+
+    @staticmethod
+    def key(trainer, images, masks):
+        opt = trainer.optimizer
+        hyper = tuple((g["lr"], g["weight_decay"], tuple(g["betas"]), g["eps"], g.get("amsgrad"), g.get("maximize"),
+                       g.get("fused"))
+                      for g in opt.param_groups)
+        if not all(h[-1] for h in hyper):
+            raise RuntimeError("Trainer.step_graph needs the fused AdamW (its step count lives on the device)")
+        eng = getattr(trainer.model, "_engine", None)
+        if getattr(eng, "drop_keep", None) is not None:
+            raise RuntimeError("Trainer.step_graph: fixed dropout keep masks (a test hook) are host inputs")
+        knobs = tuple(getattr(eng, k, None) for k in ENGINE_KNOBS)
+        ps = opt.param_groups[0]["params"]
+        st = opt.state.get(ps[-1], {})
+        store = (ps[0].data_ptr(), ps[-1].data_ptr()) + tuple(
+            st[k].data_ptr() for k in ("exp_avg", "exp_avg_sq", "step") if k in st)
+        lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight)
+        return (tuple(images.shape), images.dtype, images.device, tuple(masks.shape), masks.dtype, hyper, knobs,
+                store, lossp)
 
 
 from .evaluator import Evaluator  # noqa: E402,F401  (train_eval.Evaluator, train_eval.py:356-904)

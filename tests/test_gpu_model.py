@@ -442,3 +442,61 @@ def test_fused_bn_apply_schedule_is_exact(dtype, monkeypatch):
         assert lv == ref[0], key
         for k, g in grads.items():
             assert torch.equal(g, ref[1][k]), (key, k)
+
+
+def _graph_batches(n, H=64, W=96, B=2):
+    from eunet import synth
+    out = []
+    for i in range(n):
+        x, msk = synth.batch(B, H, W, start_index=5 * i + 1, num_classes=3, in_channels=3)
+        out.append((x.to(DEV), msk.to(DEV)))
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_step_graph_replay_is_exact(dtype):
+    """Trainer.step_graph (StepGraph: the step captured as a HIP graph, replayed per batch) against
+    eager steps from the same weights: every step's loss, the parameters, the AdamW moments and the
+    BN running statistics agree bit for bit over 2 eager warm-up steps, a capture, replays, an LR
+    change (epoch_lr_step -> re-capture) and more replays."""
+    from eunet.train_eval import Trainer
+    batches = _graph_batches(7)
+    ta = Trainer(_model(16, 3, 3, dtype), DEV, "enhanced_unet", total_epochs=12)
+    tb = Trainer(_model(16, 3, 3, dtype), DEV, "enhanced_unet", total_epochs=12)
+    tb.step_graph = True
+    for i, (x, m) in enumerate(batches):
+        if i == 4:
+            ta.epoch_lr_step(1)
+            tb.epoch_lr_step(1)
+        la = ta.step(x, m, sync_loss=False)
+        lb = tb.step(x, m, sync_loss=False)
+        assert torch.equal(la, lb), i
+    assert tb._graph is not None and tb._graph.key[5][0][0] == tb.optimizer.param_groups[0]["lr"]
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
+        sa, sb = ta.optimizer.state[p], tb.optimizer.state[q]
+        for s in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(sa[s], sb[s]), (k, s)
+    for (k, a), b in zip(ta.model.named_buffers(), tb.model.buffers()):
+        assert torch.equal(a, b), k
+
+
+def test_step_graph_train_epoch_and_bad_targets():
+    """train_epoch over a graph-replayed trainer returns the eager epoch's mean loss, and an
+    out-of-range target in a replayed batch still raises at the epoch's sync (the loss adds its
+    count into the persistent accumulator inside the graph)."""
+    from eunet.train_eval import Trainer
+    batches = [{"images": x, "batch_items": [{"semantic_mask": mm} for mm in m]} for x, m in _graph_batches(5)]
+    ta = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb.step_graph = True
+    assert ta.train_epoch(batches) == tb.train_epoch(batches)
+    assert tb._graph is not None
+    assert ta.train_epoch(batches) == tb.train_epoch(batches)
+    bad = [dict(b) for b in batches]
+    m = bad[2]["batch_items"][0]["semantic_mask"].clone()
+    m[3, 5] = 7
+    bad[2] = {"images": bad[2]["images"], "batch_items": [{"semantic_mask": m}, bad[2]["batch_items"][1]]}
+    with pytest.raises(ValueError, match="outside"):
+        tb.train_epoch(bad)
+    tb.train_epoch(batches)  # the accumulator was cleared at the raise: no error carried over

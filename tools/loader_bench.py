@@ -8,7 +8,8 @@ so max_size=640 gives the reference's 640x480 training tiles, dataset.py:141-157
               every augmentation of dataset.py:204-300 live), images/s with the GPU work included;
   trainer  -- Trainer.step on device-resident 2 x 640x480 batches (base 64, 3-ch -> 3-cls as
               train_model builds it, bf16), images/s;
-  epoch    -- Trainer.train_epoch(loader): the two together, images/s.
+  epoch    -- Trainer.train_epoch(loader): the two together, images/s (eager steps, and with
+              Trainer.step_graph: the step replayed from a captured HIP graph).
 Prints one JSON line.
 """
 from __future__ import annotations
@@ -107,8 +108,9 @@ def main():
     trainer_ips = 2 * args.steps / (time.perf_counter() - t0)
 
     epoch_rates = {}
-    for label in ("sync_free_in_loop", "sync_free_workers_prefetch"):
-        ds, loader = loaders[label]
+    for label in ("sync_free_in_loop", "sync_free_workers_prefetch", "sync_free_workers_prefetch+step_graph"):
+        ds, loader = loaders[label.split("+")[0]]
+        tr.step_graph = label.endswith("+step_graph")
         tr.train_epoch(loader)  # warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -118,7 +120,7 @@ def main():
             n += len(ds)
         torch.cuda.synchronize()
         epoch_rates[label] = round(n / (time.perf_counter() - t0), 1)
-    epoch_ips = epoch_rates["sync_free_workers_prefetch"]
+    epoch_ips = epoch_rates["sync_free_workers_prefetch+step_graph"]
     for _, ld in loaders.values():
         ld.close()
     print(json.dumps({"loader_img_s": loader_ips, "loader_img_s_by_config": rates,
