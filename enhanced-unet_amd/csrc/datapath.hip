@@ -16,6 +16,8 @@
 //   resize_u8   cv2.resize INTER_LINEAR-style bilinear (half-pixel centres,
 //               round-half-up); cv2's fixed-point weights are not reproduced.
 // All are HBM-bound byte kernels: one thread per pixel, no reductions.
+#include <climits>
+
 #include "common.h"
 
 namespace {
@@ -37,53 +39,147 @@ __device__ __forceinline__ bool on_segment(int x, int y, int x0, int y0, int x1,
   return x >= min(x0, x1) && x <= max(x0, x1) && y >= min(y0, y1) && y <= max(y0, y1);
 }
 
+// Polygon i can only paint pixels inside its vertex bounding box (the sample point x + 0.5 of an
+// inside pixel lies strictly between the extreme vertices; an edge pixel lies on the segment).
+// Both rasterisers cull by it: the work is ~ sum of the polygons' box areas x edges, not
+// pixels x all edges (a 640x480 LabelMe image with 40 cells: 205 -> ~10 us).
+//
+// Bounding boxes of polygons [p0, p0 + n) into LDS bb[0 .. n): the chunk's vertices split over the
+// block's threads (coalesced), each vertex's polygon found by binary search in the LDS copy of
+// poly_off, LDS integer min / max.  The caller syncs before (bb / offs reuse) and after.
+constexpr int RCH = NT;  // polygons per LDS chunk
+__device__ void chunk_bboxes(const int* pts, const int* poly_off, int p0, int n, int* offs, int4* bb) {
+  for (int t = threadIdx.x; t <= n; t += NT) offs[t] = poly_off[p0 + t];
+  for (int t = threadIdx.x; t < n; t += NT) bb[t] = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
+  __syncthreads();
+  const int v0 = offs[0], v1 = offs[n];
+  for (int v = v0 + (int)threadIdx.x; v < v1; v += NT) {
+    int lo = 0, hi = n - 1;  // the polygon t with offs[t] <= v < offs[t + 1] (empty polygons skipped)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (offs[mid] <= v) lo = mid;
+      else hi = mid - 1;
+    }
+    const int x = pts[2 * v], y = pts[2 * v + 1];
+    atomicMin(&bb[lo].x, x);
+    atomicMin(&bb[lo].y, y);
+    atomicMax(&bb[lo].z, x);
+    atomicMax(&bb[lo].w, y);
+  }
+}
+
+// even-odd crossing test at the pixel centre or on an edge (the fill rule above)
+__device__ __forceinline__ bool poly_covers(const int* pts, int b, int e, int x, int y) {
+  const float px = x + 0.5f, py = y + 0.5f;
+  bool in = false, edge = false;
+  for (int k = b, j = e - 1; k < e; j = k++) {
+    const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
+    edge |= on_segment(x, y, xj, yj, xi, yi);
+    if ((yi > py) != (yj > py)) {
+      const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
+      if (px < xc) in = !in;
+    }
+  }
+  return in || edge;
+}
+
+// semantic mask: one 16x16 pixel tile per block.  Per chunk of polygons the block keeps, in
+// polygon order, those whose box meets the tile (ballot compaction), then every pixel tests only
+// those: the last covering polygon wins, as dataset.py:197-201's loop paints.
+constexpr int RT = 16;
 __global__ __launch_bounds__(NT) void rasterize_kernel(const int* pts, const int* poly_off, const int* labels,
                                                        int npoly, int h, int w, int64_t* mask) {
-  const long long total = (long long)h * w;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int y = (int)(i / w), x = (int)(i - (long long)y * w);
-    const float px = x + 0.5f, py = y + 0.5f;
-    int64_t v = 0;
-    for (int p = 0; p < npoly; ++p) {
-      const int b = poly_off[p], e = poly_off[p + 1];
-      bool in = false, edge = false;
-      for (int k = b, j = e - 1; k < e; j = k++) {
-        const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
-        edge |= on_segment(x, y, xj, yj, xi, yi);
-        if ((yi > py) != (yj > py)) {
-          const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
-          if (px < xc) in = !in;
-        }
-      }
-      if (in || edge) v = labels[p];
+  __shared__ int offs[RCH + 1];
+  __shared__ int4 bb[RCH];
+  __shared__ int list[RCH];
+  __shared__ int wcnt[NT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tx0 = blockIdx.x * RT, ty0 = blockIdx.y * RT;
+  const int x = tx0 + (tid & (RT - 1)), y = ty0 + (tid >> 4);
+  const int tx1 = min(tx0 + RT, w) - 1, ty1 = min(ty0 + RT, h) - 1;
+  int64_t v = 0;
+  for (int p0 = 0; p0 < npoly; p0 += RCH) {
+    const int n = min(RCH, npoly - p0);
+    __syncthreads();
+    chunk_bboxes(pts, poly_off, p0, n, offs, bb);
+    __syncthreads();
+    bool hit = false;
+    if (tid < n) {
+      const int4 b = bb[tid];
+      hit = b.x <= tx1 && b.z >= tx0 && b.y <= ty1 && b.w >= ty0;
     }
-    mask[i] = v;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wcnt[wv] = __popcll(m);
+    __syncthreads();
+    int base = 0, cnt = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) {
+      base += i < wv ? wcnt[i] : 0;
+      cnt += wcnt[i];
+    }
+    if (hit) list[base + __popcll(m & ((1ull << lane) - 1ull))] = tid;
+    __syncthreads();
+    if (x < w && y < h)
+      for (int j = 0; j < cnt; ++j) {
+        const int t = list[j];
+        const int4 b = bb[t];
+        if (x < b.x || x > b.z || y < b.y || y > b.w) continue;
+        if (poly_covers(pts, offs[t], offs[t + 1], x, y)) v = labels[p0 + t];
+      }
   }
+  if (x < w && y < h) mask[(long long)y * w + x] = v;
 }
 
 // one uint8 mask per polygon (dataset.py:184-186: cv2.fillPoly(mask, [points], 1)), same fill rule,
 // with the training flips (dataset.py:209-222: every instance mask flipped like the image) applied
-// as a mirrored read: out[i][y][x] = raster_i[flip_v ? h-1-y : y][flip_h ? w-1-x : x]
+// as a mirrored read: out[i][y][x] = raster_i[flip_v ? h-1-y : y][flip_h ? w-1-x : x].
+// blockIdx.y = polygon, blockIdx.x = a run of 4 NT output bytes (4 per thread, one 4-byte store
+// when the run is aligned); bytes outside the polygon's box are zeros without a test.
 __global__ __launch_bounds__(NT) void rasterize_instances_kernel(const int* pts, const int* poly_off, int npoly, int h,
                                                                  int w, int flip_h, int flip_v, uint8_t* masks) {
-  const long long hw = (long long)h * w, total = hw * npoly;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int p = (int)(i / hw);
-    const long long r = i - (long long)p * hw;
+  __shared__ int4 wbb[NT / 64];
+  const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = poly_off[p], e = poly_off[p + 1];
+  int4 bx = make_int4(INT_MAX, INT_MAX, INT_MIN, INT_MIN);
+  for (int k = b + tid; k < e; k += NT) {
+    const int xx = pts[2 * k], yy = pts[2 * k + 1];
+    bx = make_int4(min(bx.x, xx), min(bx.y, yy), max(bx.z, xx), max(bx.w, yy));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    bx.x = min(bx.x, __shfl_xor(bx.x, o, 64));
+    bx.y = min(bx.y, __shfl_xor(bx.y, o, 64));
+    bx.z = max(bx.z, __shfl_xor(bx.z, o, 64));
+    bx.w = max(bx.w, __shfl_xor(bx.w, o, 64));
+  }
+  if (lane == 0) wbb[wv] = bx;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const int4 o = wbb[i];
+    bx = make_int4(min(bx.x, o.x), min(bx.y, o.y), max(bx.z, o.z), max(bx.w, o.w));
+  }
+  const long long hw = (long long)h * w;
+  const long long r0 = ((long long)blockIdx.x * NT + tid) * 4;
+  if (r0 >= hw) return;
+  uint8_t out[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[j] = 0;
+    const long long r = r0 + j;
+    if (r >= hw) continue;
     const int yo = (int)(r / w), xo = (int)(r - (long long)yo * w);
     const int y = flip_v ? h - 1 - yo : yo, x = flip_h ? w - 1 - xo : xo;
-    const float px = x + 0.5f, py = y + 0.5f;
-    const int b = poly_off[p], e = poly_off[p + 1];
-    bool in = false, edge = false;
-    for (int k = b, j = e - 1; k < e; j = k++) {
-      const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
-      edge |= on_segment(x, y, xj, yj, xi, yi);
-      if ((yi > py) != (yj > py)) {
-        const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
-        if (px < xc) in = !in;
-      }
-    }
-    masks[i] = (in || edge) ? 1 : 0;
+    if (x < bx.x || x > bx.z || y < bx.y || y > bx.w) continue;
+    out[j] = poly_covers(pts, b, e, x, y) ? 1 : 0;
+  }
+  uint8_t* dst = masks + (long long)p * hw + r0;
+  if (r0 + 4 <= hw && (((uintptr_t)dst) & 3) == 0) {
+    *(uint32_t*)dst = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) | ((uint32_t)out[3] << 24);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (r0 + j < hw) dst[j] = out[j];
   }
 }
 
@@ -183,7 +279,8 @@ int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* lab
                              int64_t* mask, void* stream) {
   EUNET_REQUIRE(mask && h > 0 && w > 0 && npoly >= 0 && (npoly == 0 || (pts && poly_off && labels)),
                 "rasterize_polygons: bad args");
-  rasterize_kernel<<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(pts, poly_off, labels, npoly, h, w, mask);
+  const dim3 g((unsigned)cdiv(w, RT), (unsigned)cdiv(h, RT));
+  rasterize_kernel<<<g, NT, 0, (hipStream_t)stream>>>(pts, poly_off, labels, npoly, h, w, mask);
   EUNET_LAUNCH_CHECK("rasterize_polygons");
   return EUNET_OK;
 }
@@ -191,8 +288,10 @@ int eunet_rasterize_polygons(const int* pts, const int* poly_off, const int* lab
 int eunet_rasterize_instances(const int* pts, const int* poly_off, int npoly, int h, int w, int flip_h,
                               int flip_v, uint8_t* masks, void* stream) {
   EUNET_REQUIRE(masks && h > 0 && w > 0 && npoly > 0 && pts && poly_off, "rasterize_instances: bad args");
-  rasterize_instances_kernel<<<grid1((long long)h * w * npoly), NT, 0, (hipStream_t)stream>>>(
-      pts, poly_off, npoly, h, w, flip_h, flip_v, masks);
+  EUNET_REQUIRE(npoly <= 65535 && ((long long)h * w + 4 * NT - 1) / (4 * NT) < (1ll << 31),
+                "rasterize_instances: too many polygons / pixels");
+  const dim3 g((unsigned)(((long long)h * w + 4 * NT - 1) / (4 * NT)), (unsigned)npoly);
+  rasterize_instances_kernel<<<g, NT, 0, (hipStream_t)stream>>>(pts, poly_off, npoly, h, w, flip_h, flip_v, masks);
   EUNET_LAUNCH_CHECK("rasterize_instances");
   return EUNET_OK;
 }

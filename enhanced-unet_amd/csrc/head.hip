@@ -1048,6 +1048,10 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
 // chains): the BN-backward algebra is folded into 4 per-channel constants,
 //   pre = h P + Q,   g_h = P gbn + h D + E   (D = -P c2 is, E = -P (c2 off + c1)),
 // and the constant A fragments (W1 for h, W2^T for s, W1^T for v) are read from LDS.
+#ifndef HEAD_ABL
+#define HEAD_ABL 0  // diagnostic builds only (tools/abl_build.sh): 1 skips the g_u / upsample-adjoint phases,
+                    // 2 the W1-gradient MFMAs, 4 the v / g_h LDS writes
+#endif
 template <int K>
 __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadArgs a) {  // (K = 3: LDS allows 2)
   constexpr int STRIDE = MID * K * 9 + MID;
@@ -1169,6 +1173,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
         v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
         // v[j][pixel] of the tile (zero where the pixel is outside the image: g is)
+        if (HEAD_ABL & 4) { agb1[0] += v0[0] + v1[1]; continue; }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (4 * q + i < KJ) vt[4 * q + i][r * T2 + x] = f2bf(v0[i]);
@@ -1178,6 +1183,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
       }
+      if (HEAD_ABL & 2) continue;
       __syncthreads();
       const int r0 = 4 * wv + 2 * rp;
       bf16x8 Bw[2];
@@ -1201,6 +1207,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
       }
       __syncthreads();
     }
+    if (HEAD_ABL & 1) continue;
     // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image
     for (int i = tid; i < 18 * 18; i += NT) {
       const int rr = i / 18, cc = i - rr * 18;

@@ -192,29 +192,38 @@ __global__ __launch_bounds__(NT) void clahe_lut_kernel(const uint8_t* src, int p
     atomicAdd(&hist[src[((long long)y * w + x) * ps]], 1u);  // LDS integer counts: order-free
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // clip + redistribute + cumulate, serially as OpenCV (256 steps)
-    int excess = 0;
-    for (int i = 0; i < 256; ++i) {
-      const int c = (int)hist[i];
-      if (c > clip) {
-        excess += c - clip;
-        hist[i] = (unsigned)clip;
-      }
-    }
-    const int batch = excess / 256, residual = excess - batch * 256;
-    for (int i = 0; i < 256; ++i) hist[i] += (unsigned)batch;
-    if (residual != 0) {
-      const int step = max(256 / residual, 1);
-      int r = residual;
-      for (int i = 0; i < 256 && r > 0; i += step, --r) hist[i] += 1u;
-    }
-    unsigned sum = 0;
-    uint8_t* lut = luts + (long long)blockIdx.x * 256;
-    for (int i = 0; i < 256; ++i) {
-      sum += hist[i];
-      lut[i] = sat_u8((float)sum * lut_scale);
-    }
+  // clip + redistribute + cumulate as OpenCV's serial loops do, one bin per thread (the serial form
+  // in one thread was 3 x 256 dependent steps with byte stores, most of the kernel's 44 us):
+  // excess = block sum, the residual's +1 lands on bins 0, step, 2 step, ... (residual of them),
+  // the LUT is the inclusive prefix sum (wave scans + the waves' totals through LDS), integer-exact
+  static_assert(NT == 256, "one histogram bin per thread");
+  __shared__ int wsum[NT / 64];
+  const int i = threadIdx.x, lane = i & 63, wv = i >> 6;
+  int c = (int)hist[i];
+  int ex = c > clip ? c - clip : 0;
+  c = min(c, clip);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ex += __shfl_xor(ex, o, 64);
+  if (lane == 0) wsum[wv] = ex;
+  __syncthreads();
+  const int excess = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const int batch = excess / 256, residual = excess - batch * 256;
+  c += batch;
+  if (residual != 0) {
+    const int step = max(256 / residual, 1);
+    if (i % step == 0 && i / step < residual) c += 1;
   }
+  unsigned sum = (unsigned)c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned v = __shfl_up(sum, o, 64);
+    if (lane >= o) sum += v;
+  }
+  __syncthreads();  // every thread has read wsum (excess)
+  if (lane == 63) wsum[wv] = (int)sum;
+  __syncthreads();
+  for (int w = 0; w < wv; ++w) sum += (unsigned)wsum[w];
+  luts[(long long)blockIdx.x * 256 + i] = sat_u8((float)sum * lut_scale);
 }
 
 // bilinear blend of the four neighbouring tile LUTs (OpenCV CLAHE_Interpolation_Body)
@@ -339,12 +348,26 @@ __global__ __launch_bounds__(NT) void edge_raw_kernel(const uint8_t* gray, int h
 // (dataset.py:81-91: fp64 normalisation, fp32 blend, astype(uint8) truncations)
 __global__ __launch_bounds__(NT) void edge_combine_kernel(const double* mag, const double* lap, const double* bmax,
                                                           int nb, long long n, uint8_t* edges) {
+  // the maxima over edge_raw's per-block rows: every block reduces them with all its threads (a
+  // serial loop over ~1200 rows in two threads was a 1200-deep chain of dependent loads, 120 us)
+  __shared__ double sm[2][NT];
   __shared__ double mx[2];
-  if (threadIdx.x < 2) {
-    double m = 0.0;
-    for (int b = 0; b < nb; ++b) m = fmax(m, bmax[2 * b + threadIdx.x]);
-    mx[threadIdx.x] = m;
+  double m1 = 0.0, m2 = 0.0;
+  for (int b = threadIdx.x; b < nb; b += NT) {
+    m1 = fmax(m1, bmax[2 * b]);
+    m2 = fmax(m2, bmax[2 * b + 1]);
   }
+  sm[0][threadIdx.x] = m1;
+  sm[1][threadIdx.x] = m2;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      sm[0][threadIdx.x] = fmax(sm[0][threadIdx.x], sm[0][threadIdx.x + s]);
+      sm[1][threadIdx.x] = fmax(sm[1][threadIdx.x], sm[1][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2) mx[threadIdx.x] = sm[threadIdx.x][0];
   __syncthreads();
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     const double e = fmin(fmax(mag[i] / (mx[0] + 1e-6) * 255.0, 0.0), 255.0);

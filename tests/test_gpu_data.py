@@ -65,6 +65,41 @@ def test_rasterize_matches_rule():
     assert (m[10:21, 10:21] == 1).all()  # a square's outline and interior are filled
 
 
+def _random_polys(rng, n, h, w):
+    polys = []
+    for i in range(n):
+        c = rng.uniform(-10, [w + 10, h + 10])  # some straddle or leave the image
+        ang = np.sort(rng.uniform(0, 2 * np.pi, rng.integers(1, 16)))  # 1-2 vertices: points / segments
+        r = rng.uniform(0, 25, len(ang))
+        pts = np.stack([c[0] + r * np.cos(ang), c[1] + r * np.sin(ang)], 1).astype(np.float32).astype(np.int32)
+        polys.append(pts)
+    return polys
+
+
+@pytest.mark.parametrize("n,h,w", [(300, 61, 77), (40, 480, 640), (1, 17, 3)])
+def test_rasterize_culling_matches_rule(n, h, w):
+    """The bounding-box culled rasterisers (16x16 tiles with per-chunk polygon lists, > 256
+    polygons = several LDS chunks; per-polygon instance masks in 4-byte runs, ragged tails, flips)
+    against the oracle's per-pixel rule over every polygon."""
+    from eunet import ops
+    rng = np.random.default_rng(n + h)
+    polys = _random_polys(rng, n, h, w)
+    labels = [1 + int(v) for v in rng.integers(0, 2, n)]
+    m = ops.rasterize_polygons(polys, labels, h, w, DEV).cpu().numpy()
+    assert np.array_equal(m, O.rasterize(polys, labels, h, w))
+    k = min(n, 24)
+    refs = [(O.rasterize([polys[i]], [1], h, w) > 0).astype(np.uint8) for i in range(k)]
+    for fh, fv in ((False, False), (True, False), (False, True), (True, True)):
+        inst = ops.rasterize_instances(polys[:k], h, w, DEV, flip_h=fh, flip_v=fv).cpu().numpy()
+        for i in range(k):
+            ref = refs[i]
+            if fh:
+                ref = ref[:, ::-1]
+            if fv:
+                ref = ref[::-1]
+            assert np.array_equal(inst[i], ref), (i, fh, fv)
+
+
 def test_cell_dataset_end_to_end(tmp_path):
     """LabelMe directory -> device batches; same split, sizes and seeded augmentation decisions."""
     from PIL import Image

@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--prefetch", type=int, default=2, help="batches prepared ahead on a side stream (0: none)")
     ap.add_argument("--host-noise", action="store_true", help="numpy noise (the reference's exact values)")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--loader-only", action="store_true", help="only the workers+prefetch loader (for rocprofv3)")
     args = ap.parse_args()
     from eunet.data import CellDataset, DataLoader, collate_fn
     from eunet.models import get_model
@@ -75,6 +76,8 @@ def main():
     loaders = {}
     rates = {}
     shape = None
+    if args.loader_only:
+        configs = configs[-1:]
     for label, kw, workers, prefetch in configs:
         ds = CellDataset(tmp, split="train", max_size=640, device=dev, **kw)
         loader = DataLoader(ds, batch_size=2, shuffle=True, collate_fn=collate_fn, workers=workers, prefetch=prefetch)
@@ -93,6 +96,9 @@ def main():
         rates[label] = round(n / (time.perf_counter() - t0), 1)
         loaders[label] = (ds, loader)
     loader_ips = rates["sync_free_workers_prefetch"]
+    if args.loader_only:
+        print(json.dumps({"loader_img_s": loader_ips, "epochs": args.epochs + 1, "train_images": len(ds)}), flush=True)
+        return
 
     model = get_model("enhanced_unet", num_classes=3, dtype="bf16").to(dev)
     tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
@@ -121,11 +127,42 @@ def main():
         torch.cuda.synchronize()
         epoch_rates[label] = round(n / (time.perf_counter() - t0), 1)
     epoch_ips = epoch_rates["sync_free_workers_prefetch+step_graph"]
+    # where an epoch's host time goes: the loader's next() (decode hand-off + the next batch's device
+    # work enqueued) vs Trainer.step, per batch, eager and graphed
+    breakdown = {}
+    ds, loader = loaders["sync_free_workers_prefetch"]
+    for graph in (False, True):
+        tr.step_graph = graph
+        tr.train_epoch(loader)
+        torch.cuda.synchronize()
+        t_next = t_step = 0.0
+        nb = 0
+        t0 = time.perf_counter()
+        for _ in range(args.epochs):
+            it = iter(loader)
+            while True:
+                ta = time.perf_counter()
+                b = next(it, None)
+                tb = time.perf_counter()
+                t_next += tb - ta
+                if b is None:
+                    break
+                m = tr._masks(b, dev, 0, 0)
+                tc = time.perf_counter()
+                tr.step(b["images"], m, sync_loss=False)
+                t_step += time.perf_counter() - tc
+                nb += 1
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        breakdown["graph" if graph else "eager"] = {"ms_per_batch": round(wall / nb * 1e3, 3),
+                                                    "next_ms": round(t_next / nb * 1e3, 3),
+                                                    "step_ms": round(t_step / nb * 1e3, 3)}
     for _, ld in loaders.values():
         ld.close()
     print(json.dumps({"loader_img_s": loader_ips, "loader_img_s_by_config": rates,
                       "trainer_img_s": round(trainer_ips, 1),
                       "train_epoch_img_s": round(epoch_ips, 1), "train_epoch_img_s_by_loader": epoch_rates,
+                      "epoch_host_breakdown": breakdown,
                       "tile": list(shape[2:]), "batch": 2,
                       "train_images": len(ds), "workers": args.workers, "prefetch": args.prefetch,
                       "host_noise": args.host_noise, "dataset_write_s": round(t_make, 1),
