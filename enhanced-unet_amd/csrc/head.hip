@@ -1184,7 +1184,9 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
       }
       if (HEAD_ABL & 2) continue;
-      __syncthreads();
+      // gw is wave-private: the wave's own LDS writes are in order before its reads (no block barrier)
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_wave_barrier();
       const int r0 = 4 * wv + 2 * rp;
       bf16x8 Bw[2];
 #pragma unroll
@@ -1205,26 +1207,33 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         accW[pb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, Bw[0], accW[pb][0], 0, 0, 0);
         accW[pb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, Bw[1], accW[pb][1], 0, 0, 0);
       }
-      __syncthreads();
+      __builtin_amdgcn_wave_barrier();  // (the next rows' gw writes stay behind these reads)
     }
+    __syncthreads();  // every wave's v rows are in vt and its Bw reads of su are done
     if (HEAD_ABL & 1) continue;
-    // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image
+    // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image;
+    // branch-free: out-of-tile taps read a clamped index and add zero
     for (int i = tid; i < 18 * 18; i += NT) {
       const int rr = i / 18, cc = i - rr * 18;
       const int oy = oy0 - 1 + rr, ox = ox0 - 1 + cc;
+      const bool img = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
+      const bool inner = img && rr >= 1 && rr <= T2 && cc >= 1 && cc <= T2;
+      const int gi = inner ? (rr - 1) * T2 + cc - 1 : 0;
       float g[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) g[k] = 0.f;
-      if (oy >= 0 && oy < H2 && ox >= 0 && ox < W2) {
-        if (rr >= 1 && rr <= T2 && cc >= 1 && cc <= T2)
+      for (int k = 0; k < K; ++k) {
+        const float v = gos[k * T2 * T2 + gi];
+        g[k] = inner ? v : 0.f;
+      }
 #pragma unroll
-          for (int k = 0; k < K; ++k) g[k] = gos[k * T2 * T2 + (rr - 1) * T2 + cc - 1];
+      for (int t = 0; t < 9; ++t) {
+        const int ky = t / 3, kx = t - ky * 3, pr = rr - ky, pc = cc - kx;  // source pixel q - d_t
+        const bool ok = img && pr >= 0 && pr < T2 && pc >= 0 && pc < T2;
+        const int vi = ok ? pr * T2 + pc : 0;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int ky = t / 3, kx = t - ky * 3, pr = rr - ky, pc = cc - kx;  // source pixel q - d_t
-          if (pr < 0 || pr >= T2 || pc < 0 || pc >= T2) continue;
-#pragma unroll
-          for (int k = 0; k < K; ++k) g[k] += bf2f(vt[k * 9 + t][pr * T2 + pc]);
+        for (int k = 0; k < K; ++k) {
+          const float v = bf2f(vt[k * 9 + t][vi]);
+          g[k] += ok ? v : 0.f;
         }
       }
 #pragma unroll
@@ -1238,15 +1247,15 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
       float hv[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) hv[k] = 0.f;
-      if (X >= 0 && X < a.w)
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int cc = 2 * px - 2 + d, ox = ox0 - 1 + cc;
-          if (cc < 0 || cc >= 18 || ox < 0 || ox >= W2) continue;
-          const float wxv = up2_adj_w(ox, a.w, X);
+      for (int d = 0; d < 4; ++d) {  // (branch-free: a tap outside the region / image weighs 0)
+        const int cc = 2 * px - 2 + d, ox = ox0 - 1 + cc;
+        const bool ok = X >= 0 && X < a.w && cc >= 0 && cc < 18 && ox >= 0 && ox < W2;
+        const float wxv = ok ? up2_adj_w(ox, a.w, X) : 0.f;
+        const int ci = ok ? cc : 0;
 #pragma unroll
-          for (int k = 0; k < K; ++k) hv[k] = fmaf(wxv, su[(rr * 18 + cc) * 3 + k], hv[k]);
-        }
+        for (int k = 0; k < K; ++k) hv[k] = fmaf(wxv, su[(rr * 18 + ci) * 3 + k], hv[k]);
+      }
 #pragma unroll
       for (int k = 0; k < K; ++k) hxs[i * 3 + k] = hv[k];
     }
@@ -1256,15 +1265,15 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
       float pv[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) pv[k] = 0.f;
-      if (Y >= 0 && Y < a.h)
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int rr = 2 * py - 2 + d, oy = oy0 - 1 + rr;
-          if (rr < 0 || rr >= 18 || oy < 0 || oy >= H2) continue;
-          const float wyv = up2_adj_w(oy, a.h, Y);
+      for (int d = 0; d < 4; ++d) {
+        const int rr = 2 * py - 2 + d, oy = oy0 - 1 + rr;
+        const bool ok = Y >= 0 && Y < a.h && rr >= 0 && rr < 18 && oy >= 0 && oy < H2;
+        const float wyv = ok ? up2_adj_w(oy, a.h, Y) : 0.f;
+        const int ri = ok ? rr : 0;
 #pragma unroll
-          for (int k = 0; k < K; ++k) pv[k] = fmaf(wyv, hxs[(rr * 10 + px) * 3 + k], pv[k]);
-        }
+        for (int k = 0; k < K; ++k) pv[k] = fmaf(wyv, hxs[(ri * 10 + px) * 3 + k], pv[k]);
+      }
 #pragma unroll
       EUNET_DASSERT(tile < a.ntiles && tid < 100);
 #pragma unroll

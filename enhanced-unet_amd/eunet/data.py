@@ -33,7 +33,9 @@ from __future__ import annotations
 import json
 import multiprocessing
 import os
+import queue
 import random
+import threading
 from collections import deque
 
 import numpy as np
@@ -243,12 +245,14 @@ class DataLoader:
     order, so a seeded run takes the same augmentation decisions either way.  (A producer thread
     plus decode threads was tried first: its hundreds of short GIL-releasing launches per batch
     ping-ponged the GIL with the other threads -- slower than no prefetch, profiles/r03_loader.txt.)
+    thread=True builds the device halves in one producer thread instead (DataLoader._threaded),
+    for a consumer whose per-batch host work is one graph launch (Trainer.step_graph).
     Datasets without host_args / from_host run in the loop."""
 
     def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, collate_fn=collate_fn,
-                 workers: int = 0, prefetch: int = 0):
+                 workers: int = 0, prefetch: int = 0, thread: bool = False):
         self.dataset, self.batch_size, self.shuffle, self.collate_fn = dataset, batch_size, shuffle, collate_fn
-        self.workers, self.prefetch = workers, prefetch
+        self.workers, self.prefetch, self.thread = workers, prefetch, thread
         self._pool = None
 
     def __len__(self):
@@ -309,6 +313,9 @@ class DataLoader:
         consumer = torch.cuda.current_stream()
         side = torch.cuda.Stream(device=consumer.device)
         src = self._batches(idx)
+        if self.thread:
+            yield from self._threaded(src, consumer, side)
+            return
         ready = deque()
 
         def build():  # the next batch's device work, enqueued on the side stream
@@ -331,6 +338,54 @@ class DataLoader:
             consumer.wait_event(ev)
             _record(b, consumer)
             yield b
+
+
+    def _threaded(self, src, consumer, side):
+        """The device half of every batch built by one producer thread on the side stream, up to
+        `prefetch` batches ahead (every Python `random` draw still in item order: one producer).
+        Pays off when the consumer's own host work per batch is short -- Trainer.step_graph's single
+        graph launch -- so the two threads overlap instead of ping-ponging the GIL."""
+        q = queue.Queue(maxsize=self.prefetch)
+        stop = threading.Event()
+
+        def put(item):
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.1)
+                    return True
+                except queue.Full:
+                    continue
+            return False
+
+        def producer():
+            try:
+                torch.cuda.set_device(consumer.device)
+                with torch.cuda.stream(side):
+                    for b in src:
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                        if not put((b, ev)):
+                            return
+                put(None)
+            except BaseException as e:  # handed to the consumer, raised there
+                put(e)
+
+        t = threading.Thread(target=producer, name="eunet-loader", daemon=True)
+        t.start()
+        try:
+            while True:
+                item = q.get()
+                if item is None:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                b, ev = item
+                consumer.wait_event(ev)
+                _record(b, consumer)
+                yield b
+        finally:
+            stop.set()
+            t.join()
 
 
 def _record(obj, stream):

@@ -240,7 +240,9 @@ class StepGraph:
         try:
             for g in opt.param_groups:  # fused AdamW: the flag only gates torch's capture check
                 g["capturable"] = True
-            with torch.cuda.graph(self.graph):
+            # thread_local: a DataLoader producer thread may launch and allocate on its own stream
+            # while this thread captures (the default global mode would invalidate the capture)
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.loss = trainer._step(self.images, self.masks, False)
         finally:
             for g, c in zip(opt.param_groups, caps):

@@ -210,21 +210,38 @@ def test_sync_free_augmentation_matches_host_ratio(tmp_path):
 
 
 def test_prefetching_loader_same_batches(tmp_path):
-    """DataLoader(workers=3, prefetch=2) -- host decode threads, device work of the next batches on
-    a side stream -- yields the batches the plain loop yields for the same seeds (device noise
-    included: its generator is reseeded from np.random in item order)."""
+    """DataLoader(workers=3, prefetch=2) -- decode in worker processes, device work of the next
+    batches on a side stream, from the calling thread or from one producer thread -- yields the
+    batches the plain loop yields for the same seeds (device noise included: its generator is
+    reseeded from np.random in item order)."""
     from eunet.data import CellDataset, DataLoader
     _write_cells(tmp_path, n=14)
     ds = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV)
     runs = []
-    for workers, prefetch in ((0, 0), (3, 2)):
+    for workers, prefetch, thread in ((0, 0, False), (3, 2, False), (3, 2, True), (0, 1, True)):
         random.seed(3)
         np.random.seed(3)
         torch.manual_seed(3)
+        loader = DataLoader(ds, batch_size=2, shuffle=True, workers=workers, prefetch=prefetch, thread=thread)
         got = [(b["images"].clone(), torch.stack([it["semantic_mask"] for it in b["batch_items"]]).clone())
-               for b in DataLoader(ds, batch_size=2, shuffle=True, workers=workers, prefetch=prefetch)]
+               for b in loader]
         torch.cuda.synchronize()
+        loader.close()
         runs.append(got)
-    assert len(runs[0]) == len(runs[1]) == 5
-    for (xa, ma), (xb, mb) in zip(*runs):
-        assert torch.equal(xa, xb) and torch.equal(ma, mb)
+    assert all(len(r) == 5 for r in runs)
+    for other in runs[1:]:
+        for (xa, ma), (xb, mb) in zip(runs[0], other):
+            assert torch.equal(xa, xb) and torch.equal(ma, mb)
+
+
+def test_threaded_loader_stops_early(tmp_path):
+    """Abandoning a threaded loader's epoch mid-way (break) stops its producer thread."""
+    import threading
+    from eunet.data import CellDataset, DataLoader
+    _write_cells(tmp_path, n=14)
+    ds = CellDataset(str(tmp_path), split="train", max_size=640, device=DEV)
+    loader = DataLoader(ds, batch_size=1, shuffle=False, prefetch=1, thread=True)
+    it = iter(loader)
+    next(it)
+    it.close()  # GeneratorExit at the yield -> the finally block stops and joins the producer
+    assert not any(t.name == "eunet-loader" and t.is_alive() for t in threading.enumerate())

@@ -72,15 +72,17 @@ def main():
     configs = [("round2_path", dict(host_noise=True, host_ratio=True), 0, 0),
                ("sync_free_in_loop", dict(host_noise=args.host_noise), 0, 0),
                ("sync_free_prefetch", dict(host_noise=args.host_noise), 0, args.prefetch),
-               ("sync_free_workers_prefetch", dict(host_noise=args.host_noise), args.workers, args.prefetch)]
+               ("sync_free_workers_prefetch", dict(host_noise=args.host_noise), args.workers, args.prefetch),
+               ("sync_free_workers_thread", dict(host_noise=args.host_noise), args.workers, -args.prefetch)]
     loaders = {}
     rates = {}
     shape = None
     if args.loader_only:
-        configs = configs[-1:]
+        configs = configs[-2:-1]
     for label, kw, workers, prefetch in configs:
         ds = CellDataset(tmp, split="train", max_size=640, device=dev, **kw)
-        loader = DataLoader(ds, batch_size=2, shuffle=True, collate_fn=collate_fn, workers=workers, prefetch=prefetch)
+        loader = DataLoader(ds, batch_size=2, shuffle=True, collate_fn=collate_fn, workers=workers,
+                            prefetch=abs(prefetch), thread=prefetch < 0)
         random.seed(0)
         np.random.seed(0)
         torch.manual_seed(0)
@@ -94,6 +96,7 @@ def main():
                 n += b["images"].shape[0]
         torch.cuda.synchronize()
         rates[label] = round(n / (time.perf_counter() - t0), 1)
+        print(f"loader {label}: {rates[label]} img/s", file=sys.stderr, flush=True)
         loaders[label] = (ds, loader)
     loader_ips = rates["sync_free_workers_prefetch"]
     if args.loader_only:
@@ -114,7 +117,8 @@ def main():
     trainer_ips = 2 * args.steps / (time.perf_counter() - t0)
 
     epoch_rates = {}
-    for label in ("sync_free_in_loop", "sync_free_workers_prefetch", "sync_free_workers_prefetch+step_graph"):
+    for label in ("sync_free_in_loop", "sync_free_workers_prefetch", "sync_free_workers_prefetch+step_graph",
+                  "sync_free_workers_thread", "sync_free_workers_thread+step_graph"):
         ds, loader = loaders[label.split("+")[0]]
         tr.step_graph = label.endswith("+step_graph")
         tr.train_epoch(loader)  # warm-up
@@ -126,12 +130,14 @@ def main():
             n += len(ds)
         torch.cuda.synchronize()
         epoch_rates[label] = round(n / (time.perf_counter() - t0), 1)
-    epoch_ips = epoch_rates["sync_free_workers_prefetch+step_graph"]
+        print(f"train_epoch {label}: {epoch_rates[label]} img/s", file=sys.stderr, flush=True)
+    epoch_ips = max(epoch_rates.values())
     # where an epoch's host time goes: the loader's next() (decode hand-off + the next batch's device
     # work enqueued) vs Trainer.step, per batch, eager and graphed
     breakdown = {}
-    ds, loader = loaders["sync_free_workers_prefetch"]
-    for graph in (False, True):
+    for lname, graph in (("sync_free_workers_prefetch", False), ("sync_free_workers_prefetch", True),
+                         ("sync_free_workers_thread", True)):
+        ds, loader = loaders[lname]
         tr.step_graph = graph
         tr.train_epoch(loader)
         torch.cuda.synchronize()
@@ -154,7 +160,7 @@ def main():
                 nb += 1
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        breakdown["graph" if graph else "eager"] = {"ms_per_batch": round(wall / nb * 1e3, 3),
+        breakdown[lname + ("+step_graph" if graph else "")] = {"ms_per_batch": round(wall / nb * 1e3, 3),
                                                     "next_ms": round(t_next / nb * 1e3, 3),
                                                     "step_ms": round(t_step / nb * 1e3, 3)}
     for _, ld in loaders.values():
