@@ -38,6 +38,7 @@ struct HeadArgs {
   float* stats; float* out2h; float* logits; float* part;
   void* gh; float* v; float* gu;
   float* patch;  // bf16 path: per-tile low-res adjoint patches [tile][10][10][K] (head_gh_mfma_kernel)
+  float* gram;   // bf16 path: per-block im2col second-moment rows [block][GRAM_LD] (head_gram_mfma_kernel)
   int tx, ty, ntiles;
 };
 
@@ -828,6 +829,139 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 forward statistics from the second moments of the conv's input columns.  The head conv is
+// linear in the im2col column col(p) (the 9K values of u around pixel p, zero outside the image):
+//   mean_c = w_c . m + b1_c,   var_c = w_c^T Cov w_c,   m = E[col],  Cov = E[col col^T] - m m^T,
+// with w_c = bf16(W1[c]) -- the operands head_out / bwd multiply -- so one pass accumulating
+// G = sum_p col(p) col(p)^T over the valid pixels (bf16 col values are exact, their products exact
+// in fp32) replaces computing and reducing all 64 channels of h per pixel.  The column is padded to
+// 32 (two MFMA fragments); entry 31 is the pixel's validity (1 / 0), so G[j][31] = sum_p col_j and
+// G[31][31] = the pixel count.  One partial row per block: the 00, 01 and 11 16x16 blocks of the
+// symmetric 32x32 G, C layout (row 4q + i, column x), summed over the block's 4 waves.
+// ---------------------------------------------------------------------------
+constexpr int GRAM_LD = 3 * 256;
+
+// su offset of column entry j = 16 jb + x relative to a pixel's window corner; -1: zero entry,
+// -2: the validity entry (j = 31)
+template <int K>
+__device__ __forceinline__ void gram_offsets(int x, int (&o)[2]) {
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const int j = 16 * jb + x;
+    if (j < K * 9) {
+      const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
+      o[jb] = (ky * 18 + kx) * 3 + k;
+    } else {
+      o[jb] = j == 31 ? -2 : -1;
+    }
+  }
+}
+
+// one 32-pixel group: tile rows r0, r0 + 1; pixel slot px = 8q + jj -> (r0 + (px >> 4), px & 15).
+// Lane (q, x) holds col_{16 jb + x} of slots 8q..8q+7: the A fragment of G's rows and, unchanged,
+// the B fragment of its columns.
+__device__ __forceinline__ void gram_group(const float* su, int r0, int q, const int (&o)[2], int vh, int vw,
+                                           f32x4& c00, f32x4& c01, f32x4& c11) {
+  bf16x8 f0, f1;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int px = 8 * q + jj, r = r0 + (px >> 4), c = px & 15;
+    const bool valid = r < vh && c < vw;
+    const int base = (r * 18 + c) * 3;
+    const float v0 = su[base + (o[0] < 0 ? 0 : o[0])];
+    const float v1 = su[base + (o[1] < 0 ? 0 : o[1])];
+    f0[jj] = (__bf16)(valid && o[0] >= 0 ? v0 : 0.f);
+    f1[jj] = (__bf16)(!valid ? 0.f : o[1] >= 0 ? v1 : o[1] == -2 ? 1.f : 0.f);
+  }
+  c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, f0, c00, 0, 0, 0);
+  c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, f1, c01, 0, 0, 0);
+  c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, f1, c11, 0, 0, 0);
+}
+
+// the block's three G blocks -> one partial row (fixed-order sum of the 4 waves)
+__device__ __forceinline__ void gram_store(float* red, float* row, const f32x4& c00, const f32x4& c01,
+                                           const f32x4& c11) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = (4 * q + i) * 16 + x;
+    red[wv * GRAM_LD + e] = c00[i];
+    red[wv * GRAM_LD + 256 + e] = c01[i];
+    red[wv * GRAM_LD + 512 + e] = c11[i];
+  }
+  __syncthreads();
+  for (int e = tid; e < GRAM_LD; e += NT)
+    row[e] = (red[e] + red[GRAM_LD + e]) + (red[2 * GRAM_LD + e] + red[3 * GRAM_LD + e]);
+}
+
+template <int K>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_gram_mfma_kernel(HeadArgs a) {
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
+  __shared__ float red[4 * GRAM_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  int o[2];
+  gram_offsets<K>(x, o);
+  f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  float zv[2] = {0.f, 0.f};
+  zload(a, blockIdx.x, zv);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+    stage_u(a, su, zs, zv, tile, oy0, ox0);
+    __syncthreads();
+    const int vh = min(T2, H2 - oy0), vw = min(T2, W2 - ox0);
+    gram_group(su, 4 * wv, q, o, vh, vw, c00, c01, c11);
+    gram_group(su, 4 * wv + 2, q, o, vh, vw, c00, c01, c11);
+  }
+  EUNET_DASSERT(a.gram != nullptr);
+  gram_store(red, a.gram + (long long)blockIdx.x * GRAM_LD, c00, c01, c11);
+}
+
+// G (the column sums of the partial rows, fp32) -> one (sum, M2, count) statistics row for
+// bn_finalize: per channel c (thread c) mean and variance of h_c = bf16(W1[c]) . col + b1[c], in fp64
+__device__ __forceinline__ double gram_at(const float* g, int j, int jp) {
+  if (j > jp) { const int t = j; j = jp; jp = t; }  // symmetric: the stored blocks are 00, 01, 11
+  if (jp < 16) return (double)g[j * 16 + jp];
+  if (j < 16) return (double)g[256 + j * 16 + (jp - 16)];
+  return (double)g[512 + (j - 16) * 16 + (jp - 16)];
+}
+
+template <int K>
+__global__ __launch_bounds__(MID) void head_gram_stats_kernel(const float* g, const float* w1, const float* b1,
+                                                              float* stats) {
+  constexpr int KJ = K * 9;
+  __shared__ double cov[KJ][KJ], m[KJ];
+  const int tid = threadIdx.x;
+  const double n = (double)g[512 + 15 * 16 + 15];
+  const double inv = n > 0.0 ? 1.0 / n : 0.0;
+  if (tid < KJ) m[tid] = gram_at(g, tid, 31) * inv;
+  __syncthreads();
+  for (int e = tid; e < KJ * KJ; e += MID) {
+    const int j = e / KJ, jp = e - j * KJ;
+    cov[j][jp] = gram_at(g, j, jp) * inv - m[j] * m[jp];
+  }
+  __syncthreads();
+  double wb[KJ];
+#pragma unroll
+  for (int j = 0; j < KJ; ++j) wb[j] = (double)(float)(__bf16)w1[tid * KJ + j];
+  double mean = 0.0, var = 0.0;
+#pragma unroll
+  for (int j = 0; j < KJ; ++j) {
+    mean += wb[j] * m[j];
+    double t = 0.0;
+#pragma unroll
+    for (int jp = 0; jp < KJ; ++jp) t += cov[j][jp] * wb[jp];
+    var += wb[j] * t;
+  }
+  stats[tid] = (float)((mean + (double)b1[tid]) * n);
+  stats[MID + tid] = (float)(fmax(var, 0.0) * n);
+  if (tid == 0) stats[2 * MID] = (float)n;
+}
+
 template <int K>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_out_mfma_kernel(HeadArgs a) {
   __shared__ float su[18 * 18 * 3];
@@ -1340,7 +1474,7 @@ __global__ __launch_bounds__(256) void head_patch_gather_kernel(const float* pat
 }
 
 struct WsLayout {
-  size_t stats, part1, partw, gh, v, gu, patch, scale, shift, cws, total;
+  size_t stats, part1, partw, gh, v, gu, patch, gram, gsum, scale, shift, cws, total;
   int grid, grid4;  // grid4: the bf16 forward kernels' grid (also the rows of the stats partials)
 };
 WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
@@ -1367,9 +1501,12 @@ WsLayout ws_layout(int N, int h, int w, int K, int dtype) {
   L.v = take(dtype == EUNET_F32 ? P2 * ((K * 9 + 3) & ~3) : 0);
   L.gu = take(dtype == EUNET_F32 ? P2 * K : 0);
   L.patch = take(dtype == EUNET_F32 ? 0 : (size_t)tiles * 100 * K);
+  L.gram = take(dtype == EUNET_F32 ? 0 : (size_t)L.grid4 * GRAM_LD);
+  L.gsum = take(dtype == EUNET_F32 ? 0 : (size_t)GRAM_LD);
   L.scale = take(MID);
   L.shift = take(MID);
-  L.cws = take((size_t)2 * 16 * (MID * K * 9 + MID));  // fp64 colsum stage-1 rows (<= 16 for <= 1024 rows)
+  // fp64 colsum stage-1 rows (<= 16 for <= 1024 rows)
+  L.cws = take((size_t)2 * 16 * std::max(MID * K * 9 + MID, GRAM_LD));
   L.total = off * sizeof(float);
   return L;
 }
@@ -1421,10 +1558,23 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
   a.scale = wsf + L.scale; a.shift = wsf + L.shift;
   hipStream_t s = (hipStream_t)stream;
   if (training) {
-    if (mf) HEAD_DISPATCH(head_stats_mfma_kernel, L.grid4, NT, 0, s);
-    else HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
+    int rows = L.grid4;
+    if (mf) {  // statistics from the im2col second moments (one stats row)
+      a.gram = wsf + L.gram;
+      HEAD_DISPATCH(head_gram_mfma_kernel, L.grid4, NT, 0, s);
+      EUNET_LAUNCH_CHECK("head_gram");
+      int rc = eunet_colsum_ld(a.gram, L.grid4, GRAM_LD, GRAM_LD, wsf + L.gsum, wsf + L.cws, s);
+      if (rc) return rc;
+      const float* gs = wsf + L.gsum;
+      if (k == 1) head_gram_stats_kernel<1><<<1, MID, 0, s>>>(gs, w1, b1, a.stats);
+      else if (k == 2) head_gram_stats_kernel<2><<<1, MID, 0, s>>>(gs, w1, b1, a.stats);
+      else head_gram_stats_kernel<3><<<1, MID, 0, s>>>(gs, w1, b1, a.stats);
+      rows = 1;
+    } else {
+      HEAD_DISPATCH(head_stats_kernel, L.grid, NT, 0, s);
+    }
     EUNET_LAUNCH_CHECK("head_stats");
-    int rc = eunet_bn_finalize(a.stats, L.grid4, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
+    int rc = eunet_bn_finalize(a.stats, rows, MID, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd,
                                wsf + L.scale, wsf + L.shift, nullptr, stream);
     if (rc) return rc;
   } else {

@@ -99,9 +99,12 @@ def test_dual_train_grads_match_oracle(golden_dir, base, cin, K, H):
     S, loss_ref = _oracle(base, cin, K, x, msk, keep, torch.float64)
     S32, _ = _oracle(base, cin, K, x, msk, keep, torch.float32)
     # ReLU-kink / max-pool-tie sensitivity of this input: spread of the fp64 oracle itself under
-    # 1e-6 relative weight perturbations (see test_gpu_model.test_train_grads_match_oracle)
+    # 1e-6 relative weight perturbations (see test_gpu_model.test_train_grads_match_oracle).  The
+    # gradient moves in discrete jumps here: at base 16 the deeplab BN gradients land at ~1e-6,
+    # ~1e-3 or ~4.4e-3 relative L2 from the unperturbed value depending on the perturbation's draw
+    # (seeds 3 and 4 give 4.4e-3, seeds 1 and 2 ~1e-3), so the spread takes the max over six draws
     spread = {}
-    for seed in (1, 2):
+    for seed in range(1, 7):
         Sp, _ = _oracle(base, cin, K, x, msk, keep, torch.float64, noise=1e-6, seed=seed)
         for k in S:
             if S[k].grad is not None:
@@ -230,7 +233,7 @@ def test_dual_base96_train_grads_fp32_vs_oracle():
     keep = _keep96()
     S, loss_ref = _oracle(96, 1, 2, x, msk, keep, torch.float64)
     S32, _ = _oracle(96, 1, 2, x, msk, keep, torch.float32)
-    Sp, _ = _oracle(96, 1, 2, x, msk, keep, torch.float64, noise=1e-6, seed=1)
+    sps = [_oracle(96, 1, 2, x, msk, keep, torch.float64, noise=1e-6, seed=sd)[0] for sd in (1, 2, 3)]
     m = _model(96, 1, 2, keep=keep).train()
     tr = Trainer(m, DEV, "enhanced_unet")
     out = m(x.to(DEV))
@@ -246,7 +249,7 @@ def test_dual_base96_train_grads_fp32_vs_oracle():
             # global gradient scale (test_gpu_model._pre_bn_bias)
             assert float((p.grad.double().cpu() - ref).abs().max()) < 1e-4 * scale, k
             continue
-        tol = max(1e-3, 3 * _rel_l2(S32[k].grad, ref), 1.5 * _rel_l2(Sp[k].grad, ref))
+        tol = max(1e-3, 3 * _rel_l2(S32[k].grad, ref), 1.5 * max(_rel_l2(Sp[k].grad, ref) for Sp in sps))
         rows.append((_rel_l2(p.grad, ref) / tol, k, _rel_l2(p.grad, ref), tol))
     for r in sorted(rows, reverse=True)[:6]:
         print("dual base96 grad (ratio, name, err, tol):", r)
@@ -277,7 +280,7 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
     deep supervision): every parameter gradient vs the fp64 oracle within
     max(2 x the oracle-under-bf16-autocast error, 3e-2, 2 x spread) relative L2
     (test_gpu_model.test_bf16_train_grads_vs_fp64_oracle).  spread = how far the fp64 oracle's own
-    gradient moves under a bf16-scale (1e-3 relative) perturbation of the weights: the attention
+    gradient moves under a bf16-scale (2^-8 relative) perturbation of the weights: the attention
     gate's parameter gradients are tiny sums with heavy cancellation (|g| ~ 3e-4 .. 7e-3 against
     ~0.1 for the fusion head) and move by 0.2-2x under such perturbations -- autocast's own error
     on them ranges 0.05 .. 2.1 and ours moved from 1.1 to 0.45 when the forward BN statistics were
@@ -294,7 +297,10 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
     with torch.autocast("cpu", dtype=torch.bfloat16):
         fused, aux = D.dual_forward(Sac, x, training=True, drop_masks=keep)
     D.dual_batch_loss(fused.float(), {n: a.float() for n, a in aux.items()}, msk).backward()
-    Sp, _ = _oracle(96, 1, 2, x, msk, keep, torch.float64, noise=1e-3, seed=3)
+    # spread at the bf16 rounding scale (2^-8 relative weight noise), max over three draws: the
+    # gate's gradients move by 0.04-0.07 (attention_gate.4.bias) and 0.3-1.2 (attention_gate.1.weight)
+    # relative L2 between draws -- one 1e-3 draw under-estimated that envelope
+    sps = [_oracle(96, 1, 2, x, msk, keep, torch.float64, noise=2.0 ** -8, seed=sd)[0] for sd in (1, 2, 3)]
     m = _model(96, 1, 2, dtype="bf16", keep=keep).train()
     tr = Trainer(m, DEV, "enhanced_unet")
     out = m(x.to(DEV))
@@ -309,7 +315,8 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
             err, err_ac = float((p.grad.double().cpu() - ref).abs().max()), float((Sac[k].grad.double() - ref).abs().max())
             assert err < max(2 * err_ac, 1e-3 * scale), (k, err, err_ac, scale)
             continue
-        e, eac, sp = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref), _rel_l2(Sp[k].grad, ref)
+        e, eac = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref)
+        sp = max(_rel_l2(Sp[k].grad, ref) for Sp in sps)
         rows.append((e / max(2 * eac, 3e-2, 2 * sp), k, e, eac, sp))
     for r in sorted(rows, reverse=True)[:8]:
         print("dual base96 bf16 grad (ratio, name, ours, autocast, spread):", r)

@@ -407,6 +407,44 @@ def test_head_fwd_bwd(K, dt):
     assert float(gb1.abs().max()) < 1e-3 * float(gw1.abs().max()) + 1e-5  # pre-BN bias: ~0
 
 
+@pytest.mark.parametrize("K,N,H,W,shift", [(1, 2, 12, 20, 0.0), (2, 2, 12, 20, 0.0), (3, 1, 9, 13, 0.0),
+                                            (2, 2, 32, 24, 6.0)])
+def test_head_bf16_batch_stats(K, N, H, W, shift):
+    """bf16 head statistics come from the im2col second moments (head_gram_mfma_kernel): mean and
+    1/std of h = conv3x3(bf16(u), bf16(W1)) + b1 over the 2H image, against fp64 statistics of the
+    same bf16-rounded operands.  Ragged tiles (2H, 2W not multiples of 16) and a z offset of 6
+    (mean >> std: the centering's cancellation) included."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(11)
+    z = torch.randn(N, K, H, W, generator=g, dtype=torch.float64) + shift
+    w1 = torch.randn(64, K, 3, 3, generator=g, dtype=torch.float64) / 4
+    b1 = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
+    gamma = torch.rand(64, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
+    w2 = torch.randn(K, 64, generator=g, dtype=torch.float64) / 8
+    b2 = torch.randn(K, generator=g, dtype=torch.float64) * 0.1
+    u = F.interpolate(z.float(), scale_factor=2, mode="bilinear", align_corners=False)
+    ub = u.bfloat16().double()
+    wb = w1.float().bfloat16().double()
+    h = F.conv2d(ub, wb, b1.float().double(), padding=1)
+    m_ref = h.mean((0, 2, 3))
+    v_ref = h.var((0, 2, 3), unbiased=False)
+    f = lambda t: t.float().contiguous().to(DEV)
+    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K, torch.bfloat16), dtype=torch.uint8, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    mean, inv = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    logits = torch.empty(N, K, H, W, device=DEV)
+    ops.head_fwd(f(nhwc(z)), N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2), f(b2), True, 1e-5, 0.1,
+                 rm, rv, mean, inv, None, logits, ws, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    inv_ref = 1.0 / torch.sqrt(v_ref + 1e-5)
+    assert (mean.double().cpu() - m_ref).abs().max() < 1e-4 * (m_ref.abs().max() + v_ref.sqrt().max())
+    assert rel(inv.double().cpu(), inv_ref) < 1e-4
+    n = N * 4 * H * W
+    assert rel(rv.double().cpu(), 0.9 + 0.1 * v_ref * n / (n - 1)) < 1e-4
+    assert rel(rm.double().cpu(), 0.1 * m_ref) < 1e-4
+
+
 @pytest.mark.parametrize("K", [2, 3])
 def test_loss_fwd_bwd(K):
     from oracle import eunet_ref as R
