@@ -348,9 +348,13 @@ def _head_ref(z, w1, b1, gamma, beta, w2, b2):
     return u + F.conv2d(a, w2, b2)
 
 
-@pytest.mark.parametrize("K,dt", [(2, torch.float32), (3, torch.float32), (1, torch.bfloat16),
-                                  (2, torch.bfloat16), (3, torch.bfloat16)])
-def test_head_fwd_bwd(K, dt):
+@pytest.mark.parametrize("K,dt,N,H,W", [(2, torch.float32, 2, 12, 20), (3, torch.float32, 2, 12, 20),
+                                        (1, torch.bfloat16, 2, 12, 20), (2, torch.bfloat16, 2, 12, 20),
+                                        (3, torch.bfloat16, 2, 12, 20),
+                                        # 2H tiles away from the image border (the bf16 kernels' interior
+                                        # staging path) next to border tiles
+                                        (2, torch.bfloat16, 1, 40, 28), (3, torch.bfloat16, 1, 24, 40)])
+def test_head_fwd_bwd(K, dt, N, H, W):
     """fp32: FMA path, 1e-4 of the fp64 reference.  bf16: MFMA path (bf16 operands,
     fp32 accumulation = the reference's autocast precision): each quantity within
     max(1e-2, 1.5x) the error that CPU bf16 autocast of the same head makes vs fp64
@@ -358,7 +362,6 @@ def test_head_fwd_bwd(K, dt):
     off by 2-9% there)."""
     ops = _ops()
     g = torch.Generator().manual_seed(7)
-    N, H, W = 2, 12, 20
     z = torch.randn(N, K, H, W, generator=g, dtype=torch.float64)
     w1 = torch.randn(64, K, 3, 3, generator=g, dtype=torch.float64) / 4
     b1 = torch.randn(64, generator=g, dtype=torch.float64) * 0.1
