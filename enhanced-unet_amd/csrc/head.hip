@@ -844,31 +844,34 @@ constexpr int GRAM_LD = 3 * 256;
 
 // su offset of column entry j = 16 jb + x relative to a pixel's window corner; -1: zero entry,
 // -2: the validity entry (j = 31)
-template <int K>
+template <int K, int RS>
 __device__ __forceinline__ void gram_offsets(int x, int (&o)[2]) {
 #pragma unroll
   for (int jb = 0; jb < 2; ++jb) {
     const int j = 16 * jb + x;
     if (j < K * 9) {
       const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
-      o[jb] = (ky * 18 + kx) * 3 + k;
+      o[jb] = (ky * RS + kx) * 3 + k;
     } else {
       o[jb] = j == 31 ? -2 : -1;
     }
   }
 }
 
-// one 32-pixel group: tile rows r0, r0 + 1; pixel slot px = 8q + jj -> (r0 + (px >> 4), px & 15).
+// one 32-pixel group of a region with row stride RS (RS - 2 pixels per tile row): W = 16, tile rows r0,
+// r0 + 1 (slot px = 8q + jj -> (r0 + (px >> 4), px & 15)); W = 32, tile row r0 (px -> (r0, px)).
 // Lane (q, x) holds col_{16 jb + x} of slots 8q..8q+7: the A fragment of G's rows and, unchanged,
 // the B fragment of its columns.
+template <int RS>
 __device__ __forceinline__ void gram_group(const float* su, int r0, int q, const int (&o)[2], int vh, int vw,
                                            f32x4& c00, f32x4& c01, f32x4& c11) {
+  constexpr int W = RS - 2;
   bf16x8 f0, f1;
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) {
-    const int px = 8 * q + jj, r = r0 + (px >> 4), c = px & 15;
+    const int px = 8 * q + jj, r = r0 + px / W, c = px % W;
     const bool valid = r < vh && c < vw;
-    const int base = (r * 18 + c) * 3;
+    const int base = (r * RS + c) * 3;
     const float v0 = su[base + (o[0] < 0 ? 0 : o[0])];
     const float v1 = su[base + (o[1] < 0 ? 0 : o[1])];
     f0[jj] = (__bf16)(valid && o[0] >= 0 ? v0 : 0.f);
@@ -895,27 +898,69 @@ __device__ __forceinline__ void gram_store(float* red, float* row, const f32x4& 
     row[e] = (red[e] + red[GRAM_LD + e]) + (red[2 * GRAM_LD + e] + red[3 * GRAM_LD + e]);
 }
 
+// 32 x 32 tiles at 2H (4x the pixels of the other head kernels' tiles per barrier set): the 18 x 18 x K
+// z region is staged, u = up(z) over the 34 x 34 region (zero outside the image, up2_src as stage_u),
+// then each wave accumulates 8 rows of 32 pixels.  tx / ty / ntiles of HeadArgs describe these tiles.
+constexpr int GT = 32, GR = GT + 2, GZ = GT / 2 + 2;
 template <int K>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_gram_mfma_kernel(HeadArgs a) {
-  __shared__ float su[18 * 18 * 3];
-  __shared__ float zs[ZR * ZR * 3];
+  __shared__ float su[GR * GR * 3];
+  __shared__ float zs[GZ * GZ * 3];
   __shared__ float red[4 * GRAM_LD];
+  constexpr int ZN = GZ * GZ * K, ZI = (ZN + NT - 1) / NT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   int o[2];
-  gram_offsets<K>(x, o);
+  gram_offsets<K, GR>(x, o);
   f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-  const int H2 = 2 * a.h, W2 = 2 * a.w;
-  float zv[2] = {0.f, 0.f};
-  zload(a, blockIdx.x, zv);
+  const int H2 = 2 * a.h, W2 = 2 * a.w, tpi = a.tx * a.ty;
+  auto zfetch = [&](int tile, float (&zv)[ZI]) {
+    if (tile >= a.ntiles) return;
+    const int n = tile / tpi, r = tile - n * tpi;
+    const int zy0 = (r / a.tx) * (GT / 2) - 1, zx0 = (r % a.tx) * (GT / 2) - 1;
+    const float* zb = a.z + (long long)n * a.h * a.w * K;
+#pragma unroll
+    for (int j = 0; j < ZI; ++j) {
+      const int idx = tid + j * NT;
+      if (idx < ZN) {
+        const int k = idx % K, pix = idx / K, i = pix / GZ, c = pix - i * GZ;
+        const int yy = min(max(zy0 + i, 0), a.h - 1), xx = min(max(zx0 + c, 0), a.w - 1);
+        zv[j] = zb[((long long)yy * a.w + xx) * K + k];
+      }
+    }
+  };
+  float zv[ZI];
+  zfetch(blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    int n, oy0, ox0;
-    tile_coords(a, tile, n, oy0, ox0);
+    const int n = tile / tpi, r = tile - n * tpi;
+    const int oy0 = (r / a.tx) * GT, ox0 = (r % a.tx) * GT;
+    __syncthreads();  // the previous tile's su reads are done
+#pragma unroll
+    for (int j = 0; j < ZI; ++j)
+      if (tid + j * NT < ZN) zs[tid + j * NT] = zv[j];
     __syncthreads();
-    stage_u(a, su, zs, zv, tile, oy0, ox0);
+    zfetch(tile + gridDim.x, zv);
+    const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
+    for (int i = tid; i < GR * GR; i += NT) {
+      const int hy = i / GR, hx = i - hy * GR;
+      const int oy = oy0 + hy - 1, ox = ox0 + hx - 1;
+      const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
+      int y0, y1, x0, x1;
+      float ly, lx;
+      up2_src(in ? oy : 0, a.h, y0, y1, ly);
+      up2_src(in ? ox : 0, a.w, x0, x1, lx);
+      const float* r0 = zs + ((y0 - zy0) * GZ) * K;
+      const float* r1 = zs + ((y1 - zy0) * GZ) * K;
+      const int c0 = (x0 - zx0) * K, c1 = (x1 - zx0) * K;
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
+                                 ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
+                           : 0.f;
+    }
     __syncthreads();
-    const int vh = min(T2, H2 - oy0), vw = min(T2, W2 - ox0);
-    gram_group(su, 4 * wv, q, o, vh, vw, c00, c01, c11);
-    gram_group(su, 4 * wv + 2, q, o, vh, vw, c00, c01, c11);
+    const int vh = min(GT, H2 - oy0), vw = min(GT, W2 - ox0);
+#pragma unroll 2
+    for (int rr = 0; rr < GT / 4; ++rr) gram_group<GR>(su, 8 * wv + rr, q, o, vh, vw, c00, c01, c11);
   }
   EUNET_DASSERT(a.gram != nullptr);
   gram_store(red, a.gram + (long long)blockIdx.x * GRAM_LD, c00, c01, c11);
@@ -1561,7 +1606,12 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     int rows = L.grid4;
     if (mf) {  // statistics from the im2col second moments (one stats row)
       a.gram = wsf + L.gram;
-      HEAD_DISPATCH(head_gram_mfma_kernel, L.grid4, NT, 0, s);
+      HeadArgs ag = a;  // the Gram pass tiles 2H in 32 x 32
+      ag.tx = cdiv(2 * w, GT); ag.ty = cdiv(2 * h, GT); ag.ntiles = n * ag.tx * ag.ty;
+      {
+        const HeadArgs a = ag;
+        HEAD_DISPATCH(head_gram_mfma_kernel, L.grid4, NT, 0, s);
+      }
       EUNET_LAUNCH_CHECK("head_gram");
       int rc = eunet_colsum_ld(a.gram, L.grid4, GRAM_LD, GRAM_LD, wsf + L.gsum, wsf + L.cws, s);
       if (rc) return rc;
