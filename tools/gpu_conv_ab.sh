@@ -10,7 +10,7 @@ done
 for i in $(seq 1 ${ROUNDS:-1}); do
   for L in $LIBS; do
     t=$(basename $L .so)
-    EUNET_LIB=$L timeout -k 10 150 python tools/conv_bench.py --transform --reps 10 > gpurun_out/cb_$t.log 2>&1 || { echo "cb failed $L"; tail -3 gpurun_out/cb_$t.log; exit 1; }
+    EUNET_LIB=$L timeout -k 10 150 python tools/conv_bench.py --transform --reps 10 ${CB_ARGS:-} > gpurun_out/cb_$t.log 2>&1 || { echo "cb failed $L"; tail -3 gpurun_out/cb_$t.log; exit 1; }
     echo "$t $(grep summary gpurun_out/cb_$t.log)"
   done
 done
