@@ -1093,172 +1093,6 @@ bool act_ok(const eunet_act* a) {
 int elems16(int dtype) { return dtype == EUNET_BF16 ? 8 : 4; }
 int kchunk(int dtype) { return 4 * elems16(dtype); }
 
-
-// ---------------------------------------------------------------------------
-// Pipelined bf16 forward / data gradient (CONV_PIPE builds; plain conv only: no operand transform, no
-// BN partials, no fused BN-backward reduction, no bias / Dropout scale).  One 8-wave block per CU,
-// persistent over (tile, co-block) work items; the K-chunks of all its items form one sequence of
-// steps whose operands (the halo [4 q][640][16 B] and the weights [4 q][64 co][9][16 B] of a chunk)
-// are copied into one of two LDS stages by LDS-DMA two steps ahead: the copy of step j+1 is in
-// flight during step j's MFMAs and the epilogue, and the wait before each step is a counted vmcnt
-// (never 0 inside the sequence).  Wave w computes rows 2w, 2w+1 (64 px) x 64 co with the operands
-// swapped (weights as the A operand) so a lane holds 4 consecutive channels of one pixel; the
-// epilogue packs them to bf16 in the free stage and stores whole 16-byte units.
-// ---------------------------------------------------------------------------
-#ifndef CONV_PIPE
-#define CONV_PIPE 0
-#endif
-constexpr int PT = 512;                          // threads (8 waves)
-constexpr int P_STAGE = FA_BYTES + B_LDS_BYTES;  // 77824
-constexpr int P_DMA = 10;                        // LDS-DMA wave-instructions per wave per step (80 per block:
-                                                 // 40 halo + 36 weight + 4 to a dummy slot)
-constexpr int P_LDS = 2 * P_STAGE + 1024;        // two stages + the dummy slot
-constexpr int P_OLD = 72;                        // bf16 row stride of the epilogue tile (144 B)
-static_assert(P_LDS <= 160 * 1024, "pipelined conv LDS");
-static_assert(FTH * FTW * P_OLD * 2 <= P_STAGE, "epilogue tile fits a stage");
-
-// One LDS-DMA wave-instruction (16 B per lane into lds + 16 lane) in inline asm: the compiler then
-// neither counts it nor guards the stage reads with its own vmcnt(0) (it would for the builtin: every
-// ds_read may alias the pending DMA), so the counted waits below are the only ones.
-__device__ __forceinline__ void pipe_dma16(const void* src, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(src) : "memory");
-}
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-__global__ __launch_bounds__(PT, 1) void conv3x3_pipe_kernel(FwdArgs a, int nitems) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int q = lane >> 4, li = lane & 15;
-  const int ncob = a.cout_pad / BN, tpi = a.tx * a.ty;
-  const int my_items = nitems > (int)blockIdx.x ? (nitems - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  const int nsteps = my_items * a.nkc;
-  const long long slice = (long long)a.H * a.W * a.xct;
-  // LDS-DMA of step j into stage st.  Wave-instruction r of this wave moves unit group ii = wv + 8r:
-  // 0..39 halo (quarter ii / 10, slots 64 (ii % 10) ..), 40..75 weights, 76..79 a dummy slot.  The
-  // per-lane sources of an item are computed when its first chunk is issued; later chunks add kc x
-  // the lane's chunk stride (0 for padding lanes, which read the zero vector).
-  uint32_t soff[P_DMA];  // per lane: byte offset of the source from the group's base, ~0u: padding (zero vector)
-  const char* xbase = (const char*)a.x;
-  auto item_bases = [&](int item) {
-    int ln = lane;
-    asm volatile("" : "+v"(ln));  // per-lane index math stays here (hoisted out of the step loop it spills)
-    const int tile = item / ncob, cob = item - tile * ncob;
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
-    xbase = (const char*)((const bf16_t*)a.x + __builtin_amdgcn_readfirstlane(n) * slice);
-#pragma unroll
-    for (int r = 0; r < P_DMA; ++r) {
-      const int ii = wv + 8 * r;
-      soff[r] = ~0u;
-      if (ii < 40) {
-        const int qq = ii / 10, hp = (ii - qq * 10) * 64 + ln;
-        const int hy = hp / FHW, hx = hp - hy * FHW, yy = y0 + hy - 1, xx = x0 + hx - 1;
-        if (hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-          soff[r] = (uint32_t)(((yy * a.W + xx) * a.xct + a.xco + qq * 8) * 2);
-      } else if (ii < 76) {
-        const int id = (ii - 40) * 64 + ln;
-        soff[r] = (uint32_t)(((((id / (BN * 9)) * a.cout_pad + cob * BN) * 9 + id % (BN * 9)) * 16));
-      }
-    }
-  };
-  auto issue = [&](int j, int st) {
-    const int kc = j % a.nkc;
-    if (kc == 0) item_bases((int)blockIdx.x + (j / a.nkc) * (int)gridDim.x);
-    char* stage = smem + st * P_STAGE;
-#pragma unroll
-    for (int r = 0; r < P_DMA; ++r) {
-      const int ii = wv + 8 * r;
-      char* dst = ii < 40 ? stage + ((ii / 10) * FHPXP + (ii % 10) * 64) * 16
-                          : ii < 76 ? stage + FA_BYTES + (ii - 40) * 64 * 16 : smem + 2 * P_STAGE;
-      const char* base = ii < 40 ? xbase + kc * 64 : (const char*)a.wp + (long long)kc * (4 * a.cout_pad * 9 * 16);
-      const char* src = soff[r] == ~0u ? (const char*)&g_conv_zero : base + soff[r];
-      pipe_dma16(src, __builtin_amdgcn_readfirstlane(lds_addr(dst)));
-    }
-  };
-  if (nsteps > 0) issue(0, 0);
-  if (nsteps > 1) issue(1, 1);
-  f32x4 acc[4][4];
-  for (int j = 0; j < nsteps; ++j) {
-    const int st = j & 1, kc = j % a.nkc;
-    if (j + 1 < nsteps) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's copy of step j has landed
-    __builtin_amdgcn_sched_barrier(0);
-    if (kc == 0) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    const char* As = smem + st * P_STAGE;
-    const char* Bs = As + FA_BYTES;
-    __builtin_amdgcn_s_setprio(1);
-    uint4 fa[2][4], fb[2][4];  // the next tap's fragments in flight during the current tap's MFMAs
-    auto frags = [&](int t, uint4 (&b)[4], uint4 (&f)[4]) {
-      const int ky = t / 3, kx = t - 3 * ky;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) b[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        f[mt] = *(const uint4*)(As + (q * FHPXP + (2 * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx) * 16);
-    };
-    frags(0, fb[0], fa[0]);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t + 1 < 9) frags(t + 1, fb[(t + 1) & 1], fa[(t + 1) & 1]);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[t & 1][nt]),
-                                                               __builtin_bit_cast(bf16x8, fa[t & 1][mt]), acc[mt][nt], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading stage st
-    __builtin_amdgcn_sched_barrier(0);
-    if (kc == a.nkc - 1) {  // item done: bf16 tile through the free stage, 16-byte stores
-      const int item = (int)blockIdx.x + (j / a.nkc) * (int)gridDim.x;
-      const int tile = item / ncob, cob = item - tile * ncob;
-      const int n = tile / tpi, trem = tile - n * tpi;
-      const int y0 = (trem / a.tx) * FTH, x0 = (trem % a.tx) * FTW;
-      bf16_t* stg = (bf16_t*)(smem + st * P_STAGE);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int px = (2 * wv + (mt >> 1)) * FTW + (mt & 1) * 16 + li;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const uint32_t lo = (uint32_t)f2bf(acc[mt][nt][0]) | ((uint32_t)f2bf(acc[mt][nt][1]) << 16);
-          const uint32_t hi = (uint32_t)f2bf(acc[mt][nt][2]) | ((uint32_t)f2bf(acc[mt][nt][3]) << 16);
-          *(uint2*)(stg + px * P_OLD + nt * 16 + 4 * q) = make_uint2(lo, hi);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
-#pragma unroll
-      for (int k = 0; k < FTH * FTW * 8 / PT; ++k) {
-        const int u = tid + k * PT, px = u >> 3, cu = u & 7;
-        const int r = px / FTW, c = px - r * FTW, co = cob * BN + cu * 8;
-        const uint4 v = *(const uint4*)(stg + px * P_OLD + cu * 8);
-        if (r < vh && c < vw && co < a.cout) {
-          const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
-          EUNET_DASSERT(pix < (long long)a.N * a.H * a.W && a.yco + co + 8 <= a.yct);
-          *(uint4*)((bf16_t*)a.y + pix * a.yct + a.yco + co) = v;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // the tile's LDS reads are done before stage st is refilled
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (j + 2 < nsteps) issue(j + 2, st);
-  }
-}
-
 template <bool DG>
 int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, bool bt = false) {
   const long long esz = dtype == EUNET_BF16 ? 2 : 4;
@@ -1266,20 +1100,6 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, 
                 "conv3x3: one sample's input (%d x %d x %d) must be < 3 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
   EUNET_REQUIRE((long long)a.nkc * kchunk(dtype) * a.cout_pad * 9 * esz < (1ll << 31), "conv3x3: packed weights >= 2 GiB");
   dim3 grid(a.ntiles * (a.cout_pad / BN));
-  if (CONV_PIPE && dtype == EUNET_BF16 && !out_f32 && !bt && a.cin % 32 == 0 && a.isc == nullptr && a.stats == nullptr &&
-      a.bpart == nullptr && a.gsc == nullptr && a.bias == nullptr && a.tcoef == nullptr) {
-    static int ncu = 0;
-    if (ncu == 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        ncu = 256;
-    }
-    const int items = a.ntiles * (a.cout_pad / BN);
-    allow_lds(conv3x3_pipe_kernel, P_LDS);
-    conv3x3_pipe_kernel<<<std::min(items, ncu), PT, P_LDS, (hipStream_t)stream>>>(a, items);
-    EUNET_LAUNCH_CHECK("conv3x3_pipe");
-    return EUNET_OK;
-  }
   if (dtype == EUNET_BF16 && out_f32) {
     allow_lds(conv3x3_fwd_kernel<bf16_t, true, float>, FWD_LDS);
     conv3x3_fwd_kernel<bf16_t, true, float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
