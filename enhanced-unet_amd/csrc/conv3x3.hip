@@ -1297,7 +1297,10 @@ int eunet_conv3x3_dgrad_fused(const eunet_act* g, const eunet_act* y_in, const f
 
 // weight-gradient blocks per launch: two resident per CU (1024 / 2048 measured equal / slower in
 // the bench, where the wgrad shares the chip with the data-gradient stream: profiles/r02_ab_conv.txt)
-constexpr int WG_BLOCKS = 512;
+#ifndef WG_BLOCKS_N
+#define WG_BLOCKS_N 512
+#endif
+constexpr int WG_BLOCKS = WG_BLOCKS_N;  // weight-gradient blocks per launch (two per CU)
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
   const bool bf = dtype == EUNET_BF16;
