@@ -15,6 +15,87 @@ from ._lib import Act, call, c_int, c_size_t
 
 DTYPES = {torch.float32: _lib.EUNET_F32, torch.bfloat16: _lib.EUNET_BF16}
 
+# ---- torch.ops.eunet.* ---------------------------------------------------------------------------
+# The network's device ops are registered with PyTorch's dispatcher (library "eunet", CUDA key), so they
+# appear as eunet::<op> in torch.profiler traces and go through dispatcher hooks.  A
+# decorated function keeps its Python signature: its arguments are flattened into the op schema
+# (an Act becomes (tensor, coff, c)), the dispatcher calls the CUDA impl, which rebuilds the Acts and
+# runs the original body (one C-ABI call).  Cost ~2 us of dispatcher per call (USE_DISPATCHER = False
+# calls the bodies directly; tools/ab_attr.py ops.USE_DISPATCHER=0).
+USE_DISPATCHER = True
+_LIB = torch.library.Library("eunet", "DEF")
+DISPATCHED: dict = {}
+
+
+def _dispatched(kinds: str, returns_tensor: bool = False):
+    """kinds: one token per parameter -- A (Act), T (tensor), i (int), f (float), b (bool), d (torch dtype),
+    s (str); A! / T! mark the arguments the op writes, a trailing ? an optional (None-able) argument."""
+    import inspect
+    import string
+
+    ks = kinds.split()
+
+    def deco(fn):
+        sig = inspect.signature(fn)
+        names = list(sig.parameters)
+        if len(names) != len(ks):
+            raise _lib.EunetError(f"_dispatched({fn.__name__}): {len(names)} parameters, {len(ks)} kinds")
+        letters = iter(string.ascii_lowercase)
+        parts = []
+        for nm, k in zip(names, ks):
+            q = "?" if k.endswith("?") else ""
+            base = k.rstrip("?")
+            w = base.endswith("!")
+            base = base.rstrip("!")
+            if base in ("A", "T"):
+                ty = f"Tensor({next(letters)}!){q}" if w else f"Tensor{q}"
+                parts += [f"{ty} {nm}"] + ([f"int {nm}_coff", f"int {nm}_c"] if base == "A" else [])
+            else:
+                parts.append({"i": "int", "f": "float", "b": "bool", "d": "ScalarType", "s": "str"}[base] + f"{q} {nm}")
+        _LIB.define(f"{fn.__name__}({', '.join(parts)}) -> {'Tensor' if returns_tensor else '()'}")
+
+        def impl(*flat):
+            args, j = [], 0
+            for k in ks:
+                if k.startswith("A"):
+                    t, coff, c = flat[j:j + 3]
+                    j += 3
+                    args.append(None if t is None else act(t, coff, c))
+                else:
+                    args.append(flat[j])
+                    j += 1
+            return fn(*args)
+
+        _LIB.impl(fn.__name__, impl, "CUDA")
+        _LIB.impl(fn.__name__, impl, "CPU")  # raises EunetError in _ptr / act: no CPU fallback
+        op = getattr(torch.ops.eunet, fn.__name__)
+
+        defaults = [p.default for p in sig.parameters.values()]
+        index = {nm: i for i, nm in enumerate(names)}
+        isact = [k.startswith("A") for k in ks]
+
+        def wrapper(*args, **kwargs):
+            if not USE_DISPATCHER:
+                return fn(*args, **kwargs)
+            vals = list(args) + defaults[len(args):]
+            for nm, v in kwargs.items():
+                vals[index[nm]] = v
+            flat = []
+            for a, v in zip(isact, vals):
+                if not a:
+                    flat.append(v)
+                elif v is None:
+                    flat += (None, 0, 0)
+                else:
+                    flat += (v._keep, v.coff, v.c)
+            return op(*flat)
+
+        wrapper.__name__, wrapper.__doc__, wrapper.__wrapped__ = fn.__name__, fn.__doc__, fn
+        DISPATCHED[fn.__name__] = op
+        return wrapper
+
+    return deco
+
 
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -44,6 +125,7 @@ def _ref(a):
     return None if a is None else ctypes.byref(a)
 
 
+@_dispatched("T T!")
 def nchw_to_nhwc(x: torch.Tensor, out: torch.Tensor):
     call("eunet_nchw_to_nhwc", _ptr(x), ctypes.byref(act(out)), _stream())
 
@@ -54,6 +136,7 @@ def conv3x3_packed_bytes(cout, cin, dtype):
     return b.value
 
 
+@_dispatched("T d b", returns_tensor=True)
 def conv3x3_pack(w: torch.Tensor, dtype, flip: bool) -> torch.Tensor:
     cout, cin = w.shape[0], w.shape[1]
     nbytes = conv3x3_packed_bytes(cin if flip else cout, cout if flip else cin, dtype)
@@ -87,6 +170,7 @@ def conv3x3_tiles(y_act: Act) -> int:
     return t.value
 
 
+@_dispatched("A T A! T? T? T? T!? i s?")
 def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=None, nstride=0, sub=None):
     """nstride > 0: scale/shift are per-sample [N][nstride] (BN+ReLU+Dropout2d folded).
     sub: optional kprof sub-family the launch is also credited to (e.g. the encoder forward convs)."""
@@ -99,6 +183,7 @@ def conv3x3_fwd(x: Act, wp, y: Act, bias=None, scale=None, shift=None, stats=Non
              ctypes.byref(y), _ptr(stats), _stream())
 
 
+@_dispatched("A T A! T?")
 def conv3x3_dgrad(dy: Act, wp_t, gx: Act, gscale=None):
     """plain dgrad (the block-input gradient): gx = conv(dy, W'), wp_t packed with flip=True."""
     flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
@@ -108,6 +193,7 @@ def conv3x3_dgrad(dy: Act, wp_t, gx: Act, gscale=None):
         call("eunet_conv3x3_dgrad", ctypes.byref(dy), _ptr(wp_t), ctypes.byref(gx), _ptr(gscale), _stream())
 
 
+@_dispatched("A T A! A T T T T T! T?")
 def conv3x3_dgrad_bnbwd(dy: Act, wp_t, gx: Act, y: Act, mean, invstd, scale, shift, part, gscale=None):
     """dgrad + the BN-backward partial sums of the layer it feeds (see eunet.h)."""
     flops = 2.0 * 9 * dy.c * gx.c * dy.n * dy.h * dy.w
@@ -124,6 +210,7 @@ def conv3x3_wgrad_splits(dy: Act, cin: int, dtype) -> int:
     return s.value
 
 
+@_dispatched("A A T A!? T A! A? T? T? T? T? T!? T?")
 def conv3x3_dgrad_fused(g: Act, y_in: Act, coef, gy_out: Act | None, wp_t, gx: Act, y_next: Act | None = None,
                         mean=None, invstd=None, scale=None, shift=None, part=None, gscale=None):
     """Data gradient with the BN backward of the differentiated layer fused into the operand staging
@@ -140,6 +227,7 @@ def conv3x3_dgrad_fused(g: Act, y_in: Act, coef, gy_out: Act | None, wp_t, gx: A
              _ptr(gscale), _stream())
 
 
+@_dispatched("A A T! T!? i T? T? i")
 def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=None, nstride=0):
     flops = 2.0 * 9 * x.c * dy.c * x.n * x.h * x.w
     esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
@@ -151,11 +239,13 @@ def conv3x3_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit, scale=None, shift=N
              _ptr(db_part), nsplit, _stream())
 
 
+@_dispatched("T T? i i i i T! T!?")
 def wgrad_reduce(dw_part, db_part, nsplit, cout, cin, taps, dw, db):
     call("eunet_wgrad_reduce", _ptr(dw_part), _ptr(db_part), nsplit, cout, cin, taps, _ptr(dw), _ptr(db),
          _stream())
 
 
+@_dispatched("A T T? A! T!?")
 def conv_small_fwd(x: Act, w, bias, y: Act, stats=None):
     call("eunet_conv_small_fwd", ctypes.byref(x), _ptr(w), _ptr(bias), ctypes.byref(y), _ptr(stats), _stream())
 
@@ -166,11 +256,13 @@ def conv_small_wgrad_splits(dy: Act) -> int:
     return s.value
 
 
+@_dispatched("A A T! T!? i")
 def conv_small_wgrad(x: Act, dy: Act, dw_part, db_part, nsplit):
     call("eunet_conv_small_wgrad", ctypes.byref(x), ctypes.byref(dy), _ptr(dw_part), _ptr(db_part), nsplit,
          _stream())
 
 
+@_dispatched("T i i T T f f T!? T!? T!? T!? T!? T!? T!?")
 def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, mean, invstd, scale, shift,
                 num_batches_tracked=None):
     call("eunet_bn_finalize", _ptr(stats), tiles, c, _ptr(gamma), _ptr(beta), float(eps), float(momentum),
@@ -178,24 +270,29 @@ def bn_finalize(stats, tiles, c, gamma, beta, eps, momentum, run_mean, run_var, 
          _ptr(num_batches_tracked), _stream())
 
 
+@_dispatched("T T T T f T! T!")
 def bn_eval_affine(gamma, beta, run_mean, run_var, eps, scale, shift):
     call("eunet_bn_eval_affine", gamma.numel(), _ptr(gamma), _ptr(beta), _ptr(run_mean), _ptr(run_var),
          float(eps), _ptr(scale), _ptr(shift), _stream())
 
 
+@_dispatched("A T T A!")
 def bnrelu(y: Act, scale, shift, out: Act):
     call("eunet_bnrelu", ctypes.byref(y), _ptr(scale), _ptr(shift), ctypes.byref(out), _stream())
 
 
+@_dispatched("A T T A!? A!")
 def bnrelu_pool(y: Act, scale, shift, act_out: Act | None, pooled: Act):
     call("eunet_bnrelu_pool", ctypes.byref(y), _ptr(scale), _ptr(shift), _ref(act_out), ctypes.byref(pooled),
          _stream())
 
 
+@_dispatched("A T T A!")
 def bnrelu_upsample(y: Act, scale, shift, out: Act):
     call("eunet_bnrelu_upsample", ctypes.byref(y), _ptr(scale), _ptr(shift), ctypes.byref(out), _stream())
 
 
+@_dispatched("A T T T T i T!")
 def bnrelu_conv1x1(y: Act, scale, shift, w, b, k, z):
     call("eunet_bnrelu_conv1x1", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), _ptr(b), k, _ptr(z),
          _stream())
@@ -207,6 +304,7 @@ def head_workspace_bytes(n, h, w, k, dtype=torch.float32):
     return b.value
 
 
+@_dispatched("T i i i i T T T T T T b f f T!? T!? T!? T!? T!? T!? T! d")
 def head_fwd(z, n, h, w, k, w1, b1, gamma, beta, w2, b2, training, eps, momentum, run_mean, run_var, mean,
              invstd, out2h, logits, ws, dtype=torch.float32):
     call("eunet_head_fwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2), _ptr(b2),
@@ -214,6 +312,7 @@ def head_fwd(z, n, h, w, k, w1, b1, gamma, beta, w2, b2, training, eps, momentum
          _ptr(out2h), _ptr(logits), DTYPES[dtype], _ptr(ws), _stream())
 
 
+@_dispatched("T i i i i T T T T T T T T? T? T! T! T! T! T! T! T! T! d")
 def head_bwd(z, n, h, w, k, w1, b1, gamma, beta, w2, mean, invstd, g_logits, g_out2h, gz, gw1, gb1, ggamma,
              gbeta, gw2, gb2, ws, dtype=torch.float32):
     call("eunet_head_bwd", _ptr(z), n, h, w, k, _ptr(w1), _ptr(b1), _ptr(gamma), _ptr(beta), _ptr(w2),
@@ -258,11 +357,13 @@ def bn_bwd_tiles(y: Act) -> int:
     return t.value
 
 
+@_dispatched("A A T T T T T!")
 def bn_bwd_reduce(g: Act, y: Act, mean, invstd, scale, shift, part):
     call("eunet_bn_bwd_reduce", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale),
          _ptr(shift), _ptr(part), _stream())
 
 
+@_dispatched("T i i T! i? T!?")
 def colsum(part, rows, cols, out, split=None, out_hi=None):
     """Column sums of part [rows][cols] -> out (or out[:split] / out_hi[:cols - split])."""
     b = c_size_t()
@@ -274,27 +375,32 @@ def colsum(part, rows, cols, out, split=None, out_hi=None):
         call("eunet_colsum_split", _ptr(part), rows, cols, int(split), _ptr(out), _ptr(out_hi), _ptr(ws), _stream())
 
 
+@_dispatched("A A T T T T T T A!")
 def bn_bwd_apply(g: Act, y: Act, mean, invstd, scale, shift, dbeta, dgamma, gy: Act):
     """scale / shift: the BN's forward affine (they define the ReLU mask, see eunet.h)."""
     call("eunet_bn_bwd_apply", ctypes.byref(g), ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale),
          _ptr(shift), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
 
 
+@_dispatched("T T T T T T i T!")
 def bn_bwd_coef(mean, invstd, scale, shift, dbeta, dgamma, count: int, coef):
     """coef [4][C] = (k1, kq, k2, k3) of gy = k1 g [y k1 + kq > 0] + k2 y + k3 (count = N*H*W)."""
     call("eunet_bn_bwd_coef", _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(dbeta), _ptr(dgamma),
          int(count), int(mean.numel()), _ptr(coef), _stream())
 
 
+@_dispatched("A A T A!")
 def bn_bwd_apply_coef(g: Act, y: Act, coef, gy: Act):
     call("eunet_bn_bwd_apply_coef", ctypes.byref(g), ctypes.byref(y), _ptr(coef), ctypes.byref(gy), _stream())
 
 
+@_dispatched("A A A? A!")
 def pool_bwd_add(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act):
     call("eunet_pool_bwd_add", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), ctypes.byref(gout),
          _stream())
 
 
+@_dispatched("A A!")
 def upsample_bwd(ghi: Act, glo: Act):
     call("eunet_upsample_bwd", ctypes.byref(ghi), ctypes.byref(glo), _stream())
 
@@ -305,6 +411,7 @@ def pool_bwd_add_bnr_rows(gout: Act) -> int:
     return r.value
 
 
+@_dispatched("A A A? A! A T T T T T!")
 def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act, y: Act, mean, invstd, scale, shift,
                      part):
     """pool_bwd_add + the BN-backward partial sums of the block whose output gradient gout is."""
@@ -318,6 +425,7 @@ def upsample_bwd_bnr_rows(glo: Act) -> int:
     return r.value
 
 
+@_dispatched("A A! A T T T T T!")
 def upsample_bwd_bnr(ghi: Act, glo: Act, y: Act, mean, invstd, scale, shift, part):
     """upsample_bwd + the BN-backward partial sums of the block whose output gradient glo is."""
     call("eunet_upsample_bwd_bnr", ctypes.byref(ghi), ctypes.byref(glo), ctypes.byref(y), _ptr(mean), _ptr(invstd),
@@ -330,11 +438,13 @@ def conv1x1_bwd_tiles(y: Act) -> int:
     return t.value
 
 
+@_dispatched("A T T T i T A! T!?")
 def conv1x1_bwd(y: Act, scale, shift, w, k, gz, gact: Act, part):
     call("eunet_conv1x1_bwd", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),
          ctypes.byref(gact), _ptr(part), _stream())
 
 
+@_dispatched("A T T T i T A! T!? T T T!")
 def conv1x1_bwd_bnr(y: Act, scale, shift, w, k, gz, gact: Act, part, mean, invstd, bn_part):
     """conv1x1_bwd + the BN-backward partial sums [tiles][2][C] of y's BatchNorm over gact."""
     call("eunet_conv1x1_bwd_bnr", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),

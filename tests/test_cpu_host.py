@@ -224,3 +224,20 @@ def test_loader_shuffle_matches_torch_random_sampler():
         ref = [i for b in tud.DataLoader(_Items(), batch_size=4, shuffle=shuffle, collate_fn=ident) for i in b]
         assert ours == ref and sorted(ours) == list(range(23))
         assert ours_next == torch.rand(1).item()
+
+
+def test_network_ops_registered_with_the_dispatcher():
+    """The network's device ops are torch.ops.eunet.* (SURVEY.md §8b): one schema per C-ABI entry point, the
+    written arguments alias-annotated, CPU tensors rejected (no CPU fallback) through the dispatcher too."""
+    from eunet import EunetError, ops
+    expect = {"conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bnbwd", "conv3x3_dgrad_fused", "conv3x3_wgrad",
+              "wgrad_reduce", "conv_small_fwd", "conv_small_wgrad", "bn_finalize", "bnrelu_pool", "bnrelu_upsample",
+              "bnrelu_conv1x1", "head_fwd", "head_bwd", "bn_bwd_apply", "bn_bwd_coef", "bn_bwd_apply_coef",
+              "pool_bwd_add_bnr", "upsample_bwd_bnr", "conv1x1_bwd_bnr", "colsum", "conv3x3_pack"}
+    assert expect <= set(ops.DISPATCHED)
+    sch = str(torch.ops.eunet.conv3x3_fwd.default._schema)
+    assert sch.startswith("eunet::conv3x3_fwd(Tensor x, int x_coff, int x_c, Tensor wp, Tensor(a!) y,"), sch
+    assert "Tensor(b!)? stats" in sch
+    assert str(torch.ops.eunet.conv3x3_pack.default._schema).endswith("-> Tensor")
+    with pytest.raises(EunetError):
+        torch.ops.eunet.bn_bwd_coef(*[torch.zeros(4)] * 6, 16, torch.zeros(16))

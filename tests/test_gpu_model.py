@@ -500,3 +500,30 @@ def test_step_graph_train_epoch_and_bad_targets():
     with pytest.raises(ValueError, match="outside"):
         tb.train_epoch(bad)
     tb.train_epoch(batches)  # the accumulator was cleared at the raise: no error carried over
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_dispatcher_path_is_exact_and_visible(dtype, monkeypatch):
+    """The network ops run through torch.ops.eunet.* (the default) or directly (ops.USE_DISPATCHER =
+    False): two Trainer steps give bit-identical losses and parameters, and torch.profiler records the
+    eunet:: ops of a step."""
+    from eunet import ops
+    from eunet.train_eval import Trainer
+    batches = _graph_batches(2)
+    ta = Trainer(_model(16, 3, 3, dtype), DEV, "enhanced_unet", total_epochs=12)
+    tb = Trainer(_model(16, 3, 3, dtype), DEV, "enhanced_unet", total_epochs=12)
+    for x, m in batches:
+        monkeypatch.setattr(ops, "USE_DISPATCHER", True)
+        la = ta.step(x, m, sync_loss=False)
+        monkeypatch.setattr(ops, "USE_DISPATCHER", False)
+        lb = tb.step(x, m, sync_loss=False)
+        assert torch.equal(la, lb)
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
+    monkeypatch.setattr(ops, "USE_DISPATCHER", True)
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU]) as prof:
+        ta.step(*batches[0], sync_loss=False)
+        torch.cuda.synchronize()
+    names = {e.key for e in prof.key_averages()}
+    for op in ("eunet::conv3x3_fwd", "eunet::conv3x3_wgrad", "eunet::head_bwd", "eunet::bn_finalize"):
+        assert op in names, (op, sorted(n for n in names if n.startswith("eunet::")))

@@ -12,10 +12,14 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "enhanced-unet_amd")]
 argv = sys.argv[1:]
 sep = argv.index("--") if "--" in argv else len(argv)
 sets, rest = argv[:sep], argv[sep + 1:]
+from eunet import ops  # noqa: E402
 from eunet.engine import UNetEngine  # noqa: E402
 for kv in sets:
     k, v = kv.split("=")
-    setattr(UNetEngine, k, bool(int(v)))
+    if k.startswith("ops."):  # module switches of eunet.ops (e.g. ops.USE_DISPATCHER=0)
+        setattr(ops, k[4:], bool(int(v)))
+    else:
+        setattr(UNetEngine, k, bool(int(v)))
 import bench  # noqa: E402
 sys.argv = ["bench.py"] + rest
 bench.main()
