@@ -62,13 +62,17 @@ class Trainer:
         self.warmup_scheduler = torch.optim.lr_scheduler.LinearLR(
             self.optimizer, start_factor=0.001, end_factor=1.0, total_iters=self.warmup_epochs)
         self.dp = None  # eunet.dp.DataParallel when training on several GPUs
-        # step_graph: replay deferred-loss steps from a captured HIP graph (StepGraph) once
-        # graph_warmup eager steps have run; re-captured when the shapes, the learning rate or the
-        # engine schedule change
+        # step_graph: replay deferred-loss steps from captured HIP graphs (StepGraph) once
+        # graph_warmup eager steps have run; one graph per batch shape (a ragged last batch keeps
+        # its own), at most graph_cache of them, re-captured when the engine schedule, the loss
+        # parameters or the parameter storage change (not the learning rate: AdamW runs eagerly)
         self.step_graph = False
         self.graph_warmup = 2
-        self._graph = None
+        self.graph_cache = 4
+        self._graphs = {}  # key -> StepGraph, least recently used first
+        self._graph = None  # the graph of the last replayed step
         self._graph_warm = 0
+        self.graph_captures = 0
 
     # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
     def loss_params(self):
@@ -132,19 +136,39 @@ class Trainer:
 
     def _graphed_step(self, images, masks):
         key = StepGraph.key(self, images, masks)
-        g = self._graph
-        if g is not None and g.key == key:
-            return g.replay(images, masks)
-        self._graph = None  # release the old graph's memory pool before capturing anew
-        if self._graph_warm < self.graph_warmup:
-            # eager warm-up steps (real steps): lazy allocations, fused-AdamW state, the loss tables'
-            # host copies, every kernel's first launch happen outside the capture
-            self._graph_warm += 1
-            return self._step(images, masks, False)
-        self._graph = StepGraph(self, images, masks, key)
-        return self._graph.replay(images, masks)
+        g = self._graphs.pop(key, None)
+        if g is None:
+            if self._graph_warm < self.graph_warmup:
+                # eager warm-up steps (real steps): lazy allocations, AdamW state, the loss tables'
+                # host copies, every kernel's first launch happen outside the capture
+                self._graph_warm += 1
+                return self._step(images, masks, False)
+            self._trim_graphs(max(1, self.graph_cache) - 1)  # free pools before capturing anew
+            g = StepGraph(self, images, masks, key)
+            self.graph_captures += 1
+        self._graphs[key] = g  # most recently used last
+        self._graph = g
+        self._trim_graphs(max(1, self.graph_cache))
+        return g.replay(images, masks)
+
+    def _trim_graphs(self, n):
+        """Drop least recently used graphs (and their memory pools) until n remain."""
+        while len(self._graphs) > n:
+            old = self._graphs.pop(next(iter(self._graphs)))
+            if old is self._graph:
+                self._graph = None
+            del old
 
     def _step(self, images, masks, sync_loss):
+        loss = self._forward_backward(images, masks, sync_loss)
+        self.optimizer.step()
+        if not sync_loss:
+            return loss.detach()
+        return loss.item()
+
+    def _forward_backward(self, images, masks, sync_loss):
+        """zero_grad, forward, loss, backward, DP all-reduce, clip_grad_norm_ (train_eval.py:244-345
+        up to the optimizer step); a StepGraph captures exactly this."""
         self.model.train()
         _, _, h, w = images.shape
         h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
@@ -173,10 +197,7 @@ class Trainer:
         if self.dp is not None:
             self.dp.after_backward()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1.0, foreach=True)
-        self.optimizer.step()
-        if not sync_loss:
-            return loss.detach()
-        return loss.item()
+        return loss
 
     def train_epoch(self, dataloader):
         """Mean loss over the epoch with one host sync at its end.  Out-of-range targets are counted
@@ -213,19 +234,22 @@ ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late",
 
 
 class StepGraph:
-    """One Trainer step (forward, fused loss, backward, clip_grad_norm_, fused AdamW) captured as a
-    HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch: one host launch
-    instead of several hundred, so a small tile (the reference's 640x480 batch of 2) is no longer
-    bound by Python + ctypes issue and the data loader's host work fits beside it.
+    """A Trainer step's forward, fused loss, backward and clip_grad_norm_ captured as a HIP graph
+    (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch, followed by the eager fused
+    AdamW step: two host calls instead of several hundred launches, so a small tile (the reference's
+    640x480 batch of 2) is no longer bound by Python + ctypes issue and the data loader's host work
+    fits beside it.
 
     A replay runs the eager step's kernels in the eager order with the same arguments: the engine
     launches on torch's current stream (the capture stream) and forks / joins its weight-gradient
     side stream with events; the loss adds its out-of-range target count into a persistent device
-    accumulator in place (losses.bad_target_accumulator); fused AdamW keeps its step count on the
-    device; clip_grad_norm_ and the BN running statistics never leave it.  What the graph bakes in
-    from the host is in key(): shapes, the optimizer's hyper-parameters (the learning rate changes
-    once per epoch -> one re-capture), the loss parameters, the engine schedule, and the parameter
-    / optimizer-state storage (load_state_dict replacing it -> re-capture)."""
+    accumulator in place (losses.bad_target_accumulator); clip_grad_norm_ and the BN running
+    statistics never leave the device.  The gradients live in the graph's memory pool: a replay
+    points the parameters' .grad at them before AdamW runs.  AdamW stays outside the graph because
+    its learning rate is a host double that changes every epoch (a device-tensor LR would be rounded
+    to fp32, and re-capturing per epoch costs more than the launches it saves).  What the graph
+    bakes in from the host is in key(): shapes, the loss parameters, the engine schedule and the
+    parameter storage (load_state_dict replacing it -> re-capture)."""
 
     def __init__(self, trainer, images, masks, key):
         from . import losses as _L
@@ -234,19 +258,14 @@ class StepGraph:
         self.images = torch.empty_like(images)
         self.masks = torch.empty_like(masks)
         _L.bad_target_accumulator(dev)
-        opt = trainer.optimizer
-        caps = [g.get("capturable", False) for g in opt.param_groups]
+        self.optimizer = trainer.optimizer
         self.graph = torch.cuda.CUDAGraph()
-        try:
-            for g in opt.param_groups:  # fused AdamW: the flag only gates torch's capture check
-                g["capturable"] = True
-            # thread_local: a DataLoader producer thread may launch and allocate on its own stream
-            # while this thread captures (the default global mode would invalidate the capture)
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-                self.loss = trainer._step(self.images, self.masks, False)
-        finally:
-            for g, c in zip(opt.param_groups, caps):
-                g["capturable"] = c
+        # thread_local: a DataLoader producer thread may launch and allocate on its own stream
+        # while this thread captures (the default global mode would invalidate the capture)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            self.loss = trainer._forward_backward(self.images, self.masks, False).detach()
+        self.params = [p for g in self.optimizer.param_groups for p in g["params"]]
+        self.grads = [p.grad for p in self.params]
 
     def replay(self, images, masks):
         from . import losses as _L
@@ -254,27 +273,23 @@ class StepGraph:
         self.masks.copy_(masks, non_blocking=True)
         self.graph.replay()
         _L.mark_pending()
+        for p, g in zip(self.params, self.grads):
+            if p.grad is not g:
+                p.grad = g
+        self.optimizer.step()
         return self.loss.clone()
 
     @staticmethod
     def key(trainer, images, masks):
-        opt = trainer.optimizer
-        hyper = tuple((g["lr"], g["weight_decay"], tuple(g["betas"]), g["eps"], g.get("amsgrad"), g.get("maximize"),
-                       g.get("fused"))
-                      for g in opt.param_groups)
-        if not all(h[-1] for h in hyper):
-            raise RuntimeError("Trainer.step_graph needs the fused AdamW (its step count lives on the device)")
         eng = getattr(trainer.model, "_engine", None)
         if getattr(eng, "drop_keep", None) is not None:
             raise RuntimeError("Trainer.step_graph: fixed dropout keep masks (a test hook) are host inputs")
         knobs = tuple(getattr(eng, k, None) for k in ENGINE_KNOBS)
-        ps = opt.param_groups[0]["params"]
-        st = opt.state.get(ps[-1], {})
-        store = (ps[0].data_ptr(), ps[-1].data_ptr()) + tuple(
-            st[k].data_ptr() for k in ("exp_avg", "exp_avg_sq", "step") if k in st)
+        ps = [p for g in trainer.optimizer.param_groups for p in g["params"]]
+        store = (id(trainer.optimizer), ps[0].data_ptr(), ps[-1].data_ptr(), len(ps))
         lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight)
-        return (tuple(images.shape), images.dtype, images.device, tuple(masks.shape), masks.dtype, hyper, knobs,
-                store, lossp)
+        return (tuple(images.shape), images.dtype, images.device, tuple(masks.shape), masks.dtype, knobs, store,
+                lossp)
 
 
 from .evaluator import Evaluator  # noqa: E402,F401  (train_eval.Evaluator, train_eval.py:356-904)

@@ -458,7 +458,7 @@ def test_step_graph_replay_is_exact(dtype):
     """Trainer.step_graph (StepGraph: the step captured as a HIP graph, replayed per batch) against
     eager steps from the same weights: every step's loss, the parameters, the AdamW moments and the
     BN running statistics agree bit for bit over 2 eager warm-up steps, a capture, replays, an LR
-    change (epoch_lr_step -> re-capture) and more replays."""
+    change (epoch_lr_step: AdamW runs outside the graph, so no re-capture) and more replays."""
     from eunet.train_eval import Trainer
     batches = _graph_batches(7)
     ta = Trainer(_model(16, 3, 3, dtype), DEV, "enhanced_unet", total_epochs=12)
@@ -471,7 +471,8 @@ def test_step_graph_replay_is_exact(dtype):
         la = ta.step(x, m, sync_loss=False)
         lb = tb.step(x, m, sync_loss=False)
         assert torch.equal(la, lb), i
-    assert tb._graph is not None and tb._graph.key[5][0][0] == tb.optimizer.param_groups[0]["lr"]
+    assert tb._graph is not None and tb.graph_captures == 1
+    assert ta.optimizer.param_groups[0]["lr"] == tb.optimizer.param_groups[0]["lr"] != 4e-3
     for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
         assert torch.equal(p, q), k
         sa, sb = ta.optimizer.state[p], tb.optimizer.state[q]
@@ -500,6 +501,34 @@ def test_step_graph_train_epoch_and_bad_targets():
     with pytest.raises(ValueError, match="outside"):
         tb.train_epoch(bad)
     tb.train_epoch(batches)  # the accumulator was cleared at the raise: no error carried over
+
+
+def test_step_graph_ragged_epochs_keep_one_graph_per_shape():
+    """An epoch whose last batch is smaller (an odd image count at batch 2) with an LR step between
+    epochs: one graph per batch shape, captured once and replayed in every later epoch, and the
+    epochs' mean losses and final parameters equal the eager trainer's bit for bit."""
+    from eunet.train_eval import Trainer
+    full = _graph_batches(4)
+    last = _graph_batches(1, B=1)
+    batches = [{"images": x, "batch_items": [{"semantic_mask": mm} for mm in m]} for x, m in full + last]
+    ta = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb.step_graph = True
+    for ep in range(3):
+        ta.epoch_lr_step(ep)
+        tb.epoch_lr_step(ep)
+        assert ta.train_epoch(batches) == tb.train_epoch(batches), ep
+    assert tb.graph_captures == 2 and len(tb._graphs) == 2
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
+    tb.graph_cache = 1  # a one-graph cache re-captures at every shape change and stays exact
+    for ep in range(3, 5):
+        ta.epoch_lr_step(ep)
+        tb.epoch_lr_step(ep)
+        assert ta.train_epoch(batches) == tb.train_epoch(batches), ep
+    assert tb.graph_captures == 5 and len(tb._graphs) == 1  # epoch 3: the last batch; epoch 4: both
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
