@@ -302,15 +302,19 @@ CHECKPOINT_KEYS = ("epoch", "model_state_dict", "optimizer_state_dict", "schedul
 
 def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num_epochs: int = 50,
                 skip_training: bool = False, *, train_loader=None, val_loader=None, save_dir: str = None,
-                model=None, verbose: bool = True, **model_kwargs):
+                model=None, verbose: bool = True, step_graph: bool = None, loader_workers: int = None,
+                **model_kwargs):
     """train_eval.train_model: per-epoch LR stepping (warmup LinearLR, then cosine restarts) before
     each train_epoch, semantic validation every 3 epochs, best-mIoU checkpoint in the reference's
     dict format ('checkpoints/<model>/best_model.pth'), early stop after patience 10 (epoch > 25).
 
     Without train_loader / val_loader it builds the reference's loaders (train_eval.py:1054-1075):
     eunet.data.CellDataset(data_dir, 'train' / 'val', max_size=640), batch 2 on cuda (1 otherwise),
-    the train split shuffled, val batch 1.  Any iterable of collate_fn batch dicts
-    ({'images', 'batch_items': [{'semantic_mask'}]}) may be passed instead, e.g. eunet.synth.loader."""
+    the train split shuffled, val batch 1; on cuda the training loader decodes in loader_workers
+    (default 4) worker processes and prefetches 2 batches (same augmentation draws, DataLoader).
+    Any iterable of collate_fn batch dicts ({'images', 'batch_items': [{'semantic_mask'}]}) may be
+    passed instead, e.g. eunet.synth.loader.  step_graph (default: on for the single-branch model on
+    cuda) replays the training steps from captured HIP graphs (Trainer.step_graph, bit-identical)."""
     import os
     from .models import get_model
     save_dir = save_dir or os.path.join("checkpoints", model_name)
@@ -322,9 +326,12 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
         from .data import CellDataset, DataLoader, collate_fn
         if data_dir is None:
             raise ValueError("train_model needs data_dir (a LabelMe directory) or explicit loaders")
-        batch_size = 2 if str(device).startswith("cuda") else 1  # train_eval.py:1058-1059
+        on_gpu = str(device).startswith("cuda")
+        batch_size = 2 if on_gpu else 1  # train_eval.py:1058-1059
+        workers = (4 if on_gpu else 0) if loader_workers is None else loader_workers
         train_loader = DataLoader(CellDataset(data_dir, split="train", max_size=640, device=device),
-                                  batch_size=batch_size, shuffle=True, collate_fn=collate_fn)
+                                  batch_size=batch_size, shuffle=True, collate_fn=collate_fn, workers=workers,
+                                  prefetch=2 if on_gpu else 0)
         if val_loader is None:
             val_loader = DataLoader(CellDataset(data_dir, split="val", max_size=640, device=device), batch_size=1,
                                     shuffle=False, collate_fn=collate_fn)
@@ -334,6 +341,9 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
                "val_dice": [], "learning_rate": [], "epoch_axis": []}
     train_epochs = num_epochs
     trainer = Trainer(model, device, model_name, total_epochs=train_epochs)
+    if step_graph is None:
+        step_graph = str(device).startswith("cuda") and not getattr(model, "dual_branch", False)
+    trainer.step_graph = bool(step_graph)
     best_loss, best_miou = float("inf"), 0.0
     patience = 10 if model_name == "enhanced_unet" else 8
     patience_counter = 0

@@ -245,3 +245,24 @@ def test_threaded_loader_stops_early(tmp_path):
     next(it)
     it.close()  # GeneratorExit at the yield -> the finally block stops and joins the producer
     assert not any(t.name == "eunet-loader" and t.is_alive() for t in threading.enumerate())
+
+
+def test_train_model_default_fast_path_is_exact(tmp_path):
+    """train_model from a LabelMe directory with its cuda defaults -- decode workers + prefetch and
+    the step replayed from HIP graphs (an odd train split, so every epoch ends on a 1-image batch,
+    with an LR step per epoch) -- ends with the parameters of the plain in-loop eager run, bit for bit."""
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import train_model
+    _write_cells(tmp_path, n=14)
+    finals = []
+    for graph, workers in ((True, None), (False, 0)):
+        random.seed(5)
+        np.random.seed(5)
+        torch.manual_seed(5)
+        model = EnhancedUNet(num_classes=3, in_channels=3, base_ch=16).to(DEV)
+        train_model("enhanced_unet", data_dir=str(tmp_path), device=DEV, num_epochs=2, model=model,
+                    save_dir=str(tmp_path / f"ck{int(graph)}"), verbose=False,
+                    step_graph=None if graph else False, loader_workers=workers)
+        finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+    for k in finals[0]:
+        assert torch.equal(finals[0][k], finals[1][k]), k
