@@ -720,6 +720,17 @@ __device__ __forceinline__ bf16x8 go_frag(int q, const float (&go)[K]) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
 __device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two channels per instruction, each element
+// rounded as the scalar op would round it)
+#ifndef HEAD_PK
+#define HEAD_PK 1
+#endif
+__device__ __forceinline__ f32x4 ld4v(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x2 half2(const f32x4& v, int hp) { return hp ? v.hi : v.lo; }
+__device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 relu_sel(f32x2 pre, f32x2 v) {  // v where pre > 0, else 0
+  return (f32x2){pre.x > 0.f ? v.x : 0.f, pre.y > 0.f ? v.y : 0.f};
+}
 
 // sum over the 16 pixel lanes of a row (lanes with equal q)
 __device__ __forceinline__ float sum_x16(float v) {
@@ -1039,7 +1050,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
     __syncthreads();
     stage_u(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
+#ifndef HEAD_OUT_UNROLL
+#define HEAD_OUT_UNROLL 1  // both row pairs unrolled: 321 vs 334 us/launch with its 8 spilled VGPRs (r03_ab.txt)
+#endif
+#if HEAD_OUT_UNROLL
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
     for (int rp = 0; rp < 2; ++rp) {
       float lsum[K];
 #pragma unroll
@@ -1133,6 +1151,15 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) ab2[k] = 0.f;
+#if HEAD_PK
+  f32x2 pgb[8], pgx[8], pw2[K][8];  // channel pairs (4cb + 2hp, +1)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    pgb[e] = pgx[e] = (f32x2){0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) pw2[k][e] = (f32x2){0.f, 0.f};
+  }
+#endif
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
@@ -1165,6 +1192,26 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
       const bf16x8 gb = go_frag<K>(q, go);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
+#if HEAD_PK
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int c0 = 16 * cb + 4 * q;
+        const f32x4 i4 = ld4v(pis + c0), o4 = ld4v(poff + c0), p4 = ld4v(pP + c0), q4 = ld4v(pQ + c0);
+#pragma unroll
+        for (int hp = 0; hp < 2; ++hp) {
+          const int e = 2 * cb + hp;
+          const f32x2 h = half2(acc[cb], hp);
+          const f32x2 xh = pkfma(h, half2(i4, hp), half2(o4, hp));
+          const f32x2 pre = pkfma(h, half2(p4, hp), half2(q4, hp));
+          const f32x2 act = (f32x2){fmaxf(pre.x, 0.f), fmaxf(pre.y, 0.f)};
+          const f32x2 gbn = relu_sel(pre, half2(sv[cb], hp));
+          pgb[e] += gbn;
+          pgx[e] = pkfma(gbn, xh, pgx[e]);
+#pragma unroll
+          for (int k = 0; k < K; ++k) pw2[k][e] = pkfma((f32x2){go[k], go[k]}, act, pw2[k][e]);
+        }
+      }
+#else
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int c0 = 16 * cb + 4 * q;
@@ -1182,10 +1229,20 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
           for (int k = 0; k < K; ++k) aw2[k][e] = fmaf(go[k], act, aw2[k][e]);
         }
       }
+#endif
 #pragma unroll
       for (int k = 0; k < K; ++k) ab2[k] += (q == 0) ? go[k] : 0.f;
     }
   }
+#if HEAD_PK
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    agb[e] = pgb[e >> 1][e & 1];
+    agx[e] = pgx[e >> 1][e & 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) aw2[k][e] = pw2[k][e >> 1][e & 1];
+  }
+#endif
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     agb[e] = sum_x16(agb[e]);
@@ -1217,6 +1274,145 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
   for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
 }
 
+// head_bwd1 with the GEMMs transposed (HEAD_BWD1_T, default): the im2col / g_o fragments are the A
+// operands and W1 / W2^T the B operands, so lane (q, x) receives h[pixel 4q + i][channel 16cb + x].  Its
+// 4 channels are fixed for the whole kernel: the BN-backward constants (is, off, P, Q) live in 16 VGPRs
+// instead of 16 LDS b128 reads per row, and the per-channel sums need 4 (not 16) accumulators per
+// quantity, reduced over the 4 lane groups q at the end.
+#ifndef HEAD_BWD1_T
+#define HEAD_BWD1_T 1
+#endif
+#ifndef HEAD_BWD1T_WAVES
+#define HEAD_BWD1T_WAVES 3
+#endif
+template <int K>
+__global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(HeadArgs a) {
+  constexpr int STRIDE = (K + 2) * MID + K;
+  __shared__ float su[18 * 18 * 3];
+  __shared__ float zs[ZR * ZR * 3];
+  __shared__ float red[STRIDE];
+  __shared__ __attribute__((aligned(16))) float gos[K * T2 * T2];
+  __shared__ __attribute__((aligned(16))) bf16x8 fr[8][64];  // W1, W2^T fragments (B operands here)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
+  if (wv == 0) {
+    bf16x8 A4[4];
+    load_a_w1<K>(a.w1, lane, A4);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fr[f][lane] = A4[f];
+    load_a_w2t<K>(a.w2, lane, A4);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
+  }
+  float kI[4], kO[4], kP[4], kQ[4];  // channel 16cb + x (op_sel broadcasts them to both pixel halves)
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) bwd_params(a, 16 * cb + x, kI[cb], kO[cb], kP[cb], kQ[cb]);
+  int off[8];
+  im2col_offsets<K>(q, off);
+  f32x2 pgb[4], pgx[4], pw2[K][4];  // [cb], pixel pairs (4q, 4q+1) / (4q+2, 4q+3) summed together
+  float ab2[K];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    pgb[cb] = pgx[cb] = (f32x2){0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) pw2[k][cb] = (f32x2){0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) ab2[k] = 0.f;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
+  zload(a, blockIdx.x, zv);
+  goload<K>(a, blockIdx.x, gv);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    int n, oy0, ox0;
+    tile_coords(a, tile, n, oy0, ox0);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
+    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
+    goload<K>(a, tile + gridDim.x, gv);
+    __syncthreads();
+#pragma unroll 1
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = 4 * wv + rr;
+      int fl = lane;
+      asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
+      f32x4 acc[4], sv[4];
+      {
+        const bf16x8 b = im2col_frag(su, (r * 18 + x) * 3, off);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, fr[cb][fl], z4, 0, 0, 0);
+      }
+      float gox[K];
+      f32x4 go4[K];  // g_o of pixels 4q .. 4q+3 (0 outside the image)
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        gox[k] = gos[k * T2 * T2 + r * T2 + x];
+        go4[k] = ld4v(gos + k * T2 * T2 + r * T2 + 4 * q);
+      }
+      const bf16x8 gb = go_frag<K>(q, gox);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gb, fr[4 + cb][fl], z4, 0, 0, 0);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int hp = 0; hp < 2; ++hp) {
+          const f32x2 h = half2(acc[cb], hp);
+          const f32x2 xh = pkfma(h, (f32x2){kI[cb], kI[cb]}, (f32x2){kO[cb], kO[cb]});
+          const f32x2 pre = pkfma(h, (f32x2){kP[cb], kP[cb]}, (f32x2){kQ[cb], kQ[cb]});
+          const f32x2 act = (f32x2){fmaxf(pre.x, 0.f), fmaxf(pre.y, 0.f)};
+          const f32x2 gbn = relu_sel(pre, half2(sv[cb], hp));
+          pgb[cb] += gbn;
+          pgx[cb] = pkfma(gbn, xh, pgx[cb]);
+#pragma unroll
+          for (int k = 0; k < K; ++k) pw2[k][cb] = pkfma(half2(go4[k], hp), act, pw2[k][cb]);
+        }
+#pragma unroll
+      for (int k = 0; k < K; ++k) ab2[k] += (x == 0) ? (go4[k][0] + go4[k][1]) + (go4[k][2] + go4[k][3]) : 0.f;
+    }
+  }
+  // per channel: the lane's pixel pairs, then the 4 lane groups q (fixed order), then the waves
+  float sgb[4], sgx[4], sw2[K][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    sgb[cb] = pgb[cb].x + pgb[cb].y;
+    sgx[cb] = pgx[cb].x + pgx[cb].y;
+#pragma unroll
+    for (int k = 0; k < K; ++k) sw2[k][cb] = pw2[k][cb].x + pw2[k][cb].y;
+  }
+  auto qsum = [](float v) {
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+  };
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    sgb[cb] = qsum(sgb[cb]);
+    sgx[cb] = qsum(sgx[cb]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) sw2[k][cb] = qsum(sw2[k][cb]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) ab2[k] = qsum(ab2[k]);
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w && q == 0) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int c = 16 * cb + x;
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[k * MID + c] += sw2[k][cb];
+        red[K * MID + c] += sgb[cb];
+        red[(K + 1) * MID + c] += sgx[cb];
+      }
+      if (x == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[(K + 2) * MID + k] += ab2[k];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
+}
+
 // g_h (never stored), the per-tap products v = g_h * W1 and the W1/b1 gradients (MFMA over
 // pixels from a wave-private bf16 g_h tile in LDS).  v stays in LDS: per tile the kernel forms
 // g_u = g_o + sum_t v[q - d_t][t] over the 18x18 region the tile's pixels reach and applies the
@@ -1231,6 +1427,19 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
 #define HEAD_ABL 0  // diagnostic builds only (tools/abl_build.sh): 1 skips the g_u / upsample-adjoint phases,
                     // 2 the W1-gradient MFMAs, 4 the v / g_h LDS writes
 #endif
+// HEAD_HROWS (default): the per-tap products are reduced over kx in registers as they leave the MFMA.
+// The v MFMA's A rows are ordered so that lane (q, x) receives, for the combination cmb = (k, ky) =
+// 4 jb + q, the three kx taps of pixel x (C rows 4q + kx); two row_shr DPP moves within the 16-lane
+// pixel row give H[k][ky][r][cc] = sum_kx v[k][ky][kx][r][cc - kx] over the 18 region columns cc, kept
+// in fp32.  The g_u pass then adds 3 rows of H per point and channel (was: 9 bf16 taps).
+#ifndef HEAD_HROWS
+#define HEAD_HROWS 1
+#endif
+__device__ __forceinline__ float dpp_shr(float v, int n) {  // lane x <- lane x - n of its 16-lane row, 0 below
+  const int iv = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, n == 1 ? __builtin_amdgcn_update_dpp(0, iv, 0x111, 0xf, 0xf, true)
+                                          : __builtin_amdgcn_update_dpp(0, iv, 0x112, 0xf, 0xf, true));
+}
 template <int K>
 __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadArgs a) {  // (K = 3: LDS allows 2)
   constexpr int STRIDE = MID * K * 9 + MID;
@@ -1238,13 +1447,22 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
   __shared__ float su[18 * 18 * 3];
   __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float pP[MID], pQ[MID], pD[MID], pE[MID];
-  __shared__ __attribute__((aligned(16))) bf16x8 fr[12][64];  // Ah[4], As[4], Av[jb][ch] per lane
+#if HEAD_HROWS
+  constexpr int NJB = (3 * K + 3) / 4;  // v MFMAs: 4 (k, ky) combinations each
+#else
+  constexpr int NJB = 2;
+#endif
+  __shared__ __attribute__((aligned(16))) bf16x8 fr[8 + 2 * NJB][64];  // Ah[4], As[4], Av[jb][ch] per lane
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
   __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
   static_assert(STRIDE * 4 <= (int)sizeof(gsw), "red aliases gsw");
   float* red = (float*)&gsw[0][0];  // (used after the tile loop only)
   __shared__ float gos[K * T2 * T2];
+#if HEAD_HROWS
+  __shared__ float hb[3 * K][T2][18];   // H rows of the tile, [k * 3 + ky][tile row][region column]
+#else
   __shared__ bf16_t vt[KJ][T2 * T2];    // the tile's per-tap products
+#endif
   __shared__ float hxs[18 * 10 * 3];    // horizontal upsample adjoint of g_u [18 rows][10 cols][K]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
@@ -1266,15 +1484,18 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
 #pragma unroll
     for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
+    for (int jb = 0; jb < NJB; ++jb)
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
         bf16x8 v;
+#if HEAD_HROWS
+        const int cmb = 4 * jb + (x >> 2), kx = x & 3;  // A row x -> C row 4 (x >> 2) + kx
+        const int j = (cmb < 3 * K && kx < 3) ? (cmb / 3) * 9 + (cmb % 3) * 3 + kx : KJ;
+#else
+        const int j = 16 * jb + x;
+#endif
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int j = 16 * jb + x;
-          v[jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
-        }
+        for (int jj = 0; jj < 8; ++jj) v[jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
         fr[8 + 2 * jb + ch][lane] = v;
       }
   }
@@ -1298,6 +1519,11 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
   for (int pb = 0; pb < 4; ++pb) accW[pb][0] = accW[pb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = 0.f;
+#if HEAD_PK
+  f32x2 pgb1[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) pgb1[e] = (f32x2){0.f, 0.f};
+#endif
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
@@ -1331,6 +1557,23 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
 #pragma unroll
         for (int k = 0; k < K; ++k) go[k] = gos[k * T2 * T2 + r * T2 + x];  // 0 outside the image
         const bf16x8 gb = go_frag<K>(q, go);
+#if HEAD_PK
+        const f32x2 pvf = pv ? (f32x2){1.f, 1.f} : (f32x2){0.f, 0.f};
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
+          const int c0 = 16 * cb + 4 * q;
+          const f32x4 P4 = ld4v(pP + c0), Q4 = ld4v(pQ + c0), D4 = ld4v(pD + c0), E4 = ld4v(pE + c0);
+#pragma unroll
+          for (int hp = 0; hp < 2; ++hp) {
+            const f32x2 h = half2(acc[cb], hp), P = half2(P4, hp);
+            const f32x2 gbn = relu_sel(pkfma(h, P, half2(Q4, hp)), half2(sv, hp));
+            const f32x2 g = pkfma(P, gbn, pkfma(h, half2(D4, hp), half2(E4, hp))) * pvf;
+            if (hp) acc[cb].hi = g; else acc[cb].lo = g;
+            pgb1[2 * cb + hp] += g;
+          }
+        }
+#else
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
@@ -1346,7 +1589,26 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
             agb1[4 * cb + i] += g;
           }
         }
+#endif
         const bf16x8 g0 = cfrag(acc, 0), g1 = cfrag(acc, 1);
+#if HEAD_HROWS
+#pragma unroll
+        for (int jb = 0; jb < NJB; ++jb) {
+          f32x4 vo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8 + 2 * jb][fl], g0, z4, 0, 0, 0);
+          vo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9 + 2 * jb][fl], g1, vo, 0, 0, 0);
+          // (zero where the pixel is outside the image: g is)
+          const float s1 = dpp_shr(vo[1], 1), s2 = dpp_shr(vo[2], 2), t1 = dpp_shr(vo[2], 1);
+          const int cmb = 4 * jb + q;
+          if (cmb < 3 * K) {
+            float* hr = &hb[cmb][r][0];
+            hr[x] = vo[0] + s1 + s2;
+            if (x == 15) {
+              hr[16] = vo[1] + t1;
+              hr[17] = vo[2];
+            }
+          }
+        }
+#else
         f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8][fl], g0, z4, 0, 0, 0);
         v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
         f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
@@ -1358,6 +1620,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
           if (4 * q + i < KJ) vt[4 * q + i][r * T2 + x] = f2bf(v0[i]);
           if (16 + 4 * q + i < KJ) vt[16 + 4 * q + i][r * T2 + x] = f2bf(v1[i]);
         }
+#endif
         // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
@@ -1404,6 +1667,19 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         const float v = gos[k * T2 * T2 + gi];
         g[k] = inner ? v : 0.f;
       }
+#if HEAD_HROWS
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {  // H rows of tile row rr - ky
+        const int pr = rr - ky;
+        const bool ok = img && pr >= 0 && pr < T2;
+        const int ri = ok ? pr : 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const float v = hb[k * 3 + ky][ri][cc];
+          g[k] += ok ? v : 0.f;
+        }
+      }
+#else
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3, pr = rr - ky, pc = cc - kx;  // source pixel q - d_t
@@ -1415,6 +1691,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
           g[k] += ok ? v : 0.f;
         }
       }
+#endif
 #pragma unroll
       for (int k = 0; k < K; ++k) su[i * 3 + k] = g[k];
     }
@@ -1459,6 +1736,10 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
       for (int k = 0; k < K; ++k) a.patch[((long long)tile * 100 + tid) * K + k] = pv[k];
     }
   }
+#if HEAD_PK
+#pragma unroll
+  for (int e = 0; e < 16; ++e) agb1[e] = pgb1[e >> 1][e & 1];
+#endif
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = sum_x16(agb1[e]);
   __syncthreads();
@@ -1660,7 +1941,8 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   hipStream_t s = (hipStream_t)stream;
   int rc;
   a.part = wsf + L.part1;
-  if (mf) HEAD_DISPATCH(head_bwd1_mfma_kernel, L.grid, NT, 0, s);
+  if (mf && HEAD_BWD1_T) HEAD_DISPATCH(head_bwd1t_mfma_kernel, L.grid, NT, 0, s);
+  else if (mf) HEAD_DISPATCH(head_bwd1_mfma_kernel, L.grid, NT, 0, s);
   else HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_bwd1");
   const int ld1 = (k + 2) * MID + k;
