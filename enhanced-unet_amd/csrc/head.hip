@@ -659,15 +659,15 @@ __device__ __forceinline__ void load_a_w1(const float* w1, int lane, bf16x8 (&A)
     }
 }
 
-// per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner
-template <int K>
+// per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner (su row stride RS)
+template <int K, int RS = 18>
 __device__ __forceinline__ void im2col_offsets(int q, int (&off)[8]) {
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) {
     const int j = 8 * q + jj;
     if (j < K * 9) {
       const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
-      off[jj] = (ky * 18 + kx) * 3 + k;
+      off[jj] = (ky * RS + kx) * 3 + k;
     } else {
       off[jj] = -1;
     }
@@ -722,9 +722,6 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p
 __device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 // packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two channels per instruction, each element
 // rounded as the scalar op would round it)
-#ifndef HEAD_PK
-#define HEAD_PK 1
-#endif
 __device__ __forceinline__ f32x4 ld4v(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ f32x2 half2(const f32x4& v, int hp) { return hp ? v.hi : v.lo; }
 __device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -914,60 +911,81 @@ __device__ __forceinline__ void gram_store(float* red, float* row, const f32x4& 
 // then each wave accumulates 8 rows of 32 pixels.  tx / ty / ntiles of HeadArgs describe these tiles.
 constexpr int GT = 32, GR = GT + 2, GZ = GT / 2 + 2;
 template <int K>
+struct Z32 {
+  static constexpr int ZN = GZ * GZ * K, ZI = (ZN + NT - 1) / NT;  // z values of a tile's region, per thread
+};
+__device__ __forceinline__ void tile32_coords(const HeadArgs& a, int tile, int& n, int& oy0, int& ox0) {
+  const int tpi = a.tx * a.ty;  // (a.tx / a.ty count 32 x 32 tiles)
+  n = tile / tpi;
+  const int r = tile - n * tpi;
+  oy0 = (r / a.tx) * GT;
+  ox0 = (r % a.tx) * GT;
+}
+// the 18 x 18 x K z region a 32 x 32 tile interpolates from, edge-clamped, into registers
+template <int K>
+__device__ __forceinline__ void zfetch32(const HeadArgs& a, int tile, float (&zv)[Z32<K>::ZI]) {
+  if (tile >= a.ntiles) return;
+  int n, oy0, ox0;
+  tile32_coords(a, tile, n, oy0, ox0);
+  const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
+  const float* zb = a.z + (long long)n * a.h * a.w * K;
+#pragma unroll
+  for (int j = 0; j < Z32<K>::ZI; ++j) {
+    const int idx = threadIdx.x + j * NT;
+    if (idx < Z32<K>::ZN) {
+      const int k = idx % K, pix = idx / K, i = pix / GZ, c = pix - i * GZ;
+      const int yy = min(max(zy0 + i, 0), a.h - 1), xx = min(max(zx0 + c, 0), a.w - 1);
+      zv[j] = zb[((long long)yy * a.w + xx) * K + k];
+    }
+  }
+}
+// stage the prefetched z region, prefetch the next tile's, then u = up(z) over the 34 x 34 region from LDS
+// (zero outside the image); the caller syncs before (su / zs free) and after (su complete)
+template <int K>
+__device__ void stage_u32(const HeadArgs& a, float* su, float* zs, float (&zv)[Z32<K>::ZI], int tile, int oy0,
+                          int ox0) {
+  const int tid = threadIdx.x, H2 = 2 * a.h, W2 = 2 * a.w;
+#pragma unroll
+  for (int j = 0; j < Z32<K>::ZI; ++j)
+    if (tid + j * NT < Z32<K>::ZN) zs[tid + j * NT] = zv[j];
+  __syncthreads();
+  zfetch32<K>(a, tile + gridDim.x, zv);
+  const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
+  for (int i = tid; i < GR * GR; i += NT) {
+    const int hy = i / GR, hx = i - hy * GR;
+    const int oy = oy0 + hy - 1, ox = ox0 + hx - 1;
+    const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    up2_src(in ? oy : 0, a.h, y0, y1, ly);
+    up2_src(in ? ox : 0, a.w, x0, x1, lx);
+    const float* r0 = zs + ((y0 - zy0) * GZ) * K;
+    const float* r1 = zs + ((y1 - zy0) * GZ) * K;
+    const int c0 = (x0 - zx0) * K, c1 = (x1 - zx0) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
+                               ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
+                         : 0.f;
+  }
+}
+template <int K>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_gram_mfma_kernel(HeadArgs a) {
   __shared__ float su[GR * GR * 3];
   __shared__ float zs[GZ * GZ * 3];
   __shared__ float red[4 * GRAM_LD];
-  constexpr int ZN = GZ * GZ * K, ZI = (ZN + NT - 1) / NT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   int o[2];
   gram_offsets<K, GR>(x, o);
   f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
-  const int H2 = 2 * a.h, W2 = 2 * a.w, tpi = a.tx * a.ty;
-  auto zfetch = [&](int tile, float (&zv)[ZI]) {
-    if (tile >= a.ntiles) return;
-    const int n = tile / tpi, r = tile - n * tpi;
-    const int zy0 = (r / a.tx) * (GT / 2) - 1, zx0 = (r % a.tx) * (GT / 2) - 1;
-    const float* zb = a.z + (long long)n * a.h * a.w * K;
-#pragma unroll
-    for (int j = 0; j < ZI; ++j) {
-      const int idx = tid + j * NT;
-      if (idx < ZN) {
-        const int k = idx % K, pix = idx / K, i = pix / GZ, c = pix - i * GZ;
-        const int yy = min(max(zy0 + i, 0), a.h - 1), xx = min(max(zx0 + c, 0), a.w - 1);
-        zv[j] = zb[((long long)yy * a.w + xx) * K + k];
-      }
-    }
-  };
-  float zv[ZI];
-  zfetch(blockIdx.x, zv);
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
+  float zv[Z32<K>::ZI];
+  zfetch32<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    const int n = tile / tpi, r = tile - n * tpi;
-    const int oy0 = (r / a.tx) * GT, ox0 = (r % a.tx) * GT;
+    int n, oy0, ox0;
+    tile32_coords(a, tile, n, oy0, ox0);
     __syncthreads();  // the previous tile's su reads are done
-#pragma unroll
-    for (int j = 0; j < ZI; ++j)
-      if (tid + j * NT < ZN) zs[tid + j * NT] = zv[j];
-    __syncthreads();
-    zfetch(tile + gridDim.x, zv);
-    const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
-    for (int i = tid; i < GR * GR; i += NT) {
-      const int hy = i / GR, hx = i - hy * GR;
-      const int oy = oy0 + hy - 1, ox = ox0 + hx - 1;
-      const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
-      int y0, y1, x0, x1;
-      float ly, lx;
-      up2_src(in ? oy : 0, a.h, y0, y1, ly);
-      up2_src(in ? ox : 0, a.w, x0, x1, lx);
-      const float* r0 = zs + ((y0 - zy0) * GZ) * K;
-      const float* r1 = zs + ((y1 - zy0) * GZ) * K;
-      const int c0 = (x0 - zx0) * K, c1 = (x1 - zx0) * K;
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
-                                 ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
-                           : 0.f;
-    }
+    stage_u32<K>(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
     const int vh = min(GT, H2 - oy0), vw = min(GT, W2 - ox0);
 #pragma unroll 2
@@ -1018,10 +1036,14 @@ __global__ __launch_bounds__(MID) void head_gram_stats_kernel(const float* g, co
   if (tid == 0) stats[2 * MID] = (float)n;
 }
 
+// bf16 forward output: h = conv3x3(u) by MFMA, BN + ReLU, the 1x1 by MFMA, residual, 2H output and the 2x2
+// mean.  32 x 32 tiles (a.tx / a.ty / a.ntiles count them): one z and u stage per 1024 pixels (16 x 16
+// tiles: 334 vs 281 us/launch at the bench shape, profiles/r03_ab.txt); wave w runs rows 8w .. 8w+7 as
+// row pairs of 16-pixel segments.
 template <int K>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_out_mfma_kernel(HeadArgs a) {
-  __shared__ float su[18 * 18 * 3];
-  __shared__ float zs[ZR * ZR * 3];
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void head_out32_mfma_kernel(HeadArgs a) {
+  __shared__ float su[GR * GR * 3];
+  __shared__ float zs[GZ * GZ * 3];
   __shared__ __attribute__((aligned(16))) float scs[MID], shs[MID];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   if (tid < MID) {
@@ -1036,37 +1058,31 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
     for (int jj = 0; jj < 8; ++jj)
       Ao[ch][jj] = (__bf16)(x < K ? a.w2[x * MID + perm_c(q, ch, jj)] : 0.f);
   int off[8];
-  im2col_offsets<K>(q, off);
+  im2col_offsets<K, GR>(q, off);
   float b2k[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) b2k[k] = a.b2[k];
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  float zv[2] = {0.f, 0.f};
-  zload(a, blockIdx.x, zv);
+  float zv[Z32<K>::ZI];
+  zfetch32<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
-    tile_coords(a, tile, n, oy0, ox0);
+    tile32_coords(a, tile, n, oy0, ox0);
     __syncthreads();
-    stage_u(a, su, zs, zv, tile, oy0, ox0);
+    stage_u32<K>(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
-#ifndef HEAD_OUT_UNROLL
-#define HEAD_OUT_UNROLL 1  // both row pairs unrolled: 321 vs 334 us/launch with its 8 spilled VGPRs (r03_ab.txt)
-#endif
-#if HEAD_OUT_UNROLL
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-    for (int rp = 0; rp < 2; ++rp) {
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rp = it >> 1, sx = 16 * (it & 1);
       float lsum[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) lsum[k] = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
-        const int r = 4 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + x;
+        const int r = 8 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + sx + x;
         f32x4 acc[4];
-        conv_h_mfma(su, (r * 18 + x) * 3, off, Ah, acc);
+        conv_h_mfma(su, (r * GR + sx + x) * 3, off, Ah, acc);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           const float4 s4 = ld4(scs + 16 * cb + 4 * q), t4 = ld4(shs + 16 * cb + 4 * q);
@@ -1079,12 +1095,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
         const bool pv = q == 0 && oy < H2 && ox < W2;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const float val = o[k] + b2k[k] + su[((r + 1) * 18 + x + 1) * 3 + k];
+          const float val = o[k] + b2k[k] + su[((r + 1) * GR + sx + x + 1) * 3 + k];
           if (pv && a.out2h) a.out2h[(((long long)n * K + k) * H2 + oy) * W2 + ox] = val;
           lsum[k] += val;
         }
       }
-      const int oy = oy0 + 4 * wv + 2 * rp, ox = ox0 + x;
+      const int oy = oy0 + 8 * wv + 2 * rp, ox = ox0 + sx + x;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const float t = lsum[k] + __shfl_xor(lsum[k], 1, 64);
@@ -1118,182 +1134,25 @@ __device__ __forceinline__ void goload(const HeadArgs& a, int tile, float (&gv)[
   }
 }
 
+// bf16 backward pass 1: gW2, gb2, dbeta = sum g_bn, dgamma = sum g_bn * xhat.  The GEMMs are transposed: the
+// im2col / g_o fragments are the A operands and W1 / W2^T the B operands, so lane (q, x) receives
+// h[pixel 4q + i][channel 16cb + x]; its 4 channels are fixed for the whole kernel, the BN-backward
+// constants (is, off, P, Q) live in VGPRs and each per-channel sum needs 4 accumulators, reduced over the 4
+// lane groups q at the end.  32 x 32 tiles (a.tx / a.ty / a.ntiles count them): one z, u and g_o stage per
+// 1024 pixels (16 x 16 tiles: 557 vs 497 us/launch, profiles/r03_ab.txt); wave w runs rows 8w .. 8w+7 as
+// 16-pixel segments.  The g_o tile is loaded into registers before the u stage and stored after it, so its
+// global latency hides behind the interpolation.
 template <int K>
-__global__ __launch_bounds__(NT, 3) void head_bwd1_mfma_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = (K + 2) * MID + K;
-  __shared__ float su[18 * 18 * 3];
-  __shared__ float zs[ZR * ZR * 3];
-  __shared__ __attribute__((aligned(16))) float pis[MID], poff[MID], pP[MID], pQ[MID];
+  constexpr int GO = GT * GT / NT;  // g_o values per thread and class
+  __shared__ float su[GR * GR * 3];
+  __shared__ float zs[GZ * GZ * 3];
   __shared__ float red[STRIDE];
-  __shared__ float gos[K * T2 * T2];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
-  if (tid < MID) bwd_params(a, tid, pis[tid], poff[tid], pP[tid], pQ[tid]);
-  for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
-  __shared__ __attribute__((aligned(16))) bf16x8 fr[8][64];  // Ah[4], As[4] per lane
-  if (wv == 0) {
-    bf16x8 A4[4];
-    load_a_w1<K>(a.w1, lane, A4);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) fr[f][lane] = A4[f];
-    load_a_w2t<K>(a.w2, lane, A4);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
-  }
-  int off[8];
-  im2col_offsets<K>(q, off);
-  float agb[16], agx[16], aw2[K][16], ab2[K];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    agb[e] = 0.f;
-    agx[e] = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k) aw2[k][e] = 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) ab2[k] = 0.f;
-#if HEAD_PK
-  f32x2 pgb[8], pgx[8], pw2[K][8];  // channel pairs (4cb + 2hp, +1)
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    pgb[e] = pgx[e] = (f32x2){0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < K; ++k) pw2[k][e] = (f32x2){0.f, 0.f};
-  }
-#endif
-  const int H2 = 2 * a.h, W2 = 2 * a.w;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
-  zload(a, blockIdx.x, zv);
-  goload<K>(a, blockIdx.x, gv);
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    int n, oy0, ox0;
-    tile_coords(a, tile, n, oy0, ox0);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
-    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
-    goload<K>(a, tile + gridDim.x, gv);
-    __syncthreads();
-#pragma unroll 1
-    for (int rr = 0; rr < 4; ++rr) {
-      const int r = 4 * wv + rr, oy = oy0 + r, ox = ox0 + x;
-      const bool pv = oy < H2 && ox < W2;
-      int fl = lane;
-      asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
-      f32x4 acc[4], sv[4];
-      {
-        const bf16x8 b = im2col_frag(su, (r * 18 + x) * 3, off);
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[cb][fl], b, z4, 0, 0, 0);
-      }
-      float go[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) go[k] = gos[k * T2 * T2 + r * T2 + x];  // 0 outside the image
-      const bf16x8 gb = go_frag<K>(q, go);
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
-#if HEAD_PK
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int c0 = 16 * cb + 4 * q;
-        const f32x4 i4 = ld4v(pis + c0), o4 = ld4v(poff + c0), p4 = ld4v(pP + c0), q4 = ld4v(pQ + c0);
-#pragma unroll
-        for (int hp = 0; hp < 2; ++hp) {
-          const int e = 2 * cb + hp;
-          const f32x2 h = half2(acc[cb], hp);
-          const f32x2 xh = pkfma(h, half2(i4, hp), half2(o4, hp));
-          const f32x2 pre = pkfma(h, half2(p4, hp), half2(q4, hp));
-          const f32x2 act = (f32x2){fmaxf(pre.x, 0.f), fmaxf(pre.y, 0.f)};
-          const f32x2 gbn = relu_sel(pre, half2(sv[cb], hp));
-          pgb[e] += gbn;
-          pgx[e] = pkfma(gbn, xh, pgx[e]);
-#pragma unroll
-          for (int k = 0; k < K; ++k) pw2[k][e] = pkfma((f32x2){go[k], go[k]}, act, pw2[k][e]);
-        }
-      }
-#else
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        const int c0 = 16 * cb + 4 * q;
-        const float4 i4 = ld4(pis + c0), o4 = ld4(poff + c0), p4 = ld4(pP + c0), q4 = ld4(pQ + c0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int e = 4 * cb + i;
-          const float xh = fmaf(acc[cb][i], f4(i4, i), f4(o4, i));
-          const float pre = fmaf(acc[cb][i], f4(p4, i), f4(q4, i));
-          const float act = fmaxf(pre, 0.f);
-          const float gbn = pre > 0.f ? sv[cb][i] : 0.f;
-          agb[e] += gbn;
-          agx[e] = fmaf(gbn, xh, agx[e]);
-#pragma unroll
-          for (int k = 0; k < K; ++k) aw2[k][e] = fmaf(go[k], act, aw2[k][e]);
-        }
-      }
-#endif
-#pragma unroll
-      for (int k = 0; k < K; ++k) ab2[k] += (q == 0) ? go[k] : 0.f;
-    }
-  }
-#if HEAD_PK
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    agb[e] = pgb[e >> 1][e & 1];
-    agx[e] = pgx[e >> 1][e & 1];
-#pragma unroll
-    for (int k = 0; k < K; ++k) aw2[k][e] = pw2[k][e >> 1][e & 1];
-  }
-#endif
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    agb[e] = sum_x16(agb[e]);
-    agx[e] = sum_x16(agx[e]);
-#pragma unroll
-    for (int k = 0; k < K; ++k) aw2[k][e] = sum_x16(aw2[k][e]);
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) ab2[k] = sum_x16(ab2[k]);
-  for (int w = 0; w < 4; ++w) {
-    __syncthreads();
-    if (wv == w && x == 0) {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 16 * cb + 4 * q + i, e = 4 * cb + i;
-#pragma unroll
-          for (int k = 0; k < K; ++k) red[k * MID + c] += aw2[k][e];
-          red[K * MID + c] += agb[e];
-          red[(K + 1) * MID + c] += agx[e];
-        }
-      if (q == 0)
-#pragma unroll
-        for (int k = 0; k < K; ++k) red[(K + 2) * MID + k] += ab2[k];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
-}
-
-// head_bwd1 with the GEMMs transposed (HEAD_BWD1_T, default): the im2col / g_o fragments are the A
-// operands and W1 / W2^T the B operands, so lane (q, x) receives h[pixel 4q + i][channel 16cb + x].  Its
-// 4 channels are fixed for the whole kernel: the BN-backward constants (is, off, P, Q) live in 16 VGPRs
-// instead of 16 LDS b128 reads per row, and the per-channel sums need 4 (not 16) accumulators per
-// quantity, reduced over the 4 lane groups q at the end.
-#ifndef HEAD_BWD1_T
-#define HEAD_BWD1_T 1
-#endif
-#ifndef HEAD_BWD1T_WAVES
-#define HEAD_BWD1T_WAVES 3
-#endif
-template <int K>
-__global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(HeadArgs a) {
-  constexpr int STRIDE = (K + 2) * MID + K;
-  __shared__ float su[18 * 18 * 3];
-  __shared__ float zs[ZR * ZR * 3];
-  __shared__ float red[STRIDE];
-  __shared__ __attribute__((aligned(16))) float gos[K * T2 * T2];
+  __shared__ __attribute__((aligned(16))) float gos[K * GT * GT];
   __shared__ __attribute__((aligned(16))) bf16x8 fr[8][64];  // W1, W2^T fragments (B operands here)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
+  const int H2 = 2 * a.h, W2 = 2 * a.w;
   for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
   if (wv == 0) {
     bf16x8 A4[4];
@@ -1308,8 +1167,8 @@ __global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(H
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) bwd_params(a, 16 * cb + x, kI[cb], kO[cb], kP[cb], kQ[cb]);
   int off[8];
-  im2col_offsets<K>(q, off);
-  f32x2 pgb[4], pgx[4], pw2[K][4];  // [cb], pixel pairs (4q, 4q+1) / (4q+2, 4q+3) summed together
+  im2col_offsets<K, GR>(q, off);
+  f32x2 pgb[4], pgx[4], pw2[K][4];
   float ab2[K];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
@@ -1320,35 +1179,43 @@ __global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(H
 #pragma unroll
   for (int k = 0; k < K; ++k) ab2[k] = 0.f;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
-  zload(a, blockIdx.x, zv);
-  goload<K>(a, blockIdx.x, gv);
+  float zv[Z32<K>::ZI];
+  zfetch32<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
-    tile_coords(a, tile, n, oy0, ox0);
-    __syncthreads();
+    tile32_coords(a, tile, n, oy0, ox0);
+    float gv[K][GO];
 #pragma unroll
-    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
-    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
-    goload<K>(a, tile + gridDim.x, gv);
+    for (int e = 0; e < GO; ++e) {
+      const int p = tid + e * NT, oy = oy0 + p / GT, ox = ox0 + p % GT;
+      const bool in = oy < H2 && ox < W2;
+#pragma unroll
+      for (int k = 0; k < K; ++k) gv[k][e] = in ? g_out(a, K, n, k, oy, ox) : 0.f;
+    }
+    __syncthreads();  // the previous tile's su / gos reads are done
+    stage_u32<K>(a, su, zs, zv, tile, oy0, ox0);
+#pragma unroll
+    for (int e = 0; e < GO; ++e)
+#pragma unroll
+      for (int k = 0; k < K; ++k) gos[k * GT * GT + tid + e * NT] = gv[k][e];
     __syncthreads();
 #pragma unroll 1
-    for (int rr = 0; rr < 4; ++rr) {
-      const int r = 4 * wv + rr;
+    for (int rs = 0; rs < 2 * GT / 4; ++rs) {
+      const int r = 8 * wv + (rs >> 1), sx = 16 * (rs & 1);
       int fl = lane;
       asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
       f32x4 acc[4], sv[4];
       {
-        const bf16x8 b = im2col_frag(su, (r * 18 + x) * 3, off);
+        const bf16x8 b = im2col_frag(su, (r * GR + sx + x) * 3, off);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, fr[cb][fl], z4, 0, 0, 0);
       }
       float gox[K];
-      f32x4 go4[K];  // g_o of pixels 4q .. 4q+3 (0 outside the image)
+      f32x4 go4[K];  // g_o of pixels 4q .. 4q+3 of the segment (0 outside the image)
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        gox[k] = gos[k * T2 * T2 + r * T2 + x];
-        go4[k] = ld4v(gos + k * T2 * T2 + r * T2 + 4 * q);
+        gox[k] = gos[k * GT * GT + r * GT + sx + x];
+        go4[k] = ld4v(gos + k * GT * GT + r * GT + sx + 4 * q);
       }
       const bf16x8 gb = go_frag<K>(q, gox);
 #pragma unroll
@@ -1371,7 +1238,6 @@ __global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(H
       for (int k = 0; k < K; ++k) ab2[k] += (x == 0) ? (go4[k][0] + go4[k][1]) + (go4[k][2] + go4[k][3]) : 0.f;
     }
   }
-  // per channel: the lane's pixel pairs, then the 4 lane groups q (fixed order), then the waves
   float sgb[4], sgx[4], sw2[K][4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
@@ -1414,27 +1280,25 @@ __global__ __launch_bounds__(NT, HEAD_BWD1T_WAVES) void head_bwd1t_mfma_kernel(H
 }
 
 // g_h (never stored), the per-tap products v = g_h * W1 and the W1/b1 gradients (MFMA over
-// pixels from a wave-private bf16 g_h tile in LDS).  v stays in LDS: per tile the kernel forms
-// g_u = g_o + sum_t v[q - d_t][t] over the 18x18 region the tile's pixels reach and applies the
-// x2 upsample adjoint to it, writing the tile's 10x10 low-res patch of g_z; head_patch_gather
-// adds the (at most four) patches covering each low-res pixel in a fixed order.  No v / g_u
-// round trip through HBM (it was 0.6 GB written and read per step at 1024^2 x 4).
-// Register budget (<= 128 VGPRs -> 4 waves/SIMD to overlap the dependent MFMA -> VALU
-// chains): the BN-backward algebra is folded into 4 per-channel constants,
+// pixels from a wave-private bf16 g_h tile in LDS).  v stays on chip (as the H rows below): per tile
+// the kernel forms g_u = g_o + sum_t v[q - d_t][t] over the 18x18 region the tile's pixels reach and
+// applies the x2 upsample adjoint to it, writing the tile's 10x10 low-res patch of g_z;
+// head_patch_gather adds the (at most four) patches covering each low-res pixel in a fixed order.  No
+// v / g_u round trip through HBM (it was 0.6 GB written and read per step at 1024^2 x 4).
+// Register budget (3 waves/SIMD to overlap the dependent MFMA -> VALU chains): the BN-backward
+// algebra is folded into 4 per-channel constants, evaluated two channels per packed fp32 op,
 //   pre = h P + Q,   g_h = P gbn + h D + E   (D = -P c2 is, E = -P (c2 off + c1)),
 // and the constant A fragments (W1 for h, W2^T for s, W1^T for v) are read from LDS.
 #ifndef HEAD_ABL
 #define HEAD_ABL 0  // diagnostic builds only (tools/abl_build.sh): 1 skips the g_u / upsample-adjoint phases,
-                    // 2 the W1-gradient MFMAs, 4 the v / g_h LDS writes
+                    // 2 the W1-gradient MFMAs
 #endif
-// HEAD_HROWS (default): the per-tap products are reduced over kx in registers as they leave the MFMA.
+// The per-tap products are reduced over kx in registers as they leave the MFMA.
 // The v MFMA's A rows are ordered so that lane (q, x) receives, for the combination cmb = (k, ky) =
 // 4 jb + q, the three kx taps of pixel x (C rows 4q + kx); two row_shr DPP moves within the 16-lane
 // pixel row give H[k][ky][r][cc] = sum_kx v[k][ky][kx][r][cc - kx] over the 18 region columns cc, kept
-// in fp32.  The g_u pass then adds 3 rows of H per point and channel (was: 9 bf16 taps).
-#ifndef HEAD_HROWS
-#define HEAD_HROWS 1
-#endif
+// in fp32.  The g_u pass then adds 3 rows of H per point and channel (9 bf16 taps before: 960 vs 900
+// us/launch, and packed fp32 for the BN-backward algebra 1023 vs 900, profiles/r03_ab.txt).
 __device__ __forceinline__ float dpp_shr(float v, int n) {  // lane x <- lane x - n of its 16-lane row, 0 below
   const int iv = __builtin_bit_cast(int, v);
   return __builtin_bit_cast(float, n == 1 ? __builtin_amdgcn_update_dpp(0, iv, 0x111, 0xf, 0xf, true)
@@ -1447,22 +1311,14 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
   __shared__ float su[18 * 18 * 3];
   __shared__ float zs[ZR * ZR * 3];
   __shared__ __attribute__((aligned(16))) float pP[MID], pQ[MID], pD[MID], pE[MID];
-#if HEAD_HROWS
   constexpr int NJB = (3 * K + 3) / 4;  // v MFMAs: 4 (k, ky) combinations each
-#else
-  constexpr int NJB = 2;
-#endif
   __shared__ __attribute__((aligned(16))) bf16x8 fr[8 + 2 * NJB][64];  // Ah[4], As[4], Av[jb][ch] per lane
   constexpr int GLD = MID + 16;  // padded row: conflict-free transposed reads
   __shared__ __attribute__((aligned(16))) bf16_t gsw[4][32 * GLD];
   static_assert(STRIDE * 4 <= (int)sizeof(gsw), "red aliases gsw");
   float* red = (float*)&gsw[0][0];  // (used after the tile loop only)
   __shared__ float gos[K * T2 * T2];
-#if HEAD_HROWS
   __shared__ float hb[3 * K][T2][18];   // H rows of the tile, [k * 3 + ky][tile row][region column]
-#else
-  __shared__ bf16_t vt[KJ][T2 * T2];    // the tile's per-tap products
-#endif
   __shared__ float hxs[18 * 10 * 3];    // horizontal upsample adjoint of g_u [18 rows][10 cols][K]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
@@ -1488,12 +1344,8 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
         bf16x8 v;
-#if HEAD_HROWS
         const int cmb = 4 * jb + (x >> 2), kx = x & 3;  // A row x -> C row 4 (x >> 2) + kx
         const int j = (cmb < 3 * K && kx < 3) ? (cmb / 3) * 9 + (cmb % 3) * 3 + kx : KJ;
-#else
-        const int j = 16 * jb + x;
-#endif
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) v[jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
         fr[8 + 2 * jb + ch][lane] = v;
@@ -1519,11 +1371,9 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
   for (int pb = 0; pb < 4; ++pb) accW[pb][0] = accW[pb][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = 0.f;
-#if HEAD_PK
   f32x2 pgb1[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) pgb1[e] = (f32x2){0.f, 0.f};
-#endif
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
@@ -1557,7 +1407,6 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
 #pragma unroll
         for (int k = 0; k < K; ++k) go[k] = gos[k * T2 * T2 + r * T2 + x];  // 0 outside the image
         const bf16x8 gb = go_frag<K>(q, go);
-#if HEAD_PK
         const f32x2 pvf = pv ? (f32x2){1.f, 1.f} : (f32x2){0.f, 0.f};
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
@@ -1573,25 +1422,7 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
             pgb1[2 * cb + hp] += g;
           }
         }
-#else
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[4 + cb][fl], gb, z4, 0, 0, 0);
-          const int c0 = 16 * cb + 4 * q;
-          const float4 P4 = ld4(pP + c0), Q4 = ld4(pQ + c0), D4 = ld4(pD + c0), E4 = ld4(pE + c0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float h = acc[cb][i];
-            const float pre = fmaf(h, f4(P4, i), f4(Q4, i));
-            const float gbn = pre > 0.f ? sv[i] : 0.f;
-            const float g = pv ? fmaf(f4(P4, i), gbn, fmaf(h, f4(D4, i), f4(E4, i))) : 0.f;
-            acc[cb][i] = g;
-            agb1[4 * cb + i] += g;
-          }
-        }
-#endif
         const bf16x8 g0 = cfrag(acc, 0), g1 = cfrag(acc, 1);
-#if HEAD_HROWS
 #pragma unroll
         for (int jb = 0; jb < NJB; ++jb) {
           f32x4 vo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8 + 2 * jb][fl], g0, z4, 0, 0, 0);
@@ -1608,19 +1439,6 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
             }
           }
         }
-#else
-        f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8][fl], g0, z4, 0, 0, 0);
-        v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9][fl], g1, v0, 0, 0, 0);
-        f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[10][fl], g0, z4, 0, 0, 0);
-        v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[11][fl], g1, v1, 0, 0, 0);
-        // v[j][pixel] of the tile (zero where the pixel is outside the image: g is)
-        if (HEAD_ABL & 4) { agb1[0] += v0[0] + v1[1]; continue; }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (4 * q + i < KJ) vt[4 * q + i][r * T2 + x] = f2bf(v0[i]);
-          if (16 + 4 * q + i < KJ) vt[16 + 4 * q + i][r * T2 + x] = f2bf(v1[i]);
-        }
-#endif
         // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
@@ -1667,7 +1485,6 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
         const float v = gos[k * T2 * T2 + gi];
         g[k] = inner ? v : 0.f;
       }
-#if HEAD_HROWS
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {  // H rows of tile row rr - ky
         const int pr = rr - ky;
@@ -1679,19 +1496,6 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
           g[k] += ok ? v : 0.f;
         }
       }
-#else
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int ky = t / 3, kx = t - ky * 3, pr = rr - ky, pc = cc - kx;  // source pixel q - d_t
-        const bool ok = img && pr >= 0 && pr < T2 && pc >= 0 && pc < T2;
-        const int vi = ok ? pr * T2 + pc : 0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float v = bf2f(vt[k * 9 + t][vi]);
-          g[k] += ok ? v : 0.f;
-        }
-      }
-#endif
 #pragma unroll
       for (int k = 0; k < K; ++k) su[i * 3 + k] = g[k];
     }
@@ -1736,10 +1540,8 @@ __global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadAr
       for (int k = 0; k < K; ++k) a.patch[((long long)tile * 100 + tid) * K + k] = pv[k];
     }
   }
-#if HEAD_PK
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = pgb1[e >> 1][e & 1];
-#endif
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = sum_x16(agb1[e]);
   __syncthreads();
@@ -1913,7 +1715,12 @@ int eunet_head_fwd(const float* z, int n, int h, int w, int k, const float* w1, 
     int rc = eunet_bn_eval_affine(MID, gamma, beta, run_mean, run_var, eps, wsf + L.scale, wsf + L.shift, stream);
     if (rc) return rc;
   }
-  if (mf) HEAD_DISPATCH(head_out_mfma_kernel, L.grid4, NT, 0, s);
+  if (mf) {
+    HeadArgs ag = a;  // 32 x 32 tiles
+    ag.tx = cdiv(2 * w, GT); ag.ty = cdiv(2 * h, GT); ag.ntiles = n * ag.tx * ag.ty;
+    const HeadArgs a = ag;
+    HEAD_DISPATCH(head_out32_mfma_kernel, L.grid4, NT, 0, s);
+  }
   else HEAD_DISPATCH(head_out_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_out");
   return EUNET_OK;
@@ -1941,8 +1748,12 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   hipStream_t s = (hipStream_t)stream;
   int rc;
   a.part = wsf + L.part1;
-  if (mf && HEAD_BWD1_T) HEAD_DISPATCH(head_bwd1t_mfma_kernel, L.grid, NT, 0, s);
-  else if (mf) HEAD_DISPATCH(head_bwd1_mfma_kernel, L.grid, NT, 0, s);
+  if (mf) {
+    HeadArgs ag = a;  // 32 x 32 tiles
+    ag.tx = cdiv(2 * w, GT); ag.ty = cdiv(2 * h, GT); ag.ntiles = n * ag.tx * ag.ty;
+    const HeadArgs a = ag;
+    HEAD_DISPATCH(head_bwd1t32_mfma_kernel, L.grid, NT, 0, s);
+  }
   else HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_bwd1");
   const int ld1 = (k + 2) * MID + k;
