@@ -675,8 +675,7 @@ __global__ __launch_bounds__(NT) void colsum_stage1(const float* part, int rows,
   if (rg == 0 && col < cols) ws[(long long)blockIdx.y * cols + col] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
 }
 
-__global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, int cols, float* out, int split,
-                                                    float* out_hi) {
+__global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, int cols, ColSegs segs) {
   __shared__ double sh[4][64];
   const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int col = blockIdx.x * 64 + cl;
@@ -687,10 +686,10 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
   __syncthreads();
   if (rg == 0 && col < cols) {
     const float v = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
-    if (out_hi != nullptr && col >= split)
-      out_hi[col - split] = v;
-    else
-      out[col] = v;
+    int i = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) i = (j < segs.n && col >= segs.start[j]) ? j : i;
+    segs.out[i][col - segs.start[i]] = v;
   }
 }
 
@@ -1304,15 +1303,24 @@ static int colsum_rb(int rows) {
 
 size_t eunet_colsum_ws(int rows, int cols) { return (size_t)colsum_rb(rows) * cols * sizeof(double); }
 
-int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s, int split,
-                    float* out_hi) {
-  EUNET_REQUIRE(part && out && ws && rows > 0 && cols > 0 && ld >= cols, "colsum: bad args");
+int eunet_colsum_segs(const float* part, int rows, int cols, int ld, const ColSegs& segs, void* ws, hipStream_t s) {
+  EUNET_REQUIRE(part && ws && rows > 0 && cols > 0 && ld >= cols && segs.n >= 1 && segs.n <= 4 && segs.start[0] == 0,
+                "colsum: bad args");
+  for (int i = 0; i < segs.n; ++i)
+    EUNET_REQUIRE(segs.out[i] && (i == 0 || (segs.start[i] > segs.start[i - 1] && segs.start[i] < cols)),
+                  "colsum: bad segments");
   const int rb = colsum_rb(rows);
   const int chunk = cdiv(rows, rb);
   colsum_stage1<<<dim3(cdiv(cols, 64), rb), NT, 0, s>>>(part, rows, cols, ld, chunk, (double*)ws);
-  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, out, split, out_hi);
+  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, segs);
   EUNET_LAUNCH_CHECK("colsum");
   return EUNET_OK;
+}
+
+int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s, int split,
+                    float* out_hi) {
+  ColSegs g = {{out, out_hi, nullptr, nullptr}, {0, split, 0, 0}, out_hi != nullptr ? 2 : 1};
+  return eunet_colsum_segs(part, rows, cols, ld, g, ws, s);
 }
 
 extern "C" {

@@ -194,6 +194,14 @@ __device__ __forceinline__ float up2_adj_w(int o, int in, int i) {
 // >= split go to out_hi[col - split] when out_hi != nullptr
 int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s,
                     int split = 0, float* out_hi = nullptr);
+// the same over several outputs: column c goes to out[i][c - start[i]] for the last segment i with
+// start[i] <= c (start[0] = 0; one launch pair for a partial row that packs several gradients)
+struct ColSegs {
+  float* out[4];
+  int start[4];
+  int n;
+};
+int eunet_colsum_segs(const float* part, int rows, int cols, int ld, const ColSegs& segs, void* ws, hipStream_t s);
 
 // kernels with > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
 template <typename K>

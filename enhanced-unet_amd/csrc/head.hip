@@ -1757,10 +1757,10 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   else HEAD_DISPATCH(head_bwd1_kernel, L.grid, NT, 0, s);
   EUNET_LAUNCH_CHECK("head_bwd1");
   const int ld1 = (k + 2) * MID + k;
-  if ((rc = eunet_colsum_ld(a.part, L.grid, k * MID, ld1, gw2, cws, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + k * MID, L.grid, MID, ld1, gbeta, cws, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + (k + 1) * MID, L.grid, MID, ld1, ggamma, cws, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + (k + 2) * MID, L.grid, k, ld1, gb2, cws, s))) return rc;
+  {  // one column sum over the packed row [gW2 | dbeta | dgamma | gb2]
+    const ColSegs g = {{gw2, gbeta, ggamma, gb2}, {0, k * MID, (k + 1) * MID, (k + 2) * MID}, 4};
+    if ((rc = eunet_colsum_segs(a.part, L.grid, ld1, ld1, g, cws, s))) return rc;
+  }
   a.dbeta = gbeta; a.dgamma = ggamma;
   const long long P2 = (long long)n * 4 * h * w;
   const int gridw = L.grid;
@@ -1778,8 +1778,7 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
     EUNET_LAUNCH_CHECK("head_wgrad");
   }
   const int ldw = MID * k * 9 + MID;
-  if ((rc = eunet_colsum_ld(a.part, gridw, MID * k * 9, ldw, gw1, cws, s))) return rc;
-  if ((rc = eunet_colsum_ld(a.part + MID * k * 9, gridw, MID, ldw, gb1, cws, s))) return rc;
+  if ((rc = eunet_colsum_ld(a.part, gridw, MID * k * 9 + MID, ldw, gw1, cws, s, MID * k * 9, gb1))) return rc;
   if (mf) {
     const unsigned gg = (unsigned)(((long long)n * h * w + 255) / 256);
     if (k == 1) head_patch_gather_kernel<1><<<gg, 256, 0, s>>>(a.patch, gz, n, h, w, a.tx, a.ty);
