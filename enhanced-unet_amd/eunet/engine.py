@@ -105,6 +105,12 @@ class UNetEngine:
     # next level's HBM-bound upsample / max-pool adjoints instead of the dgrad (they ran 2.7x longer:
     # +0.85 ms/step in a same-box A/B, profiles/r03_ab.txt)
     fuse_bn_apply_a = False
+    # dgrad_first -- after a DoubleConv's BN-a backward, conv .0's data gradient is issued on the launch
+    # stream before the side-stream weight gradients (which wait on an event recorded right after the
+    # apply, not on the launch stream's tail): the host no longer issues the weight-gradient launches and
+    # three stream joins between the apply and the dgrad, a ~24 us launch-stream gap per block
+    # (profiles/r03_step_timeline.txt)
+    dgrad_first = True
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -283,16 +289,27 @@ class UNetEngine:
                              bn["shift"], dbeta, dgamma, ops.act(gy))
             return gy
 
+        def dgrad0(gya):  # conv .0's data gradient (the block's input gradient)
+            wpt = S["wp"].get(p + ".0.weight^T") if S.get("wp") else None
+            if wpt is None:
+                wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
+            gx = _e((N, H, W, X.c), dt, dev)
+            ops.conv3x3_dgrad(ops.act(gya), wpt, ops.act(gx))
+            return gx
+
         main = torch.cuda.current_stream(dev)
         side = side_stream(dev) if self.overlap_wgrad else None
 
-        def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False, on_main=False):
+        def wgrad(conv, xa: ops.Act, gy, scale=None, shift=None, small_conv=False, on_main=False, ready=None):
             # the gradient slots are allocated on the launch stream (their consumers run there)
             dw = sink.slot(conv + ".weight", (C, xa.c, 3, 3))
             db = sink.slot(conv + ".bias", (C,))
             if side is None or on_main:
                 return wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
-            side.wait_stream(main)  # gy (and everything before it) is ready
+            if ready is not None:
+                side.wait_event(ready)  # recorded on the launch stream once gy was complete
+            else:
+                side.wait_stream(main)  # gy (and everything before it) is ready
             with torch.cuda.stream(side):
                 wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
             for t in (gy, xa._keep, dw, db):  # the caching allocator must not hand these out early
@@ -333,28 +350,35 @@ class UNetEngine:
         ops.conv3x3_dgrad_bnbwd(ops.act(gyb), wpt, ops.act(gaa), ops.act(ya), bna["mean"], bna["invstd"],
                                 bna["scale"], bna["shift"], cpart)
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
+        ev = None
+        gx = None
+        if side is not None and self.dgrad_first and need_gx:
+            ev = torch.cuda.Event()
+            ev.record(main)  # gyb, gya and the BN-parameter gradients are complete
+            gx = dgrad0(gya)
         if self.wg3_late:
-            wgrad3()
+            if s.get("za") is not None:
+                wgrad(p + ".3", ops.act(s["za"]), gyb, ready=ev)
+            else:
+                wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"], ready=ev)
         del gyb
         # the trunk's last weight gradient (no data gradient follows it): on the main stream, which is
         # otherwise idle here, instead of queueing behind the side stream's conv .3 wgrad
-        wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx)
+        wgrad(p + ".0", X, gya, small_conv=small, on_main=not need_gx, ready=ev)
         del gaa
         names = [f"{p}.{i}.{w}" for i in (0, 1, 3, 4) for w in ("weight", "bias")]
         if side is None:
             sink.ready(names)
         else:  # a bucket all-reduce launched here orders after both streams' work, without stalling main
-            side.wait_stream(main)
+            if ev is not None:
+                side.wait_event(ev)
+            else:
+                side.wait_stream(main)
             with torch.cuda.stream(side):
                 sink.ready(names)
         if not need_gx:
             return None
-        wpt = S["wp"].get(p + ".0.weight^T") if S.get("wp") else None
-        if wpt is None:
-            wpt = ops.conv3x3_pack(P[p + ".0.weight"], dt, flip=True)
-        gx = _e((N, H, W, X.c), dt, dev)
-        ops.conv3x3_dgrad(ops.act(gya), wpt, ops.act(gx))
-        return gx
+        return gx if gx is not None else dgrad0(gya)
 
     def _block_bwd_fused(self, nm, G, S, P, sink, need_gx, small, gred, wgrad, side, main):
         """_block_bwd with each BN backward's apply fused into the data gradient that consumes it:

@@ -230,7 +230,8 @@ class Trainer:
         return self.optimizer.param_groups[0]["lr"]
 
 
-ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late", "fuse_bn_apply", "fuse_bn_apply_a")
+ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late", "fuse_bn_apply", "fuse_bn_apply_a",
+                "dgrad_first")
 
 
 class StepGraph:

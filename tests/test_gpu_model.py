@@ -319,22 +319,24 @@ def test_materialised_activation_is_exact(dtype, monkeypatch):
 
 def test_backward_stream_schedules_are_exact(monkeypatch):
     """The weight gradients on the side stream (conv .3's enqueued early or after the block's BN-a
-    backward, UNetEngine.wg3_late) or all on the launch stream run the same kernels on the same
-    operands: every gradient agrees bit for bit."""
+    backward, UNetEngine.wg3_late; conv .0's data gradient issued before or after them,
+    UNetEngine.dgrad_first) or all on the launch stream run the same kernels on the same operands:
+    every gradient agrees bit for bit."""
     from eunet import engine, synth
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 64, 64, start_index=5, num_classes=2, in_channels=1)
     out = {}
-    for overlap, late in ((True, True), (True, False), (False, True)):
+    for overlap, late, first in ((True, True, True), (True, True, False), (True, False, True), (False, True, True)):
         monkeypatch.setattr(engine.UNetEngine, "wg3_late", late)
         monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", overlap)
+        monkeypatch.setattr(engine.UNetEngine, "dgrad_first", first)
         m = _model(16, 1, 2, "bf16")
         m.train()
         loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
         loss.backward()
         torch.cuda.synchronize()
-        out[(overlap, late)] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
-    ref = out[(True, True)]
+        out[(overlap, late, first)] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    ref = out[(True, True, True)]
     for key, grads in out.items():
         for k, g in grads.items():
             assert torch.equal(g, ref[k]), (key, k)
