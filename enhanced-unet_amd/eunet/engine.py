@@ -107,10 +107,11 @@ class UNetEngine:
     fuse_bn_apply_a = False
     # dgrad_first -- after a DoubleConv's BN-a backward, conv .0's data gradient is issued on the launch
     # stream before the side-stream weight gradients (which wait on an event recorded right after the
-    # apply, not on the launch stream's tail): the host no longer issues the weight-gradient launches and
-    # three stream joins between the apply and the dgrad, a ~24 us launch-stream gap per block
-    # (profiles/r03_step_timeline.txt)
-    dgrad_first = True
+    # apply, not on the launch stream's tail).  Closes half of the ~24 us apply -> dgrad launch-stream gap
+    # per block, but the dgrads then take the CUs first and the squeezed weight gradients spread over the
+    # HBM-bound kernels: step time unchanged in a same-box A/B (+0.1 %), the conv family's wall-time
+    # fraction 0.369 -> 0.341 (profiles/r03_ab.txt).  Off by default.
+    dgrad_first = False
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
