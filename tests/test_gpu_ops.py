@@ -407,6 +407,48 @@ def test_head_fwd_bwd(K, dt, N, H, W):
         tols = [max(1e-2, 1.5 * rel(a, r)) for a, r in zip(acv, refs)]
     for nm, o, r, t in zip(names, ours, refs, tols):
         assert rel(o, r) < t, (nm, rel(o, r), t)
+
+
+def test_head_bf16_persistent_tile_loop():
+    """bf16 head at a size where the persistent blocks loop over several 32 x 32 / 16 x 16 2H tiles (with
+    the next tile's z / g_o prefetched across iterations) and tiles are ragged at the border: forward,
+    logits and every gradient against an fp32 torch autograd reference of the same head on the GPU
+    (bf16 operand rounding ~1e-2; an indexing fault shows as O(1))."""
+    ops = _ops()
+    K, N, H, W = 2, 2, 408, 392
+    g = torch.Generator(device=DEV).manual_seed(11)
+    r = lambda *sh, sc=1.0: torch.randn(*sh, device=DEV, generator=g) * sc  # noqa: E731
+    z, w1, b1 = r(N, K, H, W), r(64, K, 3, 3, sc=0.25), r(64, sc=0.1)
+    gamma, beta = torch.rand(64, device=DEV, generator=g) + 0.5, r(64, sc=0.1)
+    w2, b2, glog = r(K, 64, 1, 1, sc=0.125), r(K, sc=0.1), r(N, K, H, W)
+    leaves = [t.clone().requires_grad_(True) for t in (z, w1, b1, gamma, beta, w2, b2)]
+    out = _head_ref(*leaves)
+    logit_ref = F.avg_pool2d(out, 2)
+    logit_ref.backward(glog)
+    zd = nhwc(z).contiguous()
+    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K, torch.bfloat16), dtype=torch.uint8, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    mean, inv = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    out2h = torch.empty(N, K, 2 * H, 2 * W, device=DEV)
+    logits = torch.empty(N, K, H, W, device=DEV)
+    w2f = w2.reshape(K, 64).contiguous()
+    ops.head_fwd(zd, N, H, W, K, w1, b1, gamma, beta, w2f, b2, True, 1e-5, 0.1, rm, rv, mean, inv, out2h, logits,
+                 ws, dtype=torch.bfloat16)
+    gz = torch.empty(N, H, W, K, device=DEV)
+    gw1, gb1 = torch.empty(64, K, 3, 3, device=DEV), torch.empty(64, device=DEV)
+    gg, gbt = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    gw2, gb2 = torch.empty(K, 64, device=DEV), torch.empty(K, device=DEV)
+    ops.head_bwd(zd, N, H, W, K, w1, b1, gamma, beta, w2f, mean, inv, glog.contiguous(), None, gz, gw1, gb1, gg,
+                 gbt, gw2, gb2, ws, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    checks = [("out2h", out2h, out, 2e-2), ("logits", logits, logit_ref, 2e-2),
+              ("gz", gz, nhwc(leaves[0].grad), 0.1), ("gw1", gw1, leaves[1].grad, 0.1),
+              ("gg", gg, leaves[3].grad, 3e-2), ("gbt", gbt, leaves[4].grad, 3e-2),
+              ("gw2", gw2, leaves[5].grad.reshape(K, 64), 3e-2), ("gb2", gb2, leaves[6].grad, 1e-3)]
+    errs = {nm: rel(o, ref) for nm, o, ref, _ in checks}
+    print("head bf16 persistent-loop errors vs fp32:", errs)
+    for nm, _, _, t in checks:
+        assert errs[nm] < t, (nm, errs[nm], t)
     assert float(gb1.abs().max()) < 1e-3 * float(gw1.abs().max()) + 1e-5  # pre-BN bias: ~0
 
 
