@@ -39,6 +39,7 @@ class DualEngine:
         self.ea = UNetEngine(model, prefix="unetpp.")
         self.eb = UNetEngine(model, prefix="deeplab.")
         self.drop_keep = None  # tests: fixed ([N,256], [N,128]) keep masks instead of bernoulli draws
+        self.keep_state = False  # tests: keep the last training forward's state as last_state (engine.py)
 
     @property
     def dtype(self):
@@ -291,6 +292,8 @@ class DualFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, engine, sink_factory, *params):
         out, aux_a, aux_b, S = engine.forward(x, training=True)
+        if engine.keep_state:
+            engine.last_state = S
         ctx.S, ctx.engine, ctx.sink_factory = S, engine, sink_factory
         ctx.names = [n for n, _ in engine.m.named_parameters()]
         return out, aux_a, aux_b

@@ -112,6 +112,10 @@ class UNetEngine:
     # HBM-bound kernels: step time unchanged in a same-box A/B (+0.1 %), the conv family's wall-time
     # fraction 0.369 -> 0.341 (profiles/r03_ab.txt).  Off by default.
     dgrad_first = False
+    # keep_state -- tests: the last training forward's saved tensors (pre-BN conv outputs, BN affines)
+    # stay reachable as self.last_state, so a checker can read the branch configuration (ReLU masks,
+    # max-pool argmax) the kernels took (tests/_pins.py)
+    keep_state = False
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -567,6 +571,8 @@ class UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, want, engine, sink_factory, *params):
         out, S = engine.forward(x, training=True, want=want)
+        if engine.keep_state:
+            engine.last_state = S
         ctx.S = S
         ctx.engine = engine
         ctx.sink_factory = sink_factory

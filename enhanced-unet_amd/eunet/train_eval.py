@@ -285,7 +285,10 @@ class StepGraph:
         eng = getattr(trainer.model, "_engine", None)
         if getattr(eng, "drop_keep", None) is not None:
             raise RuntimeError("Trainer.step_graph: fixed dropout keep masks (a test hook) are host inputs")
-        knobs = tuple(getattr(eng, k, None) for k in ENGINE_KNOBS)
+        # the compute dtype is baked into the captured kernels and buffers: EnhancedUNet.set_dtype
+        # (which only changes the engine's dtype) must re-capture
+        knobs = tuple(getattr(eng, k, None) for k in ENGINE_KNOBS) + (
+            str(getattr(eng, "dtype", None)), str(getattr(trainer.model, "compute_dtype", None)))
         ps = [p for g in trainer.optimizer.param_groups for p in g["params"]]
         store = (id(trainer.optimizer), ps[0].data_ptr(), ps[-1].data_ptr(), len(ps))
         lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight)
@@ -311,8 +314,11 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
 
     Without train_loader / val_loader it builds the reference's loaders (train_eval.py:1054-1075):
     eunet.data.CellDataset(data_dir, 'train' / 'val', max_size=640), batch 2 on cuda (1 otherwise),
-    the train split shuffled, val batch 1; on cuda the training loader decodes in loader_workers
-    (default 4) worker processes and prefetches 2 batches (same augmentation draws, DataLoader).
+    the train split shuffled, val batch 1; on cuda the training loader prefetches 2 batches and,
+    with loader_workers > 0 (opt-in; default 0 = the reference's num_workers=0), decodes in that many
+    'spawn' worker processes -- the calling script then needs an `if __name__ == "__main__":` guard.
+    The Python `random` augmentation decisions follow the reference's draw order; the Gaussian noise
+    values do so only with host_noise (eunet.data.CellDataset).
     Any iterable of collate_fn batch dicts ({'images', 'batch_items': [{'semantic_mask'}]}) may be
     passed instead, e.g. eunet.synth.loader.  step_graph (default: on for the single-branch model on
     cuda) replays the training steps from captured HIP graphs (Trainer.step_graph, bit-identical)."""
@@ -323,13 +329,14 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
     checkpoint_path = os.path.join(save_dir, "best_model.pth")
     if os.path.exists(checkpoint_path) and skip_training:
         return checkpoint_path
+    own_loader = train_loader is None
     if train_loader is None:
         from .data import CellDataset, DataLoader, collate_fn
         if data_dir is None:
             raise ValueError("train_model needs data_dir (a LabelMe directory) or explicit loaders")
         on_gpu = str(device).startswith("cuda")
         batch_size = 2 if on_gpu else 1  # train_eval.py:1058-1059
-        workers = (4 if on_gpu else 0) if loader_workers is None else loader_workers
+        workers = 0 if loader_workers is None else loader_workers
         train_loader = DataLoader(CellDataset(data_dir, split="train", max_size=640, device=device),
                                   batch_size=batch_size, shuffle=True, collate_fn=collate_fn, workers=workers,
                                   prefetch=2 if on_gpu else 0)
@@ -345,8 +352,20 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
     if step_graph is None:
         step_graph = str(device).startswith("cuda") and not getattr(model, "dual_branch", False)
     trainer.step_graph = bool(step_graph)
-    best_loss, best_miou = float("inf"), 0.0
     patience = 10 if model_name == "enhanced_unet" else 8
+    try:
+        _train_epochs(trainer, model, model_name, device, train_loader, val_loader, history, checkpoint_path,
+                      train_epochs, patience, verbose)
+    finally:
+        close = getattr(train_loader, "close", None) if own_loader else None
+        if callable(close):  # worker processes end with the training, not at garbage collection
+            close()
+    return checkpoint_path
+
+
+def _train_epochs(trainer, model, model_name, device, train_loader, val_loader, history, checkpoint_path,
+                  train_epochs, patience, verbose):
+    best_loss, best_miou = float("inf"), 0.0
     patience_counter = 0
     for epoch in range(train_epochs):
         current_lr = trainer.epoch_lr_step(epoch)
@@ -374,7 +393,6 @@ def train_model(model_name: str, data_dir: str = None, device: str = "cuda", num
                 patience_counter += 1
         if patience_counter >= patience and epoch > 25:
             break
-    return checkpoint_path
 
 
 def _numpy_safe_globals():

@@ -75,17 +75,11 @@ def dual_formula_weights(base=64, in_ch=3, K=3, dtype=torch.float64) -> Dict[str
     return out
 
 
-def branch_forward(S, prefix: str, x, training: bool):
-    """BasicUNet trunk (models.py:227-237) ending at input resolution: dec1(d2)."""
-    T = {"model." + k[len(prefix) + 1:]: v for k, v in S.items() if k.startswith(prefix + ".")}
-    e1 = R._double_conv(T, "enc1", x, training)
-    e2 = R._double_conv(T, "enc2", F.max_pool2d(e1, 2), training)
-    e3 = R._double_conv(T, "enc3", F.max_pool2d(e2, 2), training)
-    e4 = R._double_conv(T, "enc4", F.max_pool2d(e3, 2), training)
-    d4 = R._double_conv(T, "dec4", torch.cat([R._up2(e4), e3], 1), training)
-    d3 = R._double_conv(T, "dec3", torch.cat([R._up2(d4), e2], 1), training)
-    d2 = R._double_conv(T, "dec2", torch.cat([R._up2(d3), e1], 1), training)
-    return F.conv2d(d2, T["model.dec1.weight"], T["model.dec1.bias"])
+def branch_forward(S, prefix: str, x, training: bool, pins=None):
+    """BasicUNet trunk (models.py:227-237) ending at input resolution: dec1(d2).  pins: the trunk's
+    branch configuration (eunet_ref.trunk)."""
+    d2, _ = R.trunk(S, x, training, pins, prefix=prefix + ".")
+    return F.conv2d(d2, S[prefix + ".dec1.weight"], S[prefix + ".dec1.bias"])
 
 
 def _drop(h, mask, p, training):
@@ -96,11 +90,14 @@ def _drop(h, mask, p, training):
     return h * mask.to(h.dtype)[:, :, None, None] / (1.0 - p)
 
 
-def dual_forward(S, x, training: bool = True, drop_masks=None):
+def dual_forward(S, x, training: bool = True, drop_masks=None, pins=None):
     """x [B,C,H,W] -> (fused [B,K,H,W], {'unetpp': .., 'deeplab': ..}); models.py:316-333.
-    drop_masks: optional ([B,256], [B,128]) 0/1 keep masks for the two Dropout2d."""
-    out_main = branch_forward(S, "unetpp", x, training)
-    out_aux = branch_forward(S, "deeplab", x, training)
+    drop_masks: optional ([B,256], [B,128]) 0/1 keep masks for the two Dropout2d.
+    pins: optional branch configuration {'unetpp': trunk pins, 'deeplab': trunk pins,
+    'fusion_head.1' / '.5' / '.9': ReLU masks} (eunet_ref._relu)."""
+    pins = pins or {}
+    out_main = branch_forward(S, "unetpp", x, training, pins.get("unetpp"))
+    out_aux = branch_forward(S, "deeplab", x, training, pins.get("deeplab"))
     ff = torch.cat([out_main, out_aux], 1)
     a = F.conv2d(ff, S["attention_gate.0.weight"], padding=1)
     a = F.gelu(R._bn(S, "attention_gate.1", a, training))
@@ -108,11 +105,14 @@ def dual_forward(S, x, training: bool = True, drop_masks=None):
     att = torch.sigmoid(R._bn(S, "attention_gate.4", a, training))
     ff = ff * att
     dm = drop_masks or (None, None)
-    h = F.relu(R._bn(S, "fusion_head.1", F.conv2d(ff, S["fusion_head.0.weight"], padding=1), training))
+    h = R._relu(R._bn(S, "fusion_head.1", F.conv2d(ff, S["fusion_head.0.weight"], padding=1), training),
+                pins.get("fusion_head.1"))
     h = _drop(h, dm[0], DROP_P[0], training)
-    h = F.relu(R._bn(S, "fusion_head.5", F.conv2d(h, S["fusion_head.4.weight"], padding=1), training))
+    h = R._relu(R._bn(S, "fusion_head.5", F.conv2d(h, S["fusion_head.4.weight"], padding=1), training),
+                pins.get("fusion_head.5"))
     h = _drop(h, dm[1], DROP_P[1], training)
-    h = F.relu(R._bn(S, "fusion_head.9", F.conv2d(h, S["fusion_head.8.weight"], padding=1), training))
+    h = R._relu(R._bn(S, "fusion_head.9", F.conv2d(h, S["fusion_head.8.weight"], padding=1), training),
+                pins.get("fusion_head.9"))
     fused = F.conv2d(h, S["fusion_head.11.weight"], S["fusion_head.11.bias"])
     fused = fused + F.conv2d(ff, S["fusion_residual.weight"], S["fusion_residual.bias"])
     return fused, {"unetpp": out_main, "deeplab": out_aux}

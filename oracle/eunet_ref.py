@@ -103,34 +103,75 @@ def _bn(S, prefix, h, training, momentum=0.1, eps=1e-5):
                         S[prefix + ".weight"], S[prefix + ".bias"], training, momentum, eps)
 
 
-def _double_conv(S, name, h, training):
-    p = f"model.{name}"
+# Branch pinning (test infrastructure).  The step is piecewise smooth: ReLU (models.py:221, 224, 311)
+# and MaxPool2d (models.py:214) choose a branch per element, and an fp32 implementation whose
+# activations sit within rounding of a kink or a tie may take the other one -- then its gradient
+# jumps by a finite amount against any oracle that chose differently.  With `pins` (from the GPU's
+# own saved pre-BN activations and BN affines, tests/_pins.py) the oracle evaluates the SAME
+# function on the branch configuration the kernels took: ReLU(h) -> h * mask, max-pool -> gather at
+# the given 2x2 argmax.  Where the masks agree with the oracle's own branches (every element not at
+# a kink) this is the reference forward exactly; its backward is the exact derivative there.
+def _relu(h, pin):
+    return F.relu(h) if pin is None else h * pin.to(h.dtype)
+
+
+def _pool(h, idx):
+    """MaxPool2d(2) (models.py:214); with idx [B,C,H/2,W/2] in 0..3 (row-major in the 2x2 window):
+    the element at idx instead of the max."""
+    if idx is None:
+        return F.max_pool2d(h, 2)
+    B, C, H, W = h.shape
+    w = h.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+    return w.gather(-1, idx.long().unsqueeze(-1)).squeeze(-1)
+
+
+def _double_conv(S, name, h, training, pins=None, prefix="model.", record=None):
+    """record: optional dict receiving the BatchNorm outputs (the ReLU inputs) under name + '.1' / '.4'."""
+    p = f"{prefix}{name}"
+    pins = pins or {}
     h = F.conv2d(h, S[p + ".0.weight"], S[p + ".0.bias"], padding=1)
-    h = F.relu(_bn(S, p + ".1", h, training))
+    h = _bn(S, p + ".1", h, training)
+    if record is not None:
+        record[name + ".1"] = h.detach()
+    h = _relu(h, pins.get(name + ".1"))
     h = F.conv2d(h, S[p + ".3.weight"], S[p + ".3.bias"], padding=1)
-    return F.relu(_bn(S, p + ".4", h, training))
+    h = _bn(S, p + ".4", h, training)
+    if record is not None:
+        record[name + ".4"] = h.detach()
+    return _relu(h, pins.get(name + ".4"))
 
 
 def _up2(h):
     return F.interpolate(h, scale_factor=2, mode="bilinear", align_corners=False)
 
 
+def trunk(S, x, training, pins=None, prefix="model.", record=None):
+    """BasicUNet encoder/decoder (models.py:227-235): d2.  pins: optional branch configuration
+    {'enc1.1': mask, ..., 'dec2.4': mask, 'pool1' .. 'pool3': argmax} (see _relu / _pool);
+    record: optional dict receiving every ReLU input (_double_conv)."""
+    pins = pins or {}
+    dc = lambda nm, h: _double_conv(S, nm, h, training, pins, prefix, record)  # noqa: E731
+    e1 = dc("enc1", x)
+    e2 = dc("enc2", _pool(e1, pins.get("pool1")))
+    e3 = dc("enc3", _pool(e2, pins.get("pool2")))
+    e4 = dc("enc4", _pool(e3, pins.get("pool3")))
+    d4 = dc("dec4", torch.cat([_up2(e4), e3], 1))
+    d3 = dc("dec3", torch.cat([_up2(d4), e2], 1))
+    d2 = dc("dec2", torch.cat([_up2(d3), e1], 1))
+    return d2, dict(e1=e1, e2=e2, e3=e3, e4=e4, d4=d4, d3=d3, d2=d2)
+
+
 def forward(S: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True,
-            return_levels: bool = False):
-    """x [B,C,H,W] -> logits [B,K,2H,2W]; BN running stats in S are updated in train mode."""
-    e1 = _double_conv(S, "enc1", x, training)
-    e2 = _double_conv(S, "enc2", F.max_pool2d(e1, 2), training)
-    e3 = _double_conv(S, "enc3", F.max_pool2d(e2, 2), training)
-    e4 = _double_conv(S, "enc4", F.max_pool2d(e3, 2), training)
-    d4 = _double_conv(S, "dec4", torch.cat([_up2(e4), e3], 1), training)
-    d3 = _double_conv(S, "dec3", torch.cat([_up2(d4), e2], 1), training)
-    d2 = _double_conv(S, "dec2", torch.cat([_up2(d3), e1], 1), training)
+            return_levels: bool = False, pins=None):
+    """x [B,C,H,W] -> logits [B,K,2H,2W]; BN running stats in S are updated in train mode.
+    pins: branch configuration of the trunk (trunk()) and of the head's ReLU ('enhance.1')."""
+    d2, lv = trunk(S, x, training, pins)
     u = F.conv2d(_up2(d2), S["model.dec1.weight"], S["model.dec1.bias"])
     h = F.conv2d(u, S["enhance.0.weight"], S["enhance.0.bias"], padding=1)
-    h = F.relu(_bn(S, "enhance.1", h, training))
+    h = _relu(_bn(S, "enhance.1", h, training), (pins or {}).get("enhance.1"))
     out = u + F.conv2d(h, S["enhance.3.weight"], S["enhance.3.bias"])
     if return_levels:
-        return out, dict(e1=e1, e2=e2, e3=e3, e4=e4, d4=d4, d3=d3, d2=d2, u=u)
+        return out, dict(lv, u=u)
     return out
 
 

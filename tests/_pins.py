@@ -1,0 +1,86 @@
+"""Branch configuration of a GPU training forward, for the branch-pinned oracle (test infrastructure).
+
+The kernels decide each ReLU from the BatchNorm affine of the stored pre-BN conv output,
+fmaf(y, scale, shift) > 0 (conv3x3 operand staging, bnrelu_pool / bnrelu_upsample / bnrelu_conv1x1,
+and every BN-backward site), and each 2x2 max-pool from round(relu(fmaf(y, scale, shift))) in the
+compute dtype with the first maximum in row-major order winning (bnrelu_pool_kernel; the adjoint
+recomputes the same argmax).  The same rules evaluated here on the engine's own saved tensors
+(UNetEngine.keep_state) give the oracle (oracle/eunet_ref.py _relu / _pool) the branches the GPU
+took.  In fp64, y * scale is exact for fp32 / bf16 operands, so the sign of y * scale + shift is the
+sign of the fused multiply-add's exact result -- the mask is the kernel's.  The pooled values are
+rounded fp64 -> fp32 (-> bf16): a double rounding that can differ from the kernel's single rounding
+only for results exactly between two representable values, which does not occur in these tests'
+inputs in practice (a wrong pin would show as a single-element gradient outlier).
+
+Not pinned: the 2H head's ReLU (enhance.1; its pre-BN input is recomputed inside the head kernels and
+never stored) -- the oracle keeps its own branches there.  With K <= 3 input channels the head conv's
+fp32 error is ~1e-7 relative, so a branch can differ only for activations within ~1e-7 of the kink.
+"""
+import torch
+
+POOLED = ("enc1", "enc2", "enc3")
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2)
+
+
+def relu_mask(y, scale, shift):
+    """fmaf(y, scale, shift) > 0 per element, y NHWC (any float dtype), scale / shift [C] or [N, C];
+    returns a bool NCHW tensor on the CPU."""
+    y = y.detach().double().cpu()
+    sc, sh = scale.detach().double().cpu(), shift.detach().double().cpu()
+    if sc.dim() == 2:
+        sc, sh = sc[:, None, None, :], sh[:, None, None, :]
+    return _nchw((y * sc + sh) > 0).contiguous()
+
+
+def pool_argmax(y, scale, shift, dtype):
+    """2x2 argmax (0..3, row-major, first maximum wins) of round_dtype(relu(fmaf(y, scale, shift)))."""
+    y = y.detach().double().cpu()
+    v = (y * scale.detach().double().cpu() + shift.detach().double().cpu()).float()
+    if dtype == torch.bfloat16:
+        v = v.bfloat16().float()
+    v = _nchw(v.clamp_min(0.0))
+    B, C, H, W = v.shape
+    w = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+    idx = torch.zeros(B, C, H // 2, W // 2, dtype=torch.long)
+    best = w[..., 0].clone()
+    for j in (1, 2, 3):
+        gt = w[..., j] > best  # strictly greater: the first maximum stays
+        idx[gt] = j
+        best = torch.where(gt, w[..., j], best)
+    return idx
+
+
+def trunk_pins(S, dtype):
+    """UNetEngine.forward_trunk state -> eunet_ref.trunk pins."""
+    pins = {}
+    for nm in ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2"):
+        s = S[nm]
+        pins[nm + ".1"] = relu_mask(s["ya"], s["bna"]["scale"], s["bna"]["shift"])
+        pins[nm + ".4"] = relu_mask(s["yb"], s["bnb"]["scale"], s["bnb"]["shift"])
+    for i, nm in enumerate(POOLED, 1):
+        s = S[nm]
+        pins[f"pool{i}"] = pool_argmax(s["yb"], s["bnb"]["scale"], s["bnb"]["shift"], dtype)
+    return pins
+
+
+def model_pins(model):
+    """Pins of the last training forward of an EnhancedUNet whose engine had keep_state set."""
+    eng = model._engine
+    S = eng.last_state
+    if not getattr(model, "dual_branch", False):
+        return trunk_pins(S, eng.dtype)
+    pins = {"unetpp": trunk_pins(S["SA"], eng.dtype), "deeplab": trunk_pins(S["SB"], eng.dtype)}
+    # fusion head: the ReLU after each BN is applied by the next kernel with the BN affine
+    # (Dropout2d folded in: relu(x) * m = relu(x * m) for m >= 0; a dropped channel passes nothing
+    # either way, so the mask of the un-dropped affine is used)
+    for key, y, h in (("fusion_head.1", "y1", "h1"), ("fusion_head.5", "y2", "h2"), ("fusion_head.9", "y3", "h3")):
+        pins[key] = relu_mask(S[y], S[h]["scale"], S[h]["shift"])
+    return pins
+
+
+def keep(model, on=True):
+    model._engine.keep_state = on
+    return model

@@ -212,3 +212,150 @@ def test_dp_nccl_world1_configs3_workload_bit_identical():
     assert res["buckets"] == 4 and res["mb"] > 29, res  # 31 MB of gradients in 8 MiB buckets
     assert res["grads_equal"], "DP gradients (world 1, RCCL) must equal the plain backward bit for bit"
     assert res["same_step"], "two Trainer steps with DataParallel must equal the plain steps bit for bit"
+
+
+def _flat_state(model, which):
+    ts = [p.detach() for p in model.parameters()] if which == "params" else \
+        [b.detach() for b in model.buffers() if b.dtype.is_floating_point]
+    return torch.cat([t.reshape(-1).float().cpu() for t in ts])
+
+
+def _trainer_worker(rank, world, port, q, cfg):
+    """World-2 Trainer steps through DataParallel with the HIP engine, gloo carrying the collectives
+    (both ranks share the one GPU): bf16, default 8 MiB buckets, weight gradients on the side stream.
+    Per step: every rank's parameters equal bit for bit; the BN running statistics differ before the
+    broadcast (each replica normalised its own shard) and equal bit for bit after it.  cfg 'fp32'
+    additionally returns the step's averaged, clipped gradients and each rank's branch-pinned oracle
+    gradients of its shard (fp64 and fp32) for the mean-of-shards check in the parent."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "enhanced-unet_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import dual_ref as D
+        from oracle import eunet_ref as R
+        from eunet import synth
+        from eunet.dp import DataParallel
+        from eunet.engine import UNetEngine
+        from eunet.models import EnhancedUNet
+        from eunet.train_eval import Trainer
+        assert UNetEngine.overlap_wgrad
+        dual = cfg == "dual"
+        base, H, dt = {"single": (64, 256, "bf16"), "dual": (16, 64, "bf16"), "fp32": (16, 64, "fp32")}[cfg]
+        W = (D.dual_formula_weights if dual else R.formula_weights)(base, 1, 2)
+        mod = EnhancedUNet(num_classes=2, in_channels=1, base_ch=base, dtype=dt, dual_branch=dual)
+        mod.load_state_dict({k: (v.float() if v.is_floating_point() else v) for k, v in W.items()})
+        mod = mod.cuda().train()
+        if dual:
+            gen = torch.Generator().manual_seed(9 + rank)
+            mod._engine.drop_keep = ((torch.rand(2, 256, generator=gen) > 0.2).float(),
+                                     (torch.rand(2, 128, generator=gen) > 0.15).float())
+        tr = Trainer(mod, "cuda", "enhanced_unet")
+        for g in tr.optimizer.param_groups:
+            g["lr"] = 1e-3
+        tr.dp = DataParallel(mod)  # default buckets
+        out = dict(rank=rank, buckets=len(tr.dp.buckets), steps=[])
+        if cfg == "fp32":
+            import _pins
+            _pins.keep(mod)
+        for step in range(3):
+            x, m = synth.batch(2, H, H, start_index=300 + 10 * step + 2 * rank, num_classes=2, in_channels=1,
+                               device="cuda")
+            loss = tr.step(x, m)
+            torch.cuda.synchronize()
+            params = _flat_state(mod, "params")
+            pre = _flat_state(mod, "buffers")
+            tr.dp.before_forward()  # the broadcast the next step starts with
+            torch.cuda.synchronize()
+            post = _flat_state(mod, "buffers")
+            gs = [torch.zeros_like(t) for t in (params, pre, post) for _ in range(world)]
+            for i, t in enumerate((params, pre, post)):
+                dist.all_gather(gs[i * world:(i + 1) * world], t)
+            rec = dict(loss=loss, params_equal=torch.equal(gs[0], gs[1]), pre_differ=not torch.equal(gs[2], gs[3]),
+                       post_equal=torch.equal(gs[4], gs[5]))
+            if cfg == "fp32" and step == 0:
+                pins = _pins.model_pins(mod)
+                rec["grads"] = {k: p.grad.detach().double().cpu() for k, p in mod.named_parameters()}
+                for odt, key in ((torch.float64, "oracle64"), (torch.float32, "oracle32")):
+                    S = R.formula_weights(base, 1, 2, dtype=odt)
+                    for k in S:
+                        if S[k].is_floating_point() and "running" not in k:
+                            S[k].requires_grad_(True)
+                    R.batch_loss(R.forward(S, x.cpu().to(odt), True, pins=pins), m.cpu()).backward()
+                    rec[key] = {k: S[k].grad.double() for k in rec["grads"]}
+            out["steps"].append(rec)
+        q.put(out)
+    except Exception as e:  # report instead of hanging the parent on q.get
+        import traceback
+        q.put(dict(rank=rank, error=traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_world2(cfg):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, cfg)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=500) for _ in procs), key=lambda r: r["rank"])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert "error" not in r, r["error"]
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cfg", ["single", "dual"])
+def test_dp_world2_trainer_steps_keep_replicas_identical(cfg):
+    """Three clipped AdamW Trainer steps at world size 2 (train_eval.py:337-343 per rank + the
+    gradient all-reduce): single-branch base 64 at 256^2 and the dual model (its own bucket order:
+    fusion head -> gate -> unetpp -> deeplab) at base 16; bf16, default buckets, side-stream weight
+    gradients.  After every step both ranks hold bit-identical parameters; the BN running statistics
+    differ between the replicas until rank 0's are broadcast, and are bit-identical after it."""
+    res = _run_world2(cfg)
+    for r in res:
+        print(cfg, "rank", r["rank"], "buckets", r["buckets"], [(s["loss"], s["params_equal"], s["pre_differ"],
+                                                                   s["post_equal"]) for s in r["steps"]])
+        assert len(r["steps"]) == 3
+        for s in r["steps"]:
+            assert s["params_equal"] and s["post_equal"] and s["pre_differ"], s
+    assert res[0]["steps"][-1]["loss"] != res[1]["steps"][-1]["loss"]  # the shards really differ
+
+
+@pytest.mark.timeout(600)
+def test_dp_world2_step_is_mean_of_shards_oracle():
+    """fp32 world-2 step (base 16, 64^2, B 2 per rank): the all-reduced, clipped gradients every rank
+    applies equal the oracle's mean over the two shards of each shard's branch-pinned gradient (its
+    own BatchNorm statistics, as per-replica BN under DDP), clipped to total norm 1.0
+    (train_eval.py:341), within max(1e-3, 3x the fp32 oracle's error) relative L2 per tensor."""
+    res = _run_world2("fp32")
+    s0, s1 = res[0]["steps"][0], res[1]["steps"][0]
+    for s in (s0, s1):
+        assert s["params_equal"] and s["post_equal"]
+
+    def mean_clipped(key):
+        g = {k: 0.5 * (s0[key][k] + s1[key][k]) for k in s0[key]}
+        norm = float(torch.sqrt(sum((v ** 2).sum() for v in g.values())))
+        c = min(1.0, 1.0 / (norm + 1e-6))
+        return {k: v * c for k, v in g.items()}
+
+    ref, ref32 = mean_clipped("oracle64"), mean_clipped("oracle32")
+    scale = max(float(v.abs().max()) for v in ref.values())
+    rows = []
+    for k, g in s0["grads"].items():
+        assert torch.equal(g, s1["grads"][k]), k
+        if k.endswith((".0.bias", ".3.bias")) and not k.startswith("enhance.3"):
+            assert float((g - ref[k]).abs().max()) < 1e-4 * scale, k
+            continue
+        err = float((g - ref[k]).norm() / ref[k].norm().clamp_min(1e-30))
+        tol = max(1e-3, 3 * float((ref32[k] - ref[k]).norm() / ref[k].norm().clamp_min(1e-30)))
+        rows.append((err / tol, k, err, tol))
+    for r in sorted(rows, reverse=True)[:4]:
+        print("world-2 mean-of-shards grad (ratio, name, err, tol):", r)
+    assert all(r[0] < 1.0 for r in rows), sorted(rows, reverse=True)[:3]

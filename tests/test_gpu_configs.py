@@ -1,0 +1,209 @@
+"""BASELINE.json configs at their own workloads on the GPU (not only in the bench).
+
+configs[1]: base 64, 1 x 512^2 -> 2 classes, batch 8, fp32 (models.py:217-238, train_eval.py:236-353):
+  logits per pixel and the loss vs the fp64 oracle, every parameter gradient vs the fp32 CPU oracle --
+  both evaluated on the branch configuration the GPU took (tests/_pins.py).
+configs[4]: dual-branch base 96 + deep supervision, 2048^2, batch 2, bf16 (models.py:253-333,
+  train_eval.py:199-234): an fp64 oracle at this size is out of reach of the host, so full-size
+  properties -- finite loss; two runs bit-identical; the side-stream and the serial weight-gradient
+  schedules bit-identical; BN running statistics equal to an fp64 reduction of the stored pre-BN
+  tensors; the loss decreasing over 3 steps -- plus a 256^2 slice of the same model vs the oracle.
+"""
+import pytest
+import torch
+
+from oracle import dual_ref as D
+from oracle import eunet_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel_l2(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _rel_px(a, b, floor=1e-2):
+    """test_gpu_model's per-pixel gate: |a - b| / max(|b|, floor x max|b|)."""
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float(((a - b).abs() / b.abs().clamp_min(floor * float(b.abs().max()))).max())
+
+
+def _pre_bn_bias(k):
+    return k.endswith((".0.bias", ".3.bias")) and not k.startswith("enhance.3")
+
+
+def test_configs1_fp32_512_batch8_vs_oracle():
+    """BASELINE configs[1] (base 64, c 1, K 2, fp32, 512^2, B 8): one training step.
+    Logits [8,2,512,512] per pixel within 1e-3 of the fp64 oracle (floor 1e-2 of max|ref|, as every
+    per-pixel gate here), loss within 1e-4; every parameter gradient within 1e-3 relative L2 of the
+    pinned fp32 CPU oracle (conv biases ahead of a BatchNorm, whose true gradient is 0, against the
+    global gradient scale).  The fp64 backward at this size is left out (host time)."""
+    import _pins
+    from eunet import synth
+    from eunet.losses import combined_loss
+    from eunet.models import EnhancedUNet
+    x, msk = synth.batch(8, 512, 512, start_index=41, num_classes=2, in_channels=1)
+    m = EnhancedUNet(num_classes=2, in_channels=1, base_ch=64, dtype="fp32")
+    m.load_state_dict({k: (v.float() if v.is_floating_point() else v) for k, v in R.formula_weights(64, 1, 2).items()})
+    m = _pins.keep(m.to(DEV).train())
+    logits = m.forward_lowres(x.to(DEV))
+    loss = combined_loss(logits, msk.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    pins = _pins.model_pins(m)
+    m._engine.last_state = None
+    logits = logits.detach().cpu()
+    with torch.no_grad():
+        S64 = R.formula_weights(64, 1, 2)
+        out64 = R.forward(S64, x.double(), training=True, pins=pins)
+        loss64 = R.batch_loss(out64, msk)
+        ref64 = torch.nn.functional.avg_pool2d(out64, 2)
+        del out64
+    px = _rel_px(logits, ref64)
+    print("configs[1] logits per-pixel vs fp64:", px, "loss", loss.item(), float(loss64))
+    assert px < 1e-3
+    assert abs(loss.item() - float(loss64)) < 1e-4 * abs(float(loss64))
+    del ref64
+    S = R.formula_weights(64, 1, 2, dtype=torch.float32)
+    for k in S:
+        if S[k].is_floating_point() and "running" not in k:
+            S[k].requires_grad_(True)
+    R.batch_loss(R.forward(S, x, training=True, pins=pins), msk).backward()
+    scale = max(float(S[k].grad.abs().max()) for k in S if S[k].grad is not None)
+    rows = []
+    for k, p in m.named_parameters():
+        ref = S[k].grad
+        if _pre_bn_bias(k):
+            assert float((p.grad.double().cpu() - ref.double()).abs().max()) < 1e-4 * scale, k
+            continue
+        rows.append((_rel_l2(p.grad, ref), k))
+    for r in sorted(rows, reverse=True)[:5]:
+        print("configs[1] grad vs pinned fp32 oracle (relL2, name):", r)
+    assert all(r[0] < 1e-3 for r in rows), sorted(rows, reverse=True)[:3]
+    for k, v in m.state_dict().items():
+        if "running" in k:
+            assert _rel_l2(v, S[k]) < 1e-4, k
+
+
+# ---- configs[4]: dual-branch base 96, 2048^2, B 2, bf16 ---------------------------------------------------
+B4, H4 = 2, 2048
+
+
+def _keep(seed=3):
+    gen = torch.Generator().manual_seed(seed)
+    return ((torch.rand(B4, 256, generator=gen) > 0.2).float(), (torch.rand(B4, 128, generator=gen) > 0.15).float())
+
+
+def _dual96(dtype="bf16"):
+    from eunet.models import EnhancedUNet
+    m = EnhancedUNet(num_classes=2, in_channels=1, base_ch=96, dtype=dtype, dual_branch=True)
+    m.load_state_dict({k: (v.float() if v.is_floating_point() else v)
+                       for k, v in D.dual_formula_weights(96, 1, 2).items()})
+    m = m.to(DEV).train()
+    m._engine.drop_keep = _keep()
+    return m
+
+
+@pytest.fixture(scope="module")
+def cfg4_batch():
+    from eunet import synth
+    x, msk = synth.batch(B4, H4, H4, start_index=61, num_classes=2, in_channels=1)
+    return x.to(DEV), msk.to(DEV)
+
+
+def _grads(m, x, msk):
+    from eunet.train_eval import Trainer
+    tr = Trainer(m, DEV, "enhanced_unet")
+    loss = tr.aux_loss(m(x), m.get_aux_outputs(), msk)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+
+def test_configs4_dual96_2048_deterministic_and_schedules_exact(cfg4_batch, monkeypatch):
+    """configs[4] workload: the loss is finite, two runs from the same weights / dropout masks give
+    bit-identical losses and gradients, and so does the serial schedule (weight gradients on the
+    launch stream, UNetEngine.overlap_wgrad = False) -- at 2048^2 the grids, split counts and the
+    > 2 GiB per-sample conv slices (dec2.0 input: 2048^2 x 288 channels) are the production ones."""
+    from eunet import engine
+    x, msk = cfg4_batch
+    l1, g1 = _grads(_dual96(), x, msk)
+    assert torch.isfinite(l1).all()
+    assert all(torch.isfinite(g).all() for g in g1.values())
+    l2, g2 = _grads(_dual96(), x, msk)
+    assert torch.equal(l1, l2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), ("rerun", k)
+    del g2
+    monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", False)
+    l3, g3 = _grads(_dual96(), x, msk)
+    assert torch.equal(l1, l3)
+    for k in g1:
+        assert torch.equal(g1[k], g3[k]), ("serial schedule", k)
+
+
+def test_configs4_bn_running_stats_match_fp64_reduction(cfg4_batch):
+    """One training forward at the configs[4] size from fresh running statistics (mean 0, var 1):
+    running_mean = 0.1 mean, running_var = 0.9 + 0.1 unbiased var of the layer's pre-BN output; the
+    fp64 reduction of the STORED pre-BN tensor (bf16) is the reference -- for the first conv of a trunk
+    (unetpp.enc1.1, 96 channels over 2 x 2048^2 pixels) and the fusion head's last 3x3 (fusion_head.9,
+    64 channels).  The kernels reduce the fp32 accumulators before rounding; the bf16 rounding of the
+    stored values moves a mean by << 1e-3 of the channel's std."""
+    import _pins
+    x, _ = cfg4_batch
+    m = _pins.keep(_dual96())
+    with torch.enable_grad():
+        m(x)
+    S = m._engine.last_state
+    sd = m.state_dict()
+    for key, y in (("unetpp.enc1.1", S["SA"]["enc1"]["ya"]), ("fusion_head.9", S["y3"])):
+        yd = y.double().reshape(-1, y.shape[-1])
+        n = yd.shape[0]
+        mean = yd.mean(0)
+        var = yd.var(0, unbiased=True)
+        rm, rv = sd[key + ".running_mean"].double(), sd[key + ".running_var"].double()
+        em = float(((rm - 0.1 * mean).abs() / (0.1 * var.sqrt())).max())
+        ev = float(((rv - (0.9 + 0.1 * var)).abs() / (0.1 * var)).max())
+        print(f"configs[4] {key} ({n} px): running mean err / std {em:.2e}, running var rel err {ev:.2e}")
+        assert em < 1e-3 and ev < 1e-3, (key, em, ev)
+    m._engine.last_state = None
+
+
+def test_configs4_loss_decreases_over_three_steps(cfg4_batch):
+    """Three Trainer.steps (clip, AdamW at lr 1e-3) on the configs[4] batch with fixed dropout masks:
+    the loss decreases at every step."""
+    from eunet.train_eval import Trainer
+    x, msk = cfg4_batch
+    m = _dual96()
+    tr = Trainer(m, DEV, "enhanced_unet")
+    for g in tr.optimizer.param_groups:
+        g["lr"] = 1e-3
+    losses = [tr.step(x, msk) for _ in range(4)]
+    print("configs[4] losses:", losses)
+    assert all(b < a for a, b in zip(losses, losses[1:])), losses
+
+
+def test_configs4_256_slice_vs_oracle(cfg4_batch):
+    """A 256^2 crop of the configs[4] batch through the same bf16 base-96 model (train mode, the same
+    dropout masks) vs the fp64 oracle, gated by what bf16 autocast of the oracle achieves on the same
+    crop (test_gpu_dual.test_dual_base96_bf16_vs_autocast_reference's gate), plus argmax agreement."""
+    x, _ = cfg4_batch
+    xs = x[:, :, 768:1024, 1024:1280].contiguous()
+    m = _dual96()
+    with torch.no_grad():
+        out = m(xs).double().cpu()
+    keep = _keep()
+    xc = xs.cpu()
+    with torch.no_grad():
+        ref = D.dual_forward(D.dual_formula_weights(96, 1, 2), xc.double(), True, keep)[0]
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ac = D.dual_forward(D.dual_formula_weights(96, 1, 2, dtype=torch.float32), xc, True, keep)[0].float()
+    ours, auto = _rel_l2(out, ref), _rel_l2(ac, ref)
+    agree = float((out.argmax(1) == ref.argmax(1)).double().mean())
+    agree_ac = float((ac.argmax(1) == ref.argmax(1)).double().mean())
+    print("configs[4] 256^2 slice bf16 relL2 ours", ours, "autocast", auto, "argmax agreement", agree, agree_ac)
+    assert torch.isfinite(out).all()
+    assert ours < max(2.0 * auto, 0.02), (ours, auto)
+    assert agree > min(0.97, agree_ac - 0.02), (agree, agree_ac)

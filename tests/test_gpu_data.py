@@ -248,14 +248,14 @@ def test_threaded_loader_stops_early(tmp_path):
 
 
 def test_train_model_default_fast_path_is_exact(tmp_path):
-    """train_model from a LabelMe directory with its cuda defaults -- decode workers + prefetch and
-    the step replayed from HIP graphs (an odd train split, so every epoch ends on a 1-image batch,
+    """train_model from a LabelMe directory with its cuda fast path -- decode workers (opt-in:
+    loader_workers=3) + prefetch and the step replayed from HIP graphs (an odd train split, so every epoch ends on a 1-image batch,
     with an LR step per epoch) -- ends with the parameters of the plain in-loop eager run, bit for bit."""
     from eunet.models import EnhancedUNet
     from eunet.train_eval import train_model
     _write_cells(tmp_path, n=14)
     finals = []
-    for graph, workers in ((True, None), (False, 0)):
+    for graph, workers in ((True, 3), (False, None)):
         random.seed(5)
         np.random.seed(5)
         torch.manual_seed(5)

@@ -255,3 +255,42 @@ def test_data_oracle_rules():
     assert (O.gamma(img, 1.0) == img).all()
     sq = O.rasterize([np.array([[2, 2], [5, 2], [5, 5], [2, 5]])], [2], 8, 8)
     assert sq.sum() == 2 * 16 and (sq[2:6, 2:6] == 2).all()
+
+
+def test_branch_pinned_oracle_at_its_own_branches_is_the_oracle():
+    """The branch-pinned forward (eunet_ref._relu / _pool; the GPU gradient tests feed it the kernels'
+    ReLU masks and max-pool argmax, tests/_pins.py) evaluated on the oracle's OWN branch configuration
+    is the plain oracle bit for bit -- logits, loss and every gradient -- and a pin is really used
+    (one flipped mask element changes the logits).  The pins are formed with the same helpers the GPU
+    tests use (_pins.relu_mask / pool_argmax on NHWC tensors with an identity affine)."""
+    import _pins
+    x = torch.rand(2, 1, 32, 32, generator=torch.Generator().manual_seed(1))
+    msk = (x[:, 0] > 0.5).long()
+
+    def run(pins=None, rec=None):
+        S = R.formula_weights(16, 1, 2, dtype=torch.float32)
+        for k in S:
+            if S[k].is_floating_point() and "running" not in k:
+                S[k].requires_grad_(True)
+        d2, _ = R.trunk(S, x, True, pins, record=rec)
+        u = torch.nn.functional.conv2d(R._up2(d2), S["model.dec1.weight"], S["model.dec1.bias"])
+        loss = R.batch_loss(u, msk)
+        loss.backward()
+        return u.detach(), loss.detach(), {k: v.grad for k, v in S.items() if getattr(v, "grad", None) is not None}
+
+    rec = {}
+    u0, l0, g0 = run(rec=rec)
+    nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
+    one, zero = torch.ones(1), torch.zeros(1)
+    pins = {k: _pins.relu_mask(nhwc(v), one, zero) for k, v in rec.items()}
+    for i, nm in enumerate(_pins.POOLED, 1):
+        pins[f"pool{i}"] = _pins.pool_argmax(nhwc(rec[nm + ".4"]), one, zero, torch.float32)
+    u1, l1, g1 = run(pins)
+    assert torch.equal(u0, u1) and torch.equal(l0, l1)
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    flip = dict(pins)
+    m = flip["dec2.4"].clone()
+    m.view(-1)[int(m.view(-1).nonzero()[0])] = False
+    flip["dec2.4"] = m
+    assert not torch.equal(run(flip)[0], u0)
