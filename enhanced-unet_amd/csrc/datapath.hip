@@ -13,10 +13,12 @@
 //               np.clip(img+beta,...) (:251), additive noise (:268), gamma LUT
 //               (:273-276) -- each rounding to uint8 as numpy does (fp64 math)
 //   to_tensor   transforms.ToTensor: HWC uint8 -> CHW float / 255 (:302-305)
-//   resize_u8   cv2.resize INTER_LINEAR-style bilinear (half-pixel centres,
-//               round-half-up); cv2's fixed-point weights are not reproduced.
+//   resize_u8   cv2.resize INTER_LINEAR for 8U (dataset.py:151, 158): OpenCV's fixed-point
+//               algorithm -- 11-bit coefficients, int row sums, the SIMD vertical rounding (and
+//               the 2x-downscale INTER_AREA switch); oracle/data_ref.py resize_linear_u8.
 // All are HBM-bound byte kernels: one thread per pixel, no reductions.
 #include <climits>
+#include <cmath>
 
 #include "common.h"
 
@@ -246,28 +248,53 @@ __global__ __launch_bounds__(NT) void to_tensor_kernel(const uint8_t* img, int h
   }
 }
 
+// cv::resize coefficients of one axis (resize.cpp): fx = (float)((d + 0.5) * scale - 0.5) in double
+// arithmetic with one cast, sx = floor(fx), fx -= sx; the caller clamps.  a = saturate_cast<short>
+// ((1.f - fx, fx) * 2048): round half to even.
+struct RCoef { int s, a0, a1; };
+__device__ __forceinline__ RCoef resize_coef(int d, double scale) {
+#pragma clang fp contract(off)
+  float f = (float)(((double)d + 0.5) * scale - 0.5);
+  const float fl = floorf(f);
+  const int s = (int)fl;
+  f = f - fl;
+  return RCoef{s, __float2int_rn((1.f - f) * 2048.f), __float2int_rn(f * 2048.f)};
+}
+
+// one thread per output element.  mode 0: fixed-point bilinear (HResizeLinear rows, then the SIMD
+// VResizeLinearVec_32s8u rounding for x < xvec, the scalar FixedPtCast tail after it); mode 1: the
+// exact 2x downscale cv2 runs as INTER_AREA: (a + b + c + d + 2) >> 2.
 __global__ __launch_bounds__(NT) void resize_u8_kernel(const uint8_t* src, int hi, int wi, int c, uint8_t* dst,
-                                                       int ho, int wo) {
+                                                       int ho, int wo, double scale_x, double scale_y, int mode,
+                                                       int xvec) {
   const long long total = (long long)ho * wo * c;
-  const float sy = (float)hi / ho, sx = (float)wi / wo;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     const int ch = (int)(i % c);
     const long long p = i / c;
     const int y = (int)(p / wo), x = (int)(p - (long long)y * wo);
-    float fy = (y + 0.5f) * sy - 0.5f, fx = (x + 0.5f) * sx - 0.5f;
-    fy = fy < 0.f ? 0.f : fy;
-    fx = fx < 0.f ? 0.f : fx;
-    int y0 = (int)fy, x0 = (int)fx;
-    y0 = min(y0, hi - 1);
-    x0 = min(x0, wi - 1);
-    const int y1 = min(y0 + 1, hi - 1), x1 = min(x0 + 1, wi - 1);
-    const float ly = fy - y0, lx = fx - x0;
-    const float v = (1.f - ly) * ((1.f - lx) * src[((long long)y0 * wi + x0) * c + ch] +
-                                  lx * src[((long long)y0 * wi + x1) * c + ch]) +
-                    ly * ((1.f - lx) * src[((long long)y1 * wi + x0) * c + ch] +
-                          lx * src[((long long)y1 * wi + x1) * c + ch]);
-    const float r = floorf(v + 0.5f);
-    dst[i] = (uint8_t)(r < 0.f ? 0.f : (r > 255.f ? 255.f : r));
+    if (mode == 1) {
+      const uint8_t* s0 = src + ((long long)(2 * y) * wi + 2 * x) * c + ch;
+      const uint8_t* s1 = s0 + (long long)wi * c;
+      dst[i] = (uint8_t)((s0[0] + s0[c] + s1[0] + s1[c] + 2) >> 2);
+      continue;
+    }
+    RCoef cx = resize_coef(x, scale_x);
+    if (cx.s < 0) cx = RCoef{0, 2048, 0};
+    if (cx.s >= wi - 1) cx = RCoef{wi - 1, 2048, 0};
+    const int sx1 = min(cx.s + 1, wi - 1);
+    const RCoef cy = resize_coef(y, scale_y);
+    const int y0 = min(max(cy.s, 0), hi - 1), y1 = min(max(cy.s + 1, 0), hi - 1);
+    const uint8_t* r0 = src + (long long)y0 * wi * c + ch;
+    const uint8_t* r1 = src + (long long)y1 * wi * c + ch;
+    const int d0 = r0[(long long)cx.s * c] * cx.a0 + r0[(long long)sx1 * c] * cx.a1;
+    const int d1 = r1[(long long)cx.s * c] * cx.a0 + r1[(long long)sx1 * c] * cx.a1;
+    int v;
+    if (x * c + ch < xvec) {  // 16-bit mulhi of the rows >> 4 (v_mul_hi), + 2 >> 2 (v_rshr_pack_u<2>)
+      v = ((((d0 >> 4) * cy.a0) >> 16) + (((d1 >> 4) * cy.a1) >> 16) + 2) >> 2;
+    } else {
+      v = (cy.a0 * d0 + cy.a1 * d1 + (1 << 21)) >> 22;
+    }
+    dst[i] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
   }
 }
 
@@ -336,7 +363,23 @@ int eunet_to_tensor(const uint8_t* img, int h, int w, int c, float* out, void* s
 
 int eunet_resize_u8(const uint8_t* src, int hi, int wi, int c, uint8_t* dst, int ho, int wo, void* stream) {
   EUNET_REQUIRE(src && dst && hi > 0 && wi > 0 && ho > 0 && wo > 0 && c > 0, "resize_u8: bad args");
-  resize_u8_kernel<<<grid1((long long)ho * wo * c), NT, 0, (hipStream_t)stream>>>(src, hi, wi, c, dst, ho, wo);
+  if (hi == ho && wi == wo) {  // cv::resize copies
+    const hipError_t e = hipMemcpyAsync(dst, src, (size_t)hi * wi * c, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+    EUNET_REQUIRE(e == hipSuccess, "resize_u8: copy failed");
+    return EUNET_OK;
+  }
+  // cv::hal::resize: scale = 1 / inv_scale, inv_scale = dsize / ssize; an exact 2x downscale in both
+  // directions runs as INTER_AREA
+  const double scale_x = 1.0 / ((double)wo / wi), scale_y = 1.0 / ((double)ho / hi);
+  const double ix = std::nearbyint(scale_x), iy = std::nearbyint(scale_y);
+  const double eps = 2.220446049250313e-16;
+  const int mode = std::fabs(scale_x - ix) < eps && std::fabs(scale_y - iy) < eps && ix == 2.0 && iy == 2.0;
+  // elements of a row the 128-bit vector loops of VResizeLinearVec_32s8u cover (16, then 8 at a time)
+  const int width = wo * c;
+  int xvec = width >= 16 ? width / 16 * 16 : 0;
+  while (xvec < width - 8) xvec += 8;
+  resize_u8_kernel<<<grid1((long long)ho * wo * c), NT, 0, (hipStream_t)stream>>>(src, hi, wi, c, dst, ho, wo,
+                                                                                   scale_x, scale_y, mode, xvec);
   EUNET_LAUNCH_CHECK("resize_u8");
   return EUNET_OK;
 }

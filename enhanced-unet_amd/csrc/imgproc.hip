@@ -12,8 +12,9 @@
 // cv2 is not importable in this image, so these follow OpenCV's documented algorithms and are
 // pinned to the numpy restatement in oracle/imgproc_ref.py, not to cv2 (parity unpinned):
 //   RGB2GRAY 8U    Y = (4899 R + 9617 G + 1868 B + 2^13) >> 14
-//   RGB<->Lab 8U   sRGB gamma, D65 XYZ, L*255/100, a+128, b+128 -- evaluated in fp32 and rounded
-//                  (cv2's fixed-point tables are not reproduced: +-1 level)
+//   RGB<->Lab 8U   cv2's bit-exact fixed-point conversion (color_lab.cpp, OpenCV >= 3.4): sRGB gamma /
+//                  cube-root / L->(y, fy) / inverse-gamma tables built once on the host from the same
+//                  integer-presented constants (LabTabs), RGB2Lab_b / Lab2RGBinteger integer arithmetic
 //   RGB<->HSV 8U   H in [0, 180): cv2's hsv_shift = 12 integer division tables; HSV2RGB in fp32
 //   CLAHE          OpenCV CLAHE_Impl: tiles of the image padded to a multiple of the grid by
 //                  BORDER_REFLECT_101, clip = max(int(clipLimit * tileArea / 256), 1), excess
@@ -24,6 +25,10 @@
 //   Sobel / Laplacian (CV_64F, ksize 3 / 1), BORDER_REFLECT_101
 // One thread per pixel except the CLAHE histograms (one block per tile, integer LDS counts) and
 // the edge-feature maximum (per-block maxima, reduced in a second pass).
+#include <cmath>
+#include <cstring>
+#include <mutex>
+
 #include "common.h"
 
 // every fp32 / fp64 expression below rounds per operation, as the reference's numpy arrays do
@@ -51,42 +56,57 @@ __device__ __forceinline__ uint8_t sat_u8(float v) {  // saturate_cast<uchar>(v)
 
 __device__ __forceinline__ uint8_t gray_u8(int r, int g, int b) { return (uint8_t)((4899 * r + 9617 * g + 1868 * b + (1 << 13)) >> 14); }
 
-// ---- Lab (fp32 formulas of cv2's documentation, D65, sRGB gamma) ----
-__device__ __forceinline__ float srgb_lin(float c) { return c <= 0.04045f ? c / 12.92f : powf((c + 0.055f) / 1.055f, 2.4f); }
-__device__ __forceinline__ float srgb_enc(float c) { return c <= 0.0031308f ? 12.92f * c : 1.055f * powf(c, 1.f / 2.4f) - 0.055f; }
-__device__ __forceinline__ float lab_f(float t) { return t > 0.008856f ? cbrtf(t) : 7.787f * t + 16.f / 116.f; }
-__device__ __forceinline__ float lab_finv(float f) { return f > 0.206893f ? f * f * f : (f - 16.f / 116.f) / 7.787f; }
+// ---- Lab 8U (cv2 RGB2Lab_b / Lab2RGBinteger; tables: lab_tables_build below) ----
+constexpr int LAB_SHIFT = 12, GAMMA_SHIFT = 3, LAB_SHIFT2 = LAB_SHIFT + GAMMA_SHIFT;
+constexpr int CBRT_TAB_B = 256 * 3 / 2 * (1 << GAMMA_SHIFT);  // 3072
+constexpr int INV_GAMMA_TAB = 1 << 12, LAB_BASE = 1 << 14, MIN_AB = -8145;
+struct LabTabs {
+  uint16_t gamma[256];            // sRGBGammaTab_b
+  uint16_t cbrt[CBRT_TAB_B];      // LabCbrtTab_b
+  uint16_t yf[512];               // LabToYF_b: (y, ify) per L
+  uint16_t invgamma[INV_GAMMA_TAB];  // sRGBInvGammaTab_b
+  int c_fwd[9], c_inv[9];         // RGB2Lab_b / Lab2RGBinteger coefficients, RGB order
+};
+__device__ LabTabs g_lab;
 
-__device__ __forceinline__ void rgb2lab(int R, int G, int B, uint8_t& L8, uint8_t& a8, uint8_t& b8) {
-  const float r = srgb_lin(R / 255.f), g = srgb_lin(G / 255.f), b = srgb_lin(B / 255.f);
-  const float X = (0.412453f * r + 0.357580f * g + 0.180423f * b) / 0.950456f;
-  const float Y = 0.212671f * r + 0.715160f * g + 0.072169f * b;
-  const float Z = (0.019334f * r + 0.119193f * g + 0.950227f * b) / 1.088754f;
-  const float fx = lab_f(X), fy = lab_f(Y), fz = lab_f(Z);
-  const float L = Y > 0.008856f ? 116.f * fy - 16.f : 903.3f * Y;
-  L8 = sat_u8(L * 255.f / 100.f);
-  a8 = sat_u8(500.f * (fx - fy) + 128.f);
-  b8 = sat_u8(200.f * (fy - fz) + 128.f);
+__device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
+__device__ __forceinline__ uint8_t clamp_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+__device__ __forceinline__ void rgb2lab(int R8, int G8, int B8, uint8_t& L8, uint8_t& a8, uint8_t& b8) {
+  const LabTabs& T = g_lab;
+  const int R = T.gamma[R8], G = T.gamma[G8], B = T.gamma[B8];
+  const int* C = T.c_fwd;
+  const int fX = T.cbrt[descale(R * C[0] + G * C[1] + B * C[2], LAB_SHIFT)];
+  const int fY = T.cbrt[descale(R * C[3] + G * C[4] + B * C[5], LAB_SHIFT)];
+  const int fZ = T.cbrt[descale(R * C[6] + G * C[7] + B * C[8], LAB_SHIFT)];
+  constexpr int Lscale = (116 * 255 + 50) / 100, Lshift = -((16 * 255 * (1 << LAB_SHIFT2) + 50) / 100);
+  L8 = clamp_u8(descale(Lscale * fY + Lshift, LAB_SHIFT2));
+  a8 = clamp_u8(descale(500 * (fX - fY) + 128 * (1 << LAB_SHIFT2), LAB_SHIFT2));
+  b8 = clamp_u8(descale(200 * (fY - fZ) + 128 * (1 << LAB_SHIFT2), LAB_SHIFT2));
+}
+
+// abToXZ_b[v - minABvalue], evaluated instead of tabulated (integer only)
+__device__ __forceinline__ int ab_to_xz(int v) {
+  return v <= 3390 ? v * 108 / 841 - LAB_BASE * 16 / 116 * 108 / 841 : v * v / LAB_BASE * v / LAB_BASE;
 }
 
 __device__ __forceinline__ void lab2rgb(int L8, int a8, int b8, uint8_t& R, uint8_t& G, uint8_t& B) {
-  const float L = L8 * 100.f / 255.f, a = a8 - 128.f, b = b8 - 128.f;
-  float Y, fy;
-  if (L <= 7.9996f) {  // OpenCV Lab2RGB: linear segment below L = 903.3 * 0.008856
-    Y = L / 903.3f;
-    fy = 7.787f * Y + 16.f / 116.f;
-  } else {
-    fy = (L + 16.f) / 116.f;
-    Y = fy * fy * fy;
+  const LabTabs& T = g_lab;
+  const int y = T.yf[2 * L8], ify = T.yf[2 * L8 + 1];
+  const int adiv = ((5 * a8 * 53687 + (1 << 7)) >> 13) - 128 * LAB_BASE / 500;
+  const int bdiv = ((b8 * 41943 + (1 << 4)) >> 9) - 128 * LAB_BASE / 200 + 1;
+  const int x = ab_to_xz(ify + adiv), z = ab_to_xz(ify - bdiv);
+  const int* C = T.c_inv;
+  constexpr int SH = LAB_SHIFT + (14 - 12);  // lab_shift + (base_shift - inv_gamma_shift)
+  int o[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int v = descale(C[3 * r] * x + C[3 * r + 1] * y + C[3 * r + 2] * z, SH);
+    o[r] = T.invgamma[v < 0 ? 0 : (v > INV_GAMMA_TAB - 1 ? INV_GAMMA_TAB - 1 : v)];
   }
-  const float fx = fy + a / 500.f, fz = fy - b / 200.f;
-  const float X = lab_finv(fx) * 0.950456f, Z = lab_finv(fz) * 1.088754f;
-  const float r = 3.240479f * X - 1.53715f * Y - 0.498535f * Z;
-  const float g = -0.969256f * X + 1.875991f * Y + 0.041556f * Z;
-  const float bb = 0.055648f * X - 0.204043f * Y + 1.057311f * Z;
-  R = sat_u8(255.f * srgb_enc(fminf(fmaxf(r, 0.f), 1.f)));
-  G = sat_u8(255.f * srgb_enc(fminf(fmaxf(g, 0.f), 1.f)));
-  B = sat_u8(255.f * srgb_enc(fminf(fmaxf(bb, 0.f), 1.f)));
+  R = (uint8_t)o[0];
+  G = (uint8_t)o[1];
+  B = (uint8_t)o[2];
 }
 
 // ---- HSV (8U: H in [0, 180)) ----
@@ -436,6 +456,82 @@ __global__ __launch_bounds__(NT) void chw_to_u8_kernel(const float* x, int c, in
   }
 }
 
+// ---- host: initLabTabs (color_lab.cpp) from the same integer-presented constants.  softfloat
+// operations are IEEE float32 operations (this file has FP contraction off), softdouble ones float64;
+// mulAdd is a fused multiply-add; cvRound rounds half to even (nearbyint).  oracle/imgproc_ref.py
+// lab_tables is the same construction in numpy. ----
+double apply_gamma(float x) {
+  const double xd = x;
+  return xd <= 809.0 / 20000.0 ? xd / (323.0 / 25.0) : std::pow((xd + 11.0 / 200.0) / (1.0 + 11.0 / 200.0), 12.0 / 5.0);
+}
+double apply_inv_gamma(float x) {
+  const double xd = x;
+  return xd <= 7827.0 / 2500000.0 ? xd * (323.0 / 25.0)
+                                  : std::pow(xd, 1.0 / (12.0 / 5.0)) * (1.0 + 11.0 / 200.0) - 11.0 / 200.0;
+}
+int rne(double v) { return (int)std::nearbyint(v); }
+
+LabTabs build_lab_tabs() {
+  LabTabs t{};
+  for (int i = 0; i < 256; ++i) {
+    const float g = (float)apply_gamma((float)i / 255.f);
+    t.gamma[i] = (uint16_t)rne((float)(255 * (1 << GAMMA_SHIFT)) * g);
+  }
+  const float lthresh = 216.f / 24389.f, lscale = 841.f / 108.f, lbias = 16.f / 116.f;
+  const float cbs = 1.f / (255.f * (float)(1 << GAMMA_SHIFT));
+  for (int i = 0; i < CBRT_TAB_B; ++i) {
+    const float x = cbs * (float)i;
+    const float f = x < lthresh ? (float)std::fma((double)x, (double)lscale, (double)lbias) : (float)std::cbrt((double)x);
+    t.cbrt[i] = (uint16_t)rne((float)(1 << LAB_SHIFT2) * f);
+  }
+  for (int L = 0; L < 256; ++L) {
+    int y, ify;
+    if (L <= 20) {
+      y = rne((float)(L * LAB_BASE * 20 * 9) / (float)(17 * 29 * 29 * 29));
+      ify = rne((float)LAB_BASE * (16.f / 116.f + (float)(L * 5) / (float)(3 * 17 * 29)));
+    } else {
+      const float fy = (float)(L * 100 * LAB_BASE) / (float)(255 * 116) + (float)(16 * LAB_BASE) / 116.f;
+      ify = rne(fy);
+      y = rne(fy * fy * fy / (float)(LAB_BASE * LAB_BASE));
+    }
+    t.yf[2 * L] = (uint16_t)y;
+    t.yf[2 * L + 1] = (uint16_t)ify;
+  }
+  for (int i = 0; i < INV_GAMMA_TAB; ++i) {
+    const float x = 1.f / (float)INV_GAMMA_TAB * (float)i;
+    t.invgamma[i] = (uint16_t)rne(255.f * (float)apply_inv_gamma(x));
+  }
+  const double d65[3] = {0.950456, 1.0, 1.088754};
+  const double m_fwd[9] = {0.412453, 0.357580, 0.180423, 0.212671, 0.715160, 0.072169, 0.019334, 0.119193, 0.950227};
+  const double m_inv[9] = {3.240479, -1.53715, -0.498535, -0.969256, 1.875991, 0.041556, 0.055648, -0.204043, 1.057311};
+  const double lshift = (double)(1 << LAB_SHIFT);
+  for (int r = 0; r < 3; ++r)
+    for (int j = 0; j < 3; ++j) {
+      t.c_fwd[3 * r + j] = rne(lshift * m_fwd[3 * r + j] / d65[r]);
+      t.c_inv[3 * r + j] = rne(lshift * m_inv[3 * r + j] * d65[j]);
+    }
+  return t;
+}
+
+// the tables reach each device once (a synchronous copy into the g_lab symbol, ordered before every
+// later launch from this host thread); the C-ABI still allocates nothing
+std::mutex g_lab_mu;
+bool g_lab_ready[64];
+int lab_tables_ready() {
+  int dev = 0;
+  EUNET_REQUIRE(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "Lab tables: no current device");
+  std::lock_guard<std::mutex> lk(g_lab_mu);
+  if (!g_lab_ready[dev]) {
+    static const LabTabs host = build_lab_tabs();
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lab), &host, sizeof(LabTabs)) != hipSuccess) {
+      eunet::set_error("Lab tables: copy to the device failed");
+      return EUNET_ERR_HIP;
+    }
+    g_lab_ready[dev] = true;
+  }
+  return EUNET_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -457,8 +553,17 @@ int eunet_chw_to_u8(const float* x, int c, int h, int w, void* ws, uint8_t* out,
   return EUNET_OK;
 }
 
+int eunet_lab_tables(void* out, size_t bytes) {
+  static_assert(sizeof(LabTabs) == 2 * (256 + CBRT_TAB_B + 512 + INV_GAMMA_TAB) + 4 * 18, "LabTabs layout");
+  EUNET_REQUIRE(out && bytes >= sizeof(LabTabs), "lab_tables: need %zu bytes", sizeof(LabTabs));
+  static const LabTabs t = build_lab_tabs();
+  std::memcpy(out, &t, sizeof(LabTabs));
+  return EUNET_OK;
+}
+
 int eunet_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, long long npix, void* stream) {
   EUNET_REQUIRE(rgb && lab && npix > 0, "rgb2lab_u8: bad args");
+  if (int rc = lab_tables_ready()) return rc;
   rgb2lab_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(rgb, lab, npix);
   EUNET_LAUNCH_CHECK("rgb2lab_u8");
   return EUNET_OK;
@@ -466,6 +571,7 @@ int eunet_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, long long npix, void* str
 
 int eunet_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, long long npix, void* stream) {
   EUNET_REQUIRE(rgb && lab && npix > 0, "lab2rgb_u8: bad args");
+  if (int rc = lab_tables_ready()) return rc;
   lab2rgb_kernel<<<grid1(npix), NT, 0, (hipStream_t)stream>>>(lab, rgb, npix);
   EUNET_LAUNCH_CHECK("lab2rgb_u8");
   return EUNET_OK;
@@ -502,6 +608,8 @@ int eunet_clahe_u8(const uint8_t* src, int mode, int h, int w, double clip_limit
   clahe_lut_kernel<<<tiles_x * tiles_y, NT, 0, (hipStream_t)stream>>>(src, ps, h, w, tw, th, tiles_x, clip,
                                                                      255.f / (float)area, luts);
   EUNET_LAUNCH_CHECK("clahe_lut");
+  if (mode == 1)
+    if (int rc = lab_tables_ready()) return rc;
   clahe_apply_kernel<<<grid1((long long)h * w), NT, 0, (hipStream_t)stream>>>(src, ps, h, w, luts, tiles_x, tiles_y,
                                                                               1.f / tw, 1.f / th, dst, mode);
   EUNET_LAUNCH_CHECK("clahe_apply");

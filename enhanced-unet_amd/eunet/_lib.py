@@ -120,6 +120,7 @@ SIGNATURES = {
     "eunet_resize_u8": [_f, c_int, c_int, c_int, _f, c_int, c_int, c_void_p],
     "eunet_rgb2lab_u8": [_f, _f, c_int64, c_void_p],
     "eunet_lab2rgb_u8": [_f, _f, c_int64, c_void_p],
+    "eunet_lab_tables": [c_void_p, c_size_t],
     "eunet_rgb2gray_u8": [_f, _f, c_int64, c_void_p],
     "eunet_hsv_adjust_u8": [_f, c_int64, c_float, c_float, c_float, c_int, c_void_p],
     "eunet_clahe_u8": [_f, c_int, c_int, c_int, ctypes.c_double, c_int, c_int, _f, _f, c_void_p],
@@ -162,15 +163,23 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = c_char_p
         fn.argtypes = []
+    missing = []
     for name, argt in SIGNATURES.items():
         try:
             fn = getattr(lib, name)
         except AttributeError:
-            if os.environ.get("EUNET_LIB"):  # an older build under A/B: entry points it lacks stay unbound
-                continue
-            raise
+            missing.append(name)
+            continue
         fn.restype = c_int
         fn.argtypes = argt
+    if missing:
+        # an older build under A/B may lack entry points, but only when asked for explicitly: a stale or
+        # partial library otherwise fails here, not at its first call
+        if os.environ.get("EUNET_LIB_ALLOW_PARTIAL") != "1":
+            raise EunetError(f"{path} lacks {len(missing)} entry point(s) of include/eunet.h: {missing[:6]} "
+                             "(stale build? rebuild, or set EUNET_LIB_ALLOW_PARTIAL=1 for an A/B of an older library)")
+        import warnings
+        warnings.warn(f"{path}: {len(missing)} entry point(s) unbound (EUNET_LIB_ALLOW_PARTIAL=1): {missing}")
     _lib = lib
     return lib
 

@@ -16,15 +16,19 @@ features, GaussianBlur unsharp mask, filter2D sharpening (imgproc.hip).  Image d
 PIL on the host (I/O).
 
 cv2 is absent from this image: cv2.fillPoly, cv2.resize and the cv2 colour / CLAHE / filter
-calls are replaced by kernels that follow OpenCV's documented algorithms, pinned to the
-numpy restatement in oracle/imgproc_ref.py, not to cv2 (parity unpinned).
+calls are replaced by kernels that follow OpenCV's published algorithms (cv2.resize INTER_LINEAR
+and RGB<->Lab 8U with OpenCV's own fixed-point arithmetic), pinned to the numpy restatements in
+oracle/data_ref.py / oracle/imgproc_ref.py, not to cv2 (parity unpinned, DESIGN.md §2);
+cv2.fillPoly is replaced by a documented fill rule.
 
 Feeding the GPU (round 3): a sample makes no host round trip -- host arrays reach the device
 through pinned staging buffers (ops.upload), the live ratio that selects the brightness /
 contrast ranges is read on the device (eunet_augment_ratio_u8: the host draws the same
-random.random() values random.uniform would), and the Gaussian noise is drawn on the device
-(host_noise=True keeps the reference's numpy draw: np.random.normal, bit-exact values, one host
-sync).  DataLoader(workers=W, prefetch=P) decodes JPEG + JSON in W threads and runs the device
+random.random() values random.uniform would).  The Gaussian noise is by default the reference's
+own numpy draw (host_noise=True: np.random.normal, bit-exact values and np.random stream, one
+synchronising copy per noisy sample); host_noise=False draws it on the device from a generator
+seeded by one np.random draw -- sync-free and faster, same Python `random` decisions, but other
+noise values and a shifted np.random stream.  DataLoader(workers=W, prefetch=P) decodes JPEG + JSON in W threads and runs the device
 part of the next P batches on a side stream while the trainer consumes the current one; the
 Python `random` draws stay in item order (one producer thread).
 """
@@ -98,14 +102,15 @@ def _host_load_args(args):
 
 class CellDataset:
     def __init__(self, data_dir: str, split: str = "train", transform=None, max_size: int = 1024,
-                 device: str = "cuda", cell_preprocess: bool = True, host_noise: bool = False,
+                 device: str = "cuda", cell_preprocess: bool = True, host_noise: bool = True,
                  host_ratio: bool = False):
         self.data_dir, self.split, self.transform, self.max_size = data_dir, split, transform, max_size
         self.device = device
         self.cell_preprocess = cell_preprocess  # dataset.py:204 (always on in the reference)
-        # host_noise: the reference's np.random.normal noise (exact values; a host draw of 3 H W
-        # normals + one synchronising copy per noisy sample); default: drawn on the device from a
-        # generator seeded by one np.random draw (same Python `random` decisions, other noise values)
+        # host_noise (default): the reference's np.random.normal noise (exact values and np.random
+        # stream; a host draw of 3 H W normals + one synchronising copy per noisy sample); False:
+        # drawn on the device from a generator seeded by one np.random draw (sync-free; same Python
+        # `random` decisions, other noise values)
         self.host_noise = host_noise
         # host_ratio: read the live ratio back to the host (round 2's path; one sync per sample)
         self.host_ratio = host_ratio

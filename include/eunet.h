@@ -426,8 +426,14 @@ int eunet_resize_u8(const uint8_t* src, int hi, int wi, int c, uint8_t* dst, int
  * (HSV / CLAHE / sharpen augmentations) and train_eval.py:365-395 (Evaluator preprocessing).
  * All images HWC uint8 RGB, npix = h * w.  cv2 is absent from this image: the formulas follow
  * OpenCV's documented algorithms (parity unpinned). */
+/* COLOR_RGB2LAB / COLOR_LAB2RGB for 8U (dataset.py:63, 71, 268, 272; train_eval.py:380-385): cv2's
+ * bit-exact fixed-point conversion (RGB2Lab_b / Lab2RGBinteger of OpenCV >= 3.4 color_lab.cpp).  The
+ * tables are built on the host once and copied to each device on its first call (synchronous). */
 int eunet_rgb2lab_u8(const uint8_t* rgb, uint8_t* lab, long long npix, void* stream);
 int eunet_lab2rgb_u8(const uint8_t* lab, uint8_t* rgb, long long npix, void* stream);
+/* The host-side Lab tables (no device needed; a checker's view of what the kernels use): gamma[256],
+ * cbrt[3072], yf[512], invgamma[4096] as uint16 then c_fwd[9], c_inv[9] as int32 -- 15 744 + 72 bytes. */
+int eunet_lab_tables(void* out, size_t bytes);
 /* cv2.COLOR_RGB2GRAY: (4899 R + 9617 G + 1868 B + 8192) >> 14 */
 int eunet_rgb2gray_u8(const uint8_t* rgb, uint8_t* gray, long long npix, void* stream);
 /* in place RGB -> HSV (8U, H in [0, 180)) -> adjust -> RGB.  mode bit0: S *= sat_mul

@@ -14,8 +14,7 @@ fixtures, so this file restates OpenCV's published algorithms (imgproc color_lab
 / clahe / filter / smooth modules) rather than being checked against cv2 itself.  The
 numpy steps around the cv2 calls (the 1.1 / 0.9 / 0.1 / 0.85 / 0.15 fp32 blends, the
 fp64 edge normalisation, astype(uint8) truncations) are the reference's own expressions.
-Known deviation from cv2: RGB<->Lab is evaluated with the float formulas, not cv2's 8U
-fixed-point tables (cv2 may differ by one level).  Every fp32 step rounds per operation
+RGB<->Lab 8U follows cv2's bit-exact fixed-point tables (OpenCV >= 3.4).  Every fp32 step rounds per operation
 (np.float32 arithmetic), matching the kernels, which are compiled without FMA contraction.
 """
 from __future__ import annotations
@@ -44,51 +43,114 @@ def rgb2gray(img):
     return ((4899 * r + 9617 * g + 1868 * b + (1 << 13)) >> 14).astype(np.uint8)
 
 
-# ---- Lab (float formulas, D65, sRGB gamma) ----
-def _srgb_lin(c):
-    return np.where(c <= f32(0.04045), c / f32(12.92), ((c + f32(0.055)) / f32(1.055)) ** f32(2.4)).astype(f32)
+# ---- Lab 8U: OpenCV's bit-exact fixed-point conversion (imgproc/src/color_lab.cpp, OpenCV >= 3.4:
+#      initLabTabs, RGB2Lab_b, Lab2RGBinteger; every constant "presented through integers", table
+#      entries from IEEE float32 (softfloat) / float64 (softdouble) arithmetic, cvRound = half-even) ----
+LAB_SHIFT, GAMMA_SHIFT = 12, 3                     # lab_shift (= xyz_shift), gamma_shift
+LAB_SHIFT2 = LAB_SHIFT + GAMMA_SHIFT               # 15
+CBRT_TAB_B = 256 * 3 // 2 * (1 << GAMMA_SHIFT)     # LAB_CBRT_TAB_SIZE_B = 3072
+INV_GAMMA_TAB = 1 << 12                            # INV_GAMMA_TAB_SIZE (inv_gamma_shift 12)
+LAB_BASE = 1 << 14                                 # lab_base_shift 14
+MIN_AB = -8145                                     # minABvalue
+D65 = (0.950456, 1.0, 1.088754)
+SRGB2XYZ = (0.412453, 0.357580, 0.180423, 0.212671, 0.715160, 0.072169, 0.019334, 0.119193, 0.950227)
+XYZ2SRGB = (3.240479, -1.53715, -0.498535, -0.969256, 1.875991, 0.041556, 0.055648, -0.204043, 1.057311)
+# softdouble gamma constants: 809/20000, 7827/2500000, 323/25, 12/5, 11/200
+G_THR, G_INV_THR, G_LOW, G_POW, G_XS = 809 / 20000, 7827 / 2500000, 323 / 25, 12 / 5, 11 / 200
 
 
-def _srgb_enc(c):
-    return np.where(c <= f32(0.0031308), f32(12.92) * c,
-                    f32(1.055) * c ** (f32(1.0) / f32(2.4)) - f32(0.055)).astype(f32)
+def _rne(v):
+    """cvRound of a softfloat / softdouble: round half to even."""
+    return np.rint(np.asarray(v, np.float64)).astype(np.int64)
 
 
-def _lab_f(t):
-    return np.where(t > f32(0.008856), np.cbrt(t), f32(7.787) * t + f32(16.0) / f32(116.0)).astype(f32)
+def _apply_gamma(x):  # applyGamma(softfloat) in softdouble, result -> softfloat
+    xd = x.astype(np.float64)
+    return np.where(xd <= G_THR, xd / G_LOW, np.power((xd + G_XS) / (1.0 + G_XS), G_POW)).astype(f32)
 
 
-def _lab_finv(f):
-    return np.where(f > f32(0.206893), f * f * f, (f - f32(16.0) / f32(116.0)) / f32(7.787)).astype(f32)
+def _apply_inv_gamma(x):
+    xd = x.astype(np.float64)
+    return np.where(xd <= G_INV_THR, xd * G_LOW, np.power(xd, 1.0 / G_POW) * (1.0 + G_XS) - G_XS).astype(f32)
+
+
+def _trunc_div(a, b):  # C integer division (toward zero)
+    return np.sign(a) * (np.abs(a) // b)
+
+
+def lab_tables():
+    """initLabTabs: sRGBGammaTab_b[256], LabCbrtTab_b[3072], LabToYF_b[256][2], sRGBInvGammaTab_b[4096],
+    abToXZ_b[36864] and the RGB2Lab_b / Lab2RGBinteger coefficients (RGB channel order)."""
+    i = np.arange(256)
+    gamma = _rne(f32(255 * (1 << GAMMA_SHIFT)) * _apply_gamma(i.astype(f32) / f32(255)))
+    lthresh, lscale, lbias = f32(216) / f32(24389), f32(841) / f32(108), f32(16) / f32(116)
+    x = (f32(1) / (f32(255) * f32(1 << GAMMA_SHIFT))) * np.arange(CBRT_TAB_B).astype(f32)
+    lin = (x.astype(np.float64) * np.float64(lscale) + np.float64(lbias)).astype(f32)   # mulAdd: one rounding
+    cb = np.cbrt(x.astype(np.float64)).astype(f32)
+    cbrt = _rne(f32(1 << LAB_SHIFT2) * np.where(x < lthresh, lin, cb).astype(f32))
+    yf = np.zeros((256, 2), np.int64)
+    for L in range(256):
+        if L <= 20:
+            y = _rne(f32(L * LAB_BASE * 20 * 9) / f32(17 * 29 * 29 * 29))
+            ify = _rne(f32(LAB_BASE) * (f32(16) / f32(116) + f32(L * 5) / f32(3 * 17 * 29)))
+        else:
+            fy = f32(L * 100 * LAB_BASE) / f32(255 * 116) + f32(16 * LAB_BASE) / f32(116)
+            ify = _rne(fy)
+            y = _rne(fy * fy * fy / f32(LAB_BASE * LAB_BASE))
+        yf[L] = (y, ify)
+    invgamma = _rne(f32(255) * _apply_inv_gamma(f32(1) / f32(INV_GAMMA_TAB) * np.arange(INV_GAMMA_TAB).astype(f32)))
+    v = np.arange(MIN_AB, LAB_BASE * 9 // 4 + MIN_AB, dtype=np.int64)
+    abxz = np.where(v <= 3390, _trunc_div(v * 108, 841) - LAB_BASE * 16 // 116 * 108 // 841,
+                    v * v // LAB_BASE * v // LAB_BASE)
+    lshift = float(1 << LAB_SHIFT)
+    c_fwd = np.array([_rne(lshift * SRGB2XYZ[r * 3 + j] / D65[r]) for r in range(3) for j in range(3)], np.int64)
+    c_inv = np.array([_rne(lshift * XYZ2SRGB[r * 3 + j] * D65[j]) for r in range(3) for j in range(3)], np.int64)
+    return dict(gamma=gamma, cbrt=cbrt, yf=yf, invgamma=invgamma, abxz=abxz, c_fwd=c_fwd, c_inv=c_inv)
+
+
+_TABS = None
+
+
+def _tabs():
+    global _TABS
+    if _TABS is None:
+        _TABS = lab_tables()
+    return _TABS
+
+
+def _descale(x, n):  # CV_DESCALE
+    return (x + (1 << (n - 1))) >> n
 
 
 def rgb2lab(img):
-    c = img.astype(f32) / f32(255.0)
-    r, g, b = _srgb_lin(c[..., 0]), _srgb_lin(c[..., 1]), _srgb_lin(c[..., 2])
-    X = (f32(0.412453) * r + f32(0.357580) * g + f32(0.180423) * b) / f32(0.950456)
-    Y = f32(0.212671) * r + f32(0.715160) * g + f32(0.072169) * b
-    Z = (f32(0.019334) * r + f32(0.119193) * g + f32(0.950227) * b) / f32(1.088754)
-    fx, fy, fz = _lab_f(X), _lab_f(Y), _lab_f(Z)
-    L = np.where(Y > f32(0.008856), f32(116.0) * fy - f32(16.0), f32(903.3) * Y).astype(f32)
-    return np.stack([sat_u8(L * f32(255.0) / f32(100.0)), sat_u8(f32(500.0) * (fx - fy) + f32(128.0)),
-                     sat_u8(f32(200.0) * (fy - fz) + f32(128.0))], -1)
+    """cv2.cvtColor(img, COLOR_RGB2LAB) for uint8 (RGB2Lab_b)."""
+    T = _tabs()
+    R, G, B = (T["gamma"][img[..., k].astype(np.int64)] for k in range(3))
+    C = T["c_fwd"]
+    fX, fY, fZ = (T["cbrt"][_descale(R * C[3 * r] + G * C[3 * r + 1] + B * C[3 * r + 2], LAB_SHIFT)] for r in range(3))
+    Lscale, Lshift = (116 * 255 + 50) // 100, -((16 * 255 * (1 << LAB_SHIFT2) + 50) // 100)
+    L = _descale(Lscale * fY + Lshift, LAB_SHIFT2)
+    a = _descale(500 * (fX - fY) + 128 * (1 << LAB_SHIFT2), LAB_SHIFT2)
+    b = _descale(200 * (fY - fZ) + 128 * (1 << LAB_SHIFT2), LAB_SHIFT2)
+    return np.stack([np.clip(t, 0, 255) for t in (L, a, b)], -1).astype(np.uint8)
 
 
 def lab2rgb(lab):
-    L = lab[..., 0].astype(f32) * f32(100.0) / f32(255.0)
-    a = lab[..., 1].astype(f32) - f32(128.0)
-    b = lab[..., 2].astype(f32) - f32(128.0)
-    lin = L <= f32(7.9996)
-    Y_lin = L / f32(903.3)
-    fy = np.where(lin, f32(7.787) * Y_lin + f32(16.0) / f32(116.0), (L + f32(16.0)) / f32(116.0)).astype(f32)
-    Y = np.where(lin, Y_lin, fy * fy * fy).astype(f32)
-    fx, fz = fy + a / f32(500.0), fy - b / f32(200.0)
-    X, Z = _lab_finv(fx) * f32(0.950456), _lab_finv(fz) * f32(1.088754)
-    r = f32(3.240479) * X - f32(1.53715) * Y - f32(0.498535) * Z
-    g = f32(-0.969256) * X + f32(1.875991) * Y + f32(0.041556) * Z
-    bb = f32(0.055648) * X - f32(0.204043) * Y + f32(1.057311) * Z
-    out = [sat_u8(f32(255.0) * _srgb_enc(np.clip(v, f32(0), f32(1)).astype(f32))) for v in (r, g, bb)]
-    return np.stack(out, -1)
+    """cv2.cvtColor(lab, COLOR_LAB2RGB) for uint8 (Lab2RGB_b -> Lab2RGBinteger, the bit-exact path)."""
+    T = _tabs()
+    L, a, b = (lab[..., k].astype(np.int64) for k in range(3))
+    y, ify = T["yf"][L, 0], T["yf"][L, 1]
+    adiv = ((5 * a * 53687 + (1 << 7)) >> 13) - 128 * LAB_BASE // 500
+    bdiv = ((b * 41943 + (1 << 4)) >> 9) - 128 * LAB_BASE // 200 + 1
+    x = T["abxz"][ify + adiv - MIN_AB]
+    z = T["abxz"][ify - bdiv - MIN_AB]
+    C = T["c_inv"]
+    shift = LAB_SHIFT + (14 - 12)  # lab_shift + (base_shift - inv_gamma_shift)
+    out = []
+    for r in range(3):
+        v = _descale(C[3 * r] * x + C[3 * r + 1] * y + C[3 * r + 2] * z, shift)
+        out.append(T["invgamma"][np.clip(v, 0, INV_GAMMA_TAB - 1)])
+    return np.stack(out, -1).astype(np.uint8)
 
 
 # ---- HSV 8U (H in [0, 180)) ----

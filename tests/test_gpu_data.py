@@ -1,7 +1,8 @@
 """Device-side data path (datapath.hip) vs the reference loader's numpy expressions (oracle/data_ref.py).
 
-Pixel ops, flips and ToTensor are bit-exact; the polygon fill is checked against the
-build's documented rule (cv2.fillPoly itself is absent: parity unpinned).
+Pixel ops, flips, ToTensor and cv2.resize INTER_LINEAR (OpenCV's fixed-point algorithm, restated)
+are bit-exact; the polygon fill is checked against the build's documented rule (cv2.fillPoly
+itself is absent: parity unpinned).
 """
 import json
 import os
@@ -33,6 +34,26 @@ def test_pixel_augmentations_bit_exact(alpha, beta, sigma, g):
     ops.augment_u8(d, noise=torch.from_numpy(noise).to(DEV))
     ops.augment_u8(d, lut=torch.from_numpy(data.gamma_lut(g)).to(DEV))
     assert np.array_equal(d.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo,c", [
+    (960, 1280, 480, 640, 3),   # exact 2x: cv2's INTER_AREA switch
+    (768, 1024, 480, 640, 3),   # the reference's max_size = 640 downscale (scale 1.6)
+    (375, 500, 352, 480, 3),    # /32 crop without a max_size scale (dataset.py:154-158)
+    (100, 130, 96, 128, 3),
+    (37, 53, 96, 160, 3),       # upscale: clamped borders, unclamped row coefficients
+    (61, 29, 20, 37, 1),        # 1 channel, a row of 37 elements: vector body + scalar tail
+    (50, 21, 13, 5, 3),         # 15 elements per row: 8-element step + scalar tail
+])
+def test_resize_u8_bit_exact(hi, wi, ho, wo, c):
+    """cv2.resize(image, (wo, ho), INTER_LINEAR) for uint8 (dataset.py:151, 158) vs the restatement of
+    OpenCV's fixed-point path (oracle/data_ref.py resize_linear_u8)."""
+    from eunet import ops
+    img = np.random.default_rng(hi * wi + c).integers(0, 256, (hi, wi, c), dtype=np.uint8)
+    got = ops.resize_u8(torch.from_numpy(img).to(DEV), ho, wo).cpu().numpy()
+    assert np.array_equal(got, O.resize_linear_u8(img, ho, wo))
+    same = ops.resize_u8(torch.from_numpy(img).to(DEV), hi, wi).cpu().numpy()
+    assert np.array_equal(same, img)
 
 
 def test_flips_and_to_tensor_exact():

@@ -490,6 +490,56 @@ def test_head_bf16_batch_stats(K, N, H, W, shift):
     assert rel(rm.double().cpu(), 0.1 * m_ref) < 1e-4
 
 
+@pytest.mark.parametrize("shift", [0.0, 30.0])
+def test_head_bf16_batch_stats_bench_size(shift):
+    """The Gram-statistics head BN (head_gram_mfma_kernel) at the bench's size (N 4, 1024^2, K 2: 16.8 M
+    pixels at 2H) with logits offset by 30 (|mean| / std ~ 30: the one-pass covariance's cancellation,
+    ADVICE r3): mean, 1/std and the running statistics within 1e-4 of fp64 statistics of the same bf16
+    operands.  The reference statistics come from the exact im2col second moments in fp64 (torch on the
+    GPU): mean_c = w_c . m + b1_c, var_c = w_c^T Cov w_c over the 19-entry column (9 taps x K, zero
+    padded at the borders) -- the identity the kernel uses, evaluated without rounding."""
+    ops = _ops()
+    N, K, H, W = 4, 2, 1024, 1024
+    g = torch.Generator(device=DEV).manual_seed(5)
+    z = torch.randn(N, K, H, W, generator=g, device=DEV, dtype=torch.float64) * 2 + shift
+    w1 = torch.randn(64, K, 3, 3, generator=g, device=DEV, dtype=torch.float64) / 4
+    b1 = torch.randn(64, generator=g, device=DEV, dtype=torch.float64) * 0.1
+    gamma = torch.rand(64, generator=g, device=DEV, dtype=torch.float64) + 0.5
+    beta = torch.randn(64, generator=g, device=DEV, dtype=torch.float64) * 0.1
+    w2 = torch.randn(K, 64, generator=g, device=DEV, dtype=torch.float64) / 8
+    b2 = torch.randn(K, generator=g, device=DEV, dtype=torch.float64) * 0.1
+    ub = F.interpolate(z.float(), scale_factor=2, mode="bilinear", align_corners=False).bfloat16().double()
+    wb = w1.float().bfloat16().double().reshape(64, K * 9)
+    b1f = b1.float().double()
+    n = N * 4 * H * W
+    s1 = torch.zeros(K * 9, dtype=torch.float64, device=DEV)
+    s2 = torch.zeros(K * 9, K * 9, dtype=torch.float64, device=DEV)
+    for i in range(N):  # per sample: the unfolded column is 18 x 4 M fp64
+        col = F.unfold(ub[i:i + 1], 3, padding=1)[0]
+        s1 += col.sum(1)
+        s2 += col @ col.T
+        del col
+    m = s1 / n
+    cov = s2 / n - torch.outer(m, m)
+    m_ref = wb @ m + b1f
+    v_ref = ((wb @ cov) * wb).sum(1)
+    f = lambda t: t.float().contiguous()  # noqa: E731
+    ws = torch.empty(ops.head_workspace_bytes(N, H, W, K, torch.bfloat16), dtype=torch.uint8, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    mean, inv = torch.empty(64, device=DEV), torch.empty(64, device=DEV)
+    logits = torch.empty(N, K, H, W, device=DEV)
+    ops.head_fwd(f(z.permute(0, 2, 3, 1)), N, H, W, K, f(w1), f(b1), f(gamma), f(beta), f(w2), f(b2), True, 1e-5,
+                 0.1, rm, rv, mean, inv, None, logits, ws, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    inv_ref = 1.0 / torch.sqrt(v_ref + 1e-5)
+    em = float((mean.double() - m_ref).abs().max() / v_ref.sqrt().max())
+    ei = rel(inv.double(), inv_ref)
+    print(f"head Gram stats at 1024^2 x 4, z offset {shift}: mean err / std {em:.2e}, 1/std rel {ei:.2e}")
+    assert em < 1e-4 and ei < 1e-4
+    assert rel(rv.double(), 0.9 + 0.1 * v_ref * n / (n - 1)) < 1e-4
+    assert float((rm.double() - 0.1 * m_ref).abs().max()) < 1e-5 * float(v_ref.sqrt().max())
+
+
 @pytest.mark.parametrize("K", [2, 3])
 def test_loss_fwd_bwd(K):
     from oracle import eunet_ref as R

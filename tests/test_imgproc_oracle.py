@@ -34,6 +34,35 @@ def test_lab_round_trip():
     # 8-bit Lab quantises L to 100/255 and a, b to 1: a few levels on dark saturated colours
     assert np.abs(back.astype(int) - img).max() <= 24  # near-zero channels: steep sRGB curve
     assert np.abs(back.astype(int) - img).mean() < 1.0
+    for v in (0, 255):  # black and white survive exactly
+        px = np.full((1, 1, 3), v, np.uint8)
+        assert np.array_equal(O.lab2rgb(O.rgb2lab(px)), px)
+
+
+def test_lab_tables_match_opencv_source_comments_and_the_library():
+    """The fixed-point Lab tables (color_lab.cpp initLabTabs): the value ranges the OpenCV source states
+    in its comments (LabToYF_b: 0 <= y <= BASE, 2260 <= ify <= BASE; abToXZ_b: -1335 <= v <= 88231), the
+    D65 white point's raw softdouble bits, and the host tables libeunet_hip builds for its kernels
+    (eunet_lab_tables: no GPU needed) equal the numpy construction entry for entry."""
+    import ctypes
+    import struct
+    T = O.lab_tables()
+    assert T["yf"][:, 0].min() == 0 and T["yf"][:, 0].max() == 1 << 14
+    assert T["yf"][:, 1].min() == 2260 and T["yf"][:, 1].max() == 1 << 14
+    assert T["abxz"].min() == -1335 and T["abxz"].max() == 88231
+    raw = [struct.unpack("<Q", struct.pack("<d", v))[0] for v in (O.D65[0], O.D65[2])]
+    assert raw == [0x3fee6a22b3892ee8, 0x3ff16b8950763a19]
+    from eunet import _lib
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(2 * (256 + 3072 + 512 + 4096) + 4 * 18)
+    assert lib.eunet_lab_tables(buf, len(buf)) == 0
+    u16 = np.frombuffer(buf.raw, np.uint16, 256 + 3072 + 512 + 4096)
+    i32 = np.frombuffer(buf.raw, np.int32, 18, offset=2 * u16.size)
+    o = 0
+    for key, n in (("gamma", 256), ("cbrt", 3072), ("yf", 512), ("invgamma", 4096)):
+        assert np.array_equal(u16[o:o + n], T[key].reshape(-1)), key
+        o += n
+    assert np.array_equal(i32[:9], T["c_fwd"]) and np.array_equal(i32[9:], T["c_inv"])
 
 
 def test_hsv_textbook_values_and_round_trip():
