@@ -69,8 +69,8 @@ def parse():
     ap.add_argument("--base", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-size", type=int, default=512,
-                    help="CPU baseline sample: 1 warm-up + 3 timed B=1 steps at this size")
+    ap.add_argument("--cpu-size", type=int, default=0,
+                    help="CPU baseline sample: 1 warm-up + 3 timed B=1 steps at this size (0: the bench size)")
     ap.add_argument("--dice-size", type=int, default=1024, help="Dice-vs-CPU-reference image side (0 = skip)")
     ap.add_argument("--dice-steps", type=int, default=200, help="training steps of the parity model")
     ap.add_argument("--no-overlap", action="store_true",
@@ -84,12 +84,14 @@ def parse():
 
 
 def cpu_baseline(args):
-    """Oracle train step on the host CPU (BASELINE.md 'CPU-baseline plan'): B=1 at --cpu-size,
-    1 warm-up step + 3 timed steps on distinct seeded tiles (bounded ~10-30 s)."""
+    """Oracle train step on the host CPU (BASELINE.md 'CPU-baseline plan'): B=1 at the bench size
+    (--cpu-size overrides), 1 warm-up step + 3 timed steps on distinct seeded tiles (~40 s at 1024^2)."""
     from oracle import eunet_ref as R
     from eunet import synth
     # the box exports OMP_NUM_THREADS = this job's CPU share; os.cpu_count() is the whole host
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    if not args.cpu_size:
+        args.cpu_size = args.size
     torch.set_num_threads(threads)
     S = R.formula_weights(args.base, 1, 2, dtype=torch.float32)
     tr = R.OracleTrainer(S, total_epochs=50)
@@ -112,7 +114,8 @@ def cpu_baseline(args):
             "sample": f"oracle train steps (PyTorch CPU fp32 restatement of Trainer.train_epoch, fixture-"
                       f"pinned), B=1, {args.cpu_size}x{args.cpu_size} 1-ch base {args.base} K 2: 1 warm-up + "
                       f"3 timed, {dt:.2f} s/step on {torch.get_num_threads()} threads of {os.cpu_count()} "
-                      f"({model}); value scaled to {args.size}x{args.size} images by pixel count"}
+                      f"({model})" + ("" if args.cpu_size == args.size else
+                                    f"; value scaled to {args.size}x{args.size} images by pixel count")}
 
 
 def train_parity_model(args, dev):
