@@ -397,15 +397,44 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
   constexpr int NCW = NW, NTH = FT;
   const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
+  // Bias (and, dgrad only, the Dropout2d scale) in packed fp32; on a partial tile the accumulators of
+  // pixels outside the image are zeroed afterwards (a uniform branch), so the BN sums below need no
+  // per-element masks: the sum over all 128 values of a wave's rows is the sum over its valid ones, and
+  // its M2 about the valid mean is the all-element M2 less (invalid count) x mean^2.  Two packed ops per
+  // pair of values instead of six scalar ops per value (SQ: 5.1 VALU instructions per MFMA on the
+  // 64-channel layers, profiles/r04_sq_layers.txt).
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int co = co0 + nt * 16 + li;
     const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
-    const float gv = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
+    const f32x2 b2 = {bv, bv};
+    if constexpr (DG) {
+      const float gv = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
+      const f32x2 g2 = {gv, gv};
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2) * g2;
+        const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2) * g2;
+        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+      }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x2 lo = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2;
+        const f32x2 hi = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2;
+        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+      }
+    }
+  }
+  if (vh < FTH || vw < FTW) {  // partial tile (image edge): zero the pixels outside the image
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[mt][nt][i] = (acc[mt][nt][i] + bv) * gv;
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt][i] = ok ? acc[mt][nt][i] : 0.f;
+      }
   }
   constexpr int PASS_PX = PROWS * FTW;
   float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
@@ -419,32 +448,29 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     // Chan-combined by 64 threads -- one barrier, one LDS round trip
     const int nw = max(0, min(RPW, vh - RPW * wv)) * vw;  // valid pixels in this wave's rows
     const float inv_nw = nw > 0 ? 1.f / (float)nw : 0.f;
+    const float ninv = (float)(RPW * FTW - nw);            // zeroed (invalid) values per channel
     float s1[4], s2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      float v = 0.f;
+      f32x2 v = {0.f, 0.f};
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
-          v += ok ? acc[mt][nt][i] : 0.f;
-        }
-      s1[nt] = xor32_sum(xor16_sum(v));
+      for (int mt = 0; mt < MT; ++mt) v += (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){acc[mt][nt][2], acc[mt][nt][3]};
+      s1[nt] = xor32_sum(xor16_sum(v.x + v.y));
     }
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const float mw = s1[nt] * inv_nw;
-      float v = 0.f;
+      const f32x2 m2 = {-mw, -mw};
+      f32x2 v = {0.f, 0.f};
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
-          const float d = acc[mt][nt][i] - mw;
-          v += ok ? d * d : 0.f;
-        }
-      s2[nt] = xor32_sum(xor16_sum(v));
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
+        const f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
+        v = __builtin_elementwise_fma(d0, d0, v);
+        v = __builtin_elementwise_fma(d1, d1, v);
+      }
+      // each zeroed value added (0 - mw)^2: removed once the 4 lane groups are summed
+      s2[nt] = fmaxf(xor32_sum(xor16_sum(v.x + v.y)) - ninv * mw * mw, 0.f);
     }
     if (q == 0)
 #pragma unroll
@@ -477,9 +503,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   T* yp = (T*)a.y;
   const bool bnb = a.bpart != nullptr;
   const int ucol = tid % UPX;
-  float bs1[E], bs2[E];
+  f32x2 bp1[E / 2], bp2[E / 2];
 #pragma unroll
-  for (int e = 0; e < E; ++e) { bs1[e] = 0.f; bs2[e] = 0.f; }
+  for (int e = 0; e < E / 2; ++e) { bp1[e] = (f32x2){0.f, 0.f}; bp2[e] = (f32x2){0.f, 0.f}; }
   if (bnb && tid < BN) {
     const bool ok = co0 + tid < a.cout;
     bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
@@ -548,12 +574,15 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           if constexpr (PRE) Vec16<T>::unpack(ryb[j], yv);
           else Vec16<T>::unpack(*(const uint4*)((const T*)a.by + pix * a.byct + a.byco + co), yv);
 #pragma unroll
-          for (int e = 0; e < E; ++e) {
+          for (int e = 0; e < E; e += 2) {  // packed fp32: each element rounded as the scalar ops round it
             const int cc = ucol * E + e;
-            const float xh = (yv[e] - bprm[cc]) * bprm[BN + cc];
-            const float gp = fmaf(yv[e], bprm[2 * BN + cc], bprm[3 * BN + cc]) > 0.f ? gr[e] : 0.f;
-            bs1[e] += gp;
-            bs2[e] = fmaf(gp, xh, bs2[e]);
+            const f32x2 y2 = {yv[e], yv[e + 1]};
+            const f32x2 xh = (y2 - *(const f32x2*)(bprm + cc)) * *(const f32x2*)(bprm + BN + cc);
+            const f32x2 pre = __builtin_elementwise_fma(y2, *(const f32x2*)(bprm + 2 * BN + cc),
+                                                        *(const f32x2*)(bprm + 3 * BN + cc));
+            const f32x2 gp = {pre.x > 0.f ? gr[e] : 0.f, pre.y > 0.f ? gr[e + 1] : 0.f};
+            bp1[e >> 1] += gp;
+            bp2[e >> 1] = __builtin_elementwise_fma(gp, xh, bp2[e >> 1]);
           }
         }
       }
@@ -562,9 +591,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   }
   if (bnb) {  // fixed-order reduction of the per-thread channel sums: the lanes of a wave that share a
              // channel unit (lane = ucol mod UPX) by DPP / permlane xor sums, then the 4 waves through LDS
+    float bs1[E], bs2[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      float v1 = bs1[e], v2 = bs2[e];
+      float v1 = bp1[e >> 1][e & 1], v2 = bp2[e >> 1][e & 1];
       if constexpr (UPX == 8) {  // lane bit 3: row_ror:8 within each row of 16 lanes
         v1 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v1), 0x128, 0xF, 0xF, false));
         v2 += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v2), 0x128, 0xF, 0xF, false));

@@ -476,10 +476,12 @@ class UNetEngine:
                      glog, gout2h, gz, gw1, gb1, gg, gbt, gw2, gb2, hws, dtype=dt)
         sink.ready(["enhance.0.weight", "enhance.0.bias", "enhance.1.weight", "enhance.1.bias",
                     "enhance.3.weight", "enhance.3.bias"])
-        return self.backward_trunk(S, gz, sink)
+        self.backward_trunk(S, gz, sink)
+        return sink.finish()
 
     def backward_trunk(self, S, gz: torch.Tensor, sink: GradSink):
-        """Backward of forward_trunk from gz = d loss / d z (NHWC fp32 [N,H,W,K])."""
+        """Backward of forward_trunk from gz = d loss / d z (NHWC fp32 [N,H,W,K]): every trunk gradient
+        is written into (and reported ready to) the sink; the caller calls sink.finish()."""
         P = self._P()
         N, H, W, K, b = S["N"], S["H"], S["W"], self.K, self.base
         dev, dt = gz.device, self.dtype
@@ -562,7 +564,8 @@ class UNetEngine:
         self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True, gred=red)
         if self.overlap_wgrad:
             torch.cuda.current_stream(dev).wait_stream(side_stream(dev))
-        return sink.finish()
+        # the caller finishes the sink: the dual-branch model runs two trunks into one sink (finishing it
+        # here made a DataParallel BucketSink wait for buckets the second trunk had not filled yet)
 
 
 class UNetFunction(torch.autograd.Function):

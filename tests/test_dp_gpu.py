@@ -300,14 +300,22 @@ def _run_world2(cfg):
     procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, cfg)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted((q.get(timeout=500) for _ in procs), key=lambda r: r["rank"])
-    for p in procs:
-        p.join(timeout=60)
-    for r in res:
-        assert "error" not in r, r["error"]
+    res = []
+    try:
+        for _ in procs:
+            r = q.get(timeout=500)
+            res.append(r)
+            # a rank that failed leaves its peer blocked in a collective: stop both now
+            assert "error" not in r, r["error"]
+    finally:
+        for p in procs:
+            p.join(timeout=60 if all("error" not in r for r in res) else 1)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
     for p in procs:
         assert p.exitcode == 0
-    return res
+    return sorted(res, key=lambda r: r["rank"])
 
 
 @pytest.mark.timeout(600)

@@ -6,8 +6,9 @@ configs[1]: base 64, 1 x 512^2 -> 2 classes, batch 8, fp32 (models.py:217-238, t
 configs[4]: dual-branch base 96 + deep supervision, 2048^2, batch 2, bf16 (models.py:253-333,
   train_eval.py:199-234): an fp64 oracle at this size is out of reach of the host, so full-size
   properties -- finite loss; two runs bit-identical; the side-stream and the serial weight-gradient
-  schedules bit-identical; BN running statistics equal to an fp64 reduction of the stored pre-BN
-  tensors; the loss decreasing over 3 steps -- plus a 256^2 slice of the same model vs the oracle.
+  schedules bit-identical; BN running statistics equal to the statistics of the pre-BN conv outputs
+  recomputed from the kernels' own operands; the loss decreasing over 3 steps -- plus a 256^2 slice
+  of the same model vs the oracle.
 """
 import pytest
 import torch
@@ -144,30 +145,39 @@ def test_configs4_dual96_2048_deterministic_and_schedules_exact(cfg4_batch, monk
         assert torch.equal(g1[k], g3[k]), ("serial schedule", k)
 
 
-def test_configs4_bn_running_stats_match_fp64_reduction(cfg4_batch):
+def test_configs4_bn_running_stats_match_recomputed_conv(cfg4_batch):
     """One training forward at the configs[4] size from fresh running statistics (mean 0, var 1):
-    running_mean = 0.1 mean, running_var = 0.9 + 0.1 unbiased var of the layer's pre-BN output; the
-    fp64 reduction of the STORED pre-BN tensor (bf16) is the reference -- for the first conv of a trunk
-    (unetpp.enc1.1, 96 channels over 2 x 2048^2 pixels) and the fusion head's last 3x3 (fusion_head.9,
-    64 channels).  The kernels reduce the fp32 accumulators before rounding; the bf16 rounding of the
-    stored values moves a mean by << 1e-3 of the channel's std."""
+    running_mean = 0.1 mean, running_var = 0.9 + 0.1 unbiased var of the layer's pre-BN conv output,
+    with the output recomputed from the kernels' own operands: unetpp.enc1.1 (enc1.0, the 1 -> 96
+    direct conv of the bf16 input, in fp64) and unetpp.enc1.4 (enc1.3, 96 -> 96 on the MFMA kernel, its
+    operand bf16(relu(ya * scale + shift)) and bf16 weights, conv in fp32) over 2 x 2048^2 pixels.  The
+    kernels reduce their fp32 accumulators before any rounding, so the statistics of the stored bf16
+    tensor would NOT do as a reference (rounding adds ~5e-6 (1 + mean^2 / var) to the variance: 1.2e-3
+    on enc1.0, whose mean is ~15 standard deviations)."""
     import _pins
+    import torch.nn.functional as F
     x, _ = cfg4_batch
     m = _pins.keep(_dual96())
     with torch.enable_grad():
         m(x)
-    S = m._engine.last_state
+    S = m._engine.last_state["SA"]
     sd = m.state_dict()
-    for key, y in (("unetpp.enc1.1", S["SA"]["enc1"]["ya"]), ("fusion_head.9", S["y3"])):
-        yd = y.double().reshape(-1, y.shape[-1])
-        n = yd.shape[0]
-        mean = yd.mean(0)
-        var = yd.var(0, unbiased=True)
+    P = dict(m.named_parameters())
+    xin = S["xin"].permute(0, 3, 1, 2).double()                          # the kernels' bf16 input
+    y1 = F.conv2d(xin, P["unetpp.enc1.0.weight"].double(), P["unetpp.enc1.0.bias"].double(), padding=1)
+    ya, bna = S["enc1"]["ya"], S["enc1"]["bna"]
+    za = torch.relu(ya.float() * bna["scale"] + bna["shift"]).bfloat16().float().permute(0, 3, 1, 2)
+    w3 = P["unetpp.enc1.3.weight"].bfloat16().float()
+    y3 = F.conv2d(za, w3, P["unetpp.enc1.3.bias"].float(), padding=1)
+    del za
+    for key, y in (("unetpp.enc1.1", y1), ("unetpp.enc1.4", y3)):
+        yd = y.double().transpose(0, 1).reshape(y.shape[1], -1)
+        mean, var = yd.mean(1), yd.var(1, unbiased=True)
         rm, rv = sd[key + ".running_mean"].double(), sd[key + ".running_var"].double()
         em = float(((rm - 0.1 * mean).abs() / (0.1 * var.sqrt())).max())
         ev = float(((rv - (0.9 + 0.1 * var)).abs() / (0.1 * var)).max())
-        print(f"configs[4] {key} ({n} px): running mean err / std {em:.2e}, running var rel err {ev:.2e}")
-        assert em < 1e-3 and ev < 1e-3, (key, em, ev)
+        print(f"configs[4] {key} ({yd.shape[1]} px): running mean err / std {em:.2e}, running var rel err {ev:.2e}")
+        assert em < 1e-4 and ev < 1e-4, (key, em, ev)
     m._engine.last_state = None
 
 
