@@ -143,7 +143,9 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 // (the dual-branch gate backward reads the 2K-channel g_f2 in fp32; no fused BN reduction then)
 // BT: the dgrad with the BN-backward transform in its staging (eunet_conv3x3_dgrad_fused; bf16) -- its
 // own instantiation, so the plain data-gradient launches keep their register allocation.
-template <typename T, bool DG, typename TO = T, bool BT = false>
+// BNB: the fused BN-backward reduction of the dgrad epilogue (a.bpart set) -- a template parameter so the
+// forward and the plain data-gradient launches carry none of its code.
+template <typename T, bool DG, typename TO = T, bool BT = false, bool BNB = false>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -274,12 +276,28 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
         }
       } else if (a.isc != nullptr) {  // BN + ReLU of the producing layer; padding stays zero
-        float f[E];
-        Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
         const bool ok = cok && aoff[i] < FWD_OOB;
+        if constexpr (sizeof(T) == 2) {
+          // packed fp32 FMA per bf16 pair, rounded to bf16, ReLU on the rounded pair (sign bit:
+          // round(max(x, 0)) == max(round(x), 0)) -- as the weight gradient's staging does
+          u32x4 o;
 #pragma unroll
-        for (int j = 0; j < E; ++j) f[j] = ok ? fmaxf(fmaf(f[j], asc[j >> 2][j & 3], ash[j >> 2][j & 3]), 0.f) : 0.f;
-        v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
+          for (int d = 0; d < 4; ++d) {
+            const f32x2 x = {__uint_as_float(v[d] << 16), __uint_as_float(v[d] & 0xFFFF0000u)};
+            const f32x2 r = __builtin_elementwise_fma(
+                x, (f32x2){asc[d >> 1][2 * (d & 1)], asc[d >> 1][2 * (d & 1) + 1]},
+                (f32x2){ash[d >> 1][2 * (d & 1)], ash[d >> 1][2 * (d & 1) + 1]});
+            const s16x2 b = __builtin_bit_cast(s16x2, (uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16));
+            o[d] = ok ? __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0})) : 0u;
+          }
+          v = o;
+        } else {
+          float f[E];
+          Vec16<T>::unpack(__builtin_bit_cast(uint4, v), f);
+#pragma unroll
+          for (int j = 0; j < E; ++j) f[j] = ok ? fmaxf(fmaf(f[j], asc[j >> 2][j & 3], ash[j >> 2][j & 3]), 0.f) : 0.f;
+          v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
+        }
       }
       *(u32x4*)(As + (qq * FHPXP + hp) * 16) = v;
     }
@@ -501,7 +519,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
   static_assert(NTH % UPX == 0, "a thread's channel unit must be fixed across store iterations");
   T* yp = (T*)a.y;
-  const bool bnb = a.bpart != nullptr;
+  constexpr bool bnb = BNB;
   const int ucol = tid % UPX;
   f32x2 bp1[E / 2], bp2[E / 2];
 #pragma unroll
@@ -514,6 +532,14 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
   }
   constexpr int SJ = PASS_PX * UPX / NTH;      // output units per thread per pass
+  // output / y addresses: a block-uniform base (the tile's corner) + row x row stride + the thread's
+  // (column, unit) offset, instead of a 64-bit pixel index per unit
+  const long long yrs = (long long)a.W * a.yct;
+  const long long tile_px = (long long)(n * a.H + y0) * a.W + x0;
+  T* const ybase = yp + tile_px * a.yct + a.yco + co0;
+  float* const yfbase = (float*)a.y + tile_px * a.yct + a.yco + co0;
+  const long long brs = (long long)a.W * a.byct;
+  const T* const bybase = BNB ? (const T*)a.by + tile_px * a.byct + a.byco + co0 : nullptr;
   constexpr bool PRE = sizeof(T) == 2;         // bf16: prefetch the pass's y (BN-backward input)
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
@@ -531,8 +557,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           const int co = co0 + u * E;
           ryb[j] = make_uint4(0, 0, 0, 0);
           if (r < vh && c < vw && co < a.cout)
-            ryb[j] = *(const uint4*)((const T*)a.by + ((long long)(n * a.H + y0 + r) * a.W + x0 + c) * a.byct +
-                                     a.byco + co);
+            ryb[j] = *(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E));
         }
       }
     }
@@ -558,21 +583,22 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         float f[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) f[e] = sp[e];
-        const long long pix = (long long)(n * a.H + y0 + r) * a.W + x0 + c;
-        EUNET_DASSERT(pix < (long long)a.N * a.H * a.W && co + E <= a.cout && a.yco + co + E <= a.yct);
+        const long long off = (long long)r * yrs + (c * a.yct + u * E);
+        EUNET_DASSERT(tile_px + (long long)r * a.W + c < (long long)a.N * a.H * a.W && co + E <= a.cout &&
+                      a.yco + co + E <= a.yct);
         const uint4 packed = Vec16<T>::pack(f);
         if constexpr (sizeof(TO) == sizeof(T)) {
-          *(uint4*)(yp + pix * a.yct + a.yco + co) = packed;
+          *(uint4*)(ybase + off) = packed;
         } else {  // fp32 output of a bf16 kernel: E = 8 floats, two 16-byte stores
-          float* yo = (float*)a.y + pix * a.yct + a.yco + co;
+          float* yo = yfbase + off;
           *(float4*)yo = make_float4(f[0], f[1], f[2], f[3]);
           *(float4*)(yo + 4) = make_float4(f[4], f[5], f[6], f[7]);
         }
-        if (bnb) {
+        if constexpr (BNB) {
           float gr[E], yv[E];
           Vec16<T>::unpack(packed, gr);
           if constexpr (PRE) Vec16<T>::unpack(ryb[j], yv);
-          else Vec16<T>::unpack(*(const uint4*)((const T*)a.by + pix * a.byct + a.byco + co), yv);
+          else Vec16<T>::unpack(*(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E)), yv);
 #pragma unroll
           for (int e = 0; e < E; e += 2) {  // packed fp32: each element rounded as the scalar ops round it
             const int cc = ucol * E + e;
@@ -1130,18 +1156,23 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, 
                 "conv3x3: one sample's input (%d x %d x %d) must be < 3 GiB (buffer-descriptor staging)", a.H, a.W, a.xct);
   EUNET_REQUIRE((long long)a.nkc * kchunk(dtype) * a.cout_pad * 9 * esz < (1ll << 31), "conv3x3: packed weights >= 2 GiB");
   dim3 grid(a.ntiles * (a.cout_pad / BN));
+  const bool bnb = DG && a.bpart != nullptr;
+  EUNET_REQUIRE(!(out_f32 && bnb), "conv3x3: an fp32-output data gradient has no fused BN-backward reduction");
+  auto go = [&](auto kern) {
+    allow_lds(kern, FWD_LDS);
+    kern<<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+  };
   if (dtype == EUNET_BF16 && out_f32) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t, true, float>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t, true, float><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    go(conv3x3_fwd_kernel<bf16_t, true, float>);
   } else if (dtype == EUNET_BF16 && DG && bt) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t, true, bf16_t, true><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true, true>);
+    else go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true, false>);
   } else if (dtype == EUNET_BF16) {
-    allow_lds(conv3x3_fwd_kernel<bf16_t, DG>, FWD_LDS);
-    conv3x3_fwd_kernel<bf16_t, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, false, true>);
+    else go(conv3x3_fwd_kernel<bf16_t, DG>);
   } else {
-    allow_lds(conv3x3_fwd_kernel<float, DG>, FWD_LDS);
-    conv3x3_fwd_kernel<float, DG><<<grid, FT, FWD_LDS, (hipStream_t)stream>>>(a);
+    if (bnb) go(conv3x3_fwd_kernel<float, true, float, false, true>);
+    else go(conv3x3_fwd_kernel<float, DG>);
   }
   EUNET_LAUNCH_CHECK("conv3x3_fwd");
   return EUNET_OK;

@@ -276,14 +276,16 @@ def _trainer_worker(rank, world, port, q, cfg):
                        post_equal=torch.equal(gs[4], gs[5]))
             if cfg == "fp32" and step == 0:
                 pins = _pins.model_pins(mod)
-                rec["grads"] = {k: p.grad.detach().double().cpu() for k, p in mod.named_parameters()}
+                # numpy arrays travel through the queue by value (torch CPU tensors would be shared through
+                # files that vanish with this process)
+                rec["grads"] = {k: p.grad.detach().double().cpu().numpy() for k, p in mod.named_parameters()}
                 for odt, key in ((torch.float64, "oracle64"), (torch.float32, "oracle32")):
                     S = R.formula_weights(base, 1, 2, dtype=odt)
                     for k in S:
                         if S[k].is_floating_point() and "running" not in k:
                             S[k].requires_grad_(True)
                     R.batch_loss(R.forward(S, x.cpu().to(odt), True, pins=pins), m.cpu()).backward()
-                    rec[key] = {k: S[k].grad.double() for k in rec["grads"]}
+                    rec[key] = {k: S[k].grad.double().numpy() for k in rec["grads"]}
             out["steps"].append(rec)
         q.put(out)
     except Exception as e:  # report instead of hanging the parent on q.get
@@ -346,6 +348,10 @@ def test_dp_world2_step_is_mean_of_shards_oracle():
     s0, s1 = res[0]["steps"][0], res[1]["steps"][0]
     for s in (s0, s1):
         assert s["params_equal"] and s["post_equal"]
+
+    for s in (s0, s1):
+        for key in ("grads", "oracle64", "oracle32"):
+            s[key] = {k: torch.from_numpy(v) for k, v in s[key].items()}
 
     def mean_clipped(key):
         g = {k: 0.5 * (s0[key][k] + s1[key][k]) for k in s0[key]}

