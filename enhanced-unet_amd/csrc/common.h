@@ -100,6 +100,12 @@ __device__ __forceinline__ float xor32_sum(float v) {
 }
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two floats -> one dword of two bf16 (lo, hi), rounded to nearest even: a single v_cvt_pk_bf16_f32
+// (f2bf(lo) | f2bf(hi) << 16 compiles to two conversions and a permute)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
+}
 
 template <typename T> struct Elem;
 template <> struct Elem<float> {
@@ -138,7 +144,7 @@ template <> struct Vec16<bf16_t> {
   static __device__ __forceinline__ uint4 pack(const float* f) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pk_bf16(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

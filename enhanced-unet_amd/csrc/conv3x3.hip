@@ -287,7 +287,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
             const f32x2 r = __builtin_elementwise_fma(
                 x, (f32x2){asc[d >> 1][2 * (d & 1)], asc[d >> 1][2 * (d & 1) + 1]},
                 (f32x2){ash[d >> 1][2 * (d & 1)], ash[d >> 1][2 * (d & 1) + 1]});
-            const s16x2 b = __builtin_bit_cast(s16x2, (uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16));
+            const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(r[0], r[1]));
             o[d] = ok ? __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0})) : 0u;
           }
           v = o;
@@ -532,6 +532,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
   }
   constexpr int SJ = PASS_PX * UPX / NTH;      // output units per thread per pass
+  constexpr int PXJ = NTH / UPX;                // pixels per unit step
+  static_assert(FTW % PXJ == 0, "a unit step covers a fraction of one tile row (row compile-time per step)");
+  const int tu = tid;
   // output / y addresses: a block-uniform base (the tile's corner) + row x row stride + the thread's
   // (column, unit) offset, instead of a 64-bit pixel index per unit
   const long long yrs = (long long)a.W * a.yct;
@@ -551,9 +554,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       if (bnb) {
 #pragma unroll
         for (int j = 0; j < SJ; ++j) {
-          const int id = tid + j * NTH;
-          const int px = id / UPX, u = id - px * UPX;
-          const int r = pass * PROWS + px / FTW, c = px % FTW;
+          const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
           const int co = co0 + u * E;
           ryb[j] = make_uint4(0, 0, 0, 0);
           if (r < vh && c < vw && co < a.cout)
@@ -574,9 +575,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
-      const int id = tid + j * NTH;
-      const int px = id / UPX, u = id - px * UPX;
-      const int r = pass * PROWS + px / FTW, c = px % FTW;
+      // unit tid + j NTH = (pixel px, channel unit u): u = tid mod UPX, px = tid / UPX + PXJ j, and since
+      // PXJ divides FTW the row of px is compile-time per (pass, j)
+      const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
+      const int px = (r - pass * PROWS) * FTW + c;
       const int co = co0 + u * E;
       if (r < vh && c < vw && co < a.cout) {
         const float* sp = stg + px * OUT_LD + u * E;
@@ -784,48 +786,63 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
-  auto dma_d = [&](int tile) {  // dY tile straight into LDS: wave-instruction j = units 64j..64j+63
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+  // Tile staging by buffer LDS-DMA (buffer_load ... lds) through per-sample descriptors: one 32-bit
+  // byte offset per lane, padding / out-of-range units at FWD_OOB (the range check reads zeros), the
+  // wave-instructions unrolled so that every per-lane term below is tile-invariant or a compile-time
+  // constant (the per-tile part is scalar).
+  const int wvs = __builtin_amdgcn_readfirstlane(wv);
+  // dY unit tid + 256 i = tile pixel (row i, column tid >> 3), LDS unit tid & 7 holding channel unit du
+  const int dcol = tid >> 3, du = (tid & 7) ^ wd_swz(dcol);
+  const bool dch_ok = co0 + du * 8 < a.cout;
+  const uint32_t dlane = (uint32_t)((dcol * a.dct + a.dco + co0 + du * 8) * 2);
+  const uint32_t dslice = (uint32_t)(a.H * a.W * a.dct) * 2u, xslice = (uint32_t)(a.H * a.W * a.xct) * 2u;
+  auto dma_d = [&](int n, int y0, int x0) {
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const bf16_t*)a.dy + (long long)n * a.H * a.W * a.dct), 0, (int)dslice, 0x00020000);
+    const bool xok = dch_ok & (dcol < a.W - x0);
+    const uint32_t rb = (uint32_t)((y0 * a.W + x0) * a.dct) * 2u, rstep = (uint32_t)(a.W * a.dct) * 2u;
     char* Ds = smem + WX_LDS;
-    for (int j = wv; j < WD_ITERS * NTHR / 64; j += NTHR / 64) {
-      const int id = j * 64 + lane;
-      const int px = id >> 3, u = (id & 7) ^ wd_swz(px);  // LDS unit id & 7 holds channel unit u
-      const int r = px / TW, c = px - r * TW;
-      const int yy = y0 + r, xx = x0 + c, co = co0 + u * 8;
-      const void* src = (yy < a.H && xx < a.W && co < a.cout)
-                            ? (const void*)((const bf16_t*)a.dy + ((long long)(n * a.H + yy) * a.W + xx) * a.dct + a.dco + co)
-                            : (const void*)&g_conv_zero;
-      EUNET_DASSERT(!(yy < a.H && xx < a.W && co < a.cout) || (n < a.N && a.dco + co + 8 <= a.dct));
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(Ds + j * 64 * 16), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TH; ++i) {
+      const bool ok = xok & (y0 + i < a.H);
+      const uint32_t off = dlane + rb + i * rstep;
+      EUNET_DASSERT(!ok || off + 16u <= dslice);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (__attribute__((address_space(3))) void*)(Ds + (wvs + 4 * i) * 1024),
+                                               16, ok ? off : FWD_OOB, 0, 0, 0);
     }
   };
-  // X halo raw into LDS: slot s = oc * HPXP + hp, wave-instruction j = slots 64j..64j+63
-  auto dma_x = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
-    for (int j = wv; j < 8 * HPXP / 64; j += NTHR / 64) {
-      const int sl = j * 64 + lane, oc = sl / HPXP, hp = sl - oc * HPXP - wx_shift(oc);
-      const int hy = hp / HW_, hx = hp - hy * HW_;
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      const int c = kc * KCW + oc * 8;
-      const void* src = (hp >= 0 && hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin)
-                            ? (const void*)((const bf16_t*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + c)
-                            : (const void*)&g_conv_zero;
-      EUNET_DASSERT(!(hp >= 0 && hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W && c < a.cin) ||
-                    (n < a.N && a.xco + c + 8 <= a.xct));
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(smem + j * 64 * 16), 16, 0, 0);
+  static_assert(WD_ITERS == TH && TW * 8 == NTHR, "dma_d: one tile row per wave-instruction group");
+  // X halo raw into LDS: slot s = tid + 256 i = oc * HPXP + wx_shift(oc) + hp
+  static_assert(8 * HPXP == 4 * 64 * WX_ITERS, "dma_x: 11 wave-instructions per wave");
+  auto dma_x = [&](int n, int y0, int x0) {
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const bf16_t*)a.x + (long long)n * a.H * a.W * a.xct), 0, (int)xslice, 0x00020000);
+    const int tb = ((y0 - 1) * a.W + (x0 - 1)) * a.xct + a.xco + kc * KCW;  // element (y0 - 1, x0 - 1)
+    // recomputed per tile: hoisted out of the tile loop, the 11 lanes' offsets and masks would be
+    // live across the k-loop and spill
+    int t = tid;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int i = 0; i < WX_ITERS; ++i) {
+      // octant of slot tid + 256 i: k, or k + 1 from lane tid >= tk on (256 < HPXP: one boundary at most)
+      const int k = 256 * i / HPXP, tk = HPXP * (k + 1) - 256 * i;
+      const bool bump = tk < 256 && t >= tk;
+      const int oc = k + bump;
+      const int hp = t + 256 * i - HPXP * oc - wx_shift(oc);
+      const int hy = (int)((uint32_t)hp / HW_), hx = hp - hy * HW_;
+      const bool ok = ((uint32_t)hp < (uint32_t)HPX) & ((uint32_t)(y0 - 1 + hy) < (uint32_t)a.H) &
+                      ((uint32_t)(x0 - 1 + hx) < (uint32_t)a.W) & (kc * KCW + oc * 8 < a.cin);
+      const uint32_t off = (uint32_t)(tb + (hy * a.W + hx) * a.xct + oc * 8) * 2u;
+      EUNET_DASSERT(!ok || off + 16u <= xslice);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(smem + (wvs + 4 * i) * 1024),
+                                               16, ok ? off : FWD_OOB, 0, 0, 0);
     }
   };
   // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t & 7 and
   // halo pixels (t >> 3) + 32 i (i < 11): its 8 scales / shifts are read once per tile and the
   // pixel coordinates advance incrementally (32 < 34 columns: at most one row wrap per step).
   const int xo = tid & 7;
-  auto bnrelu_x = [&](int tile) {
-    const int n = tile / tpi, trem = tile - n * tpi;
-    const int y0 = (trem / a.tx) * TH, x0 = (trem % a.tx) * TW;
+  auto bnrelu_x = [&](int y0, int x0) {
     if (kc * KCW + xo * 8 >= a.cin) return;
     const f32x4 s0 = *(const f32x4*)(lsc + xo * 8), s1 = *(const f32x4*)(lsc + xo * 8 + 4);
     const f32x4 h0 = *(const f32x4*)(lsc + KCW + xo * 8), h1 = *(const f32x4*)(lsc + KCW + xo * 8 + 4);
@@ -844,7 +861,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         for (int d = 0; d < 4; ++d) {  // packed fp32 FMA, round to bf16, ReLU on the bf16 pair (sign bit)
           const f32x2 x = {__uint_as_float(w[d] << 16), __uint_as_float(w[d] & 0xFFFF0000u)};
           const f32x2 r = __builtin_elementwise_fma(x, (f32x2){sc[2 * d], sc[2 * d + 1]}, (f32x2){sh[2 * d], sh[2 * d + 1]});
-          const s16x2 b = __builtin_bit_cast(s16x2, (uint32_t)f2bf(r[0]) | ((uint32_t)f2bf(r[1]) << 16));
+          const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(r[0], r[1]));
           o[d] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
         }
         *q = o;
@@ -853,22 +870,30 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       if (hx >= HW_) { hx -= HW_; ++hy; }
     }
   };
+  // tile coordinates advance incrementally (scalar): sample tn, tile row tyi, tile column txi
+  int tn = t_begin / tpi, tyi = (t_begin - tn * tpi) / a.tx, txi = t_begin - tn * tpi - tyi * a.tx;
   for (int tile = t_begin; tile < t_end; ++tile) {
+    const int n = __builtin_amdgcn_readfirstlane(tn);
+    const int y0 = __builtin_amdgcn_readfirstlane(tyi) * TH, x0 = __builtin_amdgcn_readfirstlane(txi) * TW;
+    if (++txi == a.tx) {
+      txi = 0;
+      if (++tyi == a.ty) { tyi = 0; ++tn; }
+    }
     {  // X halo and dY both by LDS-DMA
       // the block's 64 input channels' BN scale / shift for this tile's sample: one load per thread
       // (tid < 128) instead of 16 per halo slot in the transform pass
       float rsc = 0.f;
       if (a.isc != nullptr && tid < 2 * KCW) {
         const int c = kc * KCW + (tid % KCW);
-        if (c < a.cin) rsc = (tid < KCW ? a.isc : a.ish)[c + (tile / tpi) * a.iss];
+        if (c < a.cin) rsc = (tid < KCW ? a.isc : a.ish)[c + n * a.iss];
       }
       __syncthreads();  // previous tile's LDS reads are done
-      dma_x(tile);
-      dma_d(tile);
+      dma_x(n, y0, x0);
+      dma_d(n, y0, x0);
       if (a.isc != nullptr && tid < 2 * KCW) lsc[tid] = rsc;
       __syncthreads();  // (its fence waits for the DMA)
       if (a.isc != nullptr) {
-        bnrelu_x(tile);
+        bnrelu_x(y0, x0);
         __syncthreads();
       }
     }
@@ -1409,6 +1434,9 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   a.dy = dy->ptr; a.dct = dy->ctot; a.dco = dy->coff; a.cout = dy->c;
   a.dw = dw_part; a.db = db_part;
   const bool bf = x->dtype == EUNET_BF16;
+  EUNET_REQUIRE(!bf || ((long long)a.H * a.W * a.xct * 2 < (long long)FWD_OOB &&
+                        (long long)a.H * a.W * a.dct * 2 < (long long)FWD_OOB),
+                "conv3x3_wgrad: sample slice >= 3 GiB");
   a.tx = cdiv(x->w, bf ? TW : WF_TW); a.ty = cdiv(x->h, bf ? TH : WF_TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;

@@ -152,6 +152,45 @@ def test_conv3x3_dgrad_wgrad(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_wgrad_ragged_slots(dt):
+    """The weight gradient over channel slots of concat buffers (x at channel 16, dY at 8), a partial
+    input-channel chunk (40 of 64) and output-channel block (80 = 64 + 16), ragged tile rows and columns
+    (13 x 40), a per-sample BN transform (nstride) and pixel splits whose tile ranges cross samples --
+    against the fp64 weight gradient of the transformed operand (rounded to bf16 as the kernel stages it)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(43)
+    N, H, W, Cin, Cout = 3, 13, 40, 40, 80
+    xb = torch.randn(N, H, W, Cin + 24, generator=g).to(DEV, dt)
+    dyb = torch.randn(N, H, W, Cout + 16, generator=g).to(DEV, dt)
+    ns_stride = Cin + 8
+    sc = (torch.rand(N, ns_stride, generator=g) + 0.5).to(DEV)
+    sh = (torch.randn(N, ns_stride, generator=g) * 0.3).to(DEV)
+    x = xb[..., 16:16 + Cin].double().cpu()
+    dy = dyb[..., 8:8 + Cout].double().cpu()
+    xa = (x * sc[:, None, None, :Cin].double().cpu() + sh[:, None, None, :Cin].double().cpu()).clamp_min(0.0)
+    if dt == torch.bfloat16:
+        xa = xa.float().bfloat16().double()
+    wt = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(nchw(xa), wt, None, padding=1).backward(nchw(dy))
+    th = 8 if dt == torch.bfloat16 else 4
+    ntiles = N * -(-H // th) * -(-W // 32)
+    tpi = ntiles // N
+    crossing = [s for s in range(2, ntiles) if -(-ntiles // -(-ntiles // s)) == s and (-(-ntiles // s)) % tpi]
+    assert crossing
+    xv, dv = ops.act(xb, 16, Cin), ops.act(dyb, 8, Cout)
+    for ns in (ops.conv3x3_wgrad_splits(dv, Cin, dt), crossing[0]):
+        dwp = torch.empty(ns * Cout * 9 * Cin, device=DEV)
+        dbp = torch.empty(ns * Cout, device=DEV)
+        ops.conv3x3_wgrad(xv, dv, dwp, dbp, ns, scale=sc, shift=sh, nstride=ns_stride)
+        dw = torch.empty(Cout, Cin, 3, 3, device=DEV)
+        db = torch.empty(Cout, device=DEV)
+        ops.wgrad_reduce(dwp, dbp, ns, Cout, Cin, 9, dw, db)
+        torch.cuda.synchronize()
+        assert rel(dw, wt.grad) < 1e-5, ns
+        assert rel(db, dy.sum(dim=(0, 1, 2))) < 1e-5, ns
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cin", [1, 3, 4, 6, 8])
 def test_conv_small(dt, cin):
     ops = _ops()
