@@ -137,6 +137,12 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 #ifndef CONV_PRIO
 #define CONV_PRIO 1
 #endif
+#ifndef CONV_BDMA
+#define CONV_BDMA 1
+#endif
+#ifndef CONV_ADMA
+#define CONV_ADMA 0
+#endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
 // TO: the output element type -- T, or float for a bf16 data gradient whose consumer keeps fp32
@@ -180,8 +186,24 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       (int)((uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T)), 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wp, 0, a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T), 0x00020000);
+  // forward without an operand transform (a ".0" conv: its input is already activated): the halo too goes
+  // straight into LDS by buffer_load ... lds, slot-major (wave-instruction i of wave w fills LDS slots
+  // i * FT + 64 w .. +63 = (quarter, halo pixel) slots), so a K-chunk's staging is one asynchronous round
+  // trip with no staging registers; aoff then holds the slots' offsets
+  constexpr bool ADMA_OK = CONV_ADMA && !DG && sizeof(T) == 2;
+  static_assert(!ADMA_OK || A_IT * FT == 4 * FHPXP, "dma_a: whole wave-instructions over the 4 planes");
+  const bool adma = ADMA_OK && a.isc == nullptr;
 #pragma unroll
-  for (int i = 0; i < A_IT; ++i) aoff[i] = fwd_unit_off<T>(a, y0, x0, tid + i * FT);
+  for (int i = 0; i < A_IT; ++i) {
+    if (adma) {
+      const int sl = tid + i * FT, qs = sl / FHPXP, hp = sl - qs * FHPXP;
+      const int hy = hp / FHW, hx = hp - hy * FHW, yy = y0 + hy - 1, xx = x0 + hx - 1;
+      const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+      aoff[i] = ok ? (uint32_t)((yy * a.W + xx) * a.xct + a.xco + qs * E) * (uint32_t)sizeof(T) : FWD_OOB;
+    } else {
+      aoff[i] = fwd_unit_off<T>(a, y0, x0, tid + i * FT);
+    }
+  }
 
   // dgrad: the BN-backward transform (k1 in asc, kq in ash, k2 / k3 below) and its y operand
   constexpr int BE = DG ? E / 4 : 1;
@@ -309,6 +331,32 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       if (!B_TAIL || id < B_UNITS) *(u32x4*)(Bs + id * 16) = rb[i];
     }
   };
+  // weights straight into LDS (buffer_load ... lds: no staging VGPRs, no LDS write instructions); unit id =
+  // tid + i * FT is LDS unit id, so wave-instruction i of wave w fills units i * FT + 64 w .. +63
+  const int wvs = __builtin_amdgcn_readfirstlane(wv);
+  auto dma_b = [&](int kc) {
+    static_assert(!B_TAIL, "dma_b: whole wave-instructions");
+#pragma unroll
+    for (int i = 0; i < B_IT; ++i) {
+      const int id = tid + i * FT;
+      const uint32_t wo = (uint32_t)((((kc * 4 + id / (BN * 9)) * a.cout_pad + co0) * 9 + id % (BN * 9)) * 16);
+      EUNET_DASSERT(wo + 16u <= (uint32_t)(a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T)));
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (__attribute__((address_space(3))) void*)(Bs + (i * FT + wvs * 64) * 16),
+                                               16, wo, 0, 0, 0);
+    }
+  };
+  auto dma_a = [&](int kc) {
+    const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
+    const bool full = (kc + 1) * KC <= a.cin;  // else: quarters past cin read as zeros
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+      uint32_t off = aoff[i];
+      if (!full && kc * KC + ((tid + i * FT) / FHPXP) * E >= a.cin) off = FWD_OOB;
+      EUNET_DASSERT(off == FWD_OOB || off + cadd + 16u <= slice_bytes);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + (i * FT + wvs * 64) * 16),
+                                               16, off, cadd, 0, 0);
+    }
+  };
   constexpr int AH = A_IT / 2, BH = B_IT / 2;
   auto chunk = [&]() {
 #pragma unroll 1
@@ -346,6 +394,11 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   // +15-20 % on every layer shape, profiles/r01_ab_phase.txt).
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
   auto stage_halves = [&](int kc) {
+    if (CONV_BDMA) dma_b(kc);
+    if (ADMA_OK && adma) {
+      dma_a(kc);
+      return;
+    }
     gload_affine(kc);
     if (DG && btr) {  // two loads per halo unit (g and y): thirds bound the staging registers
       constexpr int A3 = (A_IT + 2) / 3;
@@ -355,16 +408,21 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       lwrite_a(kc, A3, 2 * A3);
       gload_a(kc, 2 * A3, A_IT);
       lwrite_a(kc, 2 * A3, A_IT);
+    } else if (CONV_BDMA == 2) {
+      gload_a(kc, 0, A_IT);
+      lwrite_a(kc, 0, A_IT);
     } else {
       gload_a(kc, 0, AH);
       lwrite_a(kc, 0, AH);
       gload_a(kc, AH, A_IT);
       lwrite_a(kc, AH, A_IT);
     }
-    gload_b(kc, 0, BH);
-    lwrite_b(0, BH);
-    gload_b(kc, BH, B_IT);
-    lwrite_b(BH, B_IT);
+    if (!CONV_BDMA) {
+      gload_b(kc, 0, BH);
+      lwrite_b(0, BH);
+      gload_b(kc, BH, B_IT);
+      lwrite_b(BH, B_IT);
+    }
   };
   // co-block 0 of the fused BN-backward dgrad stores the tile interior of the staged gy (for the
   // weight gradient) from LDS right before the chunk's MFMAs, so the stores drain under them instead
@@ -385,12 +443,15 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       }
     }
   };
-  if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
+  if (ADMA_OK && adma) {
+    stage_halves(0);
+  } else if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
+    if (CONV_BDMA) dma_b(0);
     gload_affine(0);
     gload_a(0, 0, A_IT);
-    gload_b(0, 0, B_IT);
+    if (!CONV_BDMA) gload_b(0, 0, B_IT);
     lwrite_a(0, 0, A_IT);
-    lwrite_b(0, B_IT);
+    if (!CONV_BDMA) lwrite_b(0, B_IT);
   } else {
     stage_halves(0);
   }

@@ -725,6 +725,13 @@ __device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.
 __device__ __forceinline__ f32x4 ld4v(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ f32x2 half2(const f32x4& v, int hp) { return hp ? v.hi : v.lo; }
 __device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+// per 16-bit half of a (halves >= 0): 0xFFFF where nonzero, else 0 (v_pk_min_u16 + v_pk_sub_u16; written
+// in C the compiler turns it into a compare and a select per half)
+__device__ __forceinline__ uint32_t pk_nonzero_mask(uint32_t a) {
+  uint32_t m;  // (the 1 comes from a register: an inline constant would give the high half 0)
+  asm("v_pk_min_u16 %0, %1, %2\n\tv_pk_sub_u16 %0, 0, %0" : "=&v"(m) : "v"(a), "s"(0x00010001u));
+  return m;
+}
 __device__ __forceinline__ f32x2 relu_sel(f32x2 pre, f32x2 v) {  // v where pre > 0, else 0
   return (f32x2){pre.x > 0.f ? v.x : 0.f, pre.y > 0.f ? v.y : 0.f};
 }
@@ -1083,14 +1090,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
         const int r = 8 * wv + 2 * rp + rr, oy = oy0 + r, ox = ox0 + sx + x;
         f32x4 acc[4];
         conv_h_mfma(su, (r * GR + sx + x) * 3, off, Ah, acc);
+        // BN + ReLU straight into the 1x1's B fragments (cfrag order): packed fp32 FMA per channel pair,
+        // one v_cvt_pk_bf16_f32, ReLU on the rounded pair (round(max(v, 0)) == max(round(v), 0))
+        uint32_t bw[4][2];
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          const float4 s4 = ld4(scs + 16 * cb + 4 * q), t4 = ld4(shs + 16 * cb + 4 * q);
+          const f32x4 s4 = ld4v(scs + 16 * cb + 4 * q), t4 = ld4v(shs + 16 * cb + 4 * q);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[cb][i] = fmaxf(fmaf(acc[cb][i], f4(s4, i), f4(t4, i)), 0.f);
+          for (int hp = 0; hp < 2; ++hp) {
+            const f32x2 v = pkfma(half2(acc[cb], hp), half2(s4, hp), half2(t4, hp));
+            const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(v.x, v.y));
+            bw[cb][hp] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
+          }
         }
-        f32x4 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[0], cfrag(acc, 0), z4, 0, 0, 0);
-        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[1], cfrag(acc, 1), o, 0, 0, 0);
+        const bf16x8 f0 = __builtin_bit_cast(bf16x8, (u32x4){bw[0][0], bw[0][1], bw[1][0], bw[1][1]});
+        const bf16x8 f1 = __builtin_bit_cast(bf16x8, (u32x4){bw[2][0], bw[2][1], bw[3][0], bw[3][1]});
+        f32x4 o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[0], f0, z4, 0, 0, 0);
+        o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ao[1], f1, o, 0, 0, 0);
         // lanes q == 0 hold o[k = i][pixel x]
         const bool pv = q == 0 && oy < H2 && ox < W2;
 #pragma unroll
@@ -1150,7 +1166,7 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
   __shared__ float zs[GZ * GZ * 3];
   __shared__ float red[STRIDE];
   __shared__ __attribute__((aligned(16))) float gos[K * GT * GT];
-  __shared__ __attribute__((aligned(16))) bf16x8 fr[8][64];  // W1, W2^T fragments (B operands here)
+  __shared__ __attribute__((aligned(16))) bf16x8 fr[4][64];  // W1 fragments (B operands here)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   for (int i = tid; i < STRIDE; i += NT) red[i] = 0.f;
@@ -1159,26 +1175,25 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
     load_a_w1<K>(a.w1, lane, A4);
 #pragma unroll
     for (int f = 0; f < 4; ++f) fr[f][lane] = A4[f];
-    load_a_w2t<K>(a.w2, lane, A4);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
   }
   float kI[4], kO[4], kP[4], kQ[4];  // channel 16cb + x (op_sel broadcasts them to both pixel halves)
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) bwd_params(a, 16 * cb + x, kI[cb], kO[cb], kP[cb], kQ[cb]);
   int off[8];
   im2col_offsets<K, GR>(q, off);
-  f32x2 pgb[4], pgx[4], pw2[K][4];
-  float ab2[K];
+  // Per-channel sums as MFMAs over pixels with a row's g_o as the A operand (class m = lane & 15 < K, pixels
+  // 4q .. 4q+3 of both 16-pixel segments): for channel c = 16cb + x
+  //   gW2[k][c]    = sum_p g_o[p][k] relu(pre[p][c])                      (accA)
+  //   dbeta[c]     = sum_p g_bn = sum_k W2[k][c] sum_p g_o[p][k] [pre > 0]  (accM)
+  //   dgamma[c]    = sum_p g_bn xhat = sum_k W2[k][c] sum_p g_o[p][k] [pre > 0] xhat   (accN)
+  // (g_bn = [pre > 0] s, s = W2^T g_o with the bf16 operands of the s GEMM it replaces); the B operands are
+  // the bf16 pair of relu(pre), the mask (1.0 / 0) and the masked xhat, formed with 16-bit integer ops.
+  f32x4 accA[4], accM[4], accN[4];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    pgb[cb] = pgx[cb] = (f32x2){0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < K; ++k) pw2[k][cb] = (f32x2){0.f, 0.f};
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) ab2[k] = 0.f;
+  for (int cb = 0; cb < 4; ++cb) accA[cb] = accM[cb] = accN[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float ab2 = 0.f;  // lanes x < K: sum of g_o of class x over this lane's pixels
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const int gk = min(x, K - 1);
   float zv[Z32<K>::ZI];
   zfetch32<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
@@ -1200,65 +1215,71 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
       for (int k = 0; k < K; ++k) gos[k * GT * GT + tid + e * NT] = gv[k][e];
     __syncthreads();
 #pragma unroll 1
-    for (int rs = 0; rs < 2 * GT / 4; ++rs) {
-      const int r = 8 * wv + (rs >> 1), sx = 16 * (rs & 1);
+    for (int rr = 0; rr < GT / 4; ++rr) {  // row r: two 16-pixel segments, whose 8 pixels per lane fill the sums' k
+      const int r = 8 * wv + rr;
       int fl = lane;
       asm volatile("" : "+v"(fl));  // keep the fragment reads in the loop (no LICM into registers)
-      f32x4 acc[4], sv[4];
-      {
-        const bf16x8 b = im2col_frag(su, (r * GR + sx + x) * 3, off);
+      f32x4 acc[2][4];
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, fr[cb][fl], z4, 0, 0, 0);
+      for (int sg = 0; sg < 2; ++sg) {
+        const bf16x8 b = im2col_frag(su, (r * GR + 16 * sg + x) * 3, off);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+          acc[sg][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, fr[cb][fl], z4, 0, 0, 0);
       }
-      float gox[K];
-      f32x4 go4[K];  // g_o of pixels 4q .. 4q+3 of the segment (0 outside the image)
+      const bool kv = x < K;
+      uint32_t gw[4];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        gox[k] = gos[k * GT * GT + r * GT + sx + x];
-        go4[k] = ld4v(gos + k * GT * GT + r * GT + sx + 4 * q);
+      for (int sg = 0; sg < 2; ++sg) {
+        const f32x4 gA = ld4v(gos + gk * GT * GT + r * GT + 16 * sg + 4 * q);  // 0 outside the image
+        ab2 += kv ? (gA[0] + gA[1]) + (gA[2] + gA[3]) : 0.f;
+        gw[2 * sg] = kv ? pk_bf16(gA[0], gA[1]) : 0u;
+        gw[2 * sg + 1] = kv ? pk_bf16(gA[2], gA[3]) : 0u;
       }
-      const bf16x8 gb = go_frag<K>(q, gox);
+      const bf16x8 ga = __builtin_bit_cast(bf16x8, (u32x4){gw[0], gw[1], gw[2], gw[3]});
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) sv[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gb, fr[4 + cb][fl], z4, 0, 0, 0);
+      for (int cb = 0; cb < 4; ++cb) {
+        uint32_t ba[4], bm[4], bx[4];
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
+        for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-        for (int hp = 0; hp < 2; ++hp) {
-          const f32x2 h = half2(acc[cb], hp);
-          const f32x2 xh = pkfma(h, (f32x2){kI[cb], kI[cb]}, (f32x2){kO[cb], kO[cb]});
-          const f32x2 pre = pkfma(h, (f32x2){kP[cb], kP[cb]}, (f32x2){kQ[cb], kQ[cb]});
-          const f32x2 act = (f32x2){fmaxf(pre.x, 0.f), fmaxf(pre.y, 0.f)};
-          const f32x2 gbn = relu_sel(pre, half2(sv[cb], hp));
-          pgb[cb] += gbn;
-          pgx[cb] = pkfma(gbn, xh, pgx[cb]);
-#pragma unroll
-          for (int k = 0; k < K; ++k) pw2[k][cb] = pkfma(half2(go4[k], hp), act, pw2[k][cb]);
-        }
-#pragma unroll
-      for (int k = 0; k < K; ++k) ab2[k] += (x == 0) ? (go4[k][0] + go4[k][1]) + (go4[k][2] + go4[k][3]) : 0.f;
+          for (int hp = 0; hp < 2; ++hp) {
+            const f32x2 h = half2(acc[sg][cb], hp);
+            const f32x2 xh = pkfma(h, (f32x2){kI[cb], kI[cb]}, (f32x2){kO[cb], kO[cb]});
+            const f32x2 pre = pkfma(h, (f32x2){kP[cb], kP[cb]}, (f32x2){kQ[cb], kQ[cb]});
+            // relu on the rounded pair; a half is nonzero iff pre > 0 (a positive fp32 rounds to a
+            // positive bf16: the exponent ranges agree), so the mask comes from it in 16-bit integer ops
+            const uint32_t act = __builtin_bit_cast(
+                uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, pk_bf16(pre.x, pre.y)), (s16x2){0, 0}));
+            const uint32_t mw = pk_nonzero_mask(act);
+            ba[2 * sg + hp] = act;
+            bm[2 * sg + hp] = mw & 0x3F803F80u;  // bf16 1.0 where pre > 0
+            bx[2 * sg + hp] = pk_bf16(xh.x, xh.y) & mw;
+          }
+        accA[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, __builtin_bit_cast(bf16x8, (u32x4){ba[0], ba[1], ba[2], ba[3]}),
+                                                           accA[cb], 0, 0, 0);
+        accM[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, __builtin_bit_cast(bf16x8, (u32x4){bm[0], bm[1], bm[2], bm[3]}),
+                                                           accM[cb], 0, 0, 0);
+        accN[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, __builtin_bit_cast(bf16x8, (u32x4){bx[0], bx[1], bx[2], bx[3]}),
+                                                           accN[cb], 0, 0, 0);
+      }
     }
   }
+  // lanes q == 0 hold class k = e of accX[cb][e] for channel 16cb + x
   float sgb[4], sgx[4], sw2[K][4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) {
-    sgb[cb] = pgb[cb].x + pgb[cb].y;
-    sgx[cb] = pgx[cb].x + pgx[cb].y;
+    sgb[cb] = sgx[cb] = 0.f;
 #pragma unroll
-    for (int k = 0; k < K; ++k) sw2[k][cb] = pw2[k][cb].x + pw2[k][cb].y;
+    for (int k = 0; k < K; ++k) {
+      const float w2b = (float)(__bf16)a.w2[k * MID + 16 * cb + x];  // the s GEMM's bf16 W2
+      sgb[cb] = fmaf(w2b, accM[cb][k], sgb[cb]);
+      sgx[cb] = fmaf(w2b, accN[cb][k], sgx[cb]);
+      sw2[k][cb] = accA[cb][k];
+    }
   }
-  auto qsum = [](float v) {
-    v += __shfl_xor(v, 16, 64);
-    return v + __shfl_xor(v, 32, 64);
-  };
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    sgb[cb] = qsum(sgb[cb]);
-    sgx[cb] = qsum(sgx[cb]);
-#pragma unroll
-    for (int k = 0; k < K; ++k) sw2[k][cb] = qsum(sw2[k][cb]);
-  }
-#pragma unroll
-  for (int k = 0; k < K; ++k) ab2[k] = qsum(ab2[k]);
+  ab2 += __shfl_xor(ab2, 16, 64);
+  ab2 += __shfl_xor(ab2, 32, 64);
   for (int w = 0; w < 4; ++w) {
     __syncthreads();
     if (wv == w && q == 0) {
@@ -1270,9 +1291,7 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
         red[K * MID + c] += sgb[cb];
         red[(K + 1) * MID + c] += sgx[cb];
       }
-      if (x == 0)
-#pragma unroll
-        for (int k = 0; k < K; ++k) red[(K + 2) * MID + k] += ab2[k];
+      if (x < K) red[(K + 2) * MID + x] += ab2;
     }
   }
   __syncthreads();
