@@ -71,7 +71,7 @@ class Trainer:
         self.graph_cache = 4
         self._graphs = {}  # key -> StepGraph, least recently used first
         self._graph = None  # the graph of the last replayed step
-        self._graph_warm = 0
+        self._graph_warm = {}  # engine knobs + dtype (key[5]) -> eager warm-up steps run with them
         self.graph_captures = 0
 
     # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
@@ -138,10 +138,12 @@ class Trainer:
         key = StepGraph.key(self, images, masks)
         g = self._graphs.pop(key, None)
         if g is None:
-            if self._graph_warm < self.graph_warmup:
+            warm = self._graph_warm.get(key[5], 0)
+            if warm < self.graph_warmup:
                 # eager warm-up steps (real steps): lazy allocations, AdamW state, the loss tables'
-                # host copies, every kernel's first launch happen outside the capture
-                self._graph_warm += 1
+                # host copies, every kernel's first launch happen outside the capture -- again after a
+                # dtype / schedule change (its buffers and kernels are new)
+                self._graph_warm[key[5]] = warm + 1
                 return self._step(images, masks, False)
             self._trim_graphs(max(1, self.graph_cache) - 1)  # free pools before capturing anew
             g = StepGraph(self, images, masks, key)

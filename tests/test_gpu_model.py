@@ -486,6 +486,26 @@ def test_step_graph_replay_is_exact(dtype):
         assert torch.equal(a, b), k
 
 
+def test_step_graph_recaptures_after_set_dtype():
+    """EnhancedUNet.set_dtype between graph-replayed steps: the compute dtype is part of the
+    graph key, so the switch re-captures instead of replaying the bf16 kernels, and the fp32 steps that
+    follow equal an eager trainer's that made the same switch."""
+    from eunet.train_eval import Trainer
+    batches = _graph_batches(7)
+    ta = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb = Trainer(_model(16, 3, 3, "bf16"), DEV, "enhanced_unet", total_epochs=12)
+    tb.step_graph = True
+    for i, (x, m) in enumerate(batches):
+        if i == 4:
+            ta.model.set_dtype("fp32")
+            tb.model.set_dtype("fp32")
+            assert tb.graph_captures == 1
+        assert torch.equal(ta.step(x, m, sync_loss=False), tb.step(x, m, sync_loss=False)), i
+    assert tb.graph_captures == 2 and tb._graph.key[5][-2:] == ("torch.float32", "torch.float32")
+    for (k, p), q in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(p, q), k
+
+
 def test_step_graph_train_epoch_and_bad_targets():
     """train_epoch over a graph-replayed trainer returns the eager epoch's mean loss, and an
     out-of-range target in a replayed batch still raises at the epoch's sync (the loss adds its
