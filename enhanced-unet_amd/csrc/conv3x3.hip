@@ -79,12 +79,34 @@ struct FwdArgs {
 // MFMAs.  The first K-chunk is staged in one global round trip (the accumulators
 // are not live yet), later chunks in halves to bound the staging registers.  Halo
 // units are loaded 8 pixels x 4 quarters per 32 lanes so the LDS writes are
-// conflict-free.  The epilogue stages the tile through LDS and stores whole
+// conflict-free; the plain data gradient stages its halo by LDS-DMA instead (fslot).  The epilogue stages the tile through LDS and stores whole
 // 16-byte vectors.
 constexpr int FTH = 16, FTW = 32;            // output tile
 constexpr int FHW = FTW + 2;                 // 34
 constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
-constexpr int FHPXP = 640;                   // plane stride
+constexpr int FHPXP = 640;                   // halo pixel slots (612 used), 4 channel quarters each
+// LDS slot (16 B) of halo pixel hp's channel quarter q.  Plane-major [q][hp] (PIX = false: the forward
+// and the fused-apply data gradient, register staging) or pixel-major [hp][q] (PIX = true: the plain data
+// gradient, staged by LDS-DMA -- a wave-instruction then reads 16 pixels x 64 contiguous bytes from global;
+// plane-major slots would read 64 pixels x 16 B and measured slower, profiles/r04_ab.txt).  Measured per
+// layout (13 layers, tools/conv_bench.py): the forward loses 2 % pixel-major (4-way bank conflicts of the
+// fragment reads) and 6 % with the quarter XOR-swizzle that removes them (its per-read address VALU), the
+// DMA-staged data gradient gains 6 % -- so the layout follows the instantiation.
+template <bool PIX>
+__device__ __forceinline__ int fslot(int hp, int q) {
+  return PIX ? hp * 4 + q : q * FHPXP + hp;
+}
+// inverse for slot s: (halo pixel, quarter)
+template <bool PIX>
+__device__ __forceinline__ void fslot_inv(int s, int& hp, int& q) {
+  if (PIX) {
+    hp = s >> 2;
+    q = s & 3;
+  } else {
+    q = s / FHPXP;
+    hp = s - q * FHPXP;
+  }
+}
 constexpr int FT = 256;                      // threads of the forward block
 constexpr int FA_UNITS = 4 * FHPX;           // 2448
 constexpr int FA_BYTES = 4 * FHPXP * 16;     // 40960
@@ -104,9 +126,16 @@ __device__ __forceinline__ void xcd_map(int b, int ntiles, int ncob, int& tile, 
 }
 
 // unit id -> (halo pixel, quarter): 32 consecutive ids = 8 pixels x 4 quarters
+// (pixel-major: unit id IS LDS slot id, so 16 lanes write 256 contiguous bytes and read 4 pixels x 64 B;
+// plane-major: 32 consecutive ids = 8 pixels x 4 quarters)
+template <bool PIX>
 __device__ __forceinline__ void fwd_unit(int id, int& hp, int& q) {
-  hp = (id >> 5) * 8 + (id & 7);
-  q = (id >> 3) & 3;
+  if (PIX) {
+    fslot_inv<true>(id, hp, q);
+  } else {
+    hp = (id >> 5) * 8 + (id & 7);
+    q = (id >> 3) & 3;
+  }
 }
 
 // Halo staging loads go through buffer descriptors (one per sample slice of x, one for the
@@ -117,11 +146,11 @@ __device__ __forceinline__ void fwd_unit(int id, int& hp, int& q) {
 // slice, the dual-branch base-96 dec2.0 input of configs[4], is 2.4 GB).
 constexpr uint32_t FWD_OOB = 0xC0000000u;
 
-template <typename T>
+template <typename T, bool PIX>
 __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x0, int id) {
   constexpr int E = Vec16<T>::N;
   int hp, q;
-  fwd_unit(id, hp, q);
+  fwd_unit<PIX>(id, hp, q);
   const int hy = hp / FHW, hx = hp - hy * FHW;
   const int yy = y0 + hy - 1, xx = x0 + hx - 1;
   const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
@@ -129,7 +158,7 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 }
 
 // The halo quarter (16-byte channel group) of unit id depends only on tid: FT = 256 units per
-// staging iteration shift id by 32 * i, which leaves (id >> 3) & 3 unchanged.  So each thread
+// staging iteration shift id by 256 i, which leaves the quarter unchanged.  So each thread
 // transforms one fixed group of E channels per chunk and loads that group's BN scale / shift
 // once per chunk, with the halo loads (not per unit after its data arrived: a dependent
 // global round trip per unit).
@@ -139,9 +168,6 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 #endif
 #ifndef CONV_BDMA
 #define CONV_BDMA 1
-#endif
-#ifndef CONV_ADMA
-#define CONV_ADMA 0
 #endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
@@ -179,32 +205,15 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   char* const As = smem;
   char* const Bs = smem + FA_BYTES;
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
-  const int sq = (tid >> 3) & 3;  // this thread's halo quarter (fwd_unit), the same for every unit
+  // this thread's halo quarter (fwd_unit), the same for every unit (ids tid + FT i)
+  constexpr bool PIX = DG && !BT && sizeof(T) == 2;  // halo layout / staging (fslot)
+  const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const T*)a.x + (long long)ns * a.H * a.W * a.xct), 0,
       (int)((uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T)), 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.wp, 0, a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T), 0x00020000);
-  // forward without an operand transform (a ".0" conv: its input is already activated): the halo too goes
-  // straight into LDS by buffer_load ... lds, slot-major (wave-instruction i of wave w fills LDS slots
-  // i * FT + 64 w .. +63 = (quarter, halo pixel) slots), so a K-chunk's staging is one asynchronous round
-  // trip with no staging registers; aoff then holds the slots' offsets
-  constexpr bool ADMA_OK = CONV_ADMA && !DG && sizeof(T) == 2;
-  static_assert(!ADMA_OK || A_IT * FT == 4 * FHPXP, "dma_a: whole wave-instructions over the 4 planes");
-  const bool adma = ADMA_OK && a.isc == nullptr;
-#pragma unroll
-  for (int i = 0; i < A_IT; ++i) {
-    if (adma) {
-      const int sl = tid + i * FT, qs = sl / FHPXP, hp = sl - qs * FHPXP;
-      const int hy = hp / FHW, hx = hp - hy * FHW, yy = y0 + hy - 1, xx = x0 + hx - 1;
-      const bool ok = hp < FHPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
-      aoff[i] = ok ? (uint32_t)((yy * a.W + xx) * a.xct + a.xco + qs * E) * (uint32_t)sizeof(T) : FWD_OOB;
-    } else {
-      aoff[i] = fwd_unit_off<T>(a, y0, x0, tid + i * FT);
-    }
-  }
-
   // dgrad: the BN-backward transform (k1 in asc, kq in ash, k2 / k3 below) and its y operand
   constexpr int BE = DG ? E / 4 : 1;
   f32x4 ak2[BE], ak3[BE];
@@ -214,6 +223,14 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr bool BTR = DG && BT && sizeof(T) == 2;
   const bool btr = BTR && a.tcoef != nullptr;
   const uint32_t slice_bytes = (uint32_t)(a.H * a.W * a.xct) * (uint32_t)sizeof(T);
+  // the plain data gradient (no operand transform; the default schedule applies the BN backward in a
+  // separate pass): its halo goes straight into LDS by buffer_load ... lds (wave-instruction i of wave w
+  // fills slots i * FT + 64 w .. +63 = 16 pixels x 4 quarters), so a K-chunk's staging is one
+  // asynchronous round trip with no staging registers
+  static_assert(!PIX || A_IT * FT == 4 * FHPXP, "dma_a: whole wave-instructions over the halo slots");
+  const bool adma = PIX && !btr;
+#pragma unroll
+  for (int i = 0; i < A_IT; ++i) aoff[i] = fwd_unit_off<T, PIX>(a, y0, x0, tid + i * FT);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(btr ? (const T*)a.tyin + (long long)ns * a.H * a.W * a.xct : nullptr), 0, btr ? (int)slice_bytes : 0,
       0x00020000);
@@ -280,7 +297,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
       int hp, qq;
-      fwd_unit(tid + i * FT, hp, qq);
+      fwd_unit<PIX>(tid + i * FT, hp, qq);
       if (hp >= FHPX) continue;
       u32x4 v = ra[i];
       if constexpr (DG) {
@@ -321,7 +338,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           v = __builtin_bit_cast(u32x4, Vec16<T>::pack(f));
         }
       }
-      *(u32x4*)(As + (qq * FHPXP + hp) * 16) = v;
+      *(u32x4*)(As + fslot<PIX>(hp, qq) * 16) = v;
     }
   };
   auto lwrite_b = [&](int i0, int i1) {
@@ -351,7 +368,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       uint32_t off = aoff[i];
-      if (!full && kc * KC + ((tid + i * FT) / FHPXP) * E >= a.cin) off = FWD_OOB;
+      if (!full && kc * KC + (tid & 3) * E >= a.cin) off = FWD_OOB;  // (quarter of slot tid + FT i)
       EUNET_DASSERT(off == FWD_OOB || off + cadd + 16u <= slice_bytes);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + (i * FT + wvs * 64) * 16),
                                                16, off, cadd, 0, 0);
@@ -370,7 +387,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
-          const uint4 fa = *(const uint4*)(As + (q * FHPXP + hp) * 16);
+          const uint4 fa = *(const uint4*)(As + fslot<PIX>(hp, q) * 16);
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
             if constexpr (sizeof(T) == 2) {
@@ -395,7 +412,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
   auto stage_halves = [&](int kc) {
     if (CONV_BDMA) dma_b(kc);
-    if (ADMA_OK && adma) {
+    if (PIX && adma) {
       dma_a(kc);
       return;
     }
@@ -436,14 +453,14 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         const int px = u & (FTW - 1), qq = (u >> 5) & 3, py = u >> 7;
         const int yy = y0 + py, xx = x0 + px;
         const bool ok = yy < a.H && xx < a.W && kc * KC + qq * E < a.cin;
-        const u32x4 v = *(const u32x4*)(As + (qq * FHPXP + (py + 1) * FHW + px + 1) * 16);
+        const u32x4 v = *(const u32x4*)(As + fslot<PIX>((py + 1) * FHW + px + 1, qq) * 16);
         const uint32_t off = ok ? (uint32_t)(((yy * a.W + xx) * a.xct + a.xco + kc * KC + qq * E) * (int)sizeof(T)) : FWD_OOB;
         EUNET_DASSERT(!ok || off + 16u <= slice_bytes);
         __builtin_amdgcn_raw_buffer_store_b128(v, gr, off, 0, 0);
       }
     }
   };
-  if (ADMA_OK && adma) {
+  if (PIX && adma) {
     stage_halves(0);
   } else if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
     if (CONV_BDMA) dma_b(0);
@@ -583,6 +600,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr bool bnb = BNB;
   const int ucol = tid % UPX;
   f32x2 bp1[E / 2], bp2[E / 2];
+  f32x2 km[E / 2], ki[E / 2], ks[E / 2], kh[E / 2];  // BN-backward mean, istd, scale, shift of the unit
 #pragma unroll
   for (int e = 0; e < E / 2; ++e) { bp1[e] = (f32x2){0.f, 0.f}; bp2[e] = (f32x2){0.f, 0.f}; }
   if (bnb && tid < BN) {
@@ -634,6 +652,16 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         }
     }
     __syncthreads();
+    if (BNB && pass == 0) {  // this thread's channel unit is fixed: its BN-backward constants into registers
+#pragma unroll
+      for (int e = 0; e < E / 2; ++e) {
+        const int cc = ucol * E + 2 * e;
+        km[e] = *(const f32x2*)(bprm + cc);
+        ki[e] = *(const f32x2*)(bprm + BN + cc);
+        ks[e] = *(const f32x2*)(bprm + 2 * BN + cc);
+        kh[e] = *(const f32x2*)(bprm + 3 * BN + cc);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
       // unit tid + j NTH = (pixel px, channel unit u): u = tid mod UPX, px = tid / UPX + PXJ j, and since
@@ -664,11 +692,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           else Vec16<T>::unpack(*(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E)), yv);
 #pragma unroll
           for (int e = 0; e < E; e += 2) {  // packed fp32: each element rounded as the scalar ops round it
-            const int cc = ucol * E + e;
             const f32x2 y2 = {yv[e], yv[e + 1]};
-            const f32x2 xh = (y2 - *(const f32x2*)(bprm + cc)) * *(const f32x2*)(bprm + BN + cc);
-            const f32x2 pre = __builtin_elementwise_fma(y2, *(const f32x2*)(bprm + 2 * BN + cc),
-                                                        *(const f32x2*)(bprm + 3 * BN + cc));
+            const f32x2 xh = (y2 - km[e >> 1]) * ki[e >> 1];
+            const f32x2 pre = __builtin_elementwise_fma(y2, ks[e >> 1], kh[e >> 1]);
             const f32x2 gp = {pre.x > 0.f ? gr[e] : 0.f, pre.y > 0.f ? gr[e + 1] : 0.f};
             bp1[e >> 1] += gp;
             bp2[e >> 1] = __builtin_elementwise_fma(gp, xh, bp2[e >> 1]);
@@ -785,6 +811,8 @@ __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initiali
 #endif
 __device__ __forceinline__ int wd_swz(int p) { return WG_SWZ_D ? (p & 3) ^ (((p >> 3) & 1) << 2) : 0; }
 __device__ __forceinline__ int wx_shift(int oc) { return WG_SWZ_X ? (oc & 1) * 4 : 0; }
+// last slot a bnrelu_x group of ni slots per thread reads (octant 7, thread pixel 31)
+constexpr int xo_max_slot(int ni) { return 7 * HPXP + (WG_SWZ_X ? 4 : 0) + 31 + 32 * (ni - 1); }
 
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
 // w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
@@ -842,9 +870,11 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbv[8];  // bias gradient: thread owns channels co0 + 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i
+  // bias gradient: thread owns channels co0 + 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i, as
+  // (even, odd) channel pairs summed in packed fp32
+  f32x2 dbv[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) dbv[e] = 0.f;
+  for (int e = 0; e < 4; ++e) dbv[e] = (f32x2){0.f, 0.f};
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
   // Tile staging by buffer LDS-DMA (buffer_load ... lds) through per-sample descriptors: one 32-bit
@@ -900,8 +930,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     }
   };
   // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t & 7 and
-  // halo pixels (t >> 3) + 32 i (i < 11): its 8 scales / shifts are read once per tile and the
-  // pixel coordinates advance incrementally (32 < 34 columns: at most one row wrap per step).
+  // halo pixels (t >> 3) + 32 i (i < 11): its 8 scales / shifts are read once per tile.
   const int xo = tid & 7;
   auto bnrelu_x = [&](int y0, int x0) {
     if (kc * KCW + xo * 8 >= a.cin) return;
@@ -910,25 +939,35 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
     const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
     char* const plane = smem + (xo * HPXP + wx_shift(xo)) * 16;
-    int hp = tid >> 3, hy = 0, hx = hp;
+    // groups of G slots: all G reads issued before the first write (the reads of padding / past-the-halo
+    // slots are harmless -- they stay inside the stage -- and only valid slots are written back)
+    // NI = 12 >= 11 whole groups: slot 352 + 31 of the last plane still lies inside the stage (in the dY tile)
+    constexpr int G = 4, NI = ((HPX + 31) / 32 + G - 1) / G * G;
+    static_assert((xo_max_slot(NI) + 1) * 16 <= WSTAGE, "bnrelu_x: group reads stay inside the stage");
 #pragma unroll 1
-    for (int i = 0; i < (HPX + 31) / 32; ++i, hp += 32) {
-      const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-      if (hp < HPX && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-        u32x4* q = (u32x4*)(plane + hp * 16);
-        const u32x4 w = *q;
+    for (int i0 = 0; i0 < NI; i0 += G) {  // (unrolled, the groups' registers spill)
+      u32x4 w[G];
+      bool ok[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int hp = (tid >> 3) + 32 * (i0 + j), hy = hp / HW_, hx = hp - hy * HW_;
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        ok[j] = (hp < HPX) & ((uint32_t)yy < (uint32_t)a.H) & ((uint32_t)xx < (uint32_t)a.W);
+        w[j] = *(const u32x4*)(plane + hp * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int hp = (tid >> 3) + 32 * (i0 + j);
         u32x4 o;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // packed fp32 FMA, round to bf16, ReLU on the bf16 pair (sign bit)
-          const f32x2 x = {__uint_as_float(w[d] << 16), __uint_as_float(w[d] & 0xFFFF0000u)};
+          const f32x2 x = {__uint_as_float(w[j][d] << 16), __uint_as_float(w[j][d] & 0xFFFF0000u)};
           const f32x2 r = __builtin_elementwise_fma(x, (f32x2){sc[2 * d], sc[2 * d + 1]}, (f32x2){sh[2 * d], sh[2 * d + 1]});
           const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(r[0], r[1]));
           o[d] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
         }
-        *q = o;
+        if (ok[j]) *(u32x4*)(plane + hp * 16) = o;
       }
-      hx += 32;
-      if (hx >= HW_) { hx -= HW_; ++hy; }
     }
   };
   // tile coordinates advance incrementally (scalar): sample tn, tile row tyi, tile column txi
@@ -964,11 +1003,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       const bf16_t* d = (const bf16_t*)Ds;
 #pragma unroll
       for (int i = 0; i < TH * TW / 32; ++i) {  // independent 16-B reads, no per-read wait
-        float f[8];
         const int px = (tid >> 3) + 32 * i;
-        Vec16<bf16_t>::unpack(*(const uint4*)(d + px * 64 + ((tid & 7) ^ wd_swz(px)) * 8), f);
+        const u32x4 w = *(const u32x4*)(d + px * 64 + ((tid & 7) ^ wd_swz(px)) * 8);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dbv[e] += f[e];
+        for (int e = 0; e < 4; ++e) dbv[e] += (f32x2){__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xFFFF0000u)};
       }
     }
     // dY^T fragments of k-step ks (32 pixels x 4 co tiles); channel unit 2ct + (p4 >> 1) of pixel
@@ -1023,7 +1061,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     float* dbred = (float*)smem;  // [32 pixel groups][64 co], over the finished tile stage
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dbred[(tid >> 3) * 64 + (tid & 7) * 8 + e] = dbv[e];
+    for (int e = 0; e < 8; ++e) dbred[(tid >> 3) * 64 + (tid & 7) * 8 + e] = dbv[e >> 1][e & 1];
     __syncthreads();
     if (tid < 64 && co0 + tid < a.cout) {
       float t = 0.f;

@@ -1323,8 +1323,11 @@ __device__ __forceinline__ float dpp_shr(float v, int n) {  // lane x <- lane x 
   return __builtin_bit_cast(float, n == 1 ? __builtin_amdgcn_update_dpp(0, iv, 0x111, 0xf, 0xf, true)
                                           : __builtin_amdgcn_update_dpp(0, iv, 0x112, 0xf, 0xf, true));
 }
+// resident blocks per CU (K = 3: LDS allows 2).  Measured: 2 blocks / CU for K = 2, with or without the
+// two rows of a pair unrolled, 1125-1141 vs 898-903 us (profiles/r04_ab.txt)
+constexpr int gh_occ(int K) { return K == 3 ? 2 : 3; }
 template <int K>
-__global__ __launch_bounds__(NT, K == 3 ? 2 : 3) void head_gh_mfma_kernel(HeadArgs a) {  // (K = 3: LDS allows 2)
+__global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = MID * K * 9 + MID;
   constexpr int KJ = K * 9;
   __shared__ float su[18 * 18 * 3];
@@ -1782,10 +1785,11 @@ int eunet_head_bwd(const float* z, int n, int h, int w, int k, const float* w1, 
   }
   a.dbeta = gbeta; a.dgamma = ggamma;
   const long long P2 = (long long)n * 4 * h * w;
-  const int gridw = L.grid;
+  // the gh grid: its resident blocks (256 CUs x gh_occ), no second partial round
+  const int gridw = mf ? std::min(L.grid, 256 * gh_occ(k)) : L.grid;
   if (mf) {
     a.part = wsf + L.partw;  // g_h, v, the g_z patches and the W1/b1 partials in one pass
-    HEAD_DISPATCH(head_gh_mfma_kernel, L.grid, NT, 0, s);
+    HEAD_DISPATCH(head_gh_mfma_kernel, gridw, NT, 0, s);
     EUNET_LAUNCH_CHECK("head_gh_mfma");
   } else {
     HEAD_DISPATCH_T(head_bwd_gh_kernel, float, L.grid, NT, 0, s);
