@@ -166,6 +166,24 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 #ifndef CONV_PRIO
 #define CONV_PRIO 1
 #endif
+// Diagnostic build only (tools/conv_stamps.py builds it with -DCONV_STAMP=1): wave 0 of every block
+// of conv3x3_fwd_kernel stamps s_memtime around its phases -- staging (+ its barriers), the MFMA
+// chunks (issue), the epilogue -- and writes per-block sums to g_conv_stamps (read back by
+// eunet_conv_stamps).  The product build has none of it.
+#ifndef CONV_STAMP
+#define CONV_STAMP 0
+#endif
+#if CONV_STAMP
+constexpr int STAMP_BLOCKS = 1 << 16;
+__device__ unsigned long long g_conv_stamps[STAMP_BLOCKS * 5];  // [block][t_start, total, stage, mfma, epilogue]
+__device__ __forceinline__ unsigned long long conv_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
 #ifndef CONV_BDMA
 #define CONV_BDMA 1
 #endif
@@ -460,6 +478,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       }
     }
   };
+#if CONV_STAMP
+  unsigned long long st_t0 = conv_stamp(), st_stage = 0, st_mfma = 0, st_a, st_b;
+  st_a = st_t0;
+#endif
   if (PIX && adma) {
     stage_halves(0);
   } else if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
@@ -478,16 +500,31 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if CONV_STAMP
+  st_b = conv_stamp();
+  st_stage += st_b - st_a;
+#endif
   for (int kc = 0; kc < a.nkc; ++kc) {
     if (kc > 0) {
+#if CONV_STAMP
+      st_a = conv_stamp();
+#endif
       __syncthreads();  // every wave is done reading the stage
       stage_halves(kc);
       __syncthreads();
       if (wgy) store_gy(kc);
+#if CONV_STAMP
+      st_b = conv_stamp();
+      st_stage += st_b - st_a;
+#endif
     }
     if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
     chunk();
     if (CONV_PRIO) __builtin_amdgcn_s_setprio(0);
+#if CONV_STAMP
+    st_a = conv_stamp();
+    st_mfma += st_a - st_b;
+#endif
   }
 
   // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
@@ -735,6 +772,17 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       if (co0 + cc < a.cout) a.bpart[((long long)tile * 2 + which) * a.cout + co0 + cc] = t;
     }
   }
+#if CONV_STAMP
+  const unsigned long long st_e = conv_stamp();
+  if (tid == 0 && blockIdx.x < STAMP_BLOCKS) {
+    unsigned long long* o = g_conv_stamps + (size_t)blockIdx.x * 5;
+    o[0] = st_t0;
+    o[1] = st_e - st_t0;
+    o[2] = st_stage;
+    o[3] = st_mfma;
+    o[4] = st_e - st_a;
+  }
+#endif
 }
 
 
@@ -1516,6 +1564,15 @@ int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsp
   *nsplit = cdiv(ntiles, per_split);
   return EUNET_OK;
 }
+
+#if CONV_STAMP
+int eunet_conv_stamps(void* out, size_t bytes) {  // diagnostic builds only (tools/conv_stamps.py)
+  EUNET_REQUIRE(out && bytes <= sizeof(g_conv_stamps), "conv_stamps: bad args");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_conv_stamps), bytes, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return EUNET_ERR_HIP;
+  return EUNET_OK;
+}
+#endif
 
 int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* in_shift, int in_nstride,
                         const eunet_act* dy, float* dw_part, float* db_part, int nsplit, void* stream) {

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Diagnostic build: conv3x3.hip with -DCONV_STAMP=1 linked with the in-tree objects -> abl/libstamp.so
+# (tools/conv_stamps.py reads its per-block phase stamps).  Never used by the product path.
+set -e
+cd "$(dirname "$0")/../enhanced-unet_amd"
+make -s -j8 >/dev/null
+mkdir -p ../abl
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable -DCONV_STAMP=1 \
+  -c csrc/conv3x3.hip -o ../abl/conv3x3_stamp.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../abl/libstamp.so $(ls build/*.o | grep -v "/conv3x3.o") \
+  ../abl/conv3x3_stamp.o
+echo ../abl/libstamp.so
