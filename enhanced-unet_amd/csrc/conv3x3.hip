@@ -175,7 +175,9 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 #endif
 #if CONV_STAMP
 constexpr int STAMP_BLOCKS = 1 << 16;
-__device__ unsigned long long g_conv_stamps[STAMP_BLOCKS * 5];  // [block][t_start, total, stage, mfma, epilogue]
+constexpr int STAMP_N = 11;  // [t_start, total, stage, mfma, epilogue | epilogue: pre-pass (bias, stats),
+                             //  pass 0 LDS staging + barrier, pass 0 stores, pass 1 staging, pass 1 stores, reduction]
+__device__ unsigned long long g_conv_stamps[STAMP_BLOCKS * STAMP_N];
 __device__ __forceinline__ unsigned long long conv_stamp() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -631,6 +633,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     }
     if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
   }
+#if CONV_STAMP
+  unsigned long long st_ep[6] = {conv_stamp(), 0, 0, 0, 0, 0};
+#endif
   constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
   static_assert(NTH % UPX == 0, "a thread's channel unit must be fixed across store iterations");
   T* yp = (T*)a.y;
@@ -689,6 +694,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         }
     }
     __syncthreads();
+#if CONV_STAMP
+    st_ep[1 + 2 * pass] = conv_stamp();
+#endif
     if (BNB && pass == 0) {  // this thread's channel unit is fixed: its BN-backward constants into registers
 #pragma unroll
       for (int e = 0; e < E / 2; ++e) {
@@ -739,6 +747,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         }
       }
     }
+#if CONV_STAMP
+    st_ep[2 + 2 * pass] = conv_stamp();
+#endif
     if (pass + 1 < NPASS) __syncthreads();
   }
   if (bnb) {  // fixed-order reduction of the per-thread channel sums: the lanes of a wave that share a
@@ -775,12 +786,18 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #if CONV_STAMP
   const unsigned long long st_e = conv_stamp();
   if (tid == 0 && blockIdx.x < STAMP_BLOCKS) {
-    unsigned long long* o = g_conv_stamps + (size_t)blockIdx.x * 5;
+    unsigned long long* o = g_conv_stamps + (size_t)blockIdx.x * STAMP_N;
     o[0] = st_t0;
     o[1] = st_e - st_t0;
     o[2] = st_stage;
     o[3] = st_mfma;
     o[4] = st_e - st_a;
+    o[5] = st_ep[0] - st_a;
+    o[6] = st_ep[1] - st_ep[0];
+    o[7] = st_ep[2] - st_ep[1];
+    o[8] = st_ep[3] - st_ep[2];
+    o[9] = st_ep[4] - st_ep[3];
+    o[10] = st_e - st_ep[4];
   }
 #endif
 }

@@ -1326,6 +1326,22 @@ __device__ __forceinline__ float dpp_shr(float v, int n) {  // lane x <- lane x 
 // resident blocks per CU (K = 3: LDS allows 2).  Measured: 2 blocks / CU for K = 2, with or without the
 // two rows of a pair unrolled, 1125-1141 vs 898-903 us (profiles/r04_ab.txt)
 constexpr int gh_occ(int K) { return K == 3 ? 2 : 3; }
+// Diagnostic build only (-DHEAD_STAMP=1, tools/head_stamps.py): per block of head_gh_mfma_kernel, wave 0's
+// s_memtime sums over its tiles of staging (z / u / g_o, with the barriers), the row phase (h, s, BN
+// backward, v, the W1-gradient MFMAs) and the tail (g_u, x2 upsample adjoint, patch store).
+#ifndef HEAD_STAMP
+#define HEAD_STAMP 0
+#endif
+#if HEAD_STAMP
+__device__ unsigned long long g_head_stamps[1024 * 5];  // [block][total, staging, rows, tail, final reduction]
+__device__ __forceinline__ unsigned long long head_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
 template <int K>
 __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a) {
   constexpr int STRIDE = MID * K * 9 + MID;
@@ -1402,6 +1418,10 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
   float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
   zload(a, blockIdx.x, zv);
   goload<K>(a, blockIdx.x, gv);
+#if HEAD_STAMP
+  const unsigned long long hs0 = head_stamp();
+  unsigned long long hs_a = hs0, hs_b, hs_stage = 0, hs_rows = 0, hs_tail = 0;
+#endif
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int n, oy0, ox0;
     tile_coords(a, tile, n, oy0, ox0);
@@ -1411,6 +1431,10 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
     goload<K>(a, tile + gridDim.x, gv);
     __syncthreads();
+#if HEAD_STAMP
+    hs_b = head_stamp();
+    hs_stage += hs_b - hs_a;
+#endif
 #pragma unroll 1
     for (int rp = 0; rp < 2; ++rp) {
 #pragma unroll 1
@@ -1492,6 +1516,10 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
       __builtin_amdgcn_wave_barrier();  // (the next rows' gw writes stay behind these reads)
     }
     __syncthreads();  // every wave's v rows are in vt and its Bw reads of su are done
+#if HEAD_STAMP
+    hs_a = head_stamp();
+    hs_rows += hs_a - hs_b;
+#endif
     if (HEAD_ABL & 1) continue;
     // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image;
     // branch-free: out-of-tile taps read a clamped index and add zero
@@ -1561,6 +1589,11 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
 #pragma unroll
       for (int k = 0; k < K; ++k) a.patch[((long long)tile * 100 + tid) * K + k] = pv[k];
     }
+#if HEAD_STAMP
+    hs_b = head_stamp();
+    hs_tail += hs_b - hs_a;
+    hs_a = hs_b;
+#endif
   }
 #pragma unroll
   for (int e = 0; e < 16; ++e) agb1[e] = pgb1[e >> 1][e & 1];
@@ -1590,6 +1623,17 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
   }
   __syncthreads();
   for (int i = tid; i < STRIDE; i += NT) a.part[(long long)blockIdx.x * STRIDE + i] = red[i];
+#if HEAD_STAMP
+  const unsigned long long hs_e = head_stamp();
+  if (tid == 0 && blockIdx.x < 1024) {
+    unsigned long long* o = g_head_stamps + (size_t)blockIdx.x * 5;
+    o[0] = hs_e - hs0;
+    o[1] = hs_stage;
+    o[2] = hs_rows;
+    o[3] = hs_tail;
+    o[4] = hs_e - hs_a;
+  }
+#endif
 }
 
 // g_z[n][y][x][k] = sum of the (at most four) tile patches covering low-res pixel (y, x), in a
@@ -1681,6 +1725,15 @@ extern "C" int eunet_upsample_bwd(const eunet_act* ghi, const eunet_act* glo, vo
   } while (0)
 
 extern "C" {
+
+#if HEAD_STAMP
+int eunet_head_stamps(void* out, size_t bytes) {  // diagnostic builds only (tools/head_stamps.py)
+  EUNET_REQUIRE(out && bytes <= sizeof(g_head_stamps), "head_stamps: bad args");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_head_stamps), bytes, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return EUNET_ERR_HIP;
+  return EUNET_OK;
+}
+#endif
 
 int eunet_head_workspace_bytes(int n, int h, int w, int k, int dtype, size_t* bytes) {
   EUNET_REQUIRE(bytes && n > 0 && h > 0 && w > 0 && k >= 1 && k <= 3, "head_workspace_bytes: bad args");

@@ -1,7 +1,9 @@
 """Phase shares of conv3x3_fwd_kernel blocks from a stamp-instrumented diagnostic build (-DCONV_STAMP=1,
 tools/build_stamp.sh -> abl/libstamp.so): wave 0 of each block records s_memtime around its staging
 (+ barriers), MFMA chunks (issue) and epilogue.  Read the SHARES, not the lengths: the stamps' waits
-forbid some overlap the product kernel has.
+forbid some overlap the product kernel has.  The epilogue is split into its pre-pass (bias, BN
+statistics), the two LDS-staged store passes (staging + barrier, stores + fused reduction) and the
+final cross-wave reduction.
 
     EUNET_LIB=abl/libstamp.so python tools/conv_stamps.py [--only enc1.3]
 
@@ -25,13 +27,18 @@ from conv_bench import layers  # noqa: E402
 from eunet import _lib, ops  # noqa: E402
 
 
+NST = 11  # conv3x3.hip STAMP_N
+EPI = ("pre", "p0_stage", "p0_store", "p1_stage", "p1_store", "reduce")
+
+
 def read_stamps(nblocks):
-    buf = np.zeros(nblocks * 5, dtype=np.uint64)
+    buf = np.zeros(nblocks * NST, dtype=np.uint64)
     lib = _lib.load()
     rc = lib.eunet_conv_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_size_t(buf.nbytes))
     if rc:
         raise SystemExit(f"eunet_conv_stamps rc={rc}: is EUNET_LIB a -DCONV_STAMP=1 build?")
-    return buf.reshape(nblocks, 5).astype(np.float64)
+    st = buf.reshape(nblocks, NST).astype(np.float64)
+    return st[st[:, 1] > 0]  # blocks that wrote their row
 
 
 def report(name, kind, nblocks, fn):
@@ -40,12 +47,14 @@ def report(name, kind, nblocks, fn):
     fn()
     torch.cuda.synchronize()
     st = read_stamps(nblocks)
-    t0, tot, stage, mfma, epi = st.T
+    t0, tot, stage, mfma, epi = st[:, :5].T
     span = (t0 + tot).max() - t0.min()
-    row = {"layer": name, "pass": kind, "blocks": int(nblocks), "cyc_per_block": round(float(tot.mean())),
+    row = {"layer": name, "pass": kind, "blocks": int(len(st)), "cyc_per_block": round(float(tot.mean())),
            "stage": round(float(stage.sum() / tot.sum()), 3), "mfma": round(float(mfma.sum() / tot.sum()), 3),
            "epilogue": round(float(epi.sum() / tot.sum()), 3),
-           "blocks_in_flight_per_cu": round(float(tot.sum() / span / 256), 2), "span_cyc": round(float(span))}
+           "blocks_in_flight_per_cu": round(float(tot.sum() / span / 256), 2)}
+    for i, k in enumerate(EPI):  # the epilogue's parts, as shares of the whole block
+        row["epi_" + k] = round(float(st[:, 5 + i].sum() / tot.sum()), 3)
     print(json.dumps(row), flush=True)
 
 

@@ -12,3 +12,6 @@ timeout -k 10 600 python bench.py --dual --base 96 --size 2048 --batch 2 --steps
   --dice-size 0 --no-dp-world1 --no-fp32-leg > gpurun_out/bench_dual.log 2>&1 || { echo "dual bench failed"; tail -5 gpurun_out/bench_dual.log; exit 1; }
 grep "^{" gpurun_out/bench_dual.log | tail -1 > profiles/r04_bench_dual_cfg5.json
 echo done
+EUNET_LIB=abl/libstamp.so timeout -k 10 300 python tools/conv_stamps.py > gpurun_out/conv_stamps_final.txt 2>&1 || { echo "conv stamps failed"; exit 1; }
+EUNET_LIB=abl/libstamp.so timeout -k 10 200 python tools/head_stamps.py > gpurun_out/head_stamps_final.txt 2>&1 || { echo "head stamps failed"; tail -3 gpurun_out/head_stamps_final.txt; exit 1; }
+grep -h "layer\|kernel" gpurun_out/conv_stamps_final.txt gpurun_out/head_stamps_final.txt | tail -30
