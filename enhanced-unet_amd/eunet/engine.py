@@ -93,6 +93,11 @@ class UNetEngine:
     # this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7
     # alternating pairs on one box (profiles/r02_ab_conv.txt)
     wg3_late = True
+    # wg3_early_last -- except in the trunk's last block (no input gradient, so no conv .0 data gradient
+    # follows to overlap): there conv .3's weight gradient joins the side stream as soon as its dY is
+    # ready and overlaps conv .3's data gradient, instead of running at the step's tail beside the
+    # trunk's last (small-Cin) weight gradient (profiles/r04_step_timeline.txt)
+    wg3_early_last = True
     # fuse_bn_apply -- the apply half of the DoubleConv's second BatchNorm backward (gy = k1 g' + k2
     # y + k3) inside conv .3's data-gradient operand staging (eunet_conv3x3_dgrad_fused), which also
     # stores gy for conv .3's weight gradient.  Same values, bit for bit, but measured slower: the
@@ -344,7 +349,8 @@ class UNetEngine:
                 wgrad(p + ".3", ops.act(s["za"]), gyb)
             else:
                 wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
-        if not self.wg3_late:
+        early3 = not self.wg3_late or (self.wg3_early_last and not need_gx)
+        if early3:
             wgrad3()
         wpt = S["wp"].get(p + ".3.weight^T") if S.get("wp") else None
         if wpt is None:
@@ -361,7 +367,7 @@ class UNetEngine:
             ev = torch.cuda.Event()
             ev.record(main)  # gyb, gya and the BN-parameter gradients are complete
             gx = dgrad0(gya)
-        if self.wg3_late:
+        if not early3:
             if s.get("za") is not None:
                 wgrad(p + ".3", ops.act(s["za"]), gyb, ready=ev)
             else:
@@ -424,7 +430,8 @@ class UNetEngine:
                 wgrad(p + ".3", ops.act(s["za"]), gyb)
             else:
                 wgrad(p + ".3", ops.act(ya), gyb, bna["scale"], bna["shift"])
-        if not self.wg3_late:
+        early3 = not self.wg3_late or (self.wg3_early_last and not need_gx)
+        if early3:
             wgrad3()
         coefa = bn_coef(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
         if self.wg3_late:
