@@ -93,11 +93,11 @@ class UNetEngine:
     # this way the wgrad overlaps conv .0's data gradient instead.  A/B +0.6 % img/s, 6 of 7
     # alternating pairs on one box (profiles/r02_ab_conv.txt)
     wg3_late = True
-    # wg3_early_last -- except in the trunk's last block (no input gradient, so no conv .0 data gradient
-    # follows to overlap): there conv .3's weight gradient joins the side stream as soon as its dY is
-    # ready and overlaps conv .3's data gradient, instead of running at the step's tail beside the
-    # trunk's last (small-Cin) weight gradient (profiles/r04_step_timeline.txt)
-    wg3_early_last = True
+    # wg3_early_last -- in the trunk's last block (no input gradient, so no conv .0 data gradient follows
+    # to overlap), conv .3's weight gradient joins the side stream as soon as its dY is ready instead of
+    # running at the step's tail (profiles/r04_step_timeline.txt).  Measured neutral (173.0-174.7 vs
+    # 173.6-174.2 img/s, three alternating pairs, profiles/r04_ab.txt): off
+    wg3_early_last = False
     # fuse_bn_apply -- the apply half of the DoubleConv's second BatchNorm backward (gy = k1 g' + k2
     # y + k3) inside conv .3's data-gradient operand staging (eunet_conv3x3_dgrad_fused), which also
     # stores gy for conv .3's weight gradient.  Same values, bit for bit, but measured slower: the
