@@ -343,10 +343,27 @@ __global__ __launch_bounds__(FNT) void bn_finalize_kernel(const float* st, int t
     m2 += qb + d * d * (n * nb / nt);
     n = nt;
   };
-  for (int t = tid; t < tiles; t += FNT) {
-    const double nb = (double)cnt[t];
-    if (nb > 0.0)
-      merge(n, mean, m2, nb, (double)st[((long long)t * 2) * C + c] / nb, (double)st[((long long)t * 2 + 1) * C + c]);
+  // the loads of FB tiles are issued before their merges (same merge order, bit-identical).  At 64
+  // channels x 16k tiles the launch (~21 us) is bound by its strided reads on 64 CUs (each wave
+  // load touches 64 lines); a two-launch form over channel-coalesced tile slices measured no faster
+  // per step (the extra launch costs what it saves, profiles/r04_ab.txt)
+  constexpr int FB = 8;
+  for (int t0 = tid; t0 < tiles; t0 += FB * FNT) {
+    float vn[FB], vs[FB], vq[FB];
+#pragma unroll
+    for (int i = 0; i < FB; ++i) {
+      const bool in = t0 + i * FNT < tiles;
+      const long long ti = min(t0 + i * FNT, tiles - 1);  // unconditional loads, then the select
+      const float a = cnt[ti], b = st[(ti * 2) * C + c], q = st[(ti * 2 + 1) * C + c];
+      vn[i] = in ? a : 0.f;
+      vs[i] = in ? b : 0.f;
+      vq[i] = in ? q : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < FB; ++i) {
+      const double nb = (double)vn[i];
+      if (nb > 0.0) merge(n, mean, m2, nb, (double)vs[i] / nb, (double)vq[i]);
+    }
   }
   shn[tid] = n; shm[tid] = mean; shq[tid] = m2;
   __syncthreads();
@@ -668,8 +685,20 @@ __global__ __launch_bounds__(NT) void colsum_stage1(const float* part, int rows,
   const int col = blockIdx.x * 64 + cl;
   const int r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
   double s = 0.0;
-  if (col < cols)
-    for (int r = r0 + rg; r < r1; r += 4) s += (double)part[(long long)r * ld + col];
+  if (col < cols) {
+    // 8 loads in flight per thread, added in the same row order as one at a time
+    // (+0.0 for the rows past the chunk: s starts at +0.0 and never becomes -0.0, so adding it is exact)
+    for (int r = r0 + rg; r < r1; r += 32) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {  // unconditional loads (clamped row), then the select
+        const float x = part[(long long)min(r + 4 * i, r1 - 1) * ld + col];
+        v[i] = r + 4 * i < r1 ? x : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += (double)v[i];
+    }
+  }
   sh[rg][cl] = s;
   __syncthreads();
   if (rg == 0 && col < cols) ws[(long long)blockIdx.y * cols + col] = sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl];
@@ -680,8 +709,18 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
   const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int col = blockIdx.x * 64 + cl;
   double s = 0.0;
-  if (col < cols)
-    for (int r = rg; r < rb; r += 4) s += ws[(long long)r * cols + col];
+  if (col < cols) {
+    for (int r = rg; r < rb; r += 32) {
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double x = ws[(long long)min(r + 4 * i, rb - 1) * cols + col];
+        v[i] = r + 4 * i < rb ? x : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
+    }
+  }
   sh[rg][cl] = s;
   __syncthreads();
   if (rg == 0 && col < cols) {
@@ -1353,7 +1392,10 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, 
 int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit, "conv_small_wgrad_splits: bad args");
   const int ntiles = dy->n * cdiv(dy->h, STH) * cdiv(dy->w, STW);
-  int s = cdiv(512, cdiv(dy->c, 64));
+#ifndef SMALL_WG_BLOCKS
+#define SMALL_WG_BLOCKS 512  // 768 / 1024 measured slower (enc1.0: 213 -> 283 / 309 us)
+#endif
+  int s = cdiv(SMALL_WG_BLOCKS, cdiv(dy->c, 64));
   s = s > ntiles ? ntiles : (s < 1 ? 1 : s);
   const int per = cdiv(ntiles, s);
   *nsplit = cdiv(ntiles, per);

@@ -836,17 +836,43 @@ __global__ void pack_kernel(const float* w, int cout, int cin, int flip, T* wp, 
   if (id < (long long)cin_p * cout_p * 9) pack_elem<T>(w, cout, cin, flip, wp, cout_p, cin_p, id);
 }
 
-// every weight tensor of a step packed in one launch: blockIdx.y = tensor
+// every weight tensor of a step packed in one launch: the blocks of tensor i are
+// [bstart[i], bstart[i + 1]) of a flat grid (no idle blocks for the small tensors), a thread
+// writes one 16-byte unit of E consecutive GEMM input channels (same values as pack_elem)
 struct PackBatch {
   eunet_pack_desc d[EUNET_PACK_MAX];
   int cout_p[EUNET_PACK_MAX], cin_p[EUNET_PACK_MAX];
+  int bstart[EUNET_PACK_MAX + 1];
+  int n;
 };
 template <typename T>
-__global__ void pack_many_kernel(PackBatch b) {
-  const eunet_pack_desc& d = b.d[blockIdx.y];
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id < (long long)b.cin_p[blockIdx.y] * b.cout_p[blockIdx.y] * 9)
-    pack_elem<T>(d.w, d.cout, d.cin, d.flip, (T*)d.wp, b.cout_p[blockIdx.y], b.cin_p[blockIdx.y], id);
+__global__ __launch_bounds__(256) void pack_many_kernel(PackBatch b) {
+  constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
+  const int bid = blockIdx.x;
+  int k = 0;
+  for (int i = 1; i < b.n; ++i) k = bid >= b.bstart[i] ? i : k;  // block-uniform
+  const eunet_pack_desc& d = b.d[k];
+  const int cout_p = b.cout_p[k];
+  const long long u = (long long)(bid - b.bstart[k]) * 256 + threadIdx.x;  // 16-byte unit
+  if (u >= (long long)b.cin_p[k] * cout_p * 9 / E) return;
+  long long r = u;
+  const int t = (int)(r % 9); r /= 9;
+  const int o = (int)(r % cout_p); r /= cout_p;
+  const int qq = (int)(r % 4);
+  const int kc = (int)(r / 4);
+  const int i0 = kc * KC + qq * E;
+  float v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = i0 + e;
+    v[e] = 0.f;
+    if (!d.flip) {
+      if (o < d.cout && i < d.cin) v[e] = d.w[((long long)o * d.cin + i) * 9 + t];
+    } else if (o < d.cin && i < d.cout) {
+      v[e] = d.w[((long long)i * d.cin + o) * 9 + (8 - t)];
+    }
+  }
+  *(uint4*)((T*)d.wp + u * E) = Vec16<T>::pack(v);
 }
 
 // ---------------------------------------------------------------------------
@@ -1395,19 +1421,24 @@ int eunet_conv3x3_pack(const float* w, int cout, int cin, int flip, void* wp, in
 int eunet_conv3x3_pack_many(const eunet_pack_desc* descs, int n, int dtype, void* stream) {
   EUNET_REQUIRE(descs && n > 0 && n <= EUNET_PACK_MAX, "conv3x3_pack_many: 1..%d tensors", EUNET_PACK_MAX);
   PackBatch b;
-  long long most = 0;
+  const int E = dtype == EUNET_BF16 ? 8 : 4;
+  long long blocks = 0;
   for (int i = 0; i < n; ++i) {
     const eunet_pack_desc& d = descs[i];
     EUNET_REQUIRE(d.w && d.wp && d.cout > 0 && d.cin > 0, "conv3x3_pack_many: bad descriptor %d", i);
+    EUNET_REQUIRE(((uintptr_t)d.wp & 15) == 0, "conv3x3_pack_many: packed operand %d not 16-byte aligned", i);
     b.d[i] = d;
     const int go = d.flip ? d.cin : d.cout, gi = d.flip ? d.cout : d.cin;
     b.cout_p[i] = cdiv(go, BN) * BN;
-    b.cin_p[i] = cdiv(gi, kchunk(dtype)) * kchunk(dtype);
-    most = std::max(most, (long long)b.cout_p[i] * b.cin_p[i] * 9);
+    b.cin_p[i] = cdiv(gi, kchunk(dtype)) * kchunk(dtype);  // a multiple of 4 E
+    b.bstart[i] = (int)blocks;
+    blocks += ((long long)b.cout_p[i] * b.cin_p[i] * 9 / E + 255) / 256;
   }
-  dim3 grid((unsigned)((most + 255) / 256), (unsigned)n);
-  if (dtype == EUNET_BF16) pack_many_kernel<bf16_t><<<grid, 256, 0, (hipStream_t)stream>>>(b);
-  else pack_many_kernel<float><<<grid, 256, 0, (hipStream_t)stream>>>(b);
+  EUNET_REQUIRE(blocks < (1ll << 31), "conv3x3_pack_many: too large");
+  b.bstart[n] = (int)blocks;
+  b.n = n;
+  if (dtype == EUNET_BF16) pack_many_kernel<bf16_t><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(b);
+  else pack_many_kernel<float><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(b);
   EUNET_LAUNCH_CHECK("conv3x3_pack_many");
   return EUNET_OK;
 }

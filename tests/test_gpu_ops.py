@@ -1011,3 +1011,22 @@ def test_conv3x3_dgrad_bf16_fp32_output():
     assert torch.equal(gf.to(torch.bfloat16), gb)
     ref = nhwc(F.conv_transpose2d(nchw(dy.double().cpu()), w.to(torch.bfloat16).double().cpu(), padding=1))
     assert rel(gf, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_pack_many_matches_pack(dt):
+    """eunet_conv3x3_pack_many (flat block map, 16-byte units) writes exactly what the one-tensor
+    pack writes, padding included, for ragged channel counts and both operand roles, across more
+    tensors than one launch holds."""
+    ops = _ops()
+    torch.manual_seed(5)
+    shapes = [(64, 1), (64, 3), (5, 7), (96, 130), (512, 256), (33, 64), (2, 17), (128, 192)]
+    items = [(torch.randn(co, ci, 3, 3, device=DEV), flip) for co, ci in shapes for flip in (False, True)]
+    items = items * 3  # 48 > EUNET_PACK_MAX: two launches
+    many = ops.conv3x3_pack_many(items, dt)
+    for (w, flip), got in zip(items, many):
+        ref = ops.conv3x3_pack(w, dt, flip=flip)
+        assert got.shape == ref.shape
+        assert torch.equal(got.view(torch.int16 if dt == torch.bfloat16 else torch.int32),
+                           ref.view(torch.int16 if dt == torch.bfloat16 else torch.int32)), (w.shape, flip)
+
