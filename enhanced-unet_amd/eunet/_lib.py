@@ -38,6 +38,12 @@ class LossParams(ctypes.Structure):
                 ("focal_norm", c_int)]
 
 
+class OptTensor(ctypes.Structure):
+    """eunet_opt_tensor (include/eunet.h): one parameter's data / grad / AdamW state / step counter."""
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("step", c_void_p), ("numel", ctypes.c_longlong)]
+
+
 _P = POINTER(Act)
 _f = c_void_p  # float* / void* device pointers are passed as integers
 
@@ -59,6 +65,9 @@ SIGNATURES = {
     "eunet_conv_small_wgrad_splits": [_P, POINTER(c_int)],
     "eunet_conv_small_wgrad": [_P, _P, _f, _f, c_int, c_void_p],
     "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_opt_table": [c_void_p, c_int, c_void_p, POINTER(c_int)],
+    "eunet_clip_adamw": [c_void_p, c_int, c_int, c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                         ctypes.c_double, ctypes.c_double, _f, _f, _f, c_void_p],
     "eunet_bn_eval_affine": [c_int, _f, _f, _f, _f, c_float, _f, _f, c_void_p],
     "eunet_bnrelu": [_P, _f, _f, _P, c_void_p],
     "eunet_bnrelu_pool": [_P, _f, _f, _P, _P, c_void_p],

@@ -13,7 +13,8 @@ Differences that are implementation, not semantics:
     kernel (per-sample sums are kept per sample);
   * the 2H->H bilinear resize of the logits (train_eval.py:306-310) is fused
     into the network tail as the exact 2x2 mean it is;
-  * clip_grad_norm_ / AdamW stay PyTorch (foreach/fused kernels).
+  * clip_grad_norm_ + AdamW run as one native step (eunet.optim.ClipAdamW) on torch's AdamW state;
+    Trainer.native_clip_adamw = False restores torch's clip + fused AdamW.
 """
 from __future__ import annotations
 
@@ -62,6 +63,10 @@ class Trainer:
         self.warmup_scheduler = torch.optim.lr_scheduler.LinearLR(
             self.optimizer, start_factor=0.001, end_factor=1.0, total_iters=self.warmup_epochs)
         self.dp = None  # eunet.dp.DataParallel when training on several GPUs
+        # clip_grad_norm_ + AdamW as one native step (eunet.optim.ClipAdamW, csrc/optim.hip) when the
+        # optimizer allows it (CUDA fp32 parameters, one group); False: torch's clip + fused AdamW
+        self.native_clip_adamw = True
+        self._clip_adamw = None
         # step_graph: replay deferred-loss steps from captured HIP graphs (StepGraph) once
         # graph_warmup eager steps have run; one graph per batch shape (a ragged last batch keeps
         # its own), at most graph_cache of them, re-captured when the engine schedule, the loss
@@ -161,16 +166,33 @@ class Trainer:
                 self._graph = None
             del old
 
+    def _native_opt(self) -> bool:
+        from . import optim
+        if not self.native_clip_adamw or not optim.supported(self.optimizer):
+            return False
+        if self._clip_adamw is None or self._clip_adamw.optimizer is not self.optimizer:
+            self._clip_adamw = optim.ClipAdamW(self.optimizer)
+        return True
+
+    def _optimizer_step(self):
+        """train_eval.py:341-343's clip_grad_norm_(max_norm=1.0) + optimizer.step(): the clip runs
+        here (fused with AdamW) on the native path, in _forward_backward otherwise."""
+        if self._native_opt():
+            self._clip_adamw.step(1.0)
+        else:
+            self.optimizer.step()
+
     def _step(self, images, masks, sync_loss):
         loss = self._forward_backward(images, masks, sync_loss)
-        self.optimizer.step()
+        self._optimizer_step()
         if not sync_loss:
             return loss.detach()
         return loss.item()
 
     def _forward_backward(self, images, masks, sync_loss):
-        """zero_grad, forward, loss, backward, DP all-reduce, clip_grad_norm_ (train_eval.py:244-345
-        up to the optimizer step); a StepGraph captures exactly this."""
+        """zero_grad, forward, loss, backward, DP all-reduce and -- unless the native optimizer step
+        runs it fused with AdamW -- clip_grad_norm_ (train_eval.py:244-345 up to the optimizer step); a
+        StepGraph captures exactly this."""
         self.model.train()
         _, _, h, w = images.shape
         h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
@@ -198,7 +220,8 @@ class Trainer:
         loss.backward()
         if self.dp is not None:
             self.dp.after_backward()
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1.0, foreach=True)
+        if not self._native_opt():
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=1.0, foreach=True)
         return loss
 
     def train_epoch(self, dataloader):
@@ -237,16 +260,17 @@ ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late",
 
 
 class StepGraph:
-    """A Trainer step's forward, fused loss, backward and clip_grad_norm_ captured as a HIP graph
-    (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch, followed by the eager fused
-    AdamW step: two host calls instead of several hundred launches, so a small tile (the reference's
+    """A Trainer step's forward, fused loss and backward (+ clip_grad_norm_ on the torch optimizer
+    path) captured as a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch,
+    followed by the eager optimizer step (the native clip + AdamW, or torch's fused AdamW): a few host
+    calls instead of several hundred launches, so a small tile (the reference's
     640x480 batch of 2) is no longer bound by Python + ctypes issue and the data loader's host work
     fits beside it.
 
     A replay runs the eager step's kernels in the eager order with the same arguments: the engine
     launches on torch's current stream (the capture stream) and forks / joins its weight-gradient
     side stream with events; the loss adds its out-of-range target count into a persistent device
-    accumulator in place (losses.bad_target_accumulator); clip_grad_norm_ and the BN running
+    accumulator in place (losses.bad_target_accumulator); the gradient norm and the BN running
     statistics never leave the device.  The gradients live in the graph's memory pool: a replay
     points the parameters' .grad at them before AdamW runs.  AdamW stays outside the graph because
     its learning rate is a host double that changes every epoch (a device-tensor LR would be rounded
@@ -262,6 +286,7 @@ class StepGraph:
         self.masks = torch.empty_like(masks)
         _L.bad_target_accumulator(dev)
         self.optimizer = trainer.optimizer
+        self.optimizer_step = trainer._optimizer_step
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: a DataLoader producer thread may launch and allocate on its own stream
         # while this thread captures (the default global mode would invalidate the capture)
@@ -279,7 +304,7 @@ class StepGraph:
         for p, g in zip(self.params, self.grads):
             if p.grad is not g:
                 p.grad = g
-        self.optimizer.step()
+        self.optimizer_step()
         return self.loss.clone()
 
     @staticmethod
@@ -293,7 +318,8 @@ class StepGraph:
             str(getattr(eng, "dtype", None)), str(getattr(trainer.model, "compute_dtype", None)))
         ps = [p for g in trainer.optimizer.param_groups for p in g["params"]]
         store = (id(trainer.optimizer), ps[0].data_ptr(), ps[-1].data_ptr(), len(ps))
-        lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight)
+        lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight,
+                 trainer._native_opt())  # where the clip runs (in the graph or in the native step)
         return (tuple(images.shape), images.dtype, images.device, tuple(masks.shape), masks.dtype, knobs, store,
                 lossp)
 

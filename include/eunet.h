@@ -294,6 +294,21 @@ int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* s
                           const float* w, int k, const float* gz, const eunet_act* gact, float* part,
                           const float* mean, const float* invstd, float* bn_part, void* stream);
 
+/* ---- optimizer tail of the Trainer step (optim.hip; train_eval.py:341-343, AdamW from :120)
+ * clip_grad_norm_(max_norm) + AdamW (decoupled weight decay) over every parameter tensor in three
+ * launches.  One eunet_opt_tensor per parameter: its fp32 data, gradient (scaled in place by the
+ * clip coefficient, as clip_grad_norm_ leaves it), AdamW exp_avg / exp_avg_sq and the fp32 device
+ * step counter torch's fused AdamW keeps (incremented here).  eunet_opt_table writes the nt x 7
+ * int64 host table (copy it to the device) and the launch's block count; partial holds nblocks
+ * doubles; coef (1 float) receives the clip coefficient, total_norm (nullable) the gradient norm. */
+typedef struct {
+  float* param; float* grad; float* exp_avg; float* exp_avg_sq; float* step; long long numel;
+} eunet_opt_tensor;
+int eunet_opt_table(const eunet_opt_tensor* tensors, int nt, int64_t* table, int* nblocks);
+int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float max_norm, double lr, double beta1,
+                     double beta2, double eps, double weight_decay, double* partial, float* coef,
+                     float* total_norm, void* stream);
+
 /* ---- evaluation path (evalpath.hip) ---------------------------------------
  * Semantic metric counts (metrics.py:29-58, calculate_semantic_metrics): pred, gt
  * int64 [n][hw]; counts int64 [n][3 classes][3] = (#pred==c, #gt==c, #both==c),

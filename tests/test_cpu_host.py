@@ -241,3 +241,28 @@ def test_network_ops_registered_with_the_dispatcher():
     assert str(torch.ops.eunet.conv3x3_pack.default._schema).endswith("-> Tensor")
     with pytest.raises(EunetError):
         torch.ops.eunet.bn_bwd_coef(*[torch.zeros(4)] * 6, 16, torch.zeros(16))
+
+
+def test_opt_table_layout_and_supported():
+    """eunet_opt_table (host code of the native clip + AdamW step): one 7-column row per parameter
+    (pointers, numel, first block of 2048 elements), the launch's block count; optim.supported
+    accepts only a one-group AdamW of fp32 CUDA tensors (CPU parameters keep torch's step)."""
+    import ctypes
+    from eunet import _lib, optim
+    ns = [1, 2048, 2049, 70001]
+    rows = [(0x1000 * (k + 1), 0x2000 * (k + 1), 0x3000 * (k + 1), 0x4000 * (k + 1), 0x5000 * (k + 1), n)
+            for k, n in enumerate(ns)]
+    descs = (_lib.OptTensor * len(rows))(*[_lib.OptTensor(*r) for r in rows])
+    table = (ctypes.c_int64 * (7 * len(rows)))()
+    nb = ctypes.c_int()
+    _lib.call("eunet_opt_table", ctypes.cast(descs, ctypes.c_void_p), len(rows), ctypes.cast(table, ctypes.c_void_p),
+              ctypes.byref(nb))
+    b0 = 0
+    for k, r in enumerate(rows):
+        assert list(table[7 * k:7 * k + 6]) == list(r)
+        assert table[7 * k + 6] == b0
+        b0 += -(-r[5] // 2048)
+    assert nb.value == b0 == 1 + 1 + 2 + 35
+    p = torch.nn.Parameter(torch.zeros(3))
+    assert not optim.supported(torch.optim.AdamW([p]))  # CPU parameter
+    assert not optim.supported(torch.optim.SGD([p], lr=0.1))

@@ -1,0 +1,109 @@
+"""Native clip_grad_norm_ + AdamW (eunet.optim.ClipAdamW, csrc/optim.hip) against PyTorch's
+clip_grad_norm_(foreach) + AdamW(fused) -- the reference's train_eval.py:341-343 on the optimizer of
+:120 -- over several steps with learning-rate changes, clipping active and inactive (GPU only)."""
+import copy
+import re
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+SHAPES = [(64, 1, 3, 3), (64,), (3,), (1,), (2049,), (128, 64, 3, 3), (70001,), (2, 64), (512, 256, 3, 3)]
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _pair(seed, lr=4e-3, wd=1e-4):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    base = [torch.randn(s, generator=g) * 0.1 for s in SHAPES]
+    pa = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    pb = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    oa = torch.optim.AdamW(pa, lr=lr, weight_decay=wd, betas=(0.9, 0.999), fused=True)
+    ob = torch.optim.AdamW(pb, lr=lr, weight_decay=wd, betas=(0.9, 0.999), fused=True)
+    return g, pa, pb, oa, ob
+
+
+@pytest.mark.parametrize("gscale", [1.0, 1e-3])  # total norm >> 1 (clipped) / < 1 (coefficient 1)
+def test_clip_adamw_matches_torch(gscale):
+    from eunet.optim import ClipAdamW, supported
+    g, pa, pb, oa, ob = _pair(3)
+    assert supported(ob)
+    native = ClipAdamW(ob)
+    for it, lr in enumerate([4e-3, 4e-3, 1e-3, 2.5e-4]):
+        for o in (oa, ob):
+            o.param_groups[0]["lr"] = lr
+        grads = [torch.randn(p.shape, generator=g) * gscale for p in pa]
+        for p, q, gr in zip(pa, pb, grads):
+            p.grad = gr.to(DEV)
+            q.grad = gr.to(DEV)
+        na = torch.nn.utils.clip_grad_norm_(pa, max_norm=1.0, foreach=True)
+        oa.step()
+        nb = native.step(1.0)
+        torch.cuda.synchronize()
+        assert rel(nb, na) < 1e-6, it
+        for p, q in zip(pa, pb):
+            assert rel(q.grad, p.grad) < 1e-6, (it, p.shape)  # p.grad left clipped
+            assert rel(q, p) < 1e-6, (it, p.shape)
+            sa, sb = oa.state[p], ob.state[q]
+            assert float(sa["step"]) == float(sb["step"]) == it + 1
+            assert sb["step"].dtype == torch.float32 and sb["step"].is_cuda
+            assert rel(sb["exp_avg"], sa["exp_avg"]) < 1e-6, (it, p.shape)
+            assert rel(sb["exp_avg_sq"], sa["exp_avg_sq"]) < 1e-6, (it, p.shape)
+    # torch's own step continues from the native state (same layout), and state_dict round-trips
+    ob.load_state_dict(copy.deepcopy(oa.state_dict()))  # (shallow: the two would share state tensors)
+    for p, q in zip(pa, pb):
+        gr = torch.randn(p.shape, generator=g).to(DEV)
+        p.grad, q.grad = gr.clone(), gr.clone()
+    oa.step()
+    ob.step()
+    for p, q in zip(pa, pb):
+        assert rel(q, p) < 1e-6
+
+
+def test_clip_adamw_skips_parameters_without_grad():
+    from eunet.optim import ClipAdamW
+    g, pa, pb, oa, ob = _pair(4)
+    native = ClipAdamW(ob)
+    for p, q in zip(pa, pb):
+        if p.dim() == 1 and p.numel() < 10:
+            continue  # no gradient: torch skips the parameter (no state, no update)
+        gr = torch.randn(p.shape, generator=g).to(DEV)
+        p.grad, q.grad = gr.clone(), gr.clone()
+    na = torch.nn.utils.clip_grad_norm_([p for p in pa if p.grad is not None], max_norm=1.0, foreach=True)
+    oa.step()
+    nb = native.step(1.0)
+    assert rel(nb, na) < 1e-6
+    for p, q in zip(pa, pb):
+        assert (q in ob.state) == (p in oa.state)
+        assert rel(q, p) < 1e-6
+
+
+def test_trainer_native_step_matches_torch_path():
+    """Trainer.step with the native optimizer step vs Trainer.native_clip_adamw = False (torch's
+    clip_grad_norm_ + fused AdamW), same seeded model and batches: parameters after 3 steps."""
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    torch.manual_seed(0)
+    x = torch.rand(2, 1, 64, 64, device=DEV)
+    m = torch.randint(0, 2, (2, 64, 64), device=DEV)
+    out = []
+    for native in (True, False):
+        torch.manual_seed(1)
+        model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16).to(DEV)
+        tr = Trainer(model, DEV, "enhanced_unet", total_epochs=50)
+        tr.native_clip_adamw = native
+        tr.epoch_lr_step(0)
+        for _ in range(3):
+            tr.step(x, m, sync_loss=False)
+        assert tr._native_opt() == native
+        out.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+    for k in out[0]:
+        # the biases of the convs feeding a BatchNorm get gradients of rounding noise (BN removes
+        # them), which AdamW normalises to +-lr steps of arbitrary sign: not comparable
+        if out[0][k].is_floating_point() and not re.search(r"\.[03]\.bias$", k):
+            assert rel(out[0][k], out[1][k]) < 1e-4, k
