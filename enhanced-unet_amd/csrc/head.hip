@@ -127,6 +127,13 @@ __device__ __forceinline__ float g_out(const HeadArgs& a, int K, int n, int k, i
   if (a.glog) return 0.25f * a.glog[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)];
   return a.gout2h[(((long long)n * K + k) * (2 * a.h) + oy) * (2 * a.w) + ox];
 }
+// the same without the 2x2-mean factor (g_scale): a prefetching caller's bounds-checked load then
+// has no dependent instruction in its branch, so it does not wait there for the load
+__device__ __forceinline__ float g_raw(const HeadArgs& a, int K, int n, int k, int oy, int ox) {
+  if (a.glog) return a.glog[(((long long)n * K + k) * a.h + (oy >> 1)) * a.w + (ox >> 1)];
+  return a.gout2h[(((long long)n * K + k) * (2 * a.h) + oy) * (2 * a.w) + ox];
+}
+__device__ __forceinline__ float g_scale(const HeadArgs& a) { return a.glog ? 0.25f : 1.f; }
 
 // Thread mapping: 8 lanes per pixel, lane group g = lane & 7 owns channels 8g..8g+7;
 // a 256-thread block covers 32 pixels per pass, 8 passes per 16x16 tile.
@@ -647,16 +654,31 @@ __device__ __forceinline__ bf16x8 cfrag(const f32x4 (&v)[4], int ch) {
 }
 
 // A operand of h^T: row c = 16cb + (l&15), k = j = 8q + jj
+// Weight fragments are loaded once per block, all loads first at clamped (valid) indices, an empty asm
+// on the values so the compiler cannot sink each load into the branch of its select (which made every
+// load wait for the previous one: ~50 serialized L2 round trips in a block's prologue), then the selects.
+template <int N>
+__device__ __forceinline__ void keep_loads(float (&f)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
+}
+
 template <int K>
 __device__ __forceinline__ void load_a_w1(const float* w1, int lane, bf16x8 (&A)[4]) {
   const int r = lane & 15, q = lane >> 4;
+  float f[32];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int j = 8 * q + jj;
-      A[cb][jj] = (__bf16)(j < K * 9 ? w1[(16 * cb + r) * K * 9 + j] : 0.f);
+      f[8 * cb + jj] = w1[(16 * cb + r) * K * 9 + (j < K * 9 ? j : 0)];
     }
+  keep_loads(f);
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) A[cb][jj] = (__bf16)(8 * q + jj < K * 9 ? f[8 * cb + jj] : 0.f);
 }
 
 // per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner (su row stride RS)
@@ -697,13 +719,19 @@ __device__ __forceinline__ void conv_h_mfma(const float* su, int base, const int
 template <int K>
 __device__ __forceinline__ void load_a_w2t(const float* w2, int lane, bf16x8 (&A)[4]) {
   const int r = lane & 15, q = lane >> 4;
+  float f[32];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const int kk = 8 * q + jj;
-      A[cb][jj] = (__bf16)(kk < K ? w2[kk * MID + 16 * cb + r] : 0.f);
+      f[8 * cb + jj] = w2[(kk < K ? kk : 0) * MID + 16 * cb + r];
     }
+  keep_loads(f);
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) A[cb][jj] = (__bf16)(8 * q + jj < K ? f[8 * cb + jj] : 0.f);
 }
 
 template <int K>
@@ -1059,11 +1087,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
   }
   bf16x8 Ah[4], Ao[2];
   load_a_w1<K>(a.w1, lane, Ah);
+  {
+    float f[16];
 #pragma unroll
-  for (int ch = 0; ch < 2; ++ch)
+    for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj)
-      Ao[ch][jj] = (__bf16)(x < K ? a.w2[x * MID + perm_c(q, ch, jj)] : 0.f);
+      for (int jj = 0; jj < 8; ++jj) f[8 * ch + jj] = a.w2[(x < K ? x : 0) * MID + perm_c(q, ch, jj)];
+    keep_loads(f);
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) Ao[ch][jj] = (__bf16)(x < K ? f[8 * ch + jj] : 0.f);
+  }
   int off[8];
   im2col_offsets<K, GR>(q, off);
   float b2k[K];
@@ -1146,7 +1181,7 @@ __device__ __forceinline__ void goload(const HeadArgs& a, int tile, float (&gv)[
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int p = threadIdx.x, oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
-    gv[j] = (oy < 2 * a.h && ox < 2 * a.w) ? g_out(a, K, n, j, oy, ox) : 0.f;
+    gv[j] = (oy < 2 * a.h && ox < 2 * a.w) ? g_raw(a, K, n, j, oy, ox) : 0.f;  // x g_scale when staged
   }
 }
 
@@ -1194,6 +1229,7 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
   float ab2 = 0.f;  // lanes x < K: sum of g_o of class x over this lane's pixels
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int gk = min(x, K - 1);
+  const float gsc = g_scale(a);
   float zv[Z32<K>::ZI];
   zfetch32<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
@@ -1205,14 +1241,14 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
       const int p = tid + e * NT, oy = oy0 + p / GT, ox = ox0 + p % GT;
       const bool in = oy < H2 && ox < W2;
 #pragma unroll
-      for (int k = 0; k < K; ++k) gv[k][e] = in ? g_out(a, K, n, k, oy, ox) : 0.f;
+      for (int k = 0; k < K; ++k) gv[k][e] = in ? g_raw(a, K, n, k, oy, ox) : 0.f;  // x g_scale when staged
     }
     __syncthreads();  // the previous tile's su / gos reads are done
     stage_u32<K>(a, su, zs, zv, tile, oy0, ox0);
 #pragma unroll
     for (int e = 0; e < GO; ++e)
 #pragma unroll
-      for (int k = 0; k < K; ++k) gos[k * GT * GT + tid + e * NT] = gv[k][e];
+      for (int k = 0; k < K; ++k) gos[k * GT * GT + tid + e * NT] = gv[k][e] * gsc;
     __syncthreads();
 #pragma unroll 1
     for (int rr = 0; rr < GT / 4; ++rr) {  // row r: two 16-pixel segments, whose 8 pixels per lane fill the sums' k
@@ -1377,17 +1413,29 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     load_a_w2t<K>(a.w2, lane, A4);
 #pragma unroll
     for (int f = 0; f < 4; ++f) fr[4 + f][lane] = A4[f];
+    float f[NJB * 16];
 #pragma unroll
-    for (int jb = 0; jb < NJB; ++jb)
+    for (int jb = 0; jb < NJB; ++jb) {
+      const int cmb = 4 * jb + (x >> 2), kx = x & 3;  // A row x -> C row 4 (x >> 2) + kx
+      const int j = (cmb < 3 * K && kx < 3) ? (cmb / 3) * 9 + (cmb % 3) * 3 + kx : KJ;
+#pragma unroll
+      for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) f[16 * jb + 8 * ch + jj] = a.w1[perm_c(q, ch, jj) * KJ + (j < KJ ? j : 0)];
+    }
+    keep_loads(f);
+#pragma unroll
+    for (int jb = 0; jb < NJB; ++jb) {
+      const int cmb = 4 * jb + (x >> 2), kx = x & 3;
+      const bool jv = cmb < 3 * K && kx < 3;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
         bf16x8 v;
-        const int cmb = 4 * jb + (x >> 2), kx = x & 3;  // A row x -> C row 4 (x >> 2) + kx
-        const int j = (cmb < 3 * K && kx < 3) ? (cmb / 3) * 9 + (cmb % 3) * 3 + kx : KJ;
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) v[jj] = (__bf16)(j < KJ ? a.w1[perm_c(q, ch, jj) * KJ + j] : 0.f);
+        for (int jj = 0; jj < 8; ++jj) v[jj] = (__bf16)(jv ? f[16 * jb + 8 * ch + jj] : 0.f);
         fr[8 + 2 * jb + ch][lane] = v;
       }
+    }
   }
   int off[8];
   im2col_offsets<K>(q, off);
@@ -1416,6 +1464,7 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
   bf16_t* gw = gsw[wv];
   const int q4 = x >> 2, p4 = x & 3;
   float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
+  const float gsc = g_scale(a);
   zload(a, blockIdx.x, zv);
   goload<K>(a, blockIdx.x, gv);
 #if HEAD_STAMP
@@ -1427,7 +1476,7 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     tile_coords(a, tile, n, oy0, ox0);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k];
+    for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k] * gsc;
     stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
     goload<K>(a, tile + gridDim.x, gv);
     __syncthreads();
@@ -1647,22 +1696,30 @@ __global__ __launch_bounds__(256) void head_patch_gather_kernel(const float* pat
   const int x = (int)(id % w);
   const int y = (int)((id / w) % h);
   const int n = (int)(id / ((long long)w * h));
+  // the <= 4 covering patches' values, all 9 candidates loaded first (invalid ones from the buffer
+  // start), then added in the fixed (dy, dx) order; +0.0 for a non-covering candidate leaves every
+  // bit of the sum as skipping it did (the sum starts at +0.0 and never becomes -0.0)
+  float v[9 * K];
+  bool ok[9];
+#pragma unroll
+  for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int i = 3 * (dy + 1) + dx + 1;
+      const int tr = y / 8 + dy, py = y - 8 * tr + 1, tc = x / 8 + dx, px = x - 8 * tc + 1;
+      ok[i] = tr >= 0 && tr < ty && py >= 0 && py < 10 && tc >= 0 && tc < tx && px >= 0 && px < 10;
+      const float* pp = ok[i] ? patch + ((((long long)n * ty + tr) * tx + tc) * 100 + py * 10 + px) * K : patch;
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[i * K + k] = pp[k];
+    }
+  keep_loads(v);
   float acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0.f;
 #pragma unroll
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int tr = y / 8 + dy, py = y - 8 * tr + 1;
-    if (tr < 0 || tr >= ty || py < 0 || py >= 10) continue;
+  for (int i = 0; i < 9; ++i)
 #pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int tc = x / 8 + dx, px = x - 8 * tc + 1;
-      if (tc < 0 || tc >= tx || px < 0 || px >= 10) continue;
-      const float* pp = patch + ((((long long)n * ty + tr) * tx + tc) * 100 + py * 10 + px) * K;
-#pragma unroll
-      for (int k = 0; k < K; ++k) acc[k] += pp[k];
-    }
-  }
+    for (int k = 0; k < K; ++k) acc[k] += ok[i] ? v[i * K + k] : 0.f;
 #pragma unroll
   for (int k = 0; k < K; ++k) gz[id * K + k] = acc[k];
 }
