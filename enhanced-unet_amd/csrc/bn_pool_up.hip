@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   // (one exposed global round trip per block instead of one per tile).
   constexpr int XI = ((STH + 2) * (STW + 2) * SCI + NT - 1) / NT, DI = STH * STW * 64 / E / NT;
   static_assert(STH * STW * 64 / E % NT == 0, "dY units per thread");
-  float rx[XI];
+  T rx[XI];  // raw: a conversion inside the bounds branch would make each prefetch load wait there
   uint4 rd[DI];
   auto load_tile = [&](int tile) {
     const int n = tile / tpi, trem = tile - n * tpi;
@@ -213,8 +213,8 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       const int hy = hp / (STW + 2), hx = hp - hy * (STW + 2);
       const int yy = y0 + hy - 1, xx = x0 + hx - 1;
       rx[k] = (i < (STH + 2) * (STW + 2) * cin && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-                  ? Elem<T>::ld((const T*)a.x + ((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci)
-                  : 0.f;
+                  ? ((const T*)a.x)[((long long)(n * a.H + yy) * a.W + xx) * a.xct + a.xco + ci]
+                  : T(0);
     }
 #pragma unroll
     for (int k = 0; k < DI; ++k) {
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       const int i = tid + k * NT;
       if (i < (STH + 2) * (STW + 2) * cin) {
         const int hp = i / cin, ci = i - hp * cin;
-        xs[hp * SCI + ci] = rx[k];
+        xs[hp * SCI + ci] = Elem<T>::ld(&rx[k]);
       }
     }
 #pragma unroll

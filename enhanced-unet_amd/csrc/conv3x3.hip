@@ -862,16 +862,18 @@ __global__ __launch_bounds__(256) void pack_many_kernel(PackBatch b) {
   const int kc = (int)(r / 4);
   const int i0 = kc * KC + qq * E;
   float v[E];
+  bool ok[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E; ++e) {  // every load first (index 0 for padding), then the selects
     const int i = i0 + e;
-    v[e] = 0.f;
-    if (!d.flip) {
-      if (o < d.cout && i < d.cin) v[e] = d.w[((long long)o * d.cin + i) * 9 + t];
-    } else if (o < d.cin && i < d.cout) {
-      v[e] = d.w[((long long)i * d.cin + o) * 9 + (8 - t)];
-    }
+    ok[e] = d.flip ? (o < d.cin && i < d.cout) : (o < d.cout && i < d.cin);
+    const long long src = !ok[e] ? 0 : d.flip ? ((long long)i * d.cin + o) * 9 + (8 - t) : ((long long)o * d.cin + i) * 9 + t;
+    v[e] = d.w[src];
   }
+#pragma unroll
+  for (int e = 0; e < E; ++e) asm volatile("" : "+v"(v[e]));
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = ok[e] ? v[e] : 0.f;
   *(uint4*)((T*)d.wp + u * E) = Vec16<T>::pack(v);
 }
 
