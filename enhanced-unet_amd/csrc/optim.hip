@@ -27,7 +27,13 @@ struct OptRow {
   float* p; float* g; float* m; float* v; float* step; long long n; long long b0;
 };
 
-__device__ __forceinline__ OptRow opt_row(const long long* tab, int nt, int blk) {
+// the gradients' pointers as a kernel argument (they move between steps; the table's other columns
+// do not, so the device table is built once per parameter storage and no copy runs per step)
+struct GradPtrs {
+  float* g[EUNET_OPT_KARG_MAX];
+};
+
+__device__ __forceinline__ OptRow opt_row(const long long* tab, int nt, int blk, const GradPtrs& gp) {
   int lo = 0, hi = nt - 1;  // last row whose first block <= blk (block-uniform)
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -35,13 +41,15 @@ __device__ __forceinline__ OptRow opt_row(const long long* tab, int nt, int blk)
     else hi = mid - 1;
   }
   const long long* r = tab + lo * OPT_COLS;
-  return {(float*)r[0], (float*)r[1], (float*)r[2], (float*)r[3], (float*)r[4], r[5], r[6]};
+  float* g = nt <= EUNET_OPT_KARG_MAX ? gp.g[lo] : (float*)r[1];
+  return {(float*)r[0], g, (float*)r[2], (float*)r[3], (float*)r[4], r[5], r[6]};
 }
 
-__global__ __launch_bounds__(OPT_NT) void opt_sumsq_kernel(const long long* tab, int nt, double* partial) {
+__global__ __launch_bounds__(OPT_NT) void opt_sumsq_kernel(const long long* tab, int nt, double* partial,
+                                                           GradPtrs gp) {
   __shared__ double red[OPT_NT / 64];
   const int tid = threadIdx.x, blk = blockIdx.x;
-  const OptRow r = opt_row(tab, nt, blk);
+  const OptRow r = opt_row(tab, nt, blk, gp);
   const long long e0 = (blk - r.b0) * (long long)OPT_EPB + tid;
   float v[OPT_EPT];
 #pragma unroll
@@ -84,9 +92,9 @@ __global__ __launch_bounds__(1024) void opt_norm_kernel(const double* partial, i
 }
 
 __global__ __launch_bounds__(OPT_NT) void opt_adamw_kernel(const long long* tab, int nt, const float* coefp, double lr,
-                                                           double b1, double b2, double eps, double wd) {
+                                                           double b1, double b2, double eps, double wd, GradPtrs gp) {
   const int tid = threadIdx.x, blk = blockIdx.x;
-  const OptRow r = opt_row(tab, nt, blk);
+  const OptRow r = opt_row(tab, nt, blk, gp);
   const long long e0 = (blk - r.b0) * (long long)OPT_EPB + tid;
   const float coef = *coefp;
   const float step = *r.step;  // already incremented by opt_sumsq
@@ -96,18 +104,18 @@ __global__ __launch_bounds__(OPT_NT) void opt_adamw_kernel(const long long* tab,
   const float bc1 = (float)(1.0 - pow(b1, (double)step));
   const float bc2s = (float)sqrt(1.0 - pow(b2, (double)step));
   const float step_size = (float)(lr / (double)bc1);
-  float gp[OPT_EPT], pp[OPT_EPT], mp[OPT_EPT], vp[OPT_EPT];
+  float gv[OPT_EPT], pp[OPT_EPT], mp[OPT_EPT], vp[OPT_EPT];
 #pragma unroll
   for (int j = 0; j < OPT_EPT; ++j) {
     const long long e = e0 + (long long)j * OPT_NT;
     const long long ec = e < r.n ? e : r.n - 1;
-    gp[j] = r.g[ec]; pp[j] = r.p[ec]; mp[j] = r.m[ec]; vp[j] = r.v[ec];
+    gv[j] = r.g[ec]; pp[j] = r.p[ec]; mp[j] = r.m[ec]; vp[j] = r.v[ec];
   }
 #pragma unroll
   for (int j = 0; j < OPT_EPT; ++j) {
     const long long e = e0 + (long long)j * OPT_NT;
     if (e >= r.n) continue;
-    const float g = gp[j] * coef;
+    const float g = gv[j] * coef;
     float p = (float)((double)pp[j] - lr * wd * (double)pp[j]);
     const float m = (float)(b1 * (double)mp[j] + (1.0 - b1) * (double)g);
     const float v = (float)(b2 * (double)vp[j] + (1.0 - b2) * (double)g * (double)g);
@@ -137,14 +145,26 @@ int eunet_opt_table(const eunet_opt_tensor* ts, int nt, int64_t* table, int* nbl
   return EUNET_OK;
 }
 
-int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float max_norm, double lr, double beta1, double beta2,
-                     double eps, double weight_decay, double* partial, float* coef, float* total_norm, void* stream) {
+int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float* const* grads, float max_norm, double lr,
+                     double beta1, double beta2, double eps, double weight_decay, double* partial, float* coef,
+                     float* total_norm, void* stream) {
   EUNET_REQUIRE(table && nt > 0 && nblocks > 0 && partial && coef, "clip_adamw: bad args");
+  GradPtrs gp = {};
+  if (grads != nullptr) {
+    EUNET_REQUIRE(nt <= EUNET_OPT_KARG_MAX, "clip_adamw: > %d gradient pointers: leave grads null", EUNET_OPT_KARG_MAX);
+    for (int k = 0; k < nt; ++k) {
+      EUNET_REQUIRE(grads[k], "clip_adamw: null gradient %d", k);
+      gp.g[k] = grads[k];
+    }
+  } else {
+    EUNET_REQUIRE(nt > EUNET_OPT_KARG_MAX, "clip_adamw: pass the gradient pointers (grads) for <= %d tensors",
+                  EUNET_OPT_KARG_MAX);
+  }
   hipStream_t s = (hipStream_t)stream;
-  opt_sumsq_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, partial);
+  opt_sumsq_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, partial, gp);
   opt_norm_kernel<<<1, 1024, 0, s>>>(partial, nblocks, max_norm, coef, total_norm);
   opt_adamw_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, coef, lr, beta1, beta2, eps,
-                                              weight_decay);
+                                              weight_decay, gp);
   EUNET_LAUNCH_CHECK("clip_adamw");
   return EUNET_OK;
 }

@@ -66,8 +66,8 @@ SIGNATURES = {
     "eunet_conv_small_wgrad": [_P, _P, _f, _f, c_int, c_void_p],
     "eunet_bn_finalize": [_f, c_int, c_int, _f, _f, c_float, c_float, _f, _f, _f, _f, _f, _f, _f, c_void_p],
     "eunet_opt_table": [c_void_p, c_int, c_void_p, POINTER(c_int)],
-    "eunet_clip_adamw": [c_void_p, c_int, c_int, c_float, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                         ctypes.c_double, ctypes.c_double, _f, _f, _f, c_void_p],
+    "eunet_clip_adamw": [c_void_p, c_int, c_int, c_void_p, c_float, ctypes.c_double, ctypes.c_double,
+                         ctypes.c_double, ctypes.c_double, ctypes.c_double, _f, _f, _f, c_void_p],
     "eunet_bn_eval_affine": [c_int, _f, _f, _f, _f, c_float, _f, _f, c_void_p],
     "eunet_bnrelu": [_P, _f, _f, _P, c_void_p],
     "eunet_bnrelu_pool": [_P, _f, _f, _P, _P, c_void_p],

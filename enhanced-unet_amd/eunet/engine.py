@@ -534,10 +534,9 @@ class UNetEngine:
             red2 = (bpart, tiles)
         else:
             ops.conv1x1_bwd(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part)
-        red = _e(K * b + K, torch.float32, dev)
-        ops.colsum(part, tiles, K * b + K, red)
-        sink.slot(pre + "dec1.weight", (K, b, 1, 1)).copy_(red[:K * b].view(K, b, 1, 1))
-        sink.slot(pre + "dec1.bias", (K,)).copy_(red[K * b:])
+        # the column sums go straight into the two gradient slots (colsum's split output)
+        ops.colsum(part, tiles, K * b + K, sink.slot(pre + "dec1.weight", (K, b, 1, 1)), split=K * b,
+                   out_hi=sink.slot(pre + "dec1.bias", (K,)))
         sink.ready([pre + "dec1.weight", pre + "dec1.bias"])
         # ---- decoder
         g_cat2 = self._block_bwd("dec2", gd2, S, P, sink, need_gx=True, small=False, gred=red2)

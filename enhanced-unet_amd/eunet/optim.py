@@ -18,6 +18,8 @@ import torch
 from . import _lib
 from ._lib import call
 
+KARG_MAX = 256  # EUNET_OPT_KARG_MAX
+
 
 def supported(optimizer) -> bool:
     """One AdamW parameter group of contiguous fp32 CUDA tensors, no amsgrad / maximize."""
@@ -37,9 +39,7 @@ class ClipAdamW:
         if not supported(optimizer):
             raise ValueError("ClipAdamW: needs one AdamW param group of contiguous fp32 CUDA tensors")
         self.optimizer = optimizer
-        self._key = None
-        self._table = None
-        self._nblocks = 0
+        self._tables = {}  # key -> (device table, nblocks), most recently used last
 
     def _state(self, p):
         st = self.optimizer.state[p]
@@ -55,28 +55,35 @@ class ClipAdamW:
         if not ps:
             return torch.zeros((), device=g["params"][0].device)
         dev = ps[0].device
-        rows = []
+        rows, grads = [], []
         for p in ps:
             if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                 raise ValueError("ClipAdamW: gradients must be contiguous fp32")
             st = self._state(p)
-            rows.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+            grads.append(p.grad.data_ptr())
+            rows.append((p.data_ptr(), grads[-1], st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                          st["step"].data_ptr(), p.numel()))
-        key = tuple(rows)
-        if key != self._key:  # the caching allocator usually hands the gradients the same storage
+        # the gradients travel as a kernel argument (<= KARG_MAX tensors): the table's key leaves them out
+        karg = len(rows) <= KARG_MAX
+        key = tuple(r[:1] + r[2:] for r in rows) if karg else tuple(rows)
+        hit = self._tables.pop(key, None)
+        if hit is None:  # new gradient storage (the caching allocator cycles through a few sets)
             n = len(rows)
             descs = (_lib.OptTensor * n)(*[_lib.OptTensor(*r) for r in rows])
             host = torch.empty(n * 7, dtype=torch.int64).pin_memory()
             nb = ctypes.c_int()
             call("eunet_opt_table", ctypes.cast(descs, ctypes.c_void_p), n, host.data_ptr(), ctypes.byref(nb))
-            self._table = host.to(dev, non_blocking=True)
-            self._nblocks = nb.value
-            self._key = key
-        partial = torch.empty(self._nblocks, dtype=torch.float64, device=dev)
+            hit = (host.to(dev, non_blocking=True), nb.value)
+            while len(self._tables) >= 4:
+                self._tables.pop(next(iter(self._tables)))
+        self._tables[key] = hit
+        table, nblocks = hit
+        partial = torch.empty(nblocks, dtype=torch.float64, device=dev)
         coef = torch.empty(1, dtype=torch.float32, device=dev)
         norm = torch.empty((), dtype=torch.float32, device=dev)
         b1, b2 = g["betas"]
-        call("eunet_clip_adamw", self._table.data_ptr(), len(rows), self._nblocks, float(max_norm), float(g["lr"]),
+        gptr = (ctypes.c_void_p * len(grads))(*grads) if karg else None
+        call("eunet_clip_adamw", table.data_ptr(), len(rows), nblocks, gptr, float(max_norm), float(g["lr"]),
              float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), partial.data_ptr(), coef.data_ptr(),
              norm.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
         return norm

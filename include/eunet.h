@@ -305,9 +305,13 @@ typedef struct {
   float* param; float* grad; float* exp_avg; float* exp_avg_sq; float* step; long long numel;
 } eunet_opt_tensor;
 int eunet_opt_table(const eunet_opt_tensor* tensors, int nt, int64_t* table, int* nblocks);
-int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float max_norm, double lr, double beta1,
-                     double beta2, double eps, double weight_decay, double* partial, float* coef,
-                     float* total_norm, void* stream);
+/* grads: host array of the nt gradient pointers (nt <= EUNET_OPT_KARG_MAX; they travel as a kernel
+ * argument, so a table built once serves steps whose gradients move), or null for larger nt (the
+ * table's grad column is used) */
+#define EUNET_OPT_KARG_MAX 256
+int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float* const* grads, float max_norm,
+                     double lr, double beta1, double beta2, double eps, double weight_decay,
+                     double* partial, float* coef, float* total_norm, void* stream);
 
 /* ---- evaluation path (evalpath.hip) ---------------------------------------
  * Semantic metric counts (metrics.py:29-58, calculate_semantic_metrics): pred, gt
