@@ -987,7 +987,10 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
 // store that may alias it would wait for the store).
 constexpr int UP_R = 8;
 template <typename T, typename TO, bool RED = false>
-__global__ __launch_bounds__(256) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
+#ifndef UP_WAVES
+#define UP_WAVES 1  // waves per SIMD the register allocation must allow (1: the kernel's own demand)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES))) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
                                                           int h, int w, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E, H2 = 2 * h, W2 = 2 * w, hr = (h + UP_R - 1) / UP_R, wb = (w + 1) / 2;
