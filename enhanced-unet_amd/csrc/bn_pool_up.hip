@@ -988,7 +988,7 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
 constexpr int UP_R = 8;
 template <typename T, typename TO, bool RED = false>
 #ifndef UP_WAVES
-#define UP_WAVES 1  // waves per SIMD the register allocation must allow (1: the kernel's own demand)
+X
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES))) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
                                                           int h, int w, int C, BnRed br) {
