@@ -988,7 +988,9 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
 constexpr int UP_R = 8;
 template <typename T, typename TO, bool RED = false>
 #ifndef UP_WAVES
-X
+// waves per SIMD the register allocation must allow: left alone the fused-reduction bf16 instance takes
+// 258 registers (1 wave / SIMD); at 2 it fits 256 + 12 B of scratch and runs 959 -> 796 us per step
+#define UP_WAVES 2
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES))) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
                                                           int h, int w, int C, BnRed br) {
