@@ -464,7 +464,10 @@ __global__ __launch_bounds__(256) void bnrelu_kernel(const T* y, long long P, in
 // gives the 2x2 outputs 2i+a, 2j+b with PyTorch's weights (0.25/0.75, edge rows
 // weighted 1/0 exactly as upsample_bilinear2d's clamped source index).
 template <typename T>
-__global__ __launch_bounds__(256) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
+#ifndef BNUP_WAVES
+#define BNUP_WAVES 1  // waves per SIMD the allocation must allow (1: its own 136 registers, 3 waves; 4: 497 -> 523 us)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNUP_WAVES))) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
                                                         const float* sc, const float* sh, T* out, int oct, int oco) {
   // two horizontally adjacent low-res pixels (j0, j0 + 1) per thread: 3 x 4 neighbourhood loads
   // and transforms for 2 x 4 outputs each (9 per pixel before); rows are swept one at a time
@@ -875,7 +878,10 @@ struct BnUnit {
 // round(relu(y scale + shift)), recomputed here bit for bit from the y the BN-backward reduction
 // reads anyway, so the argmax (first maximum, NaN wins, as max_pool2d) is the same.
 template <typename T, bool RED = false>
-__global__ __launch_bounds__(NT) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
+#ifndef POOLB_WAVES
+#define POOLB_WAVES 1  // (1: its own 165 registers, 3 waves; 4 spills 80 B: 699 -> 832 us per step)
+#endif
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(POOLB_WAVES))) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
                                                           int gpco, const T* gs, int gsct, int gsco, T* go, int goct,
                                                           int goco, int N, int H, int W, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
