@@ -117,6 +117,13 @@ class UNetEngine:
     # HBM-bound kernels: step time unchanged in a same-box A/B (+0.1 %), the conv family's wall-time
     # fraction 0.369 -> 0.341 (profiles/r03_ab.txt).  Off by default.
     dgrad_first = False
+    # fork_once -- after a DoubleConv's BN-a backward, the side stream's three waits on the launch stream
+    # (conv .3's and conv .0's weight gradients, the bucket hook) share one event recorded there, instead of
+    # one wait_stream each (each record is a marker packet the launch stream's next kernel, conv .0's data
+    # gradient, queues behind: ~21 us per block).  Measured slower: 173.6-174.1 vs 175.5-176.6 img/s in four
+    # alternating pairs (profiles/r04_ab.txt) -- like dgrad_first, a data gradient that reaches the CUs
+    # before the side stream's weight gradients costs the step more than the gap.  Off.
+    fork_once = False
     # keep_state -- tests: the last training forward's saved tensors (pre-BN conv outputs, BN affines)
     # stay reachable as self.last_state, so a checker can read the branch configuration (ReLU masks,
     # max-pool argmax) the kernels took (tests/_pins.py)
@@ -363,10 +370,11 @@ class UNetEngine:
         gya = bn_back(p + ".1", gaa, ya, bna, part=cpart, tiles=ctiles)
         ev = None
         gx = None
-        if side is not None and self.dgrad_first and need_gx:
+        if side is not None and (self.fork_once or (self.dgrad_first and need_gx)):
             ev = torch.cuda.Event()
             ev.record(main)  # gyb, gya and the BN-parameter gradients are complete
-            gx = dgrad0(gya)
+            if self.dgrad_first and need_gx:
+                gx = dgrad0(gya)
         if not early3:
             if s.get("za") is not None:
                 wgrad(p + ".3", ops.act(s["za"]), gyb, ready=ev)

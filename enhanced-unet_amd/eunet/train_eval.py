@@ -256,7 +256,7 @@ class Trainer:
 
 
 ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late", "fuse_bn_apply", "fuse_bn_apply_a",
-                "dgrad_first", "wg3_early_last")
+                "dgrad_first", "wg3_early_last", "fork_once")
 
 
 class StepGraph:

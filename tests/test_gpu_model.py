@@ -450,24 +450,28 @@ def test_fused_bn_apply_schedule_is_exact(dtype, monkeypatch):
 
 @pytest.mark.parametrize("dtype", ["bf16"])
 def test_wgrad_schedule_knobs_are_exact(dtype, monkeypatch):
-    """UNetEngine.wg3_late / wg3_early_last / dgrad_first only move conv .3's weight gradient between
-    the launch and side streams and in issue order: loss and every parameter gradient bit for bit."""
+    """UNetEngine.wg3_late / wg3_early_last / dgrad_first / fork_once only move conv .3's weight gradient
+    between the launch and side streams, change the issue order or the events the side stream waits on:
+    loss and every parameter gradient bit for bit."""
     from eunet import engine, synth
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 96, 64, start_index=17, num_classes=2, in_channels=1)
     out = {}
-    for late, early_last, dfirst in ((True, True, False), (True, False, False), (False, False, False),
-                                     (True, True, True)):
+    for late, early_last, dfirst, fonce in ((True, True, False, True), (True, False, False, True),
+                                            (False, False, False, True), (True, True, True, True),
+                                            (True, False, False, False), (True, False, True, False)):
         monkeypatch.setattr(engine.UNetEngine, "wg3_late", late)
         monkeypatch.setattr(engine.UNetEngine, "wg3_early_last", early_last)
         monkeypatch.setattr(engine.UNetEngine, "dgrad_first", dfirst)
+        monkeypatch.setattr(engine.UNetEngine, "fork_once", fonce)
         m = _model(32, 1, 2, dtype)
         m.train()
         loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
         loss.backward()
         torch.cuda.synchronize()
-        out[(late, early_last, dfirst)] = (loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters()})
-    ref = out[(True, False, False)]
+        out[(late, early_last, dfirst, fonce)] = (loss.item(),
+                                                  {k: p.grad.detach().clone() for k, p in m.named_parameters()})
+    ref = out[(True, False, False, False)]
     for key, (lv, grads) in out.items():
         assert lv == ref[0], key
         for k, g in grads.items():
