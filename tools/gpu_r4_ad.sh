@@ -3,8 +3,8 @@
 # launches) vs abl/libprev.so: ops + model tests, bit identity, kernel trace, alternating bench
 set -u
 export TMPDIR=/tmp
-TAG=ops TLIM=600 bash tools/gpu_run_tests.sh tests/test_gpu_ops.py || exit $?
-TAG=model TLIM=600 bash tools/gpu_run_tests.sh tests/test_gpu_model.py -k "grads or schedule" || exit $?
+EUNET_LIB=abl/libc1.so TAG=ops TLIM=600 bash tools/gpu_run_tests.sh tests/test_gpu_ops.py || exit $?
+EUNET_LIB=abl/libc1.so TAG=model TLIM=600 bash tools/gpu_run_tests.sh tests/test_gpu_model.py -k "grads or schedule" || exit $?
 timeout -k 10 400 python tools/bitcmp.py abl/libprev.so abl/libc1.so || exit $?
 EUNET_LIB=abl/libc1.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ad -o r4ad -- \
   python bench.py --steps 5 --warmup 3 --no-cpu-baseline --dice-size 0 --no-dp-world1 --no-fp32-leg \
