@@ -21,6 +21,11 @@ Also reported on the same JSON line:
   dp_world1     -- the same per-rank workload through eunet.dp.DataParallel on RCCL at world
                    size 1 (BASELINE configs[3] per rank): ms/step and overhead vs the plain step;
   fp32_configs1 -- BASELINE configs[1] (base 64, 512^2, batch 8, fp32) timed in this same run;
+  dual_configs4 -- BASELINE configs[4] per GPU (dual-branch base 96 + deep supervision, 2048^2,
+                   batch 2, bf16) timed in this same run;
+  steps_diag    -- per leg: min / median / max GPU time per step of the timed region (an event per
+                   step boundary) and, from an extra untimed pass, the whole-step kernel-busy time
+                   (union of every library launch's interval on both streams) and the idle rest;
   cpu_baseline  -- the oracle (PyTorch CPU restatement of the reference step) on the host
                    cores, bounded sample (1 warm-up + 3 timed steps), rank 0 at N=1 only;
   parity        -- after the timed region, untimed: a fresh model of the same configuration
@@ -78,6 +83,8 @@ def parse():
     ap.add_argument("--no-dp-world1", action="store_true",
                     help="skip the DataParallel-on-RCCL world-1 leg (N=1 only)")
     ap.add_argument("--no-fp32-leg", action="store_true", help="skip the fp32 BASELINE configs[1] leg (N=1 only)")
+    ap.add_argument("--no-dual-leg", action="store_true",
+                    help="skip the dual-branch BASELINE configs[4] leg (N=1 only)")
     ap.add_argument("--dual", action="store_true",
                     help="dual-branch model + deep supervision (BASELINE configs[4]: --dual --base 96 --size 2048)")
     return ap.parse_args()
@@ -275,12 +282,12 @@ def _config_tag(args):
     return "(custom)"
 
 
-def build_trainer(args, dev, dtype=None, base=None):
+def build_trainer(args, dev, dtype=None, base=None, dual=None):
     from eunet.models import EnhancedUNet
     from eunet.train_eval import Trainer
     torch.manual_seed(0)
     model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=base or args.base, dtype=dtype or args.dtype,
-                         dual_branch=args.dual).to(dev)
+                         dual_branch=args.dual if dual is None else dual).to(dev)
     tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
     tr.epoch_lr_step(0)
     return tr
@@ -295,11 +302,18 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # one event per step boundary on the launch stream (K+1 markers, no per-kernel cost): the
+    # per-step GPU spans expose a one-off stall that the mean alone would hide
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     with kprof.KernelTimer() as timer:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        marks[0].record()
+        host = [time.perf_counter()]
+        for i in range(steps):
             tr.step(x, m, sync_loss=SYNC_LOSS)
+            marks[i + 1].record()
+            host.append(time.perf_counter())
         torch.cuda.synchronize()
         t1 = time.perf_counter()
     if world > 1:
@@ -307,7 +321,42 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    timer.step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(steps)]
+    timer.host_ms = [1e3 * (host[i + 1] - host[i]) for i in range(steps)]
     return float(elapsed.item()), timer
+
+
+def step_spread(timer):
+    """min / median / max of the per-step GPU spans of the timed region (ms), the step index of the max
+    and the host time of that step's issue (Trainer.step call to return: a host-side stall shows there,
+    a GPU-side one only in the span)."""
+    s = sorted(timer.step_ms)
+    if not s:
+        return None
+    i = max(range(len(s)), key=lambda j: timer.step_ms[j])
+    return {"min": round(s[0], 3), "median": round(s[len(s) // 2], 3), "max": round(s[-1], 3), "max_at": i,
+            "host_ms_at_max": round(timer.host_ms[i], 3), "host_ms_max": round(max(timer.host_ms), 3)}
+
+
+def busy_pass(tr, x, m, steps=3):
+    """Whole-step kernel-busy figure from an extra, untimed pass of `steps` steps after the timed region:
+    every launching C-ABI call bracketed by events (kprof.BusyTimer), busy = the union of those intervals
+    over both streams.  idle = instrumented span - busy: host gaps, synchronising calls and PyTorch's own
+    kernels; the events themselves add a little to both."""
+    from eunet import kprof
+    tr.step(x, m, sync_loss=False)
+    torch.cuda.synchronize()
+    with kprof.BusyTimer() as bt:
+        for _ in range(steps):
+            tr.step(x, m, sync_loss=False)
+    busy, span = bt.busy_ms() / steps, bt.span_ms() / steps
+    return {"step_kernel_busy_ms": round(busy, 3), "instrumented_ms_per_step": round(span, 3),
+            "idle_ms_per_step": round(span - busy, 3), "launches_per_step": len(bt.iv) // steps}
+
+
+def step_record(timer, tr, x, m):
+    """The per-leg step diagnostics: per-step spread of the timed region + the busy pass."""
+    return {"step_ms": step_spread(timer), **busy_pass(tr, x, m)}
 
 
 CONV_FAMILIES = (("conv3x3_fwd", "fwd", "conv3x3_fwd_kernel"),
@@ -377,10 +426,11 @@ def conv_roofline(args, timer, steps, step_flops, elapsed, dtype):
     return roof
 
 
-def step_flops_of(args, base, size, batch):
+def step_flops_of(args, base, size, batch, dual=None):
     from oracle.eunet_ref import flops_per_pixel
     from oracle.dual_ref import dual_flops_per_pixel
-    fpp = dual_flops_per_pixel(base, 1, 2) if args.dual else flops_per_pixel(base, 1, 2)
+    dual = args.dual if dual is None else dual
+    fpp = dual_flops_per_pixel(base, 1, 2) if dual else flops_per_pixel(base, 1, 2)
     return fpp * size * size * batch
 
 
@@ -398,14 +448,14 @@ def dp_world1_leg(args, tr, x, m, dev, ms_plain):
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
     try:
         tr.dp = DataParallel(tr.model)
-        el, _ = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
+        el, t = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
         nb = len(tr.dp.buckets)
         tr.dp = None
     finally:
         dist.destroy_process_group()
     ms = 1e3 * el / args.steps
     return {"dp_world1_ms_per_step": round(ms, 3), "overhead_pct": round(100.0 * (ms - ms_plain) / ms_plain, 2),
-            "buckets": nb, "backend": "nccl (RCCL)",
+            "buckets": nb, "backend": "nccl (RCCL)", "step_ms": step_spread(t),
             "note": "same per-rank workload through eunet.dp.DataParallel at world size 1 (bucketed all-reduce "
                     "from inside the HIP backward, BN-buffer broadcast); BASELINE configs[3] per rank"}
 
@@ -418,14 +468,54 @@ def fp32_configs1_leg(args, dev):
     tr = build_trainer(args, dev, dtype="fp32", base=64)
     x, m = synth.batch(batch, size, size, start_index=0, num_classes=2, in_channels=1, device=dev)
     el, timer = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
+    diag = step_record(timer, tr, x, m)
     sf = step_flops_of(args, 64, size, batch)
     a32 = argparse.Namespace(**vars(args))
     a32.size, a32.batch, a32.dtype, a32.base = size, batch, "fp32", 64
     roof = conv_roofline(a32, timer, args.steps, sf, el, "fp32")
     out = {"value": round(batch * args.steps / el, 3), "unit": "img/s", "ms_per_step": round(1e3 * el / args.steps, 3),
            "workload": "base_ch=64, 1x512x512 1-ch->2-cls, batch 8, fp32 (BASELINE configs[1])",
-           "model_tflops": round(sf / (el / args.steps) / 1e12, 2), "roofline": roof}
+           "model_tflops": round(sf / (el / args.steps) / 1e12, 2), "roofline": roof, "steps_diag": diag}
     del tr
+    torch.cuda.empty_cache()
+    return out
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher: start N ranks under torch.distributed.run (one process per
+    GPU, rendezvous on 127.0.0.1) as a child process and return its exit code.  Runs before anything has
+    touched the GPU (torch.cuda.device_count() does not initialise it on this image)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def dual_configs4_leg(args, dev):
+    """BASELINE configs[4] per GPU (dual-branch base 96 + deep supervision, 1x2048^2, batch 2, bf16;
+    models.py:253-333, train_eval.py:199-234) timed in the same invocation: value, ms/step, the conv
+    roofline against the bf16 MFMA peak and the step diagnostics."""
+    from eunet import synth
+    size, batch, base = 2048, 2, 96
+    tr = build_trainer(args, dev, dtype="bf16", base=base, dual=True)
+    x, m = synth.batch(batch, size, size, start_index=0, num_classes=2, in_channels=1, device=dev)
+    el, timer = timed_steps(tr, x, m, args.steps, args.warmup, 1, dev)
+    diag = step_record(timer, tr, x, m)
+    sf = step_flops_of(args, base, size, batch, dual=True)
+    a4 = argparse.Namespace(**vars(args))
+    a4.size, a4.batch, a4.dtype, a4.base, a4.dual = size, batch, "bf16", base, True
+    roof = conv_roofline(a4, timer, args.steps, sf, el, "bf16")
+    roof.pop("encoder_fwd", None)
+    out = {"value": round(batch * args.steps / el, 3), "unit": "img/s", "ms_per_step": round(1e3 * el / args.steps, 3),
+           "workload": "dual-branch + deep supervision, base_ch=96, 1x2048x2048 1-ch->2-cls, batch 2/GPU, bf16 "
+                       "(BASELINE configs[4] per GPU)",
+           "model_tflops": round(sf / (el / args.steps) / 1e12, 2), "roofline": roof, "steps_diag": diag}
+    del tr, x, m
     torch.cuda.empty_cache()
     return out
 
@@ -435,10 +525,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # nccl == RCCL over xGMI; EUNET_DIST_BACKEND=gloo only to rehearse N ranks on one GPU
+    backend = os.environ.get("EUNET_DIST_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    ngpu = torch.cuda.device_count()
+    if ngpu < world and backend != "gloo":
+        sys.exit(f"bench.py: {world} ranks need {world} GPUs, {ngpu} visible")
     if world > 1:
-        # nccl == RCCL over xGMI; EUNET_DIST_BACKEND=gloo only to rehearse N ranks on one GPU
-        dist.init_process_group(os.environ.get("EUNET_DIST_BACKEND", "nccl"), init_method="env://")
-    local = local % max(1, torch.cuda.device_count())
+        dist.init_process_group(backend, init_method="env://")
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    local = local % max(1, ngpu)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -453,6 +553,7 @@ def main():
     x, m = synth.batch(args.batch, args.size, args.size, start_index=rank * args.batch, num_classes=2,
                        in_channels=1, device=dev)
     elapsed, timer = timed_steps(tr, x, m, args.steps, args.warmup, world, dev)
+    diag = step_record(timer, tr, x, m)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -470,6 +571,10 @@ def main():
     if world == 1 and not args.no_fp32_leg and not args.dual and \
             (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16"):
         fp32 = fp32_configs1_leg(args, dev)
+    dual4 = None
+    if world == 1 and not args.no_dual_leg and not args.dual and \
+            (args.base, args.size, args.batch, args.dtype) == (64, 1024, 4, "bf16"):
+        dual4 = dual_configs4_leg(args, dev)
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -483,6 +588,8 @@ def main():
         "value": round(imgs / elapsed, 3),
         "unit": "img/s",
         "n_gpus": world,
+        "world": {"size": dist.get_world_size() if world > 1 else 1,
+                  "backend": backend + (" (RCCL)" if backend == "nccl" else "") if world > 1 else None},
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_plain, 3),
@@ -497,8 +604,10 @@ def main():
                    "global_batch": world * args.batch, "image_size": args.size, "parallelism": f"dp{world}"},
         "model_tflops_per_gpu": round(step_flops / (elapsed / args.steps) / 1e12, 2),
         "roofline": roof,
+        "steps_diag": diag,
         "dp_world1": dpw1,
         "fp32_configs1": fp32,
+        "dual_configs4": dual4,
         "cpu_baseline": cpu,
         "logits_rel_err_vs_cpu": logits_err,
         "dice_vs_cpu_ref": dice,

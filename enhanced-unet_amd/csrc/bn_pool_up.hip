@@ -735,53 +735,6 @@ __global__ __launch_bounds__(NT) void colsum_stage2(const double* ws, int rb, in
   }
 }
 
-// colsum_stage1 + colsum_stage2 in one launch when there are at most 16 row chunks: wave y computes
-// chunk y's four row-group sums exactly as stage 1's four waves do (same rows, same order, the same
-// ((s0 + s1) + s2) + s3), then waves 0-3 add the chunk values as stage 2's row groups do -- the
-// same bits as the two launches, one launch and one dispatch gap fewer
-constexpr int COLSUM_ONE_MAX = 16;
-#ifndef COLSUM_ONE
-#define COLSUM_ONE 0  // off: built at round-4 end, its GPU validation (tools/gpu_r4_ad.sh) still pending
-#endif
-__global__ __launch_bounds__(1024) void colsum_one(const float* part, int rows, int cols, int ld, int chunk, int rb,
-                                                   ColSegs segs) {
-  __shared__ double cw[COLSUM_ONE_MAX][64];
-  __shared__ double sh[4][64];
-  const int cl = threadIdx.x & 63, y = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + cl;
-  if (col < cols && y < rb) {  // (>= 4 waves run: stage 2's four row groups, empty ones giving 0)
-    const int r0 = y * chunk, r1 = min(rows, r0 + chunk);
-    double sg[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg)
-      for (int r = r0 + rg; r < r1; r += 32) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float x = part[(long long)min(r + 4 * i, r1 - 1) * ld + col];
-          v[i] = r + 4 * i < r1 ? x : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) sg[rg] += (double)v[i];
-      }
-    cw[y][cl] = sg[0] + sg[1] + sg[2] + sg[3];
-  }
-  __syncthreads();
-  if (y < 4 && col < cols) {
-    double t = 0.0;
-    for (int r = y; r < rb; r += 4) t += cw[r][cl];
-    sh[y][cl] = t;
-  }
-  __syncthreads();
-  if (y == 0 && col < cols) {
-    const float v = (float)(sh[0][cl] + sh[1][cl] + sh[2][cl] + sh[3][cl]);
-    int i = 0;
-#pragma unroll
-    for (int j = 1; j < 4; ++j) i = (j < segs.n && col >= segs.start[j]) ? j : i;
-    segs.out[i][col - segs.start[i]] = v;
-  }
-}
-
 // gy = gamma istd (g' - dbeta/n - xhat dgamma/n), g' = g [y scale + shift > 0] (the forward's ReLU
 // mask: every BN-backward reduction and this apply use the forward affine, so the sums the apply
 // subtracts are over exactly the g' it applies), folded per channel into gy = K1 g' + y K2 + K3
@@ -1408,12 +1361,8 @@ int eunet_colsum_segs(const float* part, int rows, int cols, int ld, const ColSe
                   "colsum: bad segments");
   const int rb = colsum_rb(rows);
   const int chunk = cdiv(rows, rb);
-  if (COLSUM_ONE && rb <= COLSUM_ONE_MAX) {
-    colsum_one<<<cdiv(cols, 64), 64 * std::max(rb, 4), 0, s>>>(part, rows, cols, ld, chunk, rb, segs);
-  } else {
-    colsum_stage1<<<dim3(cdiv(cols, 64), rb), NT, 0, s>>>(part, rows, cols, ld, chunk, (double*)ws);
-    colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, segs);
-  }
+  colsum_stage1<<<dim3(cdiv(cols, 64), rb), NT, 0, s>>>(part, rows, cols, ld, chunk, (double*)ws);
+  colsum_stage2<<<cdiv(cols, 64), NT, 0, s>>>((const double*)ws, rb, cols, segs);
   EUNET_LAUNCH_CHECK("colsum");
   return EUNET_OK;
 }

@@ -6,7 +6,7 @@
 // the decoded uint8 image and the LabelMe polygons go to the device once and
 // everything per-pixel runs in HIP:
 //   rasterize   LabelMe polygons -> semantic mask (instance order, last wins:
-//               dataset.py:197-201; fill rule documented at the kernel)
+//               dataset.py:197-201) with cv2.fillPoly's rule (documented at the kernel)
 //   flip        cv2.flip of image / mask (dataset.py:208-222)
 //   augment_u8  the reference's numpy pixel ops in its order -- brightness
 //               np.clip(img*alpha,0,255).astype(uint8) (:243), contrast
@@ -31,18 +31,111 @@ unsigned grid1(long long n) {
   return (unsigned)(b > 65535 ? 65535 : (b < 1 ? 1 : b));
 }
 
-// Fill rule: pixel (x, y) (integer lattice, as cv2.fillPoly's int32 vertices) is inside when
-// the even-odd crossing test at (x + 0.5, y + 0.5) says so, or when it lies on an edge of the
-// polygon (cv2 always paints the outline).  pts: int32 (x, y) pairs; poly_off[i]..poly_off[i+1]
-// the vertices of polygon i; labels[i] in {1 live, 2 dead}.
-__device__ __forceinline__ bool on_segment(int x, int y, int x0, int y0, int x1, int y1) {
-  const long long cr = (long long)(x1 - x0) * (y - y0) - (long long)(y1 - y0) * (x - x0);
-  if (cr != 0) return false;
-  return x >= min(x0, x1) && x <= max(x0, x1) && y >= min(y0, y1) && y <= max(y0, y1);
+// Fill rule: cv2.fillPoly(mask, [points], 1) (dataset.py:184-186; LINE_8, shift 0) as OpenCV 4.x
+// computes it (imgproc/src/drawing.cpp, 4.5.2 and later; oracle/data_ref.py fill_poly_u8 restates it):
+//  * every edge (v[k-1], v[k]) is drawn with the 8-connected Line: LineIterator clips the endpoints
+//    (clipLine), starts at the left one and runs Bresenham with err = dx - 2dy over dx + 1 pixels --
+//    in closed form the pixel at major offset i has minor offset ceil((2 dmin i - dmaj) / (2 dmaj));
+//  * the non-horizontal edges are collected in XY_SHIFT = 16 fixed point: x + 1/2 for an edge whose
+//    endpoints are in the image, else the clipped endpoints (exact integers) re-projected to the
+//    unclipped y0, dx = C-truncated (x1 - x0) / (y1 - y0); FillEdgeCollection then fills row y between
+//    consecutive edges of the x-sorted active list (y0 <= y < y1), from x_a >> 16 to x_b >> 16.
+// Per pixel that fill is a count: with a_e = x_e(y) >> 16 of the active edges, pixel x lies in a span
+// iff #{a_e < x} is odd or some a_e == x follows an even count (#{a_e <= x} > #{a_e < x}).  Both
+// rules are exact integer / fixed-point arithmetic; clipLine's double crossings match the CPU's IEEE
+// ops (no contraction across the division).  pts: int32 (x, y) pairs; poly_off[i]..poly_off[i+1] the
+// vertices of polygon i; labels[i] in {1 live, 2 dead}.
+__device__ bool cv_clip_line(int w, int h, long long& x1, long long& y1, long long& x2, long long& y2) {
+  const long long right = w - 1, bottom = h - 1;
+  int c1 = (x1 < 0) + (x1 > right) * 2 + (y1 < 0) * 4 + (y1 > bottom) * 8;
+  int c2 = (x2 < 0) + (x2 > right) * 2 + (y2 < 0) * 4 + (y2 > bottom) * 8;
+  if ((c1 & c2) == 0 && (c1 | c2) != 0) {
+    long long a;
+    if (c1 & 12) {
+      a = c1 < 8 ? 0 : bottom;
+      x1 += (long long)((double)(a - y1) * (double)(x2 - x1) / (double)(y2 - y1));
+      y1 = a;
+      c1 = (x1 < 0) + (x1 > right) * 2;
+    }
+    if (c2 & 12) {
+      a = c2 < 8 ? 0 : bottom;
+      x2 += (long long)((double)(a - y2) * (double)(x2 - x1) / (double)(y2 - y1));
+      y2 = a;
+      c2 = (x2 < 0) + (x2 > right) * 2;
+    }
+    if ((c1 & c2) == 0 && (c1 | c2) != 0) {
+      if (c1) {
+        a = c1 == 1 ? 0 : right;
+        y1 += (long long)((double)(a - x1) * (double)(y2 - y1) / (double)(x2 - x1));
+        x1 = a;
+        c1 = 0;
+      }
+      if (c2) {
+        a = c2 == 1 ? 0 : right;
+        y2 += (long long)((double)(a - x2) * (double)(y2 - y1) / (double)(x2 - x1));
+        x2 = a;
+        c2 = 0;
+      }
+    }
+  }
+  return (c1 | c2) == 0;
 }
 
-// Polygon i can only paint pixels inside its vertex bounding box (the sample point x + 0.5 of an
-// inside pixel lies strictly between the extreme vertices; an edge pixel lies on the segment).
+__device__ bool cv_fillpoly_covers(const int* pts, int b, int e, int x, int y, int h, int w) {
+  bool on = false;
+  int clt = 0, cle = 0;
+  for (int k = b, j = e - 1; k < e; j = k++) {
+    const long long X0 = pts[2 * j], Y0 = pts[2 * j + 1], X1 = pts[2 * k], Y1 = pts[2 * k + 1];
+    const bool inimg = X0 >= 0 && X0 < w && X1 >= 0 && X1 < w && Y0 >= 0 && Y0 < h && Y1 >= 0 && Y1 < h;
+    long long cx0 = X0, cy0 = Y0, cx1 = X1, cy1 = Y1;  // clipLine's copies (Line and the edge)
+    bool vis = true;
+    if (!inimg) vis = cv_clip_line(w, h, cx0, cy0, cx1, cy1);
+    if (vis) {  // Line(img, t0, t1, 1, 8): left endpoint first
+      long long lx1 = cx0, ly1 = cy0, lx2 = cx1, ly2 = cy1;
+      if (lx2 < lx1) {
+        lx1 = cx1; ly1 = cy1; lx2 = cx0; ly2 = cy0;
+      }
+      const long long ddx = lx2 - lx1, ddy = ly2 - ly1, ady = ddy < 0 ? -ddy : ddy;
+      if (ady > ddx) {  // y major
+        const long long i = ddy < 0 ? ly1 - y : y - ly1;
+        if (i >= 0 && i <= ady) on |= x == lx1 + (2 * ddx * i + ady - 1) / (2 * ady);
+      } else {
+        const long long i = x - lx1;
+        if (i >= 0 && i <= ddx) {
+          const long long m = ddx ? (2 * ady * i + ddx - 1) / (2 * ddx) : 0;
+          on |= y == (ddy < 0 ? ly1 - m : ly1 + m);
+        }
+      }
+    }
+    if (Y0 != Y1) {  // CollectPolyEdges' PolyEdge, then its x at row y
+      long long c0x, c0y, c1x, c1y;
+      if (inimg) {
+        c0x = (X0 << 16) + 32768; c0y = Y0; c1x = (X1 << 16) + 32768; c1y = Y1;
+      } else if (cy0 != cy1) {
+        c0x = cx0 << 16; c0y = cy0; c1x = cx1 << 16; c1y = cy1;
+      } else {
+        c0x = X0 << 16; c0y = Y0; c1x = X1 << 16; c1y = Y1;
+      }
+      const long long dx = (c1x - c0x) / (c1y - c0y);  // C division: truncation toward zero
+      long long y0, y1, x0;
+      if (Y0 < Y1) {
+        y0 = Y0; y1 = Y1; x0 = c0x + (Y0 - c0y) * dx;
+      } else {
+        y0 = Y1; y1 = Y0; x0 = c1x + (Y1 - c1y) * dx;
+      }
+      if (y >= y0 && y < y1) {
+        const long long a = (x0 + (y - y0) * dx) >> 16;  // arithmetic shift: floor
+        clt += a < x;
+        cle += a <= x;
+      }
+    }
+  }
+  return on || (clt & 1) || cle > clt;
+}
+
+// Polygon i can only paint pixels inside its vertex bounding box: a Line pixel lies on its (clipped)
+// segment's box, and a filled span runs between edge x values that truncation toward zero keeps
+// within [min x, max x] of the edge's endpoints (x + 1/2 < max x + 1).
 // Both rasterisers cull by it: the work is ~ sum of the polygons' box areas x edges, not
 // pixels x all edges (a 640x480 LabelMe image with 40 cells: 205 -> ~10 us).
 //
@@ -68,21 +161,6 @@ __device__ void chunk_bboxes(const int* pts, const int* poly_off, int p0, int n,
     atomicMax(&bb[lo].z, x);
     atomicMax(&bb[lo].w, y);
   }
-}
-
-// even-odd crossing test at the pixel centre or on an edge (the fill rule above)
-__device__ __forceinline__ bool poly_covers(const int* pts, int b, int e, int x, int y) {
-  const float px = x + 0.5f, py = y + 0.5f;
-  bool in = false, edge = false;
-  for (int k = b, j = e - 1; k < e; j = k++) {
-    const int xi = pts[2 * k], yi = pts[2 * k + 1], xj = pts[2 * j], yj = pts[2 * j + 1];
-    edge |= on_segment(x, y, xj, yj, xi, yi);
-    if ((yi > py) != (yj > py)) {
-      const float xc = (float)(xj - xi) * (py - (float)yi) / (float)(yj - yi) + (float)xi;
-      if (px < xc) in = !in;
-    }
-  }
-  return in || edge;
 }
 
 // semantic mask: one 16x16 pixel tile per block.  Per chunk of polygons the block keeps, in
@@ -126,7 +204,7 @@ __global__ __launch_bounds__(NT) void rasterize_kernel(const int* pts, const int
         const int t = list[j];
         const int4 b = bb[t];
         if (x < b.x || x > b.z || y < b.y || y > b.w) continue;
-        if (poly_covers(pts, offs[t], offs[t + 1], x, y)) v = labels[p0 + t];
+        if (cv_fillpoly_covers(pts, offs[t], offs[t + 1], x, y, h, w)) v = labels[p0 + t];
       }
   }
   if (x < w && y < h) mask[(long long)y * w + x] = v;
@@ -173,7 +251,7 @@ __global__ __launch_bounds__(NT) void rasterize_instances_kernel(const int* pts,
     const int yo = (int)(r / w), xo = (int)(r - (long long)yo * w);
     const int y = flip_v ? h - 1 - yo : yo, x = flip_h ? w - 1 - xo : xo;
     if (x < bx.x || x > bx.z || y < bx.y || y > bx.w) continue;
-    out[j] = poly_covers(pts, b, e, x, y) ? 1 : 0;
+    out[j] = cv_fillpoly_covers(pts, b, e, x, y, h, w) ? 1 : 0;
   }
   uint8_t* dst = masks + (long long)p * hw + r0;
   if (r0 + 4 <= hw && (((uintptr_t)dst) & 3) == 0) {

@@ -15,7 +15,11 @@
 //               p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps), bc_i = 1 - b_i^step
 // HBM: 4 B/elem (sumsq) + 32 B/elem (adamw: p, g, m, v read and written).  The norm is an fp64 sum
 // where torch sums fp32 per-tensor norms, so the coefficient (and through it every update) can
-// differ from torch's in the last fp32 bits; tests hold it to 1e-6 relative.
+// differ from torch's in the last fp32 bits; tests hold it to 1e-6 relative.  Non-finite gradients: a
+// NaN or inf element makes the fp64 sum NaN / inf, the coefficient NaN / 0 as in torch, so every
+// gradient becomes NaN (NaN case) or 0 with NaN at the inf elements (inf case), as torch's clip leaves
+// them.  Finite fp32 gradients whose per-tensor fp32 norm overflows (|g| ~ 1e19 and up) are the one
+// case where the fp64 sum stays finite and the coefficient differs from torch's 0.
 #include "common.h"
 
 namespace {
@@ -86,7 +90,8 @@ __global__ __launch_bounds__(1024) void opt_norm_kernel(const double* partial, i
     for (int i = 0; i < 16; ++i) t += red[i];
     const float total = (float)sqrt(t);
     const float cc = max_norm / (total + 1e-6f);
-    *coef = cc < 1.f ? cc : 1.f;
+    // torch's clamp(max=1) keeps a NaN (a NaN / inf gradient poisons every parameter, as there)
+    *coef = cc != cc ? cc : (cc < 1.f ? cc : 1.f);
     if (norm_out) *norm_out = total;
   }
 }

@@ -193,9 +193,21 @@ def load(path: str = LIB_PATH):
     return lib
 
 
+# kprof.BusyTimer installs itself here: every launching entry point is then bracketed by events on
+# torch's current stream (the stream the C-ABI enqueues on), for the whole-step kernel-busy figure
+BUSY_HOOK = None
+_NO_LAUNCH = ("_tiles", "_bytes", "_splits", "_rows", "_len", "_params", "debug_", "_table", "lab_tables")
+
+
 def call(name: str, *args):
     lib = load()
-    rc = getattr(lib, name)(*args)
+    h = BUSY_HOOK
+    if h is not None and not any(s in name for s in _NO_LAUNCH):
+        e0 = h.begin()
+        rc = getattr(lib, name)(*args)
+        h.end(e0)
+    else:
+        rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.eunet_last_error().decode(errors="replace")
         raise EunetError(f"{name} failed ({rc}): {msg}")

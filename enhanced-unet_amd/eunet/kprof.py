@@ -42,19 +42,63 @@ class KernelTimer:
         event intervals across streams (launches of one family on two streams overlap, so the
         summed spans of summary() count shared time twice)."""
         torch.cuda.synchronize()
-        iv = sorted((self.origin.elapsed_time(a), self.origin.elapsed_time(b))
-                    for fam in families for a, b, _, _ in self.records.get(fam, ()))
-        tot, cur0, cur1 = 0.0, None, None
-        for a, b in iv:
-            if cur1 is None or a > cur1:
-                if cur1 is not None:
-                    tot += cur1 - cur0
-                cur0, cur1 = a, b
-            else:
-                cur1 = max(cur1, b)
-        if cur1 is not None:
-            tot += cur1 - cur0
-        return tot
+        return _union([(self.origin.elapsed_time(a), self.origin.elapsed_time(b))
+                       for fam in families for a, b, _, _ in self.records.get(fam, ())])
+
+
+def _union(iv):
+    tot, cur0, cur1 = 0.0, None, None
+    for a, b in sorted(iv):
+        if cur1 is None or a > cur1:
+            if cur1 is not None:
+                tot += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    if cur1 is not None:
+        tot += cur1 - cur0
+    return tot
+
+
+class BusyTimer:
+    """Every launching C-ABI call (eunet._lib.call) bracketed by events on torch's current stream while
+    active: busy_ms() = the union of all those intervals over both streams, i.e. the time some library
+    kernel ran.  Kernels PyTorch launches itself (a few copies / fills per step) count as idle.  The
+    events cost GPU time of their own, so bench.py runs this in an extra, untimed pass."""
+
+    def __init__(self):
+        self.iv = []
+
+    def __enter__(self):
+        from . import _lib
+        self.origin = torch.cuda.Event(enable_timing=True)
+        self.origin.record()
+        _lib.BUSY_HOOK = self
+        return self
+
+    def __exit__(self, *exc):
+        from . import _lib
+        _lib.BUSY_HOOK = None
+        self.last = torch.cuda.Event(enable_timing=True)
+        self.last.record()
+
+    def begin(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def end(self, e0):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.iv.append((e0, e1))
+
+    def busy_ms(self):
+        torch.cuda.synchronize()
+        return _union([(self.origin.elapsed_time(a), self.origin.elapsed_time(b)) for a, b in self.iv])
+
+    def span_ms(self):
+        torch.cuda.synchronize()
+        return self.origin.elapsed_time(self.last)
 
 
 _OFF = os.environ.get("EUNET_KPROF", "1") == "0"  # diagnostic: measure the event overhead itself

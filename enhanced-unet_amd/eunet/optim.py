@@ -22,11 +22,15 @@ KARG_MAX = 256  # EUNET_OPT_KARG_MAX
 
 
 def supported(optimizer) -> bool:
-    """One AdamW parameter group of contiguous fp32 CUDA tensors, no amsgrad / maximize."""
+    """One fused (or capturable) AdamW parameter group of contiguous fp32 CUDA tensors, no amsgrad /
+    maximize.  A plain foreach AdamW (the reference's optim.AdamW(...), or the Trainer's fallback) keeps
+    its step counters as CPU tensors, which the kernels cannot increment: torch's own step runs there."""
     if type(optimizer) is not torch.optim.AdamW or len(optimizer.param_groups) != 1:
         return False
     g = optimizer.param_groups[0]
     if g.get("amsgrad") or g.get("maximize") or g.get("differentiable"):
+        return False
+    if not (g.get("fused") or g.get("capturable")):
         return False
     return all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in g["params"])
 
@@ -47,6 +51,16 @@ class ClipAdamW:
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            return st
+        # state from torch's own step or load_state_dict: every tensor the kernels read or write must be
+        # contiguous fp32 on the parameter's device (a CPU step counter would be a host address there)
+        if st["step"].device != p.device or st["step"].dtype != torch.float32:
+            st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+        for k in ("exp_avg", "exp_avg_sq"):
+            t = st[k]
+            if t.device != p.device or t.dtype != torch.float32 or not t.is_contiguous() or t.shape != p.shape:
+                raise ValueError(f"ClipAdamW: AdamW state {k!r} must be a contiguous fp32 tensor shaped and "
+                                 f"placed like its parameter")
         return st
 
     def step(self, max_norm: float):

@@ -11,8 +11,14 @@ These are the reference's own numpy expressions, so they pin the HIP kernels exa
   * resize      cv2.resize(image, (w, h), interpolation=cv2.INTER_LINEAR) for uint8 images
                 (dataset.py:151, 158): OpenCV's fixed-point algorithm (imgproc/src/resize.cpp),
                 restated in resize_linear_u8 below -- parity unpinned against cv2 itself (absent).
-The polygon fill is the build's documented rule (even-odd at the pixel centre + every
-lattice pixel on an edge), NOT cv2.fillPoly (absent here): that row is parity-unpinned.
+  * fillPoly    cv2.fillPoly(mask, [points], 1) (dataset.py:184-186, default LINE_8, shift 0):
+                OpenCV 4.x's algorithm (modules/imgproc/src/drawing.cpp of 4.5.2 and later, the
+                versions `opencv-python>=4.5.0` installs today): CollectPolyEdges draws every edge
+                with the 8-connected Bresenham Line (LineIterator, endpoints clipped by clipLine)
+                and collects the non-horizontal edges in XY_SHIFT = 16 fixed point (x + 1/2 for
+                in-image edges; clipped endpoints re-projected), FillEdgeCollection fills each
+                scanline between consecutive active edges of the x-sorted list.  Restated in
+                fill_poly_u8 below -- parity unpinned against cv2 itself (absent).
 """
 from __future__ import annotations
 
@@ -41,25 +47,149 @@ def to_tensor(img):
     return (img.astype(np.float32) / np.float32(255.0)).transpose(2, 0, 1)
 
 
+# ---- cv2.fillPoly, LINE_8, shift 0 (OpenCV 4.x imgproc/src/drawing.cpp) ------------------------------
+XY_SHIFT = 16
+XY_ONE = 1 << XY_SHIFT
+
+
+def _cdiv(a, b):
+    """C++ integer division (truncation toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def clip_line(w, h, p1, p2):
+    """clipLine(Size2l, Point2l&, Point2l&): Cohen-Sutherland against [0, w-1] x [0, h-1], the
+    crossings offset by (int64)(double(a - y) * (x2 - x1) / (y2 - y1)).  Returns (inside, p1, p2)."""
+    (x1, y1), (x2, y2) = p1, p2
+    right, bottom = w - 1, h - 1
+    if w <= 0 or h <= 0:
+        return False, (x1, y1), (x2, y2)
+    c1 = (x1 < 0) + (x1 > right) * 2 + (y1 < 0) * 4 + (y1 > bottom) * 8
+    c2 = (x2 < 0) + (x2 > right) * 2 + (y2 < 0) * 4 + (y2 > bottom) * 8
+    if (c1 & c2) == 0 and (c1 | c2) != 0:
+        if c1 & 12:
+            a = 0 if c1 < 8 else bottom
+            x1 += int(float(a - y1) * (x2 - x1) / (y2 - y1))
+            y1 = a
+            c1 = (x1 < 0) + (x1 > right) * 2
+        if c2 & 12:
+            a = 0 if c2 < 8 else bottom
+            x2 += int(float(a - y2) * (x2 - x1) / (y2 - y1))
+            y2 = a
+            c2 = (x2 < 0) + (x2 > right) * 2
+        if (c1 & c2) == 0 and (c1 | c2) != 0:
+            if c1:
+                a = 0 if c1 == 1 else right
+                y1 += int(float(a - x1) * (y2 - y1) / (x2 - x1))
+                x1 = a
+                c1 = 0
+            if c2:
+                a = 0 if c2 == 1 else right
+                y2 += int(float(a - x2) * (y2 - y1) / (x2 - x1))
+                x2 = a
+                c2 = 0
+    return (c1 | c2) == 0, (x1, y1), (x2, y2)
+
+
+def line8(img, p1, p2, color=1):
+    """Line(img, pt1, pt2, color, 8): LineIterator(img, pt1, pt2, 8, leftToRight=true) -- endpoints
+    clipped to the image, the left endpoint first, Bresenham with err = dx - 2 dy, count = dx + 1."""
+    h, w = img.shape
+    (x1, y1), (x2, y2) = p1, p2
+    if not (0 <= x1 < w and 0 <= x2 < w and 0 <= y1 < h and 0 <= y2 < h):
+        ok, (x1, y1), (x2, y2) = clip_line(w, h, (x1, y1), (x2, y2))
+        if not ok:
+            return
+    dx, dy = x2 - x1, y2 - y1
+    if dx < 0:  # leftToRight: start from the left endpoint
+        dx, dy = -dx, -dy
+        x1, y1, x2, y2 = x2, y2, x1, y1
+    sy = -1 if dy < 0 else 1
+    dy = abs(dy)
+    # (major step, minor step) in (x, y); the steep case swaps the axes
+    if dy > dx:
+        dx, dy = dy, dx
+        major, minor = (0, sy), (1, 0)
+    else:
+        major, minor = (1, 0), (0, sy)
+    err = dx - (dy + dy)
+    plus_delta, minus_delta = dx + dx, -(dy + dy)
+    x, y = x1, y1
+    for _ in range(dx + 1):
+        img[y, x] = color
+        step_minor = err < 0
+        err += minus_delta + (plus_delta if step_minor else 0)
+        x += major[0] + (minor[0] if step_minor else 0)
+        y += major[1] + (minor[1] if step_minor else 0)
+
+
+def collect_poly_edges(img, pts, edges, color=1):
+    """CollectPolyEdges (LINE_8, shift 0, offset 0): draws every edge and appends the non-horizontal
+    ones as [y0, y1, x (XY_SHIFT fixed point at y0), dx per row]."""
+    h, w = img.shape
+    n = len(pts)
+    pt0 = (int(pts[n - 1][0]) << XY_SHIFT, int(pts[n - 1][1]))
+    for i in range(n):
+        pt1 = (int(pts[i][0]) << XY_SHIFT, int(pts[i][1]))
+        t0 = ((pt0[0] + (XY_ONE >> 1)) >> XY_SHIFT, pt0[1])
+        t1 = ((pt1[0] + (XY_ONE >> 1)) >> XY_SHIFT, pt1[1])
+        line8(img, t0, t1, color)
+        p0c, p1c = list(pt0), list(pt1)
+        if not (0 <= t0[0] < w and 0 <= t1[0] < w and 0 <= t0[1] < h and 0 <= t1[1] < h):
+            _, c0, c1 = clip_line(w, h, t0, t1)  # the clipped copies feed the edge even when invisible
+            if c0[1] != c1[1]:
+                p0c = [c0[0] << XY_SHIFT, c0[1]]
+                p1c = [c1[0] << XY_SHIFT, c1[1]]
+        else:
+            p0c[0] += XY_ONE >> 1
+            p1c[0] += XY_ONE >> 1
+        if pt0[1] != pt1[1]:
+            dx = _cdiv(p1c[0] - p0c[0], p1c[1] - p0c[1])
+            if pt0[1] < pt1[1]:
+                edges.append([pt0[1], pt1[1], p0c[0] + (pt0[1] - p0c[1]) * dx, dx])
+            else:
+                edges.append([pt1[1], pt0[1], p1c[0] + (pt1[1] - p1c[1]) * dx, dx])
+        pt0 = pt1
+
+
+def fill_edge_collection(img, edges, color=1):
+    """FillEdgeCollection (LINE_8: delta 0): rows y0_min .. min(y1_max, rows) - 1; per row the active
+    edges (y0 <= y < y1) sorted by x, consecutive pairs filled from (x_a >> 16) to (x_b >> 16), clipped
+    to the image; each edge's x advances by dx per row."""
+    h, w = img.shape
+    if len(edges) < 2:
+        return
+    y_min = min(e[0] for e in edges)
+    y_max = max(e[1] for e in edges)
+    xs = [e[2] for e in edges] + [e[2] + (e[1] - e[0]) * e[3] for e in edges]
+    if y_max < 0 or y_min >= h or max(xs) < 0 or min(xs) >= (w << XY_SHIFT):
+        return
+    for y in range(y_min, min(y_max, h)):
+        act = sorted(e[2] + (y - e[0]) * e[3] for e in edges if e[0] <= y < e[1])
+        if y < 0:
+            continue
+        for a, b in zip(act[0::2], act[1::2]):
+            x1, x2 = a >> XY_SHIFT, b >> XY_SHIFT
+            if x1 < w and x2 >= 0:
+                img[y, max(x1, 0):min(x2, w - 1) + 1] = color
+
+
+def fill_poly_u8(pts, h, w):
+    """cv2.fillPoly(np.zeros((h, w), np.uint8), [pts], 1) for int32 points pts [n, 2] (x, y)."""
+    img = np.zeros((h, w), np.uint8)
+    edges = []
+    collect_poly_edges(img, np.asarray(pts, np.int64), edges)
+    fill_edge_collection(img, edges)
+    return img
+
+
 def rasterize(polys, labels, h, w):
-    yy, xx = np.mgrid[0:h, 0:w]
-    px, py = (xx + 0.5).astype(np.float32), (yy + 0.5).astype(np.float32)
+    """dataset.py:184-200: one fillPoly mask per polygon, then semantic[mask > 0] = label in polygon
+    order (the last polygon wins)."""
     out = np.zeros((h, w), np.int64)
     for pts, lab in zip(polys, labels):
-        pts = np.asarray(pts, np.int64)
-        inside = np.zeros((h, w), bool)
-        edge = np.zeros((h, w), bool)
-        n = len(pts)
-        for k in range(n):
-            xi, yi = pts[k]
-            xj, yj = pts[k - 1]
-            cr = (xi - xj) * (yy - yj) - (yi - yj) * (xx - xj)
-            edge |= (cr == 0) & (xx >= min(xi, xj)) & (xx <= max(xi, xj)) & (yy >= min(yi, yj)) & (yy <= max(yi, yj))
-            if yi != yj:
-                cond = (np.float32(yi) > py) != (np.float32(yj) > py)
-                xc = np.float32(xj - xi) * (py - np.float32(yi)) / np.float32(yj - yi) + np.float32(xi)
-                inside ^= cond & (px < xc)
-        out[inside | edge] = lab
+        out[fill_poly_u8(pts, h, w) > 0] = lab
     return out
 
 

@@ -75,10 +75,10 @@ def dual_formula_weights(base=64, in_ch=3, K=3, dtype=torch.float64) -> Dict[str
     return out
 
 
-def branch_forward(S, prefix: str, x, training: bool, pins=None):
+def branch_forward(S, prefix: str, x, training: bool, pins=None, record=None):
     """BasicUNet trunk (models.py:227-237) ending at input resolution: dec1(d2).  pins: the trunk's
-    branch configuration (eunet_ref.trunk)."""
-    d2, _ = R.trunk(S, x, training, pins, prefix=prefix + ".")
+    branch configuration (eunet_ref.trunk); record: optional dict of its ReLU inputs."""
+    d2, _ = R.trunk(S, x, training, pins, prefix=prefix + ".", record=record)
     return F.conv2d(d2, S[prefix + ".dec1.weight"], S[prefix + ".dec1.bias"])
 
 
@@ -90,14 +90,20 @@ def _drop(h, mask, p, training):
     return h * mask.to(h.dtype)[:, :, None, None] / (1.0 - p)
 
 
-def dual_forward(S, x, training: bool = True, drop_masks=None, pins=None):
+def dual_forward(S, x, training: bool = True, drop_masks=None, pins=None, record=None):
     """x [B,C,H,W] -> (fused [B,K,H,W], {'unetpp': .., 'deeplab': ..}); models.py:316-333.
     drop_masks: optional ([B,256], [B,128]) 0/1 keep masks for the two Dropout2d.
     pins: optional branch configuration {'unetpp': trunk pins, 'deeplab': trunk pins,
-    'fusion_head.1' / '.5' / '.9': ReLU masks} (eunet_ref._relu)."""
+    'fusion_head.1' / '.5' / '.9': ReLU masks} (eunet_ref._relu).
+    record: optional dict receiving the ReLU inputs in the same layout as pins (tests/_pins.py audit)."""
     pins = pins or {}
-    out_main = branch_forward(S, "unetpp", x, training, pins.get("unetpp"))
-    out_aux = branch_forward(S, "deeplab", x, training, pins.get("deeplab"))
+    rec = (lambda k, h: record.__setitem__(k, h.detach())) if record is not None else (lambda k, h: None)
+    if record is not None:
+        record["unetpp"], record["deeplab"] = {}, {}
+    out_main = branch_forward(S, "unetpp", x, training, pins.get("unetpp"),
+                              record["unetpp"] if record is not None else None)
+    out_aux = branch_forward(S, "deeplab", x, training, pins.get("deeplab"),
+                             record["deeplab"] if record is not None else None)
     ff = torch.cat([out_main, out_aux], 1)
     a = F.conv2d(ff, S["attention_gate.0.weight"], padding=1)
     a = F.gelu(R._bn(S, "attention_gate.1", a, training))
@@ -105,14 +111,15 @@ def dual_forward(S, x, training: bool = True, drop_masks=None, pins=None):
     att = torch.sigmoid(R._bn(S, "attention_gate.4", a, training))
     ff = ff * att
     dm = drop_masks or (None, None)
-    h = R._relu(R._bn(S, "fusion_head.1", F.conv2d(ff, S["fusion_head.0.weight"], padding=1), training),
-                pins.get("fusion_head.1"))
-    h = _drop(h, dm[0], DROP_P[0], training)
-    h = R._relu(R._bn(S, "fusion_head.5", F.conv2d(h, S["fusion_head.4.weight"], padding=1), training),
-                pins.get("fusion_head.5"))
-    h = _drop(h, dm[1], DROP_P[1], training)
-    h = R._relu(R._bn(S, "fusion_head.9", F.conv2d(h, S["fusion_head.8.weight"], padding=1), training),
-                pins.get("fusion_head.9"))
+    h = R._bn(S, "fusion_head.1", F.conv2d(ff, S["fusion_head.0.weight"], padding=1), training)
+    rec("fusion_head.1", h)
+    h = _drop(R._relu(h, pins.get("fusion_head.1")), dm[0], DROP_P[0], training)
+    h = R._bn(S, "fusion_head.5", F.conv2d(h, S["fusion_head.4.weight"], padding=1), training)
+    rec("fusion_head.5", h)
+    h = _drop(R._relu(h, pins.get("fusion_head.5")), dm[1], DROP_P[1], training)
+    h = R._bn(S, "fusion_head.9", F.conv2d(h, S["fusion_head.8.weight"], padding=1), training)
+    rec("fusion_head.9", h)
+    h = R._relu(h, pins.get("fusion_head.9"))
     fused = F.conv2d(h, S["fusion_head.11.weight"], S["fusion_head.11.bias"])
     fused = fused + F.conv2d(ff, S["fusion_residual.weight"], S["fusion_residual.bias"])
     return fused, {"unetpp": out_main, "deeplab": out_aux}

@@ -162,10 +162,11 @@ def trunk(S, x, training, pins=None, prefix="model.", record=None):
 
 
 def forward(S: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True,
-            return_levels: bool = False, pins=None):
+            return_levels: bool = False, pins=None, record=None):
     """x [B,C,H,W] -> logits [B,K,2H,2W]; BN running stats in S are updated in train mode.
-    pins: branch configuration of the trunk (trunk()) and of the head's ReLU ('enhance.1')."""
-    d2, lv = trunk(S, x, training, pins)
+    pins: branch configuration of the trunk (trunk()) and of the head's ReLU ('enhance.1');
+    record: optional dict receiving the trunk's ReLU inputs (trunk(); tests/_pins.py audit)."""
+    d2, lv = trunk(S, x, training, pins, record=record)
     u = F.conv2d(_up2(d2), S["model.dec1.weight"], S["model.dec1.bias"])
     h = F.conv2d(u, S["enhance.0.weight"], S["enhance.0.bias"], padding=1)
     h = _relu(_bn(S, "enhance.1", h, training), (pins or {}).get("enhance.1"))

@@ -84,3 +84,60 @@ def model_pins(model):
 def keep(model, on=True):
     model._engine.keep_state = on
     return model
+
+
+# ---- audit: the pins must be the oracle's own branches up to rounding ---------------------------------
+# A pin is adopted by the oracle without question, so a kernel bug that flipped masks far from the kink
+# (a wrong shift channel, a tile-seam indexing error in the stored ya / yb) would be copied into the
+# oracle's forward and backward.  audit() compares every pin with the oracle's OWN branch at the same
+# element (the ReLU input / pool window the pinned oracle computed, record= of eunet_ref.forward /
+# dual_ref.dual_forward) and requires each disagreement to sit within `tol` x max|h| of the kink (ReLU)
+# or of a tie (pool: the oracle's top value minus its value at the pinned index).
+TOL_FP32 = 1e-5
+TOL_BF16 = 2e-2  # ~5 bf16 units of roundoff (2^-8) of the largest activation
+
+
+def _audit_trunk(pins, rec, tol, out, prefix=""):
+    for key, pin in pins.items():
+        if key.startswith("pool"):
+            continue
+        h = rec[key].double()
+        pin = pin.to(torch.bool)
+        dis = (h > 0) != pin
+        n = int(dis.sum())
+        worst = float(h[dis].abs().max() / h.abs().max()) if n else 0.0
+        out[prefix + key] = (n, worst)
+    for i in (1, 2, 3):
+        key = f"pool{i}"
+        if key not in pins:
+            continue
+        v = rec[f"enc{i}.4"].double().clamp_min(0.0)
+        B, C, H, W = v.shape
+        w = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+        top, own = w.max(-1)  # first maximum, as the kernels' rule
+        at_pin = w.gather(-1, pins[key].long().unsqueeze(-1)).squeeze(-1)
+        dis = own != pins[key].long()
+        n = int(dis.sum())
+        worst = float((top - at_pin)[dis].max() / v.max().clamp_min(1e-300)) if n else 0.0
+        out[prefix + key] = (n, worst)
+
+
+def audit(pins, rec, dtype, tol=None, label=""):
+    """Assert that every pin disagreeing with the oracle's own branch is within tol (relative to the
+    site's largest activation) of the kink / tie; return {site: (disputed count, worst ratio)} and print
+    the totals.  pins / rec: trunk dicts, or the dual layout ({'unetpp': .., 'deeplab': .., 'fusion_head.k'})."""
+    tol = tol if tol is not None else (TOL_BF16 if dtype in (torch.bfloat16, "bf16") else TOL_FP32)
+    out = {}
+    if "unetpp" in pins:
+        _audit_trunk(pins["unetpp"], rec["unetpp"], tol, out, "unetpp.")
+        _audit_trunk(pins["deeplab"], rec["deeplab"], tol, out, "deeplab.")
+        _audit_trunk({k: v for k, v in pins.items() if k.startswith("fusion_head")}, rec, tol, out)
+    else:
+        _audit_trunk(pins, rec, tol, out)
+    total = sum(n for n, _ in out.values())
+    worst = max((w, k) for k, (_, w) in out.items())
+    print(f"pin audit {label}: {total} disputed branch(es) over {len(out)} sites, worst {worst[0]:.2e} of max|h| "
+          f"at {worst[1]} (tol {tol:.0e})")
+    bad = {k: v for k, v in out.items() if v[1] > tol}
+    assert not bad, f"pins far from the oracle's own kink / tie (a kernel branch bug?): {bad}"
+    return out

@@ -284,7 +284,10 @@ def _trainer_worker(rank, world, port, q, cfg):
                     for k in S:
                         if S[k].is_floating_point() and "running" not in k:
                             S[k].requires_grad_(True)
-                    R.batch_loss(R.forward(S, x.cpu().to(odt), True, pins=pins), m.cpu()).backward()
+                    orec = {} if odt == torch.float64 else None
+                    R.batch_loss(R.forward(S, x.cpu().to(odt), True, pins=pins, record=orec), m.cpu()).backward()
+                    if orec is not None:  # every disputed branch within rounding of its kink / tie
+                        rec["pin_audit"] = _pins.audit(pins, orec, "fp32", label=f"world-2 rank {rank}")
                     rec[key] = {k: S[k].grad.double().numpy() for k in rec["grads"]}
             out["steps"].append(rec)
         q.put(out)

@@ -56,17 +56,36 @@ def test_configs1_fp32_512_batch8_vs_oracle():
     pins = _pins.model_pins(m)
     m._engine.last_state = None
     logits = logits.detach().cpu()
+    rec = {}
     with torch.no_grad():
         S64 = R.formula_weights(64, 1, 2)
-        out64 = R.forward(S64, x.double(), training=True, pins=pins)
+        out64 = R.forward(S64, x.double(), training=True, pins=pins, record=rec)
         loss64 = R.batch_loss(out64, msk)
         ref64 = torch.nn.functional.avg_pool2d(out64, 2)
         del out64
+    # the pins are the oracle's own branches up to fp32 rounding (tests/_pins.audit)
+    _pins.audit(pins, rec, "fp32", label="configs[1]")
+    del rec
     px = _rel_px(logits, ref64)
-    print("configs[1] logits per-pixel vs fp64:", px, "loss", loss.item(), float(loss64))
+    print("configs[1] logits per-pixel vs pinned fp64:", px, "loss", loss.item(), float(loss64))
     assert px < 1e-3
     assert abs(loss.item() - float(loss64)) < 1e-4 * abs(float(loss64))
-    del ref64
+    # UNPINNED: the plain fp64 oracle (its own branches everywhere).  Pixels downstream of a disputed kink
+    # are those where the pinned and the unpinned fp64 oracles themselves differ (> 1e-4, same per-pixel
+    # measure); outside that reported set the GPU logits meet the 1e-3 per-pixel gate against the plain
+    # reference forward.
+    with torch.no_grad():
+        ref64u = torch.nn.functional.avg_pool2d(R.forward(R.formula_weights(64, 1, 2), x.double(), training=True), 2)
+    den = ref64u.abs().clamp_min(1e-2 * float(ref64u.abs().max()))
+    near = ((ref64 - ref64u).abs() / den) > 1e-4
+    pxu = ((logits.double() - ref64u).abs() / den)
+    n_near = int(near.sum())
+    pxu_out = float(pxu[~near].max())
+    print(f"configs[1] logits per-pixel vs UNPINNED fp64: {pxu_out:.2e} outside {n_near} of {near.numel()} "
+          f"logits downstream of disputed kinks (all: {float(pxu.max()):.2e})")
+    assert pxu_out < 1e-3
+    assert n_near <= 1e-3 * near.numel(), n_near
+    del ref64, ref64u, pxu, near, den
     S = R.formula_weights(64, 1, 2, dtype=torch.float32)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:

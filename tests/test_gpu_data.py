@@ -1,8 +1,9 @@
 """Device-side data path (datapath.hip) vs the reference loader's numpy expressions (oracle/data_ref.py).
 
-Pixel ops, flips, ToTensor and cv2.resize INTER_LINEAR (OpenCV's fixed-point algorithm, restated)
-are bit-exact; the polygon fill is checked against the build's documented rule (cv2.fillPoly
-itself is absent: parity unpinned).
+Pixel ops, flips, ToTensor, cv2.resize INTER_LINEAR (OpenCV's fixed-point algorithm, restated) and
+cv2.fillPoly (OpenCV 4.x's Bresenham outline + fixed-point scanline fill, restated in
+oracle/data_ref.py fill_poly_u8) are bit-exact against the restatements; cv2 itself is absent, so
+parity with cv2 is unpinned.
 """
 import json
 import os
@@ -98,7 +99,7 @@ def _random_polys(rng, n, h, w):
 
 
 @pytest.mark.parametrize("n,h,w", [(300, 61, 77), (40, 480, 640), (1, 17, 3)])
-def test_rasterize_culling_matches_rule(n, h, w):
+def test_rasterize_culling_matches_rule(n, h, w):  # noqa: C901
     """The bounding-box culled rasterisers (16x16 tiles with per-chunk polygon lists, > 256
     polygons = several LDS chunks; per-polygon instance masks in 4-byte runs, ragged tails, flips)
     against the oracle's per-pixel rule over every polygon."""
@@ -287,3 +288,46 @@ def test_train_model_default_fast_path_is_exact(tmp_path):
         finals.append({k: v.detach().clone() for k, v in model.state_dict().items()})
     for k in finals[0]:
         assert torch.equal(finals[0][k], finals[1][k]), k
+
+
+def _shape_polys(h, w):
+    """Concave, self-touching, self-intersecting, rectilinear, degenerate and clipped polygons."""
+    rng = np.random.default_rng(17)
+    polys = []
+    for i in range(10):  # concave stars: alternating radii
+        c = rng.uniform(8, [w - 8, h - 8])
+        k = int(rng.integers(4, 9))
+        ang = np.arange(2 * k) * np.pi / k + rng.uniform(0, 1)
+        r = np.where(np.arange(2 * k) % 2 == 0, rng.uniform(8, 20), rng.uniform(2, 6))
+        polys.append(np.stack([c[0] + r * np.cos(ang), c[1] + r * np.sin(ang)], 1).astype(np.float32).astype(np.int32))
+    polys += [np.array(p, np.int32) for p in (
+        [[5, 5], [25, 5], [25, 15], [15, 15], [15, 25], [5, 25]],            # L shape: horizontal / vertical edges
+        [[30, 5], [50, 25], [50, 5], [30, 25]],                             # bow tie (self-intersecting)
+        [[5, 30], [15, 30], [10, 40], [15, 50], [5, 50], [10, 40]],         # two triangles touching at a vertex
+        [[20, 30], [40, 30], [40, 50], [30, 40], [20, 50]],                 # concave notch
+        [[44, 44], [44, 44], [60, 44]],                                     # repeated vertex, horizontal segment
+        [[3, 60], [3, 70]],                                                 # two points: vertical segment
+        [[7, 7]],                                                           # one point
+        [[-5, -5], [w + 4, 3], [w // 2, h + 6]],                             # clipped on every side
+        [[w - 1, 0], [w, h // 2], [w - 3, h]],                               # x == w: the reference's scaled edge case
+        [[0, h], [w // 3, h - 9], [w // 2, h]],                               # y == h
+        [[-40, 20], [-10, 30], [-20, 60]],                                  # entirely left of the image
+        [[10, 10], [11, 60], [12, 10]],                                     # thin steep sliver
+        [[0, 20], [w - 1, 21], [0, 22]])]                                   # thin shallow sliver
+    return polys
+
+
+@pytest.mark.parametrize("h,w", [(64, 72), (63, 65)])
+def test_rasterize_fillpoly_shapes_bit_exact(h, w):
+    """cv2.fillPoly cases that separate it from a centre-sampled even-odd rule: Bresenham outline pixels
+    on slanted edges, concave vertices, self-touching / self-intersecting outlines, horizontal and
+    vertical edges, 1-2 point polygons and clipping at (and beyond) every image border -- semantic mask
+    (last polygon wins) and the per-instance masks, bit-exact vs oracle/data_ref.py fill_poly_u8."""
+    from eunet import ops
+    polys = _shape_polys(h, w)
+    labels = [1 + (i % 2) for i in range(len(polys))]
+    m = ops.rasterize_polygons(polys, labels, h, w, DEV).cpu().numpy()
+    assert np.array_equal(m, O.rasterize(polys, labels, h, w))
+    inst = ops.rasterize_instances(polys, h, w, DEV).cpu().numpy()
+    for i, p in enumerate(polys):
+        assert np.array_equal(inst[i], O.fill_poly_u8(p, h, w)), (i, p.tolist())

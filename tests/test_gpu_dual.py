@@ -71,12 +71,17 @@ def test_dual_forward_matches_reference_fixture(golden_dir):
     assert _rel(out_e, g["out_eval"]) < 1e-3
 
 
-def _oracle(base, cin, K, x, msk, keep, dtype, pins=None):
+def _oracle(base, cin, K, x, msk, keep, dtype, pins=None, gpu_dtype="fp32"):
+    """Oracle step; pinned fp64 runs also audit the pins (tests/_pins.audit)."""
+    import _pins
     S = D.dual_formula_weights(base, cin, K, dtype=dtype)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:
             S[k].requires_grad_(True)
-    fused, aux = D.dual_forward(S, x.to(dtype), training=True, drop_masks=keep, pins=pins)
+    rec = {} if pins is not None and dtype == torch.float64 else None
+    fused, aux = D.dual_forward(S, x.to(dtype), training=True, drop_masks=keep, pins=pins, record=rec)
+    if rec is not None:
+        _pins.audit(pins, rec, gpu_dtype, label=f"dual b{base} c{cin} K{K} {tuple(x.shape[-2:])} {gpu_dtype}")
     loss = D.dual_batch_loss(fused, aux, msk)
     loss.backward()
     return S, loss
@@ -286,7 +291,7 @@ def test_dual_base96_train_grads_bf16_vs_fp64_oracle():
     keep = _keep96()
     m = _model(96, 1, 2, dtype="bf16", keep=keep).train()
     loss, pins = _gpu_step(m, x, msk)
-    S, loss_ref = _oracle(96, 1, 2, x, msk, keep, torch.float64, pins)
+    S, loss_ref = _oracle(96, 1, 2, x, msk, keep, torch.float64, pins, gpu_dtype="bf16")
     Sac = D.dual_formula_weights(96, 1, 2, dtype=torch.float32)
     for k in Sac:
         if Sac[k].is_floating_point() and "running" not in k:

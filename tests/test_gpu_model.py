@@ -112,12 +112,18 @@ def _pre_bn_bias(k):
     return k.endswith((".0.bias", ".3.bias")) and not k.startswith("enhance.3")
 
 
-def _oracle_grads(base, cin, K, x, msk, dtype, pins=None):
+def _oracle_grads(base, cin, K, x, msk, dtype, pins=None, gpu_dtype="fp32"):
+    """Oracle step; pinned fp64 runs also audit the pins against the oracle's own branches (every
+    disputed ReLU / pool branch within rounding of its kink / tie: tests/_pins.audit)."""
+    import _pins
     S = R.formula_weights(base, cin, K, dtype=dtype)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:
             S[k].requires_grad_(True)
-    loss = R.batch_loss(R.forward(S, x.to(dtype), training=True, pins=pins), msk)
+    rec = {} if pins is not None and dtype == torch.float64 else None
+    loss = R.batch_loss(R.forward(S, x.to(dtype), training=True, pins=pins, record=rec), msk)
+    if rec is not None:
+        _pins.audit(pins, rec, gpu_dtype, label=f"b{base} c{cin} K{K} {tuple(x.shape[-2:])} {gpu_dtype}")
     loss.backward()
     return S, loss
 
@@ -394,10 +400,15 @@ def test_bf16_train_grads_vs_fp64_oracle():
     S, loss_ref = _oracle_grads(64, 1, 2, x, msk, torch.float64)
     Sac, loss_ac = _oracle_grads_autocast(64, 1, 2, x, msk)
     m = _model(64, 1, 2, dtype="bf16")
-    m.train()
-    loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
-    loss.backward()
-    torch.cuda.synchronize()
+    _, loss, pins = _gpu_step_with_pins(m, x, msk)
+    # the gradients below are compared with the unpinned oracle; the bf16 branch configuration is still
+    # audited: every bf16 ReLU / pool branch that differs from the fp64 oracle's is within bf16 rounding
+    # of its kink / tie (tests/_pins.audit, TOL_BF16)
+    import _pins
+    rec = {}
+    with torch.no_grad():
+        R.forward(R.formula_weights(64, 1, 2), x.double(), training=True, pins=pins, record=rec)
+    _pins.audit(pins, rec, "bf16", label="bf16 b64 128^2")
     print("bf16 step loss", loss.item(), "fp64", loss_ref.item(), "autocast", loss_ac.item())
     assert abs(loss.item() - loss_ref.item()) < max(2 * abs(loss_ac.item() - loss_ref.item()), 1e-2 * abs(loss_ref.item()))
     scale = max(float(S[k].grad.abs().max()) for k in S if S[k].grad is not None)

@@ -107,3 +107,69 @@ def test_trainer_native_step_matches_torch_path():
         # them), which AdamW normalises to +-lr steps of arbitrary sign: not comparable
         if out[0][k].is_floating_point() and not re.search(r"\.[03]\.bias$", k):
             assert rel(out[0][k], out[1][k]) < 1e-4, k
+
+
+def test_plain_foreach_adamw_is_not_taken():
+    """The reference's plain optim.AdamW(...) (foreach, not capturable) keeps CPU step counters once torch
+    has stepped it: the native path refuses it, and the Trainer then runs torch's clip + step."""
+    from eunet.optim import ClipAdamW, supported
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in SHAPES[:4]]
+    o = torch.optim.AdamW(ps, lr=1e-3, foreach=True)
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    o.step()
+    assert not o.state[ps[0]]["step"].is_cuda  # the hazard the check guards against
+    assert not supported(o)
+    with pytest.raises(ValueError):
+        ClipAdamW(o)
+
+
+def test_capturable_adamw_after_torch_step_and_cpu_state():
+    """A capturable AdamW stepped by torch first, then natively; and a state whose step counter was
+    loaded onto the CPU (load_state_dict of a CPU-mapped checkpoint) is moved to the device first."""
+    from eunet.optim import ClipAdamW, supported
+    g = torch.Generator(device="cpu").manual_seed(7)
+    base = [torch.randn(s, generator=g) * 0.1 for s in SHAPES]
+    pa = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    pb = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    oa = torch.optim.AdamW(pa, lr=4e-3, weight_decay=1e-4, capturable=True)
+    ob = torch.optim.AdamW(pb, lr=4e-3, weight_decay=1e-4, capturable=True)
+    assert supported(ob)
+    for it in range(3):
+        grads = [torch.randn(p.shape, generator=g) for p in pa]
+        for p, q, gr in zip(pa, pb, grads):
+            p.grad, q.grad = gr.to(DEV), gr.to(DEV)
+        torch.nn.utils.clip_grad_norm_(pa, max_norm=1.0, foreach=True)
+        oa.step()
+        if it == 0:  # torch's own first step on ob, then a CPU step counter on one tensor
+            torch.nn.utils.clip_grad_norm_(pb, max_norm=1.0, foreach=True)
+            ob.step()
+            ob.state[pb[1]]["step"] = ob.state[pb[1]]["step"].cpu()
+            native = ClipAdamW(ob)
+        else:
+            native.step(1.0)
+        torch.cuda.synchronize()
+        for p, q in zip(pa, pb):
+            assert rel(q, p) < 1e-6, (it, p.shape)
+            assert ob.state[q]["step"].is_cuda or it == 0
+            assert float(ob.state[q]["step"]) == it + 1
+
+
+def test_clip_adamw_nan_gradient_poisons_like_torch():
+    """A NaN gradient element: torch's clamp(max=1) keeps the NaN coefficient, so every clipped
+    gradient and every updated parameter becomes NaN; the native step does the same."""
+    from eunet.optim import ClipAdamW
+    g, pa, pb, oa, ob = _pair(5)
+    native = ClipAdamW(ob)
+    for p, q in zip(pa, pb):
+        gr = torch.randn(p.shape, generator=g).to(DEV)
+        p.grad, q.grad = gr.clone(), gr.clone()
+    pa[3].grad.view(-1)[0] = float("nan")
+    pb[3].grad.view(-1)[0] = float("nan")
+    torch.nn.utils.clip_grad_norm_(pa, max_norm=1.0, foreach=True)
+    oa.step()
+    native.step(1.0)
+    torch.cuda.synchronize()
+    for p, q in zip(pa, pb):
+        assert torch.isnan(p).all() and torch.isnan(q).all()
+        assert torch.isnan(q.grad).all()

@@ -11,6 +11,7 @@ import torch
 
 from oracle import eunet_ref as R
 from oracle.weights import uniform01
+from oracle import data_ref as O  # noqa: E402
 
 
 def _load(golden_dir, name):
@@ -247,7 +248,7 @@ def test_dual_train_step_matches_reference(golden_dir):
 
 
 def test_data_oracle_rules():
-    """oracle/data_ref.py: the reference's numpy pixel lines and the documented fill rule."""
+    """oracle/data_ref.py: the reference's numpy pixel lines and cv2.fillPoly's square."""
     from oracle import data_ref as O
     img = np.arange(256, dtype=np.uint8).reshape(16, 16, 1)
     assert O.brightness(img, 2.0)[15, 15, 0] == 255 and O.brightness(img, 0.5)[0, 3, 0] == 1
@@ -294,3 +295,131 @@ def test_branch_pinned_oracle_at_its_own_branches_is_the_oracle():
     m.view(-1)[int(m.view(-1).nonzero()[0])] = False
     flip["dec2.4"] = m
     assert not torch.equal(run(flip)[0], u0)
+
+
+def test_pin_audit_accepts_rounding_and_catches_branch_bugs():
+    """tests/_pins.audit: pins taken from an fp32 run of the oracle (an implementation whose branches
+    differ from fp64 only by rounding) pass the fp32 audit against the fp64 oracle's own branches; pins
+    with one ReLU mask flipped far from its kink, with a 2x2 pool index moved off a clear maximum, or
+    formed with the BN shift of the wrong channel are rejected."""
+    import _pins
+    x = torch.rand(2, 1, 64, 64, generator=torch.Generator().manual_seed(3))
+    nhwc = lambda t: t.permute(0, 2, 3, 1)  # noqa: E731
+    one, zero = torch.ones(1), torch.zeros(1)
+
+    def pins_of(S, xx):
+        rec = {}
+        with torch.no_grad():
+            R.trunk(S, xx, True, record=rec)
+        pins = {k: _pins.relu_mask(nhwc(v), one, zero) for k, v in rec.items()}
+        for i, nm in enumerate(_pins.POOLED, 1):
+            pins[f"pool{i}"] = _pins.pool_argmax(nhwc(rec[nm + ".4"]), one, zero, torch.float32)
+        return pins, rec
+
+    p32, rec32 = pins_of(R.formula_weights(16, 1, 2, dtype=torch.float32), x)
+    rec64 = {}
+    with torch.no_grad():
+        R.trunk(R.formula_weights(16, 1, 2), x.double(), True, pins=p32, record=rec64)
+    out = _pins.audit(p32, rec64, torch.float32, label="fp32 oracle vs fp64")
+    assert set(out) == set(p32)
+
+    h = rec64["enc2.1"]
+    i = int(h.abs().argmax())  # the element farthest from its kink
+    bad = dict(p32)
+    m = bad["enc2.1"].clone()
+    m.view(-1)[i] = ~m.view(-1)[i]
+    bad["enc2.1"] = m
+    with pytest.raises(AssertionError):
+        _pins.audit(bad, rec64, torch.float32)
+
+    v = rec64["enc1.4"].clamp_min(0)
+    B, C, H, W = v.shape
+    w = v.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+    gap = w.max(-1).values - w.min(-1).values
+    j = int(gap.argmax())
+    bad = dict(p32)
+    pl = bad["pool1"].clone()
+    pl.view(-1)[j] = int(w.reshape(-1, 4)[j].argmin())
+    bad["pool1"] = pl
+    with pytest.raises(AssertionError):
+        _pins.audit(bad, rec64, torch.float32)
+
+    # a wrong shift channel: the masks of enc3.4 formed with the channels' shifts rolled by one
+    hh = nhwc(rec32["enc3.4"])
+    shift = torch.linspace(-0.5, 0.5, hh.shape[-1])
+    bad = dict(p32)
+    bad["enc3.4"] = _pins.relu_mask(hh - shift + shift.roll(1), one, zero)
+    with pytest.raises(AssertionError):
+        _pins.audit(bad, rec64, torch.float32)
+
+
+def _fillpoly_per_pixel(pts, h, w):
+    """The HIP kernels' per-pixel statement of cv2.fillPoly (csrc/datapath.hip cv_fillpoly_covers):
+    closed-form Bresenham membership per edge + the span count over the row's active edges.  An
+    independent formulation of the same algorithm, checked against the literal scanline restatement."""
+    def cdiv(a, b):
+        q = abs(a) // abs(b)
+        return q if (a >= 0) == (b >= 0) else -q
+    P = [(int(a), int(b)) for a, b in pts]
+    out = np.zeros((h, w), np.uint8)
+    for y in range(h):
+        for x in range(w):
+            on, clt, cle = False, 0, 0
+            for k in range(len(P)):
+                (X0, Y0), (X1, Y1) = P[k - 1], P[k]
+                inimg = 0 <= X0 < w and 0 <= X1 < w and 0 <= Y0 < h and 0 <= Y1 < h
+                vis, (cx0, cy0), (cx1, cy1) = (True, (X0, Y0), (X1, Y1)) if inimg else \
+                    O.clip_line(w, h, (X0, Y0), (X1, Y1))
+                if vis:
+                    (lx1, ly1), (lx2, ly2) = sorted([(cx0, cy0), (cx1, cy1)], key=lambda q: q[0]) \
+                        if cx1 < cx0 else ((cx0, cy0), (cx1, cy1))
+                    ddx, ddy = lx2 - lx1, ly2 - ly1
+                    ady = abs(ddy)
+                    if ady > ddx:
+                        i = ly1 - y if ddy < 0 else y - ly1
+                        on |= 0 <= i <= ady and x == lx1 + (2 * ddx * i + ady - 1) // (2 * ady)
+                    else:
+                        i = x - lx1
+                        if 0 <= i <= ddx:
+                            mm = (2 * ady * i + ddx - 1) // (2 * ddx) if ddx else 0
+                            on |= y == (ly1 - mm if ddy < 0 else ly1 + mm)
+                if Y0 != Y1:
+                    if inimg:
+                        c0, c1 = ((X0 << 16) + 32768, Y0), ((X1 << 16) + 32768, Y1)
+                    elif cy0 != cy1:
+                        c0, c1 = (cx0 << 16, cy0), (cx1 << 16, cy1)
+                    else:
+                        c0, c1 = (X0 << 16, Y0), (X1 << 16, Y1)
+                    dx = cdiv(c1[0] - c0[0], c1[1] - c0[1])
+                    y0, y1, x0 = (Y0, Y1, c0[0] + (Y0 - c0[1]) * dx) if Y0 < Y1 else (Y1, Y0, c1[0] + (Y1 - c1[1]) * dx)
+                    if y0 <= y < y1:
+                        a = (x0 + (y - y0) * dx) >> 16
+                        clt += a < x
+                        cle += a <= x
+            out[y, x] = on or (clt & 1) or cle > clt
+    return out
+
+
+def test_fillpoly_restatement_known_answers_and_per_pixel_form():
+    """oracle/data_ref.py fill_poly_u8 (cv2.fillPoly, OpenCV 4.x drawing.cpp restated; cv2 absent, so
+    parity with cv2 itself is unpinned): hand-derived answers of the algorithm -- a right triangle's
+    staircase (Bresenham diagonal from the left endpoint, x + 1/2 spans), a square's outline + interior,
+    one point, a clipped triangle -- and agreement with the per-pixel form the HIP kernels evaluate on
+    300 random polygons, a third of them crossing the image border."""
+    tri = O.fill_poly_u8([[0, 0], [4, 0], [0, 4]], 6, 6)
+    exp = np.zeros((6, 6), np.uint8)
+    for r in range(5):
+        exp[r, :5 - r] = 1
+    assert np.array_equal(tri, exp)
+    sq = O.fill_poly_u8([[2, 2], [5, 2], [5, 5], [2, 5]], 8, 8)
+    assert sq.sum() == 16 and (sq[2:6, 2:6] == 1).all()
+    pt = O.fill_poly_u8([[3, 4]], 6, 6)
+    assert pt.sum() == 1 and pt[4, 3] == 1
+    assert O.fill_poly_u8([[-9, -9], [-1, -3], [-5, -1]], 6, 6).sum() == 0
+    rng = np.random.default_rng(0)
+    for t in range(300):
+        h, w = int(rng.integers(4, 20)), int(rng.integers(4, 20))
+        n = int(rng.integers(1, 9))
+        lo, hi = (-3, 3) if t % 3 == 0 else (0, 1)
+        pts = np.stack([rng.integers(lo, w + hi, n), rng.integers(lo, h + hi, n)], 1)
+        assert np.array_equal(O.fill_poly_u8(pts, h, w), _fillpoly_per_pixel(pts, h, w)), (pts.tolist(), h, w)

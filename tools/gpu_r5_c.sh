@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 5: the driver's exact bench command three times (the fp32 leg's one-off stall: where and whose)
+set -u
+mkdir -p gpurun_out
+for i in 1 2 3; do
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --dice-size 0 > gpurun_out/r5c_drv$i.log 2>&1 || { echo fail$i; tail -20 gpurun_out/r5c_drv$i.log; exit 1; }
+done
+echo done
