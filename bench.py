@@ -305,6 +305,7 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
     # one event per step boundary on the launch stream (K+1 markers, no per-kernel cost): the
     # per-step GPU spans expose a one-off stall that the mean alone would hide
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    ms0 = torch.cuda.memory_stats(dev)
     with kprof.KernelTimer() as timer:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -323,6 +324,11 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     timer.step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(steps)]
     timer.host_ms = [1e3 * (host[i + 1] - host[i]) for i in range(steps)]
+    ms1 = torch.cuda.memory_stats(dev)
+    # device allocations / frees / OOM retries of the caching allocator inside the timed region (each
+    # hipMalloc / hipFree can block the host; a retry frees the whole cache after a device sync)
+    timer.alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries")}
+    timer.alloc["reserved_gb"] = round(ms1.get("reserved_bytes.all.current", 0) / 2 ** 30, 2)
     return float(elapsed.item()), timer
 
 
@@ -335,7 +341,8 @@ def step_spread(timer):
         return None
     i = max(range(len(s)), key=lambda j: timer.step_ms[j])
     return {"min": round(s[0], 3), "median": round(s[len(s) // 2], 3), "max": round(s[-1], 3), "max_at": i,
-            "host_ms_at_max": round(timer.host_ms[i], 3), "host_ms_max": round(max(timer.host_ms), 3)}
+            "host_ms_at_max": round(timer.host_ms[i], 3), "host_ms_max": round(max(timer.host_ms), 3),
+            "allocator": timer.alloc}
 
 
 def busy_pass(tr, x, m, steps=3):

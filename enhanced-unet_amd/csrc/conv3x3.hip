@@ -583,7 +583,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     // Chan-combined by 64 threads -- one barrier, one LDS round trip
     const int nw = max(0, min(RPW, vh - RPW * wv)) * vw;  // valid pixels in this wave's rows
     const float inv_nw = nw > 0 ? 1.f / (float)nw : 0.f;
-    const float ninv = (float)(RPW * FTW - nw);            // zeroed (invalid) values per channel
+    const bool part = vh < FTH || vw < FTW;                 // block-uniform: an edge tile
     float s1[4], s2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -597,15 +597,30 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       const float mw = s1[nt] * inv_nw;
       const f32x2 m2 = {-mw, -mw};
       f32x2 v = {0.f, 0.f};
+      if (!part) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
-        const f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
-        v = __builtin_elementwise_fma(d0, d0, v);
-        v = __builtin_elementwise_fma(d1, d1, v);
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
+          const f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
+          v = __builtin_elementwise_fma(d0, d0, v);
+          v = __builtin_elementwise_fma(d1, d1, v);
+        }
+      } else {  // the pixels outside the image contribute nothing (no (0 - mw)^2 to cancel afterwards)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const bool rok = RPW * wv + (mt >> 1) < vh;
+          const int c0 = (mt & 1) * 16 + q * 4;
+          f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
+          f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
+          d0.x = rok && c0 + 0 < vw ? d0.x : 0.f;
+          d0.y = rok && c0 + 1 < vw ? d0.y : 0.f;
+          d1.x = rok && c0 + 2 < vw ? d1.x : 0.f;
+          d1.y = rok && c0 + 3 < vw ? d1.y : 0.f;
+          v = __builtin_elementwise_fma(d0, d0, v);
+          v = __builtin_elementwise_fma(d1, d1, v);
+        }
       }
-      // each zeroed value added (0 - mw)^2: removed once the 4 lane groups are summed
-      s2[nt] = fmaxf(xor32_sum(xor16_sum(v.x + v.y)) - ninv * mw * mw, 0.f);
+      s2[nt] = xor32_sum(xor16_sum(v.x + v.y));
     }
     if (q == 0)
 #pragma unroll

@@ -64,6 +64,11 @@ def side_stream(device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
+def _per_block(flag, nm) -> bool:
+    """An engine knob that is a bool (every block) or a collection of block names."""
+    return bool(flag) if isinstance(flag, bool) else nm in flag
+
+
 class UNetEngine:
     """One BasicUNet trunk (+ the enhance head for the single-branch model).  prefix names the
     trunk's parameters in the owning module ('model.' for EnhancedUNet, 'unetpp.' / 'deeplab.'
@@ -104,6 +109,7 @@ class UNetEngine:
     # dgrad's staging carries two loads per halo unit, the transform and the gy stores while the
     # standalone apply streams at ~4.9 TB/s beside the side stream's weight gradients -- 26.0-26.1 vs
     # 25.3-25.5 ms/step in three alternating same-box rounds (profiles/r03_ab.txt).  Off by default.
+    # A set of block names ({"enc4", "dec4"}) fuses those blocks only.
     fuse_bn_apply = False
     # fuse_bn_apply_a -- the same for the first BatchNorm (conv .0's data gradient; needs
     # fuse_bn_apply).  Off: conv .0's weight gradient then has to wait for that dgrad and overlaps the
@@ -347,7 +353,7 @@ class UNetEngine:
                 ops.conv3x3_wgrad(xa, gya, dwp, dbp, ns, scale=scale, shift=shift)
             ops.wgrad_reduce(dwp, dbp, ns, C, cin, 9, dw, db)
 
-        if self.fuse_bn_apply:
+        if _per_block(self.fuse_bn_apply, nm):
             return self._block_bwd_fused(nm, G, S, P, sink, need_gx, small, gred, wgrad, side, main)
         gyb = bn_back(p + ".4", G, yb, bnb, part=gred[0], tiles=gred[1])
 
@@ -447,7 +453,7 @@ class UNetEngine:
         del gyb
         gya = torch.empty_like(ya)
         gx = None
-        if need_gx and self.fuse_bn_apply_a:
+        if need_gx and _per_block(self.fuse_bn_apply_a, nm):
             gx = _e((N, H, W, X.c), dt, dev)
             ops.conv3x3_dgrad_fused(ops.act(gaa), ops.act(ya), coefa, ops.act(gya), packed(p + ".0"), ops.act(gx))
             wgrad(p + ".0", X, gya, small_conv=small)

@@ -18,6 +18,8 @@ Differences that are implementation, not semantics:
 """
 from __future__ import annotations
 
+import collections
+
 import math
 import warnings
 from typing import Dict
@@ -78,6 +80,15 @@ class Trainer:
         self._graph = None  # the graph of the last replayed step
         self._graph_warm = {}  # engine knobs + dtype (key[5]) -> eager warm-up steps run with them
         self.graph_captures = 0
+        # max_inflight: deferred-loss steps (sync_loss=False) the host may run ahead of the GPU.  The weight
+        # gradients' operands are record_stream-ed on the side stream, so the caching allocator can reuse
+        # them only once the GPU has passed that step: a host that ran 20+ steps ahead reserved a step's
+        # activations per queued step until hipMalloc failed, and the allocator's retry (device sync,
+        # free every cached block, allocate again) idled the GPU for 1.5-6 s (bench r5: allocator
+        # num_alloc_retries 2 inside the timed region).  Two steps in flight keep the GPU fed (a step's
+        # host issue takes ~6 ms, its GPU time >= 22 ms) with a bounded footprint.
+        self.max_inflight = 2
+        self._inflight = collections.deque()
 
     # ---- reference loss API (single sample, logits [K,H,W], target [H,W]) ----
     def loss_params(self):
@@ -136,8 +147,20 @@ class Trainer:
         With self.step_graph set, a deferred-loss step (sync_loss=False, no DataParallel) replays a
         captured HIP graph of this same step (StepGraph): same kernels, same bits, one launch."""
         if self.step_graph and not sync_loss and self.dp is None and images.is_cuda:
-            return self._graphed_step(images, masks)
-        return self._step(images, masks, sync_loss)
+            out = self._graphed_step(images, masks)
+        else:
+            out = self._step(images, masks, sync_loss)
+        if not sync_loss and images.is_cuda:
+            self._bound_inflight()
+        return out
+
+    def _bound_inflight(self):
+        """Block the host until at most max_inflight deferred steps are queued on the GPU."""
+        ev = torch.cuda.Event()
+        ev.record()
+        self._inflight.append(ev)
+        while len(self._inflight) > max(1, self.max_inflight):
+            self._inflight.popleft().synchronize()
 
     def _graphed_step(self, images, masks):
         key = StepGraph.key(self, images, masks)
@@ -259,6 +282,11 @@ ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late",
                 "dgrad_first", "wg3_early_last", "fork_once")
 
 
+def _hashable(v):
+    """A per-block knob (a set of block names) as a sorted tuple, for the graph key."""
+    return tuple(sorted(v)) if isinstance(v, (set, frozenset, list)) else v
+
+
 class StepGraph:
     """A Trainer step's forward, fused loss and backward (+ clip_grad_norm_ on the torch optimizer
     path) captured as a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed per batch,
@@ -314,7 +342,7 @@ class StepGraph:
             raise RuntimeError("Trainer.step_graph: fixed dropout keep masks (a test hook) are host inputs")
         # the compute dtype is baked into the captured kernels and buffers: EnhancedUNet.set_dtype
         # (which only changes the engine's dtype) must re-capture
-        knobs = tuple(getattr(eng, k, None) for k in ENGINE_KNOBS) + (
+        knobs = tuple(_hashable(getattr(eng, k, None)) for k in ENGINE_KNOBS) + (
             str(getattr(eng, "dtype", None)), str(getattr(trainer.model, "compute_dtype", None)))
         ps = [p for g in trainer.optimizer.param_groups for p in g["params"]]
         store = (id(trainer.optimizer), ps[0].data_ptr(), ps[-1].data_ptr(), len(ps))

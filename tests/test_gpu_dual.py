@@ -72,8 +72,20 @@ def test_dual_forward_matches_reference_fixture(golden_dir):
 
 
 def _oracle(base, cin, K, x, msk, keep, dtype, pins=None, gpu_dtype="fp32"):
-    """Oracle step; pinned fp64 runs also audit the pins (tests/_pins.audit)."""
+    """Oracle step; pinned fp64 runs also audit the pins (tests/_pins.audit; bf16 against 2x the
+    bf16-autocast oracle's own disputed branches)."""
     import _pins
+    ref = None
+    if pins is not None and dtype == torch.float64 and gpu_dtype == "bf16":
+        def run_ac(record):
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                D.dual_forward(D.dual_formula_weights(base, cin, K, dtype=torch.float32), x.float(), training=True,
+                               drop_masks=keep, record=record)
+
+        def run64(p, record):
+            D.dual_forward(D.dual_formula_weights(base, cin, K), x.double(), training=True, drop_masks=keep,
+                           pins=p, record=record)
+        ref = _pins.autocast_reference(run_ac, run64)
     S = D.dual_formula_weights(base, cin, K, dtype=dtype)
     for k in S:
         if S[k].is_floating_point() and "running" not in k:
@@ -81,7 +93,8 @@ def _oracle(base, cin, K, x, msk, keep, dtype, pins=None, gpu_dtype="fp32"):
     rec = {} if pins is not None and dtype == torch.float64 else None
     fused, aux = D.dual_forward(S, x.to(dtype), training=True, drop_masks=keep, pins=pins, record=rec)
     if rec is not None:
-        _pins.audit(pins, rec, gpu_dtype, label=f"dual b{base} c{cin} K{K} {tuple(x.shape[-2:])} {gpu_dtype}")
+        _pins.audit(pins, rec, gpu_dtype, label=f"dual b{base} c{cin} K{K} {tuple(x.shape[-2:])} {gpu_dtype}",
+                    ref=ref)
     loss = D.dual_batch_loss(fused, aux, msk)
     loss.backward()
     return S, loss

@@ -405,10 +405,18 @@ def test_bf16_train_grads_vs_fp64_oracle():
     # audited: every bf16 ReLU / pool branch that differs from the fp64 oracle's is within bf16 rounding
     # of its kink / tie (tests/_pins.audit, TOL_BF16)
     import _pins
+
+    def run_ac(record):
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            R.forward(R.formula_weights(64, 1, 2, dtype=torch.float32), x.float(), training=True, record=record)
+
+    def run64(p, record):
+        R.forward(R.formula_weights(64, 1, 2), x.double(), training=True, pins=p, record=record)
+    ref = _pins.autocast_reference(run_ac, run64)
     rec = {}
     with torch.no_grad():
-        R.forward(R.formula_weights(64, 1, 2), x.double(), training=True, pins=pins, record=rec)
-    _pins.audit(pins, rec, "bf16", label="bf16 b64 128^2")
+        run64(pins, rec)
+    _pins.audit(pins, rec, "bf16", label="bf16 b64 128^2", ref=ref)
     print("bf16 step loss", loss.item(), "fp64", loss_ref.item(), "autocast", loss_ac.item())
     assert abs(loss.item() - loss_ref.item()) < max(2 * abs(loss_ac.item() - loss_ref.item()), 1e-2 * abs(loss_ref.item()))
     scale = max(float(S[k].grad.abs().max()) for k in S if S[k].grad is not None)
@@ -441,8 +449,9 @@ def test_fused_bn_apply_schedule_is_exact(dtype, monkeypatch):
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 96, 64, start_index=13, num_classes=2, in_channels=1)
     out = {}
+    deep = frozenset({"enc3", "enc4", "dec4"})  # per-block fusion (UNetEngine.fuse_bn_apply as a set)
     for fused, fused_a, overlap in ((True, False, True), (True, True, True), (False, False, True),
-                                    (True, True, False)):
+                                    (True, True, False), (deep, False, True), (deep, deep, True)):
         monkeypatch.setattr(engine.UNetEngine, "fuse_bn_apply", fused)
         monkeypatch.setattr(engine.UNetEngine, "fuse_bn_apply_a", fused_a)
         monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", overlap)

@@ -81,6 +81,40 @@ def test_conv3x3_fwd_stats(dt, transform):
     assert rel(rv, 0.9 + 0.1 * v_ref * n / (n - 1)) < tol * 10
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3x3_fwd_stats_ragged_offset_channels(dt):
+    """BN partials of edge tiles when a channel's mean is far larger than its spread (bias 300, unit
+    spread; 20 x 36 images: every tile row / column edge is ragged): the per-wave M2 of an edge tile
+    takes only the valid pixels (no (0 - mean)^2 terms to cancel afterwards), so the batch variance stays
+    at fp32 accuracy relative to the VARIANCE, not to mean^2 (the subtraction form lost ~1e-2
+    of the variance here)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(2)
+    N, H, W, Cin, Cout = 2, 20, 36, 32, 64
+    x = torch.randn(N, H, W, Cin, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) / 17.0
+    b = 300.0 + torch.randn(Cout, generator=g, dtype=torch.float64)
+    xd = x.to(DEV, dt)
+    y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
+    wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
+    tiles = ops.conv3x3_tiles(ops.act(y))
+    st = torch.empty(tiles * (2 * Cout + 1), dtype=torch.float32, device=DEV)
+    ops.conv3x3_fwd(ops.act(xd), wp, ops.act(y), bias=b.float().to(DEV), stats=st)
+    gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
+    rm, rv = torch.zeros(Cout, device=DEV), torch.ones(Cout, device=DEV)
+    mean, inv = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    s1, s2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+    ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, rm, rv, mean, inv, s1, s2)
+    torch.cuda.synchronize()
+    # the fp32 accumulators the partials are taken from: the exact conv of the kernel's operands + bias (fp32)
+    ref = nhwc(F.conv2d(nchw(xd.double().cpu()), w.to(dt).double(), b.float().double(), padding=1))
+    v_ref = ref.var(dim=(0, 1, 2), unbiased=False)
+    v_got = 1.0 / inv.double().cpu() ** 2 - 1e-5
+    err = float(((v_got - v_ref).abs() / v_ref).max())
+    print(f"{dt} ragged offset-channel variance rel err {err:.2e} (mean ~300, var ~{float(v_ref.mean()):.2f})")
+    assert err < 2e-4
+
+
 def test_conv3x3_fwd_large_sample_slice():
     """One sample's input above 2 GiB (2048^2 x 288 bf16 = 2.4 GB: the dual-branch base-96 dec2.0
     input of BASELINE configs[4]) through the buffer-descriptor staging (unsigned 32-bit offsets, slices

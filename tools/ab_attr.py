@@ -18,6 +18,8 @@ for kv in sets:
     k, v = kv.split("=")
     if k.startswith("ops."):  # module switches of eunet.ops (e.g. ops.USE_DISPATCHER=0)
         setattr(ops, k[4:], bool(int(v)))
+    elif v.startswith("{"):  # a per-block knob: fuse_bn_apply={enc4,dec4}
+        setattr(UNetEngine, k, frozenset(x for x in v.strip("{}").split(",") if x))
     else:
         setattr(UNetEngine, k, bool(int(v)))
 import bench  # noqa: E402
