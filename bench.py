@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-fp32-leg", action="store_true", help="skip the fp32 BASELINE configs[1] leg (N=1 only)")
     ap.add_argument("--no-dual-leg", action="store_true",
                     help="skip the dual-branch BASELINE configs[4] leg (N=1 only)")
+    ap.add_argument("--step-graph", type=int, default=0,
+                    help="1: Trainer.step_graph (each step's forward + loss + backward replayed from a HIP graph)")
     ap.add_argument("--dual", action="store_true",
                     help="dual-branch model + deep supervision (BASELINE configs[4]: --dual --base 96 --size 2048)")
     return ap.parse_args()
@@ -290,6 +292,7 @@ def build_trainer(args, dev, dtype=None, base=None, dual=None):
                          dual_branch=args.dual if dual is None else dual).to(dev)
     tr = Trainer(model, dev, "enhanced_unet", total_epochs=50)
     tr.epoch_lr_step(0)
+    tr.step_graph = bool(args.step_graph)
     return tr
 
 
@@ -297,8 +300,10 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
     """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; returns the
     max-over-ranks elapsed seconds and the kernel timer of the timed region."""
     from eunet import kprof
-    for _ in range(warmup):
-        tr.step(x, m)
+    graph = getattr(tr, "step_graph", False)
+    for _ in range(max(warmup, tr.graph_warmup + 2) if graph else warmup):
+        # (graph steps: deferred-loss warm-up steps, so the graph is captured before the timed region)
+        tr.step(x, m, sync_loss=not graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -71,3 +71,29 @@ def test_reference_format_checkpoint_loads(golden_dir, tmp_path):
         out = m(torch.from_numpy(g["x"]).to(DEV)).double().cpu()
     ref = torch.from_numpy(g["out_eval"]).double()
     assert float((out - ref).abs().max() / ref.abs().max()) < 1e-3
+
+
+def test_deferred_steps_bound_the_host_run_ahead():
+    """Trainer.step(sync_loss=False) keeps at most max_inflight steps queued (the weight gradients'
+    record_stream-ed operands are reusable only once the GPU has passed their step: unbounded run-ahead
+    grew the reserved memory until the allocator's OOM retry stalled the GPU for seconds), and the
+    bounded deferred steps give the same parameters as synchronous ones, bit for bit."""
+    import torch
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    torch.manual_seed(0)
+    x = torch.rand(2, 1, 64, 64, device="cuda")
+    m = torch.randint(0, 2, (2, 64, 64), device="cuda")
+    out = []
+    for deferred in (True, False):
+        torch.manual_seed(1)
+        model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16).to("cuda")
+        tr = Trainer(model, "cuda", "enhanced_unet", total_epochs=50)
+        tr.epoch_lr_step(0)
+        for _ in range(6):
+            tr.step(x, m, sync_loss=not deferred)
+            assert len(tr._inflight) <= tr.max_inflight
+        torch.cuda.synchronize()
+        out.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k

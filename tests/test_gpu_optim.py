@@ -150,7 +150,9 @@ def test_capturable_adamw_after_torch_step_and_cpu_state():
             native.step(1.0)
         torch.cuda.synchronize()
         for p, q in zip(pa, pb):
-            assert rel(q, p) < 1e-6, (it, p.shape)
+            # capturable AdamW (foreach) forms its bias corrections as fp32 tensors, the native step (like
+            # the fused one) in double: last-bit differences in the step size
+            assert rel(q, p) < 1e-5, (it, p.shape)
             assert ob.state[q]["step"].is_cuda or it == 0
             assert float(ob.state[q]["step"]) == it + 1
 
