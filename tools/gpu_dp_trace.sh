@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-dp}
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- \
-  python bench.py --steps 6 --warmup 2 --no-cpu-baseline --dice-size 0 --no-fp32-leg > gpurun_out/prof_${TAG}.log 2>&1
+  python bench.py --steps 6 --warmup 2 --no-cpu-baseline --dice-size 0 --no-fp32-leg --no-dual-leg > gpurun_out/prof_${TAG}.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/prof_${TAG}.log; exit $rc; }
 f=$(find gpurun_out/prof_${TAG} -name '*kernel_trace.csv' | head -1)
 python3 tools/trace_steps.py "$f" 2 20 > gpurun_out/dp_trace_${TAG}.txt

@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 ${PMC_TIMEOUT:-400} rocprofv3 --pmc $c --kernel-trace --output-format csv \
     -d gpurun_out/pmc_${TAG}_$c -o run -- \
-    python bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --dice-size 0 --no-dp-world1 --no-fp32-leg} > gpurun_out/pmc_${TAG}_$c.log 2>&1
+    python bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --dice-size 0 --no-dp-world1 --no-fp32-leg --no-dual-leg} > gpurun_out/pmc_${TAG}_$c.log 2>&1
   rc=$?
   echo "pmc $c rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${TAG}_$c.log; exit $rc; fi

@@ -6,7 +6,7 @@ TAG=${TAG:-mfma}
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 timeout -k 10 ${PMC_TIMEOUT:-400} rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
   -d gpurun_out/pmc_${TAG}_mfma -o run -- \
-  python bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --dice-size 0 --no-dp-world1 --no-fp32-leg} > gpurun_out/pmc_${TAG}_mfma.log 2>&1
+  python bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --dice-size 0 --no-dp-world1 --no-fp32-leg --no-dual-leg} > gpurun_out/pmc_${TAG}_mfma.log 2>&1
 rc=$?
 echo "pmc mfma rc=$rc"
 if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${TAG}_mfma.log; exit $rc; fi
