@@ -498,22 +498,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNUP_WAVES)
   // output 2i+1: rows (i, i+1) weights (0.75, 0.25) (i+1 clamped).  Same along x; x first.
   const float wya = i > 0 ? 0.25f : 1.f, wyb = i > 0 ? 0.75f : 0.f;
   const float wxa = j0 > 0 ? 0.25f : 1.f, wxb = j0 > 0 ? 0.75f : 0.f;
-  float xr[3][4][E];  // x-interpolated rows: output columns 2j0 .. 2j0 + 3
+  // packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two channels per instruction, each element rounded as the
+  // scalar op rounds it -- the same bits as one channel at a time)
+  constexpr int E2 = E / 2;
+  f32x2 s2[E2], t2[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) { s2[e] = (f32x2){s[2 * e], s[2 * e + 1]}; t2[e] = (f32x2){t[2 * e], t[2 * e + 1]}; }
+  const f32x2 q1 = {0.25f, 0.25f}, q3 = {0.75f, 0.75f};
+  const f32x2 wxa2 = {wxa, wxa}, wxb2 = {wxb, wxb}, wya2 = {wya, wya}, wyb2 = {wyb, wyb};
+  f32x2 xr[3][4][E2];  // x-interpolated rows: output columns 2j0 .. 2j0 + 3
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
-    float v[4][E];
+    f32x2 v[4][E2];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      Vec16<T>::unpack(raw[a][b], v[b]);
+      float f[E];
+      Vec16<T>::unpack(raw[a][b], f);
 #pragma unroll
-      for (int e = 0; e < E; ++e) v[b][e] = fmaxf(fmaf(v[b][e], s[e], t[e]), 0.f);
+      for (int e = 0; e < E2; ++e) {
+        const f32x2 r = __builtin_elementwise_fma((f32x2){f[2 * e], f[2 * e + 1]}, s2[e], t2[e]);
+        v[b][e] = (f32x2){fmaxf(r.x, 0.f), fmaxf(r.y, 0.f)};
+      }
     }
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      xr[a][0][e] = fmaf(wxb, v[1][e], wxa * (j0 > 0 ? v[0][e] : v[1][e]));
-      xr[a][1][e] = fmaf(0.25f, v[2][e], 0.75f * v[1][e]);
-      xr[a][2][e] = fmaf(0.75f, v[2][e], 0.25f * v[1][e]);  // column 2(j0+1): j0 + 1 > 0
-      xr[a][3][e] = fmaf(0.25f, v[3][e], 0.75f * v[2][e]);
+    for (int e = 0; e < E2; ++e) {
+      xr[a][0][e] = __builtin_elementwise_fma(wxb2, v[1][e], wxa2 * (j0 > 0 ? v[0][e] : v[1][e]));
+      xr[a][1][e] = __builtin_elementwise_fma(q1, v[2][e], q3 * v[1][e]);
+      xr[a][2][e] = __builtin_elementwise_fma(q3, v[2][e], q1 * v[1][e]);  // column 2(j0+1): j0 + 1 > 0
+      xr[a][3][e] = __builtin_elementwise_fma(q1, v[3][e], q3 * v[2][e]);
     }
   }
 #pragma unroll
@@ -521,9 +533,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNUP_WAVES)
     if (b >= 2 && !two) break;
     float o0[E], o1[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      o0[e] = fmaf(wyb, xr[1][b][e], wya * (i > 0 ? xr[0][b][e] : xr[1][b][e]));
-      o1[e] = fmaf(0.25f, xr[2][b][e], 0.75f * xr[1][b][e]);
+    for (int e = 0; e < E2; ++e) {
+      const f32x2 r0 = __builtin_elementwise_fma(wyb2, xr[1][b][e], wya2 * (i > 0 ? xr[0][b][e] : xr[1][b][e]));
+      const f32x2 r1 = __builtin_elementwise_fma(q1, xr[2][b][e], q3 * xr[1][b][e]);
+      o0[2 * e] = r0.x; o0[2 * e + 1] = r0.y;
+      o1[2 * e] = r1.x; o1[2 * e + 1] = r1.y;
     }
     const long long po = (long long)(n * H2 + 2 * i) * W2 + 2 * j0 + b;
     *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(o0);
@@ -1022,8 +1036,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES)))
       wxs[dx][1] = ok && x0 + 1 < w ? up2_adj_w(ox, w, x0 + 1) : 0.f;
     }
     const T* gn = g + (long long)n * H2 * W2 * gct + gco + c;
-    // horizontal partials of high-res row r (zero outside the image)
-    auto hrow = [&](int r, float (*hv)[E]) {
+    // horizontal partials of high-res row r (zero outside the image); packed fp32 (v_pk_fma_f32: two
+    // channels per instruction, each element rounded as the scalar fma rounds it)
+    constexpr int E2 = E / 2;
+    auto hrow = [&](int r, f32x2 (*hv)[E2]) {
       uint4 v[6];
 #pragma unroll
       for (int dx = 0; dx < 6; ++dx) {
@@ -1034,36 +1050,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES)))
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int j = 0; j < E; ++j) hv[b][j] = 0.f;
+        for (int j = 0; j < E2; ++j) hv[b][j] = (f32x2){0.f, 0.f};
 #pragma unroll
       for (int dx = 0; dx < 6; ++dx) {
         float f[E];
         Vec16<T>::unpack(v[dx], f);
+        const f32x2 w0 = {wxs[dx][0], wxs[dx][0]}, w1 = {wxs[dx][1], wxs[dx][1]};
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-          hv[0][j] = fmaf(wxs[dx][0], f[j], hv[0][j]);
-          hv[1][j] = fmaf(wxs[dx][1], f[j], hv[1][j]);
+        for (int j = 0; j < E2; ++j) {
+          const f32x2 fv = {f[2 * j], f[2 * j + 1]};
+          hv[0][j] = __builtin_elementwise_fma(w0, fv, hv[0][j]);
+          hv[1][j] = __builtin_elementwise_fma(w1, fv, hv[1][j]);
         }
       }
     };
     // row r feeds the outputs y with 2y-1 <= r <= 2y+2: carry the next output row's partial sums
     auto wrow = [&](int r, int y) { return (r >= 0 && r < H2 && y < h) ? up2_adj_w(r, h, y) : 0.f; };
-    float acur[2][E], anext[2][E], hv[2][E];
+    f32x2 acur[2][E2], anext[2][E2], hv[2][E2];
     hrow(2 * ys - 1, hv);
     {
       const float wa = wrow(2 * ys - 1, ys);
+      const f32x2 wa2 = {wa, wa};
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int j = 0; j < E; ++j) acur[b][j] = wa * hv[b][j];
+        for (int j = 0; j < E2; ++j) acur[b][j] = wa2 * hv[b][j];
     }
     hrow(2 * ys, hv);
     {
       const float wa = wrow(2 * ys, ys);
+      const f32x2 wa2 = {wa, wa};
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int j = 0; j < E; ++j) acur[b][j] = fmaf(wa, hv[b][j], acur[b][j]);
+        for (int j = 0; j < E2; ++j) acur[b][j] = __builtin_elementwise_fma(wa2, hv[b][j], acur[b][j]);
     }
 #pragma unroll 1
     for (int y = ys; y < ye; ++y) {
@@ -1077,19 +1097,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES)))
       for (int k = 1; k <= 2; ++k) {
         hrow(2 * y + k, hv);
         const float wc = wrow(2 * y + k, y), wn = wrow(2 * y + k, y + 1);
+        const f32x2 wc2 = {wc, wc}, wn2 = {wn, wn};
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int j = 0; j < E; ++j) {
-            acur[b][j] = fmaf(wc, hv[b][j], acur[b][j]);
-            anext[b][j] = k == 1 ? wn * hv[b][j] : fmaf(wn, hv[b][j], anext[b][j]);
+          for (int j = 0; j < E2; ++j) {
+            acur[b][j] = __builtin_elementwise_fma(wc2, hv[b][j], acur[b][j]);
+            anext[b][j] = k == 1 ? wn2 * hv[b][j] : __builtin_elementwise_fma(wn2, hv[b][j], anext[b][j]);
           }
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         if (x0 + b >= w) continue;
         const long long pix = (long long)(n * h + y) * w + x0 + b;
-        const uint4 packed = Vec16<TO>::pack(acur[b]);
+        float ac[E];
+#pragma unroll
+        for (int j = 0; j < E2; ++j) { ac[2 * j] = acur[b][j].x; ac[2 * j + 1] = acur[b][j].y; }
+        const uint4 packed = Vec16<TO>::pack(ac);
         *(uint4*)(o + pix * oct + oco + c) = packed;
         if constexpr (RED) {
           float gr[E], yv[E];
@@ -1106,7 +1130,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES)))
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int j = 0; j < E; ++j) acur[b][j] = anext[b][j];
+        for (int j = 0; j < E2; ++j) acur[b][j] = anext[b][j];
     }
   }
   if constexpr (RED) bnred_block<TO>(br, C, s1, s2);
