@@ -382,7 +382,7 @@ def _oracle_grads_autocast(base, cin, K, x, msk):
 
 
 BF16_GRAD_FLOOR = 3e-2  # relative L2: ~15 bf16 unit roundoffs (2^-9) compounded over 15 layers
-HEAD_BF16_GRAD_TOL = 5e-2  # explicit bound on the 2H head's parameter gradients (bf16 MFMA sums)
+HEAD_BF16_GRAD_TOL = 3e-2  # explicit bound on the 2H head's parameter gradients (bf16 MFMA sums; measured <= 1.7e-2)
 
 
 def test_bf16_train_grads_vs_fp64_oracle():
