@@ -546,13 +546,17 @@ def main():
     ngpu = torch.cuda.device_count()
     if ngpu < world and backend != "gloo":
         sys.exit(f"bench.py: {world} ranks need {world} GPUs, {ngpu} visible")
-    if world > 1:
-        dist.init_process_group(backend, init_method="env://")
-        if dist.get_world_size() != args.gpus:
-            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    # one process per GPU: bind the device before the process group, so RCCL's communicator is created on it
     local = local % max(1, ngpu)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group(backend, init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group(backend, init_method="env://")
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     from eunet import synth
     from eunet.engine import UNetEngine

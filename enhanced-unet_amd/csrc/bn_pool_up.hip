@@ -464,10 +464,9 @@ __global__ __launch_bounds__(256) void bnrelu_kernel(const T* y, long long P, in
 // gives the 2x2 outputs 2i+a, 2j+b with PyTorch's weights (0.25/0.75, edge rows
 // weighted 1/0 exactly as upsample_bilinear2d's clamped source index).
 template <typename T>
-#ifndef BNUP_WAVES
-#define BNUP_WAVES 1  // waves per SIMD the allocation must allow (1: its own 136 registers, 3 waves; 4: 497 -> 523 us)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BNUP_WAVES))) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
+// amdgpu_waves_per_eu(1): the allocation may use its own ~136 registers (3 waves per SIMD); forcing 4 ran
+// 497 -> 523 us
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
                                                         const float* sc, const float* sh, T* out, int oct, int oco) {
   // two horizontally adjacent low-res pixels (j0, j0 + 1) per thread: 3 x 4 neighbourhood loads
   // and transforms for 2 x 4 outputs each (9 per pixel before); rows are swept one at a time
@@ -892,10 +891,8 @@ struct BnUnit {
 // round(relu(y scale + shift)), recomputed here bit for bit from the y the BN-backward reduction
 // reads anyway, so the argmax (first maximum, NaN wins, as max_pool2d) is the same.
 template <typename T, bool RED = false>
-#ifndef POOLB_WAVES
-#define POOLB_WAVES 1  // (1: its own 165 registers, 3 waves; 4 spills 80 B: 699 -> 832 us per step)
-#endif
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(POOLB_WAVES))) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
+// amdgpu_waves_per_eu(1): its own ~165 registers, 3 waves per SIMD (4 spills 80 B: 699 -> 832 us per step)
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void pool_bwd_add_kernel(const T* act, int act_ct, int act_co, const T* gp, int gpct,
                                                           int gpco, const T* gs, int gsct, int gsco, T* go, int goct,
                                                           int goco, int N, int H, int W, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
@@ -1006,13 +1003,10 @@ __global__ void up_bwd_kernel(const T* g, int gct, int gco, TO* o, int oct, int 
 // the produced gradient, with the outputs' y loaded with the window rows (a load placed after a
 // store that may alias it would wait for the store).
 constexpr int UP_R = 8;
+// amdgpu_waves_per_eu(2): left alone the fused-reduction bf16 instance took 258 registers (1 wave / SIMD); at 2
+// it fits 256 and ran 959 -> 796 us per step
 template <typename T, typename TO, bool RED = false>
-#ifndef UP_WAVES
-// waves per SIMD the register allocation must allow: left alone the fused-reduction bf16 instance takes
-// 258 registers (1 wave / SIMD); at 2 it fits 256 + 12 B of scratch and runs 959 -> 796 us per step
-#define UP_WAVES 2
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UP_WAVES))) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void up_bwd_rows_kernel(const T* g, int gct, int gco, TO* o, int oct, int oco, int N,
                                                           int h, int w, int C, BnRed br) {
   constexpr int E = Vec16<T>::N;
   const int U = C / E, H2 = 2 * h, W2 = 2 * w, hr = (h + UP_R - 1) / UP_R, wb = (w + 1) / 2;
@@ -1427,9 +1421,7 @@ int eunet_conv_small_fwd(const eunet_act* x, const float* w, const float* bias, 
 int eunet_conv_small_wgrad_splits(const eunet_act* dy, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit, "conv_small_wgrad_splits: bad args");
   const int ntiles = dy->n * cdiv(dy->h, STH) * cdiv(dy->w, STW);
-#ifndef SMALL_WG_BLOCKS
-#define SMALL_WG_BLOCKS 512  // 768 / 1024 measured slower (enc1.0: 213 -> 283 / 309 us)
-#endif
+  constexpr int SMALL_WG_BLOCKS = 512;  // 768 / 1024 measured slower (enc1.0: 213 -> 283 / 309 us)
   int s = cdiv(SMALL_WG_BLOCKS, cdiv(dy->c, 64));
   s = s > ntiles ? ntiles : (s < 1 ? 1 : s);
   const int per = cdiv(ntiles, s);

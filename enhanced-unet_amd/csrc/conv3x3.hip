@@ -163,9 +163,6 @@ __device__ __forceinline__ uint32_t fwd_unit_off(const FwdArgs& a, int y0, int x
 // once per chunk, with the halo loads (not per unit after its data arrived: a dependent
 // global round trip per unit).
 
-#ifndef CONV_PRIO
-#define CONV_PRIO 1
-#endif
 // Diagnostic build only (tools/conv_stamps.py builds it with -DCONV_STAMP=1): wave 0 of every block
 // of conv3x3_fwd_kernel stamps s_memtime around its phases -- staging (+ its barriers), the MFMA
 // chunks (issue), the epilogue -- and writes per-block sums to g_conv_stamps (read back by
@@ -186,8 +183,8 @@ __device__ __forceinline__ unsigned long long conv_stamp() {
   return t;
 }
 #endif
-#ifndef CONV_BDMA
-#define CONV_BDMA 1
+#ifndef PRIO_STATIC
+#define PRIO_STATIC 0  // A/B builds only
 #endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
@@ -221,7 +218,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   f32x4 acc[MT][4];
   u32x4 ra[A_IT];
   uint32_t aoff[A_IT];  // byte offset of each halo unit in the sample slice (FWD_OOB: padding)
-  u32x4 rb[B_IT];
   char* const As = smem;
   char* const Bs = smem + FA_BYTES;
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
@@ -272,17 +268,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
       if constexpr (BTR)
         if (btr) ry[i] = __builtin_amdgcn_raw_buffer_load_b128(yr, cok ? aoff[i] + cadd : FWD_OOB, 0, 0);
-    }
-  };
-  auto gload_b = [&](int kc, int i0, int i1) {
-#pragma unroll
-    for (int i = i0; i < i1; ++i) {
-      const int id = tid + i * FT;
-      if (!B_TAIL || id < B_UNITS) {
-        const uint32_t wo = (uint32_t)((((kc * 4 + id / (BN * 9)) * a.cout_pad + co0) * 9 + id % (BN * 9)) * 16);
-        EUNET_DASSERT(wo + 16u <= (uint32_t)(a.nkc * KC * a.cout_pad * 9 * (int)sizeof(T)));
-        rb[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wo, 0, 0);
-      }
     }
   };
   // BN scale / shift of this thread's channel group, through descriptors too (no branch, so
@@ -361,13 +346,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       *(u32x4*)(As + fslot<PIX>(hp, qq) * 16) = v;
     }
   };
-  auto lwrite_b = [&](int i0, int i1) {
-#pragma unroll
-    for (int i = i0; i < i1; ++i) {
-      const int id = tid + i * FT;
-      if (!B_TAIL || id < B_UNITS) *(u32x4*)(Bs + id * 16) = rb[i];
-    }
-  };
   // weights straight into LDS (buffer_load ... lds: no staging VGPRs, no LDS write instructions); unit id =
   // tid + i * FT is LDS unit id, so wave-instruction i of wave w fills units i * FT + 64 w .. +63
   const int wvs = __builtin_amdgcn_readfirstlane(wv);
@@ -394,7 +372,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
                                                16, off, cadd, 0, 0);
     }
   };
-  constexpr int AH = A_IT / 2, BH = B_IT / 2;
+  constexpr int AH = A_IT / 2;
   auto chunk = [&]() {
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky)
@@ -430,8 +408,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   // start ~2.5k clocks late so one block's staging overlaps the other's MFMAs (ablation:
   // +15-20 % on every layer shape, profiles/r01_ab_phase.txt).
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
+  if (PRIO_STATIC && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // A/B: static priority, no flips
   auto stage_halves = [&](int kc) {
-    if (CONV_BDMA) dma_b(kc);
+    dma_b(kc);
     if (PIX && adma) {
       dma_a(kc);
       return;
@@ -445,20 +424,11 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       lwrite_a(kc, A3, 2 * A3);
       gload_a(kc, 2 * A3, A_IT);
       lwrite_a(kc, 2 * A3, A_IT);
-    } else if (CONV_BDMA == 2) {
-      gload_a(kc, 0, A_IT);
-      lwrite_a(kc, 0, A_IT);
     } else {
       gload_a(kc, 0, AH);
       lwrite_a(kc, 0, AH);
       gload_a(kc, AH, A_IT);
       lwrite_a(kc, AH, A_IT);
-    }
-    if (!CONV_BDMA) {
-      gload_b(kc, 0, BH);
-      lwrite_b(0, BH);
-      gload_b(kc, BH, B_IT);
-      lwrite_b(BH, B_IT);
     }
   };
   // co-block 0 of the fused BN-backward dgrad stores the tile interior of the staged gy (for the
@@ -487,12 +457,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   if (PIX && adma) {
     stage_halves(0);
   } else if (a.pro1) {  // first chunk in one round trip: the accumulators are not live yet
-    if (CONV_BDMA) dma_b(0);
+    dma_b(0);
     gload_affine(0);
     gload_a(0, 0, A_IT);
-    if (!CONV_BDMA) gload_b(0, 0, B_IT);
     lwrite_a(0, 0, A_IT);
-    if (!CONV_BDMA) lwrite_b(0, B_IT);
   } else {
     stage_halves(0);
   }
@@ -520,9 +488,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       st_stage += st_b - st_a;
 #endif
     }
-    if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
+    if (!PRIO_STATIC) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
     chunk();
-    if (CONV_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (!PRIO_STATIC) __builtin_amdgcn_s_setprio(0);
 #if CONV_STAMP
     st_a = conv_stamp();
     st_mfma += st_a - st_b;
@@ -911,16 +879,10 @@ __device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initiali
 //    so the 32 lanes of a transposed read (8 pixels x 4 channel quads) hit 64 distinct banks;
 //  - X halo [8 octants][HPXP]: odd channel octants start 4 slots (64 B) later, so the two octants
 //    a read spans fall in different banks.
-#ifndef WG_SWZ_D
-#define WG_SWZ_D 1
-#endif
-#ifndef WG_SWZ_X
-#define WG_SWZ_X 1
-#endif
-__device__ __forceinline__ int wd_swz(int p) { return WG_SWZ_D ? (p & 3) ^ (((p >> 3) & 1) << 2) : 0; }
-__device__ __forceinline__ int wx_shift(int oc) { return WG_SWZ_X ? (oc & 1) * 4 : 0; }
+__device__ __forceinline__ int wd_swz(int p) { return (p & 3) ^ (((p >> 3) & 1) << 2); }
+__device__ __forceinline__ int wx_shift(int oc) { return (oc & 1) * 4; }
 // last slot a bnrelu_x group of ni slots per thread reads (octant 7, thread pixel 31)
-constexpr int xo_max_slot(int ni) { return 7 * HPXP + (WG_SWZ_X ? 4 : 0) + 31 + 32 * (ni - 1); }
+constexpr int xo_max_slot(int ni) { return 7 * HPXP + 4 + 31 + 32 * (ni - 1); }
 
 // bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
 // w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
@@ -1129,7 +1091,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         f[ct] = cat_bf16x4(lo, hi);
       }
     };
-    if (CONV_PRIO) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
     for (int ks = 0; ks < TH; ++ks) {
       bf16x8 af[4];
@@ -1149,7 +1111,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         }
       }
     }
-    if (CONV_PRIO) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   }
   float* out = a.dw + (long long)split * a.cout * 9 * a.cin;
   const int ci = kc * KCW + wv * 16 + i16;
@@ -1595,20 +1557,14 @@ int eunet_conv3x3_dgrad_fused(const eunet_act* g, const eunet_act* y_in, const f
 
 // weight-gradient blocks per launch: two resident per CU (1024 / 2048 measured equal / slower in
 // the bench, where the wgrad shares the chip with the data-gradient stream: profiles/r02_ab_conv.txt)
-#ifndef WG_BLOCKS_N
-#define WG_BLOCKS_N 512
-#endif
-constexpr int WG_BLOCKS = WG_BLOCKS_N;  // weight-gradient blocks per launch (two per CU)
+constexpr int WG_BLOCKS = 512;  // weight-gradient blocks per launch (two per CU)
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
   const bool bf = dtype == EUNET_BF16;
   const int ntiles = dy->n * cdiv(dy->h, bf ? TH : WF_TH) * cdiv(dy->w, bf ? TW : WF_TW);
   const int blocks = cdiv(dy->c, 64) * cdiv(cin, bf ? KCW : WF_CI);
   int s = cdiv(WG_BLOCKS, blocks);
-#ifndef WG_FILL
-#define WG_FILL 1
-#endif
-  if (WG_FILL) {
+  {
     // fewest launch waves per unit of work: a split count whose blocks leave a nearly empty last wave
     // (the decoder's concat inputs: 48 / 12 / 3 block columns -> 528 / 516 / 513 blocks) runs that
     // wave's tail alone; pick s in [s0/2, 2 s0] minimising waves / s (ties: fewer splits)

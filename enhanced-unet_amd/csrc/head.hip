@@ -1344,10 +1344,6 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
 // algebra is folded into 4 per-channel constants, evaluated two channels per packed fp32 op,
 //   pre = h P + Q,   g_h = P gbn + h D + E   (D = -P c2 is, E = -P (c2 off + c1)),
 // and the constant A fragments (W1 for h, W2^T for s, W1^T for v) are read from LDS.
-#ifndef HEAD_ABL
-#define HEAD_ABL 0  // diagnostic builds only (tools/abl_build.sh): 1 skips the g_u / upsample-adjoint phases,
-                    // 2 the W1-gradient MFMAs
-#endif
 // The per-tap products are reduced over kx in registers as they leave the MFMA.
 // The v MFMA's A rows are ordered so that lane (q, x) receives, for the combination cmb = (k, ky) =
 // 4 jb + q, the three kx taps of pixel x (C rows 4q + kx); two row_shr DPP moves within the 16-lane
@@ -1538,7 +1534,6 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
         *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
       }
-      if (HEAD_ABL & 2) continue;
       // gw is wave-private: the wave's own LDS writes are in order before its reads (no block barrier)
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       __builtin_amdgcn_wave_barrier();
@@ -1569,7 +1564,6 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     hs_a = head_stamp();
     hs_rows += hs_a - hs_b;
 #endif
-    if (HEAD_ABL & 1) continue;
     // g_u over the region rows / cols oy0-1 .. oy0+16 (into su, free now), zero outside the image;
     // branch-free: out-of-tile taps read a clamped index and add zero
     for (int i = tid; i < 18 * 18; i += NT) {
