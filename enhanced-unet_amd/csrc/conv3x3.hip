@@ -183,9 +183,6 @@ __device__ __forceinline__ unsigned long long conv_stamp() {
   return t;
 }
 #endif
-#ifndef PRIO_STATIC
-#define PRIO_STATIC 0  // A/B builds only
-#endif
 // DG: a tag only (the same code either way) so the dgrad launches carry their own symbol --
 // rocprofv3 and the bench report forward and data-gradient launches separately.
 // TO: the output element type -- T, or float for a bf16 data gradient whose consumer keeps fp32
@@ -408,7 +405,6 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   // start ~2.5k clocks late so one block's staging overlaps the other's MFMAs (ablation:
   // +15-20 % on every layer shape, profiles/r01_ab_phase.txt).
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);
-  if (PRIO_STATIC && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);  // A/B: static priority, no flips
   auto stage_halves = [&](int kc) {
     dma_b(kc);
     if (PIX && adma) {
@@ -488,9 +484,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
       st_stage += st_b - st_a;
 #endif
     }
-    if (!PRIO_STATIC) __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
+    __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
     chunk();
-    if (!PRIO_STATIC) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
 #if CONV_STAMP
     st_a = conv_stamp();
     st_mfma += st_a - st_b;
