@@ -85,13 +85,14 @@ constexpr int FTH = 16, FTW = 32;            // output tile
 constexpr int FHW = FTW + 2;                 // 34
 constexpr int FHPX = (FTH + 2) * FHW;        // 612 halo pixels
 constexpr int FHPXP = 640;                   // halo pixel slots (612 used), 4 channel quarters each
-// LDS slot (16 B) of halo pixel hp's channel quarter q.  Plane-major [q][hp] (PIX = false: the forward
-// and the fused-apply data gradient, register staging) or pixel-major [hp][q] (PIX = true: the plain data
-// gradient, staged by LDS-DMA -- a wave-instruction then reads 16 pixels x 64 contiguous bytes from global;
+// LDS slot (16 B) of halo pixel hp's channel quarter q.  Plane-major [q][hp] (PIX = false: the forward with
+// the BN+ReLU operand transform and the fused-apply data gradient, register staging) or pixel-major [hp][q]
+// (PIX = true: the plain data gradient and the untransformed forward, staged by LDS-DMA -- a wave-instruction then reads 16 pixels x 64 contiguous bytes from global;
 // plane-major slots would read 64 pixels x 16 B and measured slower, profiles/r04_ab.txt).  Measured per
 // layout (13 layers, tools/conv_bench.py): the forward loses 2 % pixel-major (4-way bank conflicts of the
 // fragment reads) and 6 % with the quarter XOR-swizzle that removes them (its per-read address VALU), the
-// DMA-staged data gradient gains 6 % -- so the layout follows the instantiation.
+// DMA-staged data gradient gains 6 %, the DMA-staged untransformed forward 5-13 % -- so the layout follows the
+// staging.
 template <bool PIX>
 __device__ __forceinline__ int fslot(int hp, int q) {
   return PIX ? hp * 4 + q : q * FHPXP + hp;
@@ -191,7 +192,10 @@ __device__ __forceinline__ unsigned long long conv_stamp() {
 // own instantiation, so the plain data-gradient launches keep their register allocation.
 // BNB: the fused BN-backward reduction of the dgrad epilogue (a.bpart set) -- a template parameter so the
 // forward and the plain data-gradient launches carry none of its code.
-template <typename T, bool DG, typename TO = T, bool BT = false, bool BNB = false>
+// PF: a bf16 forward without an operand transform (a DoubleConv's conv .0: its input is stored post-BN+ReLU)
+// stages its halo by LDS-DMA like the plain data gradient (pixel-major slots, no staging registers):
+// bit-identical, 5-13 % faster per layer standalone, -7 % over the six .0 layers (profiles/r05_ab.txt r5o).
+template <typename T, bool DG, typename TO = T, bool BT = false, bool BNB = false, bool PF = false>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   char* const Bs = smem + FA_BYTES;
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   // this thread's halo quarter (fwd_unit), the same for every unit (ids tid + FT i)
-  constexpr bool PIX = DG && !BT && sizeof(T) == 2;  // halo layout / staging (fslot)
+  constexpr bool PIX = ((DG && !BT) || PF) && sizeof(T) == 2;  // halo layout / staging (fslot)
   const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -1359,6 +1363,7 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, 
     else go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true, false>);
   } else if (dtype == EUNET_BF16) {
     if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, false, true>);
+    else if (!DG && a.isc == nullptr) go(conv3x3_fwd_kernel<bf16_t, false, bf16_t, false, false, true>);
     else go(conv3x3_fwd_kernel<bf16_t, DG>);
   } else {
     if (bnb) go(conv3x3_fwd_kernel<float, true, float, false, true>);
