@@ -110,4 +110,34 @@ int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream) {
   return EUNET_OK;
 }
 
+// Stream-to-stream ordering on the current device: `to` waits for the work enqueued on `from` so far.  The
+// events have a device-scope release and no timing (torch's Stream.wait_stream records an event with the
+// default system-scope release, whose cache writeback / invalidate sits between the producing kernel and
+// the recording stream's next kernel).  A ring of events per device; re-recording one whose wait is
+// already enqueued is allowed (the wait captured the earlier record).
+int eunet_stream_wait(void* from, void* to) {
+  constexpr int NDEV = 64, RING = 64;
+  static std::mutex mu;
+  static hipEvent_t ring[NDEV][RING];
+  static int next[NDEV];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= NDEV) {
+    eunet::set_error("stream_wait: no current device (or device index >= %d)", NDEV);
+    return EUNET_ERR_HIP;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  hipEvent_t& e = ring[dev][next[dev]++ % RING];
+  if (e == nullptr &&
+      hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
+    e = nullptr;
+    eunet::set_error("stream_wait: hipEventCreateWithFlags failed");
+    return EUNET_ERR_HIP;
+  }
+  if (hipEventRecord(e, (hipStream_t)from) != hipSuccess || hipStreamWaitEvent((hipStream_t)to, e, 0) != hipSuccess) {
+    eunet::set_error("stream_wait: record / wait failed");
+    return EUNET_ERR_HIP;
+  }
+  return EUNET_OK;
+}
+
 }  // extern "C"

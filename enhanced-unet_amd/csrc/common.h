@@ -1,6 +1,10 @@
 // Shared device/host helpers for libeunet_hip (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <utility>
+#include <vector>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -212,7 +216,16 @@ int eunet_colsum_segs(const float* part, int rows, int cols, int ld, const ColSe
 // kernels with > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
 template <typename K>
 inline void allow_lds(K* kernel, size_t bytes) {
-  if (bytes > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (bytes <= 65536) return;
+  // once per kernel (the attribute persists): a table of the kernels already raised, under a lock (the
+  // forward and autograd's backward thread both launch)
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, size_t>> done;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const auto& d : done)
+    if (d.first == (const void*)kernel && d.second >= bytes) return;
+  (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  done.emplace_back((const void*)kernel, bytes);
 }
 
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -50,6 +50,7 @@ _f = c_void_p  # float* / void* device pointers are passed as integers
 # name -> argtypes (restype is always c_int except the two string getters)
 SIGNATURES = {
     "eunet_nchw_to_nhwc": [_f, _P, c_void_p],
+    "eunet_stream_wait": [c_void_p, c_void_p],
     "eunet_conv3x3_packed_bytes": [c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_conv3x3_pack": [_f, c_int, c_int, c_int, _f, c_int, c_void_p],
     "eunet_conv3x3_pack_many": [c_void_p, c_int, c_int, c_void_p],
@@ -196,7 +197,8 @@ def load(path: str = LIB_PATH):
 # kprof.BusyTimer installs itself here: every launching entry point is then bracketed by events on
 # torch's current stream (the stream the C-ABI enqueues on), for the whole-step kernel-busy figure
 BUSY_HOOK = None
-_NO_LAUNCH = ("_tiles", "_bytes", "_splits", "_rows", "_len", "_params", "debug_", "_table", "lab_tables")
+_NO_LAUNCH = ("_tiles", "_bytes", "_splits", "_rows", "_len", "_params", "debug_", "_table", "lab_tables",
+              "stream_wait")
 
 
 def call(name: str, *args):

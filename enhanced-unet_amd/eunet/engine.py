@@ -130,10 +130,21 @@ class UNetEngine:
     # alternating pairs (profiles/r04_ab.txt) -- like dgrad_first, a data gradient that reaches the CUs
     # before the side stream's weight gradients costs the step more than the gap.  Off.
     fork_once = False
+    # device_fence_forks -- the side stream's forks and joins wait through eunet_stream_wait (events with a
+    # device-scope release) instead of torch's Stream.wait_stream (a system-scope release: an L2 writeback
+    # and invalidate on the launch stream at every fork)
+    device_fence_forks = True
     # keep_state -- tests: the last training forward's saved tensors (pre-BN conv outputs, BN affines)
     # stay reachable as self.last_state, so a checker can read the branch configuration (ReLU masks,
     # max-pool argmax) the kernels took (tests/_pins.py)
     keep_state = False
+
+    def _wait(self, to, frm):
+        """stream `to` waits for the work enqueued on `frm` so far"""
+        if self.device_fence_forks:
+            ops.stream_wait(frm, to)
+        else:
+            to.wait_stream(frm)
 
     def __init__(self, model, prefix: str = "model."):
         self.m = model
@@ -332,7 +343,7 @@ class UNetEngine:
             if ready is not None:
                 side.wait_event(ready)  # recorded on the launch stream once gy was complete
             else:
-                side.wait_stream(main)  # gy (and everything before it) is ready
+                self._wait(side, main)  # gy (and everything before it) is ready
             with torch.cuda.stream(side):
                 wgrad_on_stream(xa, gy, dw, db, scale, shift, small_conv)
             for t in (gy, xa._keep, dw, db):  # the caching allocator must not hand these out early
@@ -398,7 +409,7 @@ class UNetEngine:
             if ev is not None:
                 side.wait_event(ev)
             else:
-                side.wait_stream(main)
+                self._wait(side, main)
             with torch.cuda.stream(side):
                 sink.ready(names)
         if not need_gx:
@@ -469,7 +480,7 @@ class UNetEngine:
         if side is None:
             sink.ready(names)
         else:  # a bucket all-reduce launched here orders after both streams' work, without stalling main
-            side.wait_stream(main)
+            self._wait(side, main)
             with torch.cuda.stream(side):
                 sink.ready(names)
         return gx
@@ -583,7 +594,7 @@ class UNetEngine:
         del g_p1, g_cat2
         self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True, gred=red)
         if self.overlap_wgrad:
-            torch.cuda.current_stream(dev).wait_stream(side_stream(dev))
+            self._wait(torch.cuda.current_stream(dev), side_stream(dev))
         # the caller finishes the sink: the dual-branch model runs two trunks into one sink (finishing it
         # here made a DataParallel BucketSink wait for buckets the second trunk had not filled yet)
 

@@ -101,6 +101,12 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def stream_wait(frm: torch.cuda.Stream, to: torch.cuda.Stream):
+    """`to` waits for the work enqueued on `frm` so far: eunet_stream_wait (a device-scope event release,
+    where torch's Stream.wait_stream records a system-scope one)."""
+    call("eunet_stream_wait", ctypes.c_void_p(frm.cuda_stream), ctypes.c_void_p(to.cuda_stream))
+
+
 def _ptr(t):
     if t is None:
         return None

@@ -50,6 +50,11 @@ const char* eunet_last_error(void);
  * images.to(device) + NCHW->NHWC (train_eval.py:242); x [N,C,H,W] fp32 */
 int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
 
+/* ---- stream ordering (the backward's weight-gradient side stream; no reference counterpart: the
+ * reference's backward is one stream, train_eval.py:230-243) -------------------------------------
+ * `to` waits for everything enqueued on `from` so far (device-scope event release, no timing). */
+int eunet_stream_wait(void* from, void* to);
+
 /* ---- Conv2d 3x3, padding 1 (models.py:219,222 / autograd) -----------------
  * Weights are re-packed every step from the fp32 torch parameter
  * [Cout][Cin][3][3] into the MFMA-ready layout.  transpose_flip=1 packs the
