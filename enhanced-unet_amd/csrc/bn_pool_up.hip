@@ -243,9 +243,29 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       const int id = tid + k * NT;
       const int px = id / (64 / E), u = id - px * (64 / E);
       *(uint4*)(gs + px * 64 + u * E) = rd[k];
+      if constexpr (E == 8) {  // bf16: the bias gradient from the staged registers -- unit id holds channels
+                               // 8 (tid & 7) .. + 7 of pixel (tid >> 3) + 32 k, the dbv mapping below
+        float f[E];
+        Vec16<T>::unpack(rd[k], f);
+#pragma unroll
+        for (int e = 0; e < E; ++e) dbv[e] += f[e];
+      }
     }
     if (tile + 1 < t_end) load_tile(tile + 1);
     __syncthreads();
+    if constexpr (E != 8) {  // fp32: the thread's 8 channels span two units -- from the staged tile
+#pragma unroll
+      for (int i = 0; i < STH * STW / 32; ++i) {  // independent 16-B reads, no wait per element
+        const T* src = gs + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8;
+#pragma unroll
+        for (int h = 0; h < 8 / E; ++h) {
+          float f[E];
+          Vec16<T>::unpack(*(const uint4*)(src + h * E), f);
+#pragma unroll
+          for (int e = 0; e < E; ++e) dbv[h * E + e] += f[e];
+        }
+      }
+    }
 #pragma unroll 4
     for (int id = tid; id < STH * STW * icw; id += NT) {
       const int px = id / icw, j = id - px * icw;
@@ -258,17 +278,6 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
       Elem<T>::st(cs + id, v);
     }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < STH * STW / 32; ++i) {  // independent 16-B reads, no wait per element
-      const T* src = gs + ((tid >> 3) + 32 * i) * 64 + (tid & 7) * 8;
-#pragma unroll
-      for (int h = 0; h < 8 / E; ++h) {
-        float f[E];
-        Vec16<T>::unpack(*(const uint4*)(src + h * E), f);
-#pragma unroll
-        for (int e = 0; e < E; ++e) dbv[h * E + e] += f[e];
-      }
-    }
     const int cw = wv * 16;
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
