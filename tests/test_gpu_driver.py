@@ -97,3 +97,48 @@ def test_deferred_steps_bound_the_host_run_ahead():
         out.append({k: v.detach().clone() for k, v in model.state_dict().items()})
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_stream_wait_orders_the_side_stream():
+    """eunet_stream_wait (the engine's side-stream forks / joins, device-scope event release): work enqueued on
+    `to` after the wait sees everything enqueued on `from` before it, across a long producer (the consumer
+    would otherwise read the tensor mid-write), for many forks in a row (the event ring wraps)."""
+    from eunet import ops
+    main, side = torch.cuda.current_stream(), torch.cuda.Stream()
+    n = 1 << 24
+    a = torch.zeros(n, device=DEV)
+    for i in range(80):  # > the ring of 64 events per device
+        big = torch.full((n,), float(i + 1), device=DEV)
+        for _ in range(3):
+            big = big * 1.0 + 0.0  # a few dependent kernels: the producer runs for a while
+        a.copy_(big)
+        ops.stream_wait(main, side)
+        with torch.cuda.stream(side):
+            b = a.clone()
+        ops.stream_wait(side, main)
+        a.record_stream(side)
+        b.record_stream(main)
+        assert float(b[0]) == float(i + 1) and float(b[-1]) == float(i + 1)
+    # the engine's knob: the same step with torch's wait_stream is bit-identical
+    from eunet.engine import UNetEngine
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    x = torch.rand(2, 1, 64, 64, device=DEV)
+    m = torch.randint(0, 2, (2, 64, 64), device=DEV)
+    out = []
+    for dev_fence in (True, False):
+        old = UNetEngine.device_fence_forks
+        UNetEngine.device_fence_forks = dev_fence
+        try:
+            torch.manual_seed(1)
+            model = EnhancedUNet(num_classes=2, in_channels=1, base_ch=16, dtype="bf16").to(DEV)
+            tr = Trainer(model, DEV, "enhanced_unet", total_epochs=50)
+            tr.epoch_lr_step(0)
+            for _ in range(2):
+                tr.step(x, m)
+            torch.cuda.synchronize()
+            out.append({k: v.detach().clone() for k, v in model.state_dict().items()})
+        finally:
+            UNetEngine.device_fence_forks = old
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
