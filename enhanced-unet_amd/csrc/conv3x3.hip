@@ -28,6 +28,7 @@
 // wave-group-skewed one in round 2), other block orders) are recorded in DESIGN.md §4 and
 // profiles/r0*_ab_*; their code lives in the git history, not in this file.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -195,7 +196,11 @@ __device__ __forceinline__ unsigned long long conv_stamp() {
 // PF: a bf16 forward without an operand transform (a DoubleConv's conv .0: its input is stored post-BN+ReLU)
 // stages its halo by LDS-DMA like the plain data gradient (pixel-major slots, no staging registers):
 // bit-identical, 5-13 % faster per layer standalone, -7 % over the six .0 layers (profiles/r05_ab.txt r5o).
-template <typename T, bool DG, typename TO = T, bool BT = false, bool BNB = false, bool PF = false>
+// CT: the layer has a tail co-block whose channels past co0 + 32 are all padding (cout mod 64 in 1..32: the
+// 96 / 288-channel layers of base 96, configs[4]); that block runs a second copy of the K loop over co tiles
+// 0-1 only (half the MFMAs).  Its own instantiation: the copy's registers cost the other layers 0.2-0.5 %
+// (profiles/r05_ab.txt r5v), and a uniform branch inside the MFMA loop 2-10 % (r5u).
+template <typename T, bool DG, typename TO = T, bool BT = false, bool BNB = false, bool PF = false, bool CT = false>
 __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int NW = 4;                       // waves
   constexpr int RPW = FTH / NW;               // output rows per wave
@@ -374,21 +379,22 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     }
   };
   constexpr int AH = A_IT / 2;
-  auto chunk = [&]() {
+  auto chunk = [&](auto ntc) {  // NTC output tiles of 16 channels
+    constexpr int NTC = decltype(ntc)::value;
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const int t = ky * 3 + kx;
-        uint4 fb[4];
+        uint4 fb[NTC];
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
+        for (int nt = 0; nt < NTC; ++nt) fb[nt] = *(const uint4*)(Bs + (q * (BN * 9) + (nt * 16 + li) * 9 + t) * 16);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int hp = (RPW * wv + (mt >> 1) + ky) * FHW + (mt & 1) * 16 + li + kx;
           const uint4 fa = *(const uint4*)(As + fslot<PIX>(hp, q) * 16);
 #pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
+          for (int nt = 0; nt < NTC; ++nt) {
             if constexpr (sizeof(T) == 2) {
               acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
@@ -489,7 +495,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #endif
     }
     __builtin_amdgcn_s_setprio(1);  // the MFMA phase issues ahead of the other block's staging
-    chunk();
+    if (CT && co0 + BN / 2 >= a.cout)  // (block-uniform)
+      chunk(std::integral_constant<int, 2>{});
+    else
+      chunk(std::integral_constant<int, 4>{});
     __builtin_amdgcn_s_setprio(0);
 #if CONV_STAMP
     st_a = conv_stamp();
@@ -1362,9 +1371,18 @@ int launch_fwd(const FwdArgs& a, int dtype, void* stream, bool out_f32 = false, 
     if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true, true>);
     else go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, true, false>);
   } else if (dtype == EUNET_BF16) {
-    if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, false, true>);
-    else if (!DG && a.isc == nullptr) go(conv3x3_fwd_kernel<bf16_t, false, bf16_t, false, false, true>);
-    else go(conv3x3_fwd_kernel<bf16_t, DG>);
+    const int tail = a.cout % BN;
+    if (tail > 0 && tail <= BN / 2) {  // a half-empty tail co-block: the CT instantiations
+      if (bnb) go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, false, true, false, true>);
+      else if (!DG && a.isc == nullptr) go(conv3x3_fwd_kernel<bf16_t, false, bf16_t, false, false, true, true>);
+      else go(conv3x3_fwd_kernel<bf16_t, DG, bf16_t, false, false, false, true>);
+    } else if (bnb) {
+      go(conv3x3_fwd_kernel<bf16_t, true, bf16_t, false, true>);
+    } else if (!DG && a.isc == nullptr) {
+      go(conv3x3_fwd_kernel<bf16_t, false, bf16_t, false, false, true>);
+    } else {
+      go(conv3x3_fwd_kernel<bf16_t, DG>);
+    }
   } else {
     if (bnb) go(conv3x3_fwd_kernel<float, true, float, false, true>);
     else go(conv3x3_fwd_kernel<float, DG>);
