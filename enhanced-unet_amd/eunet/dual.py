@@ -33,6 +33,11 @@ BRANCHES = ("unetpp", "deeplab")
 
 
 class DualEngine:
+    # narrow_mfma -- fusion_head.0 (2K -> 256 channels, 3x3) on the MFMA forward over f2's 8 zero-padded
+    # channels instead of conv_small_fwd's per-pixel FMAs (3.7 ms per launch at configs[4]): HBM-bound on its
+    # output (profiles/r05_ab.txt r5d)
+    narrow_mfma = True
+
     def __init__(self, model):
         self.m = model
         self.K = model.num_classes
@@ -85,7 +90,11 @@ class DualEngine:
         # ---- fusion head (models.py:285-294)
         y1 = _e((N, H, W, HEAD_CH[0]), dt, dev)
         st, ct = self.ea._stats_buf(y1) if training else (None, 0)
-        ops.conv_small_fwd(ops.act(f2, 0, 2 * K), P["fusion_head.0.weight"].contiguous(), None, ops.act(y1), st)
+        if self.narrow_mfma:
+            ops.conv3x3_fwd_narrow(ops.act(f2), 2 * K, ops.conv3x3_pack(P["fusion_head.0.weight"], dt, flip=False),
+                                   ops.act(y1), stats=st)
+        else:
+            ops.conv_small_fwd(ops.act(f2, 0, 2 * K), P["fusion_head.0.weight"].contiguous(), None, ops.act(y1), st)
         h1 = bn("fusion_head.1", st, ct, HEAD_CH[0], training, P, B)
         d1 = self._dropout(h1, 0, N, training, dev)
         y2 = _e((N, H, W, HEAD_CH[1]), dt, dev)

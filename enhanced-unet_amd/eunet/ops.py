@@ -256,6 +256,18 @@ def conv_small_fwd(x: Act, w, bias, y: Act, stats=None):
     call("eunet_conv_small_fwd", ctypes.byref(x), _ptr(w), _ptr(bias), ctypes.byref(y), _ptr(stats), _stream())
 
 
+def conv3x3_fwd_narrow(x: Act, cin: int, wp, y: Act, bias=None, stats=None):
+    """A few-channel conv (cin < 8) on the MFMA forward: x is a view of 8 channels whose channels >= cin
+    are zero and wp packs the [cout][cin] weights (its padding is zero too).  Timed as the HBM-bound
+    "conv_small" family with its true FLOPs, outside the conv3x3 MFMA roofline family."""
+    flops = 2.0 * 9 * cin * y.c * x.n * x.h * x.w
+    esz = 2 if x.dtype == _lib.EUNET_BF16 else 4
+    nbytes = float(esz * x.n * x.h * x.w * (x.c + y.c))
+    with kprof.timed("conv_small", flops, nbytes):
+        call("eunet_conv3x3_fwd", ctypes.byref(x), None, None, 0, _ptr(wp), _ptr(bias), ctypes.byref(y),
+             _ptr(stats), _stream())
+
+
 def conv_small_wgrad_splits(dy: Act) -> int:
     s = c_int()
     call("eunet_conv_small_wgrad_splits", ctypes.byref(dy), ctypes.byref(s))

@@ -18,6 +18,9 @@ for kv in sets:
     k, v = kv.split("=")
     if k.startswith("ops."):  # module switches of eunet.ops (e.g. ops.USE_DISPATCHER=0)
         setattr(ops, k[4:], bool(int(v)))
+    elif k.startswith("dual."):  # DualEngine attributes (e.g. dual.narrow_mfma=0)
+        from eunet.dual import DualEngine
+        setattr(DualEngine, k[5:], bool(int(v)))
     elif v.startswith("{"):  # a per-block knob: fuse_bn_apply={enc4,dec4}
         setattr(UNetEngine, k, frozenset(x for x in v.strip("{}").split(",") if x))
     else:
