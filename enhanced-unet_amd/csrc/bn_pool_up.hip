@@ -183,7 +183,7 @@ template <typename T, int CI>  // CI = max input channels of the instance (4: en
 __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
   constexpr int SCI = CI, SJT = (CI * 9 + 15) / 16;  // LDS sized per instance (occupancy)
   constexpr int E = Vec16<T>::N;
-  __shared__ float xs[(STH + 2) * (STW + 2) * SCI];
+  __shared__ __attribute__((aligned(16))) float xs[(STH + 2) * (STW + 2) * SCI];
   __shared__ __attribute__((aligned(16))) T gs[STH * STW * 64];         // dY tile [256 px][64 co]
   __shared__ __attribute__((aligned(16))) T cs[STH * STW * SJT * 16];  // im2col [256 px][icw]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -266,16 +266,32 @@ __global__ __launch_bounds__(NT) void conv_small_wgrad_kernel(SmallWgArgs a) {
         }
       }
     }
-#pragma unroll 4
-    for (int id = tid; id < STH * STW * icw; id += NT) {
-      const int px = id / icw, j = id - px * icw;
-      float v = 0.f;
-      if (j < cin * 9) {
-        const int ci = j / 9, t = j - ci * 9;
+    {  // the im2col row of pixel px = tid: column j = ci * 9 + t, zero past cin * 9 (to icw).  Nine 16-byte
+       // reads of the halo (a tap's SCI channels at once) and icw / E 16-byte writes per thread (one element
+       // per read / write with per-element index arithmetic before: VALU-bound)
+      static_assert(STH * STW == NT, "one im2col row per thread");
+      const int px = tid, r = px / STW, c = px % STW;
+      float v[CI * 9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
-        v = xs[((px / STW + ky) * (STW + 2) + (px % STW) + kx) * SCI + ci];
+        const float* src = xs + ((r + ky) * (STW + 2) + c + kx) * SCI;
+#pragma unroll
+        for (int qq = 0; qq < CI / 4; ++qq) {
+          const f32x4 f = *(const f32x4*)(src + 4 * qq);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[(4 * qq + e) * 9 + t] = 4 * qq + e < cin ? f[e] : 0.f;  // (past cin: unstaged)
+        }
       }
-      Elem<T>::st(cs + id, v);
+      T* const dst = cs + px * icw;
+#pragma unroll
+      for (int u = 0; u < SJT * 16 / E; ++u) {
+        if (u * E >= icw) break;
+        float f[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) f[e] = u * E + e < CI * 9 ? v[u * E + e] : 0.f;
+        *(uint4*)(dst + u * E) = Vec16<T>::pack(f);
+      }
     }
     __syncthreads();
     const int cw = wv * 16;
