@@ -81,7 +81,9 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { mean[e] = 0.f; m2[e] = 0.f; }
   constexpr int E = Vec16<T>::N;
-  const bool full = (co0 + 64 <= a.cout) && ((a.yct | a.yco) % E) == 0;
+  // whole 16-byte stores for every lane whose 8 channels exist (per lane: the 96-channel layers' second
+  // co-block holds 32; element stores there ran enc1.0 at 2.1 TB/s at configs[4])
+  const bool full = (co0 + 8 * g + 8 <= a.cout) && ((a.yct | a.yco) % E) == 0;
   for (int pass = 0; pass < SFH; ++pass) {
     const int px = pass * 32 + ps;
     const int r = px / STW, c = px - r * STW;
