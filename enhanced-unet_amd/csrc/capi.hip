@@ -119,7 +119,7 @@ int eunet_stream_wait(void* from, void* to) {
   constexpr int NDEV = 64, RING = 64;
   static std::mutex mu;
   static hipEvent_t ring[NDEV][RING];
-  static int next[NDEV];
+  static unsigned next[NDEV];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= NDEV) {
     eunet::set_error("stream_wait: no current device (or device index >= %d)", NDEV);
