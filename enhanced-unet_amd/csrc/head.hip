@@ -681,7 +681,10 @@ __device__ __forceinline__ void load_a_w1(const float* w1, int lane, bf16x8 (&A)
     for (int jj = 0; jj < 8; ++jj) A[cb][jj] = (__bf16)(8 * q + jj < K * 9 ? f[8 * cb + jj] : 0.f);
 }
 
-// per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner (su row stride RS)
+// per-lane su offsets of im2col^T[j = 8q + jj][px] relative to the pixel's window corner (su row stride RS).
+// The padding entries j >= 9K read the window corner (offset 0) instead of a zero: every consumer's W1
+// fragment (load_a_w1) is zero at those k, and the staged u is finite, so they add exact zeros -- the
+// fragment is 8 reads and 4 v_cvt_pk_bf16_f32 with no per-entry select and repack.
 template <int K, int RS = 18>
 __device__ __forceinline__ void im2col_offsets(int q, int (&off)[8]) {
 #pragma unroll
@@ -691,19 +694,16 @@ __device__ __forceinline__ void im2col_offsets(int q, int (&off)[8]) {
       const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
       off[jj] = (ky * RS + kx) * 3 + k;
     } else {
-      off[jj] = -1;
+      off[jj] = 0;
     }
   }
 }
 
 __device__ __forceinline__ bf16x8 im2col_frag(const float* su, int base, const int (&off)[8]) {
-  bf16x8 b;
+  uint32_t w[4];
 #pragma unroll
-  for (int jj = 0; jj < 8; ++jj) {
-    const float v = su[base + (off[jj] < 0 ? 0 : off[jj])];
-    b[jj] = (__bf16)(off[jj] < 0 ? 0.f : v);
-  }
-  return b;
+  for (int i = 0; i < 4; ++i) w[i] = pk_bf16(su[base + off[2 * i]], su[base + off[2 * i + 1]]);
+  return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
 }
 
 // h^T (bias excluded) for the pixel row segment whose window corner is su[base]
@@ -1444,7 +1444,7 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
       const int k = j / 9, t = j - 9 * k, ky = t / 3, kx = t - 3 * ky;
       boff[jb] = (((q >> 1) + ky) * 18 + 8 * (q & 1) + kx) * 3 + k;
     } else {
-      boff[jb] = -1;
+      boff[jb] = 0;
     }
   }
   f32x4 accW[4][2];
@@ -1540,12 +1540,12 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
       const int r0 = 4 * wv + 2 * rp;
       bf16x8 Bw[2];
 #pragma unroll
-      for (int jb = 0; jb < 2; ++jb)
+      for (int jb = 0; jb < 2; ++jb) {  // (columns j >= 9K read finite u at boff 0; their sums are never stored)
+        uint32_t w[4];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const float v = su[r0 * 54 + (boff[jb] < 0 ? 0 : boff[jb]) + 3 * jj];
-          Bw[jb][jj] = (__bf16)(boff[jb] < 0 ? 0.f : v);
-        }
+        for (int i = 0; i < 4; ++i) w[i] = pk_bf16(su[r0 * 54 + boff[jb] + 6 * i], su[r0 * 54 + boff[jb] + 6 * i + 3]);
+        Bw[jb] = __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
+      }
       const int pxa = 8 * q + q4;
 #pragma unroll
       for (int pb = 0; pb < 4; ++pb) {
