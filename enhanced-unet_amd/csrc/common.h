@@ -200,6 +200,16 @@ __device__ __forceinline__ float up2_adj_w(int o, int in, int i) {
   return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
 }
 
+// the same weights of low-res index i (0 <= i < in) for the four high-res positions 2i-1 .. 2i+2 that can reach it,
+// in closed form: (1/4, 3/4, 3/4, 1/4) inside, (0, 1, 3/4, 1/4) at i = 0 and (1/4, 3/4, 1, 0) at i = in-1 (both
+// edges at in = 1: (0, 1, 1, 0)); positions outside 0 .. 2in-1 weigh 0.  Equal to up2_adj_w value by value.
+__device__ __forceinline__ f32x4 up2_adj_w4(int i, int in) {
+  f32x4 w = {0.25f, 0.75f, 0.75f, 0.25f};
+  if (i == 0) { w[0] = 0.f; w[1] = 1.f; }
+  if (i == in - 1) { w[2] = 1.f; w[3] = 0.f; }
+  return w;
+}
+
 // deterministic fp64 column sum of a [rows][ld] partial matrix (bn_pool_up.hip); columns
 // >= split go to out_hi[col - split] when out_hi != nullptr
 int eunet_colsum_ld(const float* part, int rows, int cols, int ld, float* out, void* ws, hipStream_t s,

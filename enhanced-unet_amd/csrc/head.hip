@@ -753,11 +753,22 @@ __device__ __forceinline__ float f4(const float4& v, int i) { return i == 0 ? v.
 __device__ __forceinline__ f32x4 ld4v(const float* p) { return *(const f32x4*)p; }
 __device__ __forceinline__ f32x2 half2(const f32x4& v, int hp) { return hp ? v.hi : v.lo; }
 __device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-// per 16-bit half of a (halves >= 0): 0xFFFF where nonzero, else 0 (v_pk_min_u16 + v_pk_sub_u16; written
-// in C the compiler turns it into a compare and a select per half)
-__device__ __forceinline__ uint32_t pk_nonzero_mask(uint32_t a) {
+// per 16-bit half of a (halves >= 0): 1 where nonzero, else 0 (v_pk_min_u16; inline asm here and below: written
+// in C the compiler turns the per-half ops into a compare and a select per half)
+__device__ __forceinline__ uint32_t pk_nonzero_one(uint32_t a) {
   uint32_t m;  // (the 1 comes from a register: an inline constant would give the high half 0)
-  asm("v_pk_min_u16 %0, %1, %2\n\tv_pk_sub_u16 %0, 0, %0" : "=&v"(m) : "v"(a), "s"(0x00010001u));
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(a), "s"(0x00010001u));
+  return m;
+}
+// per 16-bit half: a * b mod 2^16 (v_pk_mul_lo_u16; with b in {0, 1} a select of a or 0)
+__device__ __forceinline__ uint32_t pk_mul_u16(uint32_t a, uint32_t b) {
+  uint32_t m;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(a), "v"(b));
+  return m;
+}
+__device__ __forceinline__ uint32_t pk_mul_u16s(uint32_t a, uint32_t b) {  // b wave-uniform (an SGPR)
+  uint32_t m;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(m) : "v"(a), "s"(b));
   return m;
 }
 __device__ __forceinline__ f32x2 relu_sel(f32x2 pre, f32x2 v) {  // v where pre > 0, else 0
@@ -1287,10 +1298,10 @@ __global__ __launch_bounds__(NT, 3) void head_bwd1t32_mfma_kernel(HeadArgs a) {
             // positive bf16: the exponent ranges agree), so the mask comes from it in 16-bit integer ops
             const uint32_t act = __builtin_bit_cast(
                 uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, pk_bf16(pre.x, pre.y)), (s16x2){0, 0}));
-            const uint32_t mw = pk_nonzero_mask(act);
+            const uint32_t m1 = pk_nonzero_one(act);
             ba[2 * sg + hp] = act;
-            bm[2 * sg + hp] = mw & 0x3F803F80u;  // bf16 1.0 where pre > 0
-            bx[2 * sg + hp] = pk_bf16(xh.x, xh.y) & mw;
+            bm[2 * sg + hp] = pk_mul_u16s(m1, 0x3F803F80u);  // bf16 1.0 where pre > 0
+            bx[2 * sg + hp] = pk_mul_u16(pk_bf16(xh.x, xh.y), m1);
           }
         accA[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, __builtin_bit_cast(bf16x8, (u32x4){ba[0], ba[1], ba[2], ba[3]}),
                                                            accA[cb], 0, 0, 0);
@@ -1595,16 +1606,19 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     __syncthreads();
     const int Y0 = oy0 / 2, X0 = ox0 / 2;
     // x2 upsample adjoint, columns first: hxs[rr][px] = sum_cc wx(ox, X) g_u[rr][cc], X = X0-1+px
+    // (taps at high-res column 2X - 1 + d, region column cc; branch-free: a tap outside the region / image weighs 0)
     for (int i = tid; i < 18 * 10; i += NT) {
       const int rr = i / 10, px = i - rr * 10, X = X0 - 1 + px;
+      const f32x4 wx4 = up2_adj_w4(X, a.w);
+      const bool xv = X >= 0 && X < a.w;
       float hv[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) hv[k] = 0.f;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {  // (branch-free: a tap outside the region / image weighs 0)
-        const int cc = 2 * px - 2 + d, ox = ox0 - 1 + cc;
-        const bool ok = X >= 0 && X < a.w && cc >= 0 && cc < 18 && ox >= 0 && ox < W2;
-        const float wxv = ok ? up2_adj_w(ox, a.w, X) : 0.f;
+      for (int d = 0; d < 4; ++d) {
+        const int cc = 2 * px - 2 + d;
+        const bool ok = xv && cc >= 0 && cc < 18;
+        const float wxv = ok ? wx4[d] : 0.f;
         const int ci = ok ? cc : 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) hv[k] = fmaf(wxv, su[(rr * 18 + ci) * 3 + k], hv[k]);
@@ -1615,14 +1629,16 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     __syncthreads();
     if (tid < 100) {  // rows: patch[py][px] = sum_rr wy(oy, Y) hxs[rr][px], Y = Y0-1+py
       const int py = tid / 10, px = tid - py * 10, Y = Y0 - 1 + py;
+      const f32x4 wy4 = up2_adj_w4(Y, a.h);
+      const bool yv = Y >= 0 && Y < a.h;
       float pv[K];
 #pragma unroll
       for (int k = 0; k < K; ++k) pv[k] = 0.f;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const int rr = 2 * py - 2 + d, oy = oy0 - 1 + rr;
-        const bool ok = Y >= 0 && Y < a.h && rr >= 0 && rr < 18 && oy >= 0 && oy < H2;
-        const float wyv = ok ? up2_adj_w(oy, a.h, Y) : 0.f;
+        const int rr = 2 * py - 2 + d;
+        const bool ok = yv && rr >= 0 && rr < 18;
+        const float wyv = ok ? wy4[d] : 0.f;
         const int ri = ok ? rr : 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) pv[k] = fmaf(wyv, hxs[(ri * 10 + px) * 3 + k], pv[k]);
