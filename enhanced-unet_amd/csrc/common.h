@@ -191,6 +191,16 @@ __device__ __forceinline__ void up2_src(int o, int in, int& i0, int& i1, float& 
   l1 = s - (float)i0;
 }
 
+// the same in integer arithmetic (value-equal for 0 <= o < 2 in): o = 0 -> (0, 0); odd o = 2m+1 -> (m, 1/4);
+// even o = 2m >= 2 -> (m - 1, 3/4); i1 = min(i0 + 1, in - 1)
+__device__ __forceinline__ void up2_src_i(int o, int in, int& i0, int& i1, float& l1) {
+  const int m = o >> 1;
+  const bool odd = (o & 1) != 0;
+  i0 = odd ? m : max(m - 1, 0);
+  i1 = min(i0 + 1, in - 1);
+  l1 = odd ? 0.25f : (o == 0 ? 0.f : 0.75f);
+}
+
 // adjoint of the x2 bilinear taps: the weight of low-res index i in high-res output o; per
 // low-res row y the contributing high-res rows are 2y-1 .. 2y+2
 __device__ __forceinline__ float up2_adj_w(int o, int in, int i) {

@@ -42,6 +42,15 @@ struct HeadArgs {
   int tx, ty, ntiles;
 };
 
+// u = up(z) at one point from its four z taps (rows y0 / y1, columns x0 / x1) as one explicit fmaf sequence, the
+// same in every head kernel: the forward and the recomputing backward kernels get bit-equal u whatever
+// contraction the compiler would choose for the expression in each of them
+__device__ __forceinline__ float up_lerp(float ly, float lx, float v00, float v01, float v10, float v11) {
+  const float r0 = fmaf(lx, v01, (1.f - lx) * v00);
+  const float r1 = fmaf(lx, v11, (1.f - lx) * v10);
+  return fmaf(ly, r1, (1.f - ly) * r0);
+}
+
 __device__ __forceinline__ float up_val(const HeadArgs& a, int n, int oy, int ox, int k) {
   int y0, y1, x0, x1;
   float ly, lx;
@@ -50,7 +59,7 @@ __device__ __forceinline__ float up_val(const HeadArgs& a, int n, int oy, int ox
   const float* zb = a.z + (long long)n * a.h * a.w * a.K;
   const float v00 = zb[((long long)y0 * a.w + x0) * a.K + k], v01 = zb[((long long)y0 * a.w + x1) * a.K + k];
   const float v10 = zb[((long long)y1 * a.w + x0) * a.K + k], v11 = zb[((long long)y1 * a.w + x1) * a.K + k];
-  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+  return up_lerp(ly, lx, v00, v01, v10, v11);
 }
 
 // su[(18 x 18) region starting at (oy0-1, ox0-1)][3], zero outside the image
@@ -77,33 +86,35 @@ __device__ __forceinline__ void tile_coords(const HeadArgs& a, int tile, int& n,
 // clamped.  Each thread holds <= 2 of its values; the next tile's are loaded into registers
 // while the current tile computes, so fill_u no longer waits on global memory.
 constexpr int ZR = 10;
+template <int K>
 __device__ __forceinline__ void zload(const HeadArgs& a, int tile, float (&zv)[2]) {
   if (tile >= a.ntiles) return;
   int n, oy0, ox0;
   tile_coords(a, tile, n, oy0, ox0);
   const int zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
-  const float* zb = a.z + (long long)n * a.h * a.w * a.K;
+  const float* zb = a.z + (long long)n * a.h * a.w * K;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int idx = threadIdx.x + j * NT;
-    if (idx < ZR * ZR * a.K) {
-      const int k = idx % a.K, pix = idx / a.K, i = pix / ZR, c = pix - i * ZR;
+    if (idx < ZR * ZR * K) {
+      const int k = idx % K, pix = idx / K, i = pix / ZR, c = pix - i * ZR;
       const int yy = min(max(zy0 + i, 0), a.h - 1), xx = min(max(zx0 + c, 0), a.w - 1);
-      zv[j] = zb[((long long)yy * a.w + xx) * a.K + k];
+      zv[j] = zb[((long long)yy * a.w + xx) * K + k];
     }
   }
 }
 
 // stage the prefetched z region, prefetch the next tile's, then u = up(z) over the 18x18 halo
 // from LDS (as fill_u; the caller syncs before and after)
+template <int K>
 __device__ void stage_u(const HeadArgs& a, float* su, float* zs, float (&zv)[2], int tile, int oy0, int ox0) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int idx = threadIdx.x + j * NT;
-    if (idx < ZR * ZR * a.K) zs[idx] = zv[j];
+    if (idx < ZR * ZR * K) zs[idx] = zv[j];
   }
   __syncthreads();
-  zload(a, tile + gridDim.x, zv);
+  zload<K>(a, tile + gridDim.x, zv);
   const int H2 = 2 * a.h, W2 = 2 * a.w, zy0 = oy0 / 2 - 1, zx0 = ox0 / 2 - 1;
   for (int i = threadIdx.x; i < 18 * 18; i += NT) {
     const int hy = i / 18, hx = i - hy * 18;
@@ -111,15 +122,14 @@ __device__ void stage_u(const HeadArgs& a, float* su, float* zs, float (&zv)[2],
     const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
     int y0, y1, x0, x1;
     float ly, lx;
-    up2_src(in ? oy : 0, a.h, y0, y1, ly);
-    up2_src(in ? ox : 0, a.w, x0, x1, lx);
-    const float* r0 = zs + ((y0 - zy0) * ZR) * a.K;
-    const float* r1 = zs + ((y1 - zy0) * ZR) * a.K;
-    const int c0 = (x0 - zx0) * a.K, c1 = (x1 - zx0) * a.K;
-    for (int k = 0; k < a.K; ++k)
-      su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
-                               ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
-                         : 0.f;
+    up2_src_i(in ? oy : 0, a.h, y0, y1, ly);
+    up2_src_i(in ? ox : 0, a.w, x0, x1, lx);
+    const float* r0 = zs + ((y0 - zy0) * ZR) * K;
+    const float* r1 = zs + ((y1 - zy0) * ZR) * K;
+    const int c0 = (x0 - zx0) * K, c1 = (x1 - zx0) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      su[i * 3 + k] = in ? up_lerp(ly, lx, r0[c0 + k], r0[c1 + k], r1[c0 + k], r1[c1 + k]) : 0.f;
   }
 }
 
@@ -807,12 +817,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
   const float* shw = shs[wv];
   bool first = true;
   float zv[2] = {0.f, 0.f};
-  zload(a, blockIdx.x, zv);
+  zload<K>(a, blockIdx.x, zv);
   for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     int nn, oy0, ox0;
     tile_coords(a, tile, nn, oy0, ox0);
     __syncthreads();
-    stage_u(a, su, zs, zv, tile, oy0, ox0);
+    stage_u<K>(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
     if (first) {  // the wave's shift per channel: its first row's pixel 0 (a zero-padded 0 at an edge)
       f32x4 acc[4];
@@ -1003,16 +1013,14 @@ __device__ void stage_u32(const HeadArgs& a, float* su, float* zs, float (&zv)[Z
     const bool in = oy >= 0 && oy < H2 && ox >= 0 && ox < W2;
     int y0, y1, x0, x1;
     float ly, lx;
-    up2_src(in ? oy : 0, a.h, y0, y1, ly);
-    up2_src(in ? ox : 0, a.w, x0, x1, lx);
+    up2_src_i(in ? oy : 0, a.h, y0, y1, ly);
+    up2_src_i(in ? ox : 0, a.w, x0, x1, lx);
     const float* r0 = zs + ((y0 - zy0) * GZ) * K;
     const float* r1 = zs + ((y1 - zy0) * GZ) * K;
     const int c0 = (x0 - zx0) * K, c1 = (x1 - zx0) * K;
 #pragma unroll
     for (int k = 0; k < K; ++k)
-      su[i * 3 + k] = in ? (1.f - ly) * ((1.f - lx) * r0[c0 + k] + lx * r0[c1 + k]) +
-                               ly * ((1.f - lx) * r1[c0 + k] + lx * r1[c1 + k])
-                         : 0.f;
+      su[i * 3 + k] = in ? up_lerp(ly, lx, r0[c0 + k], r0[c1 + k], r1[c0 + k], r1[c1 + k]) : 0.f;
   }
 }
 template <int K>
@@ -1472,7 +1480,7 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
   const int q4 = x >> 2, p4 = x & 3;
   float zv[2] = {0.f, 0.f}, gv[3] = {0.f, 0.f, 0.f};
   const float gsc = g_scale(a);
-  zload(a, blockIdx.x, zv);
+  zload<K>(a, blockIdx.x, zv);
   goload<K>(a, blockIdx.x, gv);
 #if HEAD_STAMP
   const unsigned long long hs0 = head_stamp();
@@ -1484,7 +1492,7 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < K; ++k) gos[k * T2 * T2 + tid] = gv[k] * gsc;
-    stage_u(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
+    stage_u<K>(a, su, zs, zv, tile, oy0, ox0);  // (syncs after staging z)
     goload<K>(a, tile + gridDim.x, gv);
     __syncthreads();
 #if HEAD_STAMP
