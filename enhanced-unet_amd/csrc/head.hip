@@ -1533,10 +1533,20 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
           }
         }
         const bf16x8 g0 = cfrag(acc, 0), g1 = cfrag(acc, 1);
+        // every v MFMA first, then the g_h tile stores, then the kx reduction: the DPP reads of an MFMA result
+        // no longer wait out its latency right behind it
+        f32x4 vov[NJB];
 #pragma unroll
         for (int jb = 0; jb < NJB; ++jb) {
-          f32x4 vo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8 + 2 * jb][fl], g0, z4, 0, 0, 0);
-          vo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9 + 2 * jb][fl], g1, vo, 0, 0, 0);
+          vov[jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[8 + 2 * jb][fl], g0, z4, 0, 0, 0);
+          vov[jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[9 + 2 * jb][fl], g1, vov[jb], 0, 0, 0);
+        }
+        // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
+        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
+        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
+#pragma unroll
+        for (int jb = 0; jb < NJB; ++jb) {
+          const f32x4 vo = vov[jb];
           // (zero where the pixel is outside the image: g is)
           const float s1 = dpp_shr(vo[1], 1), s2 = dpp_shr(vo[2], 2), t1 = dpp_shr(vo[2], 1);
           const int cmb = 4 * jb + q;
@@ -1549,9 +1559,6 @@ __global__ __launch_bounds__(NT, gh_occ(K)) void head_gh_mfma_kernel(HeadArgs a)
             }
           }
         }
-        // wave-private g_h tile [32 px][64 positions], position 16q + 4cb + i <-> channel 16cb + 4q + i
-        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q) = g0;
-        *(bf16x8*)(gw + (rr * 16 + x) * GLD + 16 * q + 8) = g1;
       }
       // gw is wave-private: the wave's own LDS writes are in order before its reads (no block barrier)
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
