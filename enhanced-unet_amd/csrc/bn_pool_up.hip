@@ -486,60 +486,51 @@ __global__ __launch_bounds__(256) void bnrelu_kernel(const T* y, long long P, in
   }
 }
 
-// BN+ReLU -> bilinear x2 upsample (align_corners=False).  One thread per low-res pixel
-// and 16-byte channel unit: the 3x3 clamped neighbourhood is transformed once and
-// gives the 2x2 outputs 2i+a, 2j+b with PyTorch's weights (0.25/0.75, edge rows
-// weighted 1/0 exactly as upsample_bilinear2d's clamped source index).
+// BN+ReLU -> bilinear x2 upsample (align_corners=False), PyTorch's weights (0.25 / 0.75, edge rows and columns
+// weighted 1 / 0 exactly as upsample_bilinear2d's clamped source index), as a row sweep: a thread owns two
+// adjacent low-res columns (j0, j0 + 1) x one 16-byte channel unit over rpt low-res rows (8, or 4 for small grids)
+// and keeps the x-interpolated rows i-1, i, i+1 in registers, so each low-res row is loaded and transformed once
+// per sweep (4 loads per row; the per-pixel-pair form loaded a 3 x 4 neighbourhood, 12, for every pair: 534 vs
+// 459 us over the bench's three launches, bit-identical, profiles/r05_ab.txt), with the next row's loads in
+// flight while the current outputs are formed.
 template <typename T>
-// amdgpu_waves_per_eu(1): the allocation may use its own ~136 registers (3 waves per SIMD); forcing 4 ran
-// 497 -> 523 us
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void bnrelu_up_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
-                                                        const float* sc, const float* sh, T* out, int oct, int oco) {
-  // two horizontally adjacent low-res pixels (j0, j0 + 1) per thread: 3 x 4 neighbourhood loads
-  // and transforms for 2 x 4 outputs each (9 per pixel before); rows are swept one at a time
-  constexpr int E = Vec16<T>::N;
-  const int U = C / E, H2 = 2 * h, W2 = 2 * w, wb = (w + 1) / 2;
+__global__ __launch_bounds__(256) void bnrelu_up_rows_kernel(const T* y, int N, int h, int w, int C, int yct, int yco,
+                                                             const float* sc, const float* sh, T* out, int oct,
+                                                             int oco, int rpt) {
+  constexpr int E = Vec16<T>::N, E2 = E / 2;
+  const int U = C / E, H2 = 2 * h, W2 = 2 * w, wb = (w + 1) / 2, hb = (h + rpt - 1) / rpt;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)N * h * wb * U;
+  const long long total = (long long)N * hb * wb * U;
   if (id >= total) return;
   const int u = (int)(id % U);
   long long p = id / U;
   const int jb = (int)(p % wb); p /= wb;
-  const int i = (int)(p % h);
-  const int n = (int)(p / h);
-  const int c = u * E, j0 = 2 * jb;
+  const int ib = (int)(p % hb);
+  const int n = (int)(p / hb);
+  const int c = u * E, j0 = 2 * jb, i0 = ib * rpt, i1 = min(i0 + rpt, h);
   const bool two = j0 + 1 < w;
-  float s[E], t[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) { s[e] = sc[c + e]; t[e] = sh[c + e]; }
-  const int rs[3] = {max(i - 1, 0), i, min(i + 1, h - 1)};
-  const int cs[4] = {max(j0 - 1, 0), j0, min(j0 + 1, w - 1), min(j0 + 2, w - 1)};
-  uint4 raw[3][4];
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-      raw[a][b] = *(const uint4*)(y + ((long long)(n * h + rs[a]) * w + cs[b]) * yct + yco + c);
-  // output 2i: rows (i-1, i) weights (0.25, 0.75), or row i with weights (1, 0) at i = 0;
-  // output 2i+1: rows (i, i+1) weights (0.75, 0.25) (i+1 clamped).  Same along x; x first.
-  const float wya = i > 0 ? 0.25f : 1.f, wyb = i > 0 ? 0.75f : 0.f;
-  const float wxa = j0 > 0 ? 0.25f : 1.f, wxb = j0 > 0 ? 0.75f : 0.f;
-  // packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two channels per instruction, each element rounded as the
-  // scalar op rounds it -- the same bits as one channel at a time)
-  constexpr int E2 = E / 2;
   f32x2 s2[E2], t2[E2];
 #pragma unroll
-  for (int e = 0; e < E2; ++e) { s2[e] = (f32x2){s[2 * e], s[2 * e + 1]}; t2[e] = (f32x2){t[2 * e], t[2 * e + 1]}; }
+  for (int e = 0; e < E2; ++e) {
+    s2[e] = (f32x2){sc[c + 2 * e], sc[c + 2 * e + 1]};
+    t2[e] = (f32x2){sh[c + 2 * e], sh[c + 2 * e + 1]};
+  }
+  const int cs[4] = {max(j0 - 1, 0), j0, min(j0 + 1, w - 1), min(j0 + 2, w - 1)};
   const f32x2 q1 = {0.25f, 0.25f}, q3 = {0.75f, 0.75f};
-  const f32x2 wxa2 = {wxa, wxa}, wxb2 = {wxb, wxb}, wya2 = {wya, wya}, wyb2 = {wyb, wyb};
-  f32x2 xr[3][4][E2];  // x-interpolated rows: output columns 2j0 .. 2j0 + 3
+  const float wxa = j0 > 0 ? 0.25f : 1.f, wxb = j0 > 0 ? 0.75f : 0.f;
+  const f32x2 wxa2 = {wxa, wxa}, wxb2 = {wxb, wxb};
+  const T* yb = y + (long long)n * h * w * yct + yco + c;
+  auto load = [&](int r, uint4 (&raw)[4]) {
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
+    for (int b = 0; b < 4; ++b) raw[b] = *(const uint4*)(yb + ((long long)r * w + cs[b]) * yct);
+  };
+  // BN + ReLU of the four loaded columns, then the x interpolation: output columns 2 j0 .. 2 j0 + 3
+  auto xrow = [&](const uint4 (&raw)[4], f32x2 (&xr)[4][E2]) {
     f32x2 v[4][E2];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       float f[E];
-      Vec16<T>::unpack(raw[a][b], f);
+      Vec16<T>::unpack(raw[b], f);
 #pragma unroll
       for (int e = 0; e < E2; ++e) {
         const f32x2 r = __builtin_elementwise_fma((f32x2){f[2 * e], f[2 * e + 1]}, s2[e], t2[e]);
@@ -548,26 +539,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void b
     }
 #pragma unroll
     for (int e = 0; e < E2; ++e) {
-      xr[a][0][e] = __builtin_elementwise_fma(wxb2, v[1][e], wxa2 * (j0 > 0 ? v[0][e] : v[1][e]));
-      xr[a][1][e] = __builtin_elementwise_fma(q1, v[2][e], q3 * v[1][e]);
-      xr[a][2][e] = __builtin_elementwise_fma(q3, v[2][e], q1 * v[1][e]);  // column 2(j0+1): j0 + 1 > 0
-      xr[a][3][e] = __builtin_elementwise_fma(q1, v[3][e], q3 * v[2][e]);
+      xr[0][e] = __builtin_elementwise_fma(wxb2, v[1][e], wxa2 * (j0 > 0 ? v[0][e] : v[1][e]));
+      xr[1][e] = __builtin_elementwise_fma(q1, v[2][e], q3 * v[1][e]);
+      xr[2][e] = __builtin_elementwise_fma(q3, v[2][e], q1 * v[1][e]);
+      xr[3][e] = __builtin_elementwise_fma(q1, v[3][e], q3 * v[2][e]);
     }
-  }
+  };
+  auto store = [&](int orow, const f32x2 (&o)[4][E2]) {
+    const long long po = (long long)(n * H2 + orow) * W2 + 2 * j0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    if (b >= 2 && !two) break;
-    float o0[E], o1[E];
+    for (int b = 0; b < 4; ++b) {
+      if (b >= 2 && !two) break;
+      float f[E];
 #pragma unroll
-    for (int e = 0; e < E2; ++e) {
-      const f32x2 r0 = __builtin_elementwise_fma(wyb2, xr[1][b][e], wya2 * (i > 0 ? xr[0][b][e] : xr[1][b][e]));
-      const f32x2 r1 = __builtin_elementwise_fma(q1, xr[2][b][e], q3 * xr[1][b][e]);
-      o0[2 * e] = r0.x; o0[2 * e + 1] = r0.y;
-      o1[2 * e] = r1.x; o1[2 * e + 1] = r1.y;
+      for (int e = 0; e < E2; ++e) { f[2 * e] = o[b][e].x; f[2 * e + 1] = o[b][e].y; }
+      *(uint4*)(out + (po + b) * oct + oco + c) = Vec16<T>::pack(f);
     }
-    const long long po = (long long)(n * H2 + 2 * i) * W2 + 2 * j0 + b;
-    *(uint4*)(out + po * oct + oco + c) = Vec16<T>::pack(o0);
-    *(uint4*)(out + (po + W2) * oct + oco + c) = Vec16<T>::pack(o1);
+  };
+  f32x2 xp[4][E2], xc[4][E2], xn[4][E2];
+  uint4 raw[4];
+  load(max(i0 - 1, 0), raw);
+  xrow(raw, xp);
+  load(i0, raw);
+  xrow(raw, xc);
+  load(min(i0 + 1, h - 1), raw);
+#pragma unroll 1
+  for (int i = i0; i < i1; ++i) {
+    // output row 2i: rows (i-1, i) weights (0.25, 0.75), or row i with weights (1, 0) at i = 0
+    const float wya = i > 0 ? 0.25f : 1.f, wyb = i > 0 ? 0.75f : 0.f;
+    const f32x2 wya2 = {wya, wya}, wyb2 = {wyb, wyb};
+    f32x2 o[4][E2];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < E2; ++e)
+        o[b][e] = __builtin_elementwise_fma(wyb2, xc[b][e], wya2 * (i > 0 ? xp[b][e] : xc[b][e]));
+    store(2 * i, o);
+    xrow(raw, xn);  // row min(i + 1, h - 1)
+    if (i + 1 < i1) load(min(i + 2, h - 1), raw);
+    // output row 2i + 1: rows (i, i+1) weights (0.75, 0.25), i+1 clamped
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) o[b][e] = __builtin_elementwise_fma(q1, xn[b][e], q3 * xc[b][e]);
+    store(2 * i + 1, o);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) { xp[b][e] = xc[b][e]; xc[b][e] = xn[b][e]; }
   }
 }
 
@@ -1551,16 +1570,19 @@ int eunet_bnrelu_upsample(const eunet_act* y, const float* scale, const float* s
                     out->dtype == y->dtype,
                 "bnrelu_upsample: shape");
   const int E = e16(y->dtype);
-  const long long total = (long long)y->n * y->h * ((y->w + 1) / 2) * (y->c / E);
-  const unsigned g = (unsigned)((total + 255) / 256);
+  // rows per thread: 8, or 4 when the grid would have fewer than 4096 blocks (measured: 2 rows per thread is slower)
+  int rpt = 8;
+  auto blocks = [&](int r) { return ((long long)y->n * cdiv(y->h, r) * ((y->w + 1) / 2) * (y->c / E) + 255) / 256; };
+  if (blocks(rpt) < 4096) rpt = 4;
+  const unsigned g = (unsigned)blocks(rpt);
   if (y->dtype == EUNET_BF16)
-    bnrelu_up_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>((const bf16_t*)y->ptr, y->n, y->h, y->w, y->c,
-                                                                   y->ctot, y->coff, scale, shift,
-                                                                   (bf16_t*)out->ptr, out->ctot, out->coff);
+    bnrelu_up_rows_kernel<bf16_t><<<g, 256, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)y->ptr, y->n, y->h, y->w, y->c, y->ctot, y->coff, scale, shift, (bf16_t*)out->ptr,
+        out->ctot, out->coff, rpt);
   else
-    bnrelu_up_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>((const float*)y->ptr, y->n, y->h, y->w, y->c,
-                                                                  y->ctot, y->coff, scale, shift, (float*)out->ptr,
-                                                                  out->ctot, out->coff);
+    bnrelu_up_rows_kernel<float><<<g, 256, 0, (hipStream_t)stream>>>(
+        (const float*)y->ptr, y->n, y->h, y->w, y->c, y->ctot, y->coff, scale, shift, (float*)out->ptr,
+        out->ctot, out->coff, rpt);
   EUNET_LAUNCH_CHECK("bnrelu_upsample");
   return EUNET_OK;
 }

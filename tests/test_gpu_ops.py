@@ -296,6 +296,27 @@ def test_bnrelu_pool_up_conv1x1(dt):
     assert rel(z, a @ w.t() + b) < tol
 
 
+@pytest.mark.parametrize("shape", [(1, 13, 21, 16), (2, 7, 9, 32), (4, 512, 512, 128)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_bnrelu_upsample_row_sweep_shapes(shape, dt):
+    """The row-sweep BN+ReLU -> x2 bilinear upsample (bnrelu_up_rows_kernel: 4 or 8 low-res rows per thread) on
+    ragged row blocks, odd widths and the bench's largest launch (8 rows per thread), written into a concat slot,
+    against F.interpolate of the BN+ReLU output on the GPU (models.py:229-236)."""
+    ops = _ops()
+    N, H, W, C = shape
+    g = torch.Generator(device=DEV).manual_seed(7)
+    y = torch.randn(N, H, W, C, generator=g, device=DEV).to(dt)
+    sc = torch.rand(C, generator=g, device=DEV) + 0.5
+    sh = torch.randn(C, generator=g, device=DEV) * 0.3
+    up = torch.full((N, 2 * H, 2 * W, C + 8), 7.0, dtype=dt, device=DEV)
+    ops.bnrelu_upsample(ops.act(y), sc, sh, ops.act(up, 0, C))
+    a = torch.relu(y.float() * sc + sh)
+    ref = nhwc(F.interpolate(nchw(a), scale_factor=2, mode="bilinear", align_corners=False))
+    err = float((up[..., :C].float() - ref).abs().max() / ref.abs().max())
+    assert err < TOL[dt], err
+    assert bool((up[..., C:] == 7.0).all())
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_backward_helpers(dt):
     ops = _ops()

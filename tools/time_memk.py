@@ -34,3 +34,15 @@ z = torch.empty(N, H, H, 2, device=dev)
 w, b = torch.randn(2, C, device=dev), torch.randn(2, device=dev)
 ms = timeit(lambda: ops.bnrelu_conv1x1(ops.act(y), v[0], v[1], w, b, 2, z))
 print(f"bnrelu_conv1x1      {ms * 1e3:7.1f} us  {(y.numel() * 2 + z.numel() * 4) / ms / 1e9:5.2f} TB/s")
+
+# BN+ReLU -> x2 upsample into the decoder's concat slots (the bench's three launches: 128^2 x 512, 256^2 x 256,
+# 512^2 x 128 channels at N 4 -> 2x into [up | skip] buffers)
+tot = 0.0
+for h, c in ((128, 512), (256, 256), (512, 128)):
+    yu = torch.randn(N, h, h, c, device=dev).bfloat16()
+    cat = torch.empty(N, 2 * h, 2 * h, 2 * c, device=dev).bfloat16()
+    sc, sh = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.3
+    ms = timeit(lambda: ops.bnrelu_upsample(ops.act(yu), sc, sh, ops.act(cat, 0, c)))
+    tot += ms
+    print(f"bnrelu_upsample {h:4d}^2 x {c:3d} {ms * 1e3:7.1f} us  {yu.numel() * 2 * 5 / ms / 1e9:5.2f} TB/s")
+print(f"bnrelu_upsample total {tot * 1e3:7.1f} us")
