@@ -46,3 +46,18 @@ for h, c in ((128, 512), (256, 256), (512, 128)):
     tot += ms
     print(f"bnrelu_upsample {h:4d}^2 x {c:3d} {ms * 1e3:7.1f} us  {yu.numel() * 2 * 5 / ms / 1e9:5.2f} TB/s")
 print(f"bnrelu_upsample total {tot * 1e3:7.1f} us")
+
+# x2 upsample adjoint with the fused BN-backward partial sums (the bench's three launches: gradients of the
+# decoder's [up | skip] concat inputs at 256^2 / 512^2 / 1024^2 -> 128^2 x 512, 256^2 x 256, 512^2 x 128)
+tot = 0.0
+for h, c in ((128, 512), (256, 256), (512, 128)):
+    gcat = torch.randn(N, 2 * h, 2 * h, 2 * c, device=dev).bfloat16()
+    glo = torch.empty(N, h, h, c, device=dev).bfloat16()
+    yl = torch.randn(N, h, h, c, device=dev).bfloat16()
+    vv = [torch.rand(c, device=dev) + 0.5 for _ in range(4)]
+    rows = ops.upsample_bwd_bnr_rows(ops.act(glo))
+    part = torch.empty(rows * 2 * c, device=dev)
+    ms = timeit(lambda: ops.upsample_bwd_bnr(ops.act(gcat, 0, c), ops.act(glo), ops.act(yl), *vv, part))
+    tot += ms
+    print(f"upsample_bwd_bnr {h:4d}^2 x {c:3d} {ms * 1e3:7.1f} us  {glo.numel() * 2 * 6 / ms / 1e9:5.2f} TB/s")
+print(f"upsample_bwd_bnr total {tot * 1e3:7.1f} us")
