@@ -19,7 +19,7 @@ Differences that are implementation, not semantics:
 from __future__ import annotations
 
 import collections
-
+import gc
 import math
 import warnings
 from typing import Dict
@@ -317,9 +317,19 @@ class StepGraph:
         self.optimizer_step = trainer._optimizer_step
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: a DataLoader producer thread may launch and allocate on its own stream
-        # while this thread captures (the default global mode would invalidate the capture)
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.loss = trainer._forward_backward(self.images, self.masks, False).detach()
+        # while this thread captures (the default global mode would invalidate the capture).
+        # The cyclic garbage collector is off during the capture (torch.cuda.graph collects right before
+        # it): a collection inside it would run the finalizers of earlier steps' objects -- a
+        # torch.cuda.Event's hipEventDestroy among them -- in the middle of the capture, where HIP refuses
+        # them ("operation not permitted when stream is capturing", seen from the autograd thread)
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                self.loss = trainer._forward_backward(self.images, self.masks, False).detach()
+        finally:
+            if gc_was_on:
+                gc.enable()
         self.params = [p for g in self.optimizer.param_groups for p in g["params"]]
         self.grads = [p.grad for p in self.params]
 
