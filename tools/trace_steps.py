@@ -13,7 +13,14 @@ def short(name):
     base = m.group(1) if m else name[:40]
     tmpl = m.group(2) or "" if m else ""
     if "conv3x3_fwd_kernel" in base:
-        base = "dgrad" if "true" in tmpl or "1>" in tmpl else "fwd"
+        # conv3x3_fwd_kernel<T, DG, TO, BT, BNB, PF, CT>: DG = data gradient, BNB = fused BN-backward apply,
+        # PF = LDS-DMA-staged untransformed forward, CT = half-width tail co-block
+        args = [t.strip() for t in tmpl.strip("<>").split(",")]
+        flag = lambda i: len(args) > i and args[i] in ("true", "1")  # noqa: E731
+        base = ("dgrad" + ("_bnb" if flag(4) else "")) if flag(1) else ("fwd" + ("_pf" if flag(5) else ""))
+        if flag(6):
+            base += "_ct"
+        return base
     return base.replace("_kernel", "")
 
 
