@@ -3,6 +3,7 @@ host layer mirrors the reference API, and the product fails loudly without a GPU
 import os
 import re
 
+import numpy as np
 import pytest
 import torch
 
@@ -266,3 +267,44 @@ def test_opt_table_layout_and_supported():
     p = torch.nn.Parameter(torch.zeros(3))
     assert not optim.supported(torch.optim.AdamW([p]))  # CPU parameter
     assert not optim.supported(torch.optim.SGD([p], lr=0.1))
+
+
+def test_upsample_index_closed_forms_equal_the_float_rule():
+    """The head kernels' integer x2 source indices (common.h up2_src_i) and closed-form adjoint weights
+    (up2_adj_w4) restated and checked against up2_src / up2_adj_w's float rule (PyTorch's
+    area_pixel_compute_source_index at scale 1/2, align_corners=False; models.py:236's upsample) for every
+    high-res position of every size up to 70, fp32 arithmetic as on the device."""
+    f32 = np.float32
+
+    def src_float(o, n):
+        s = f32(0.5) * (f32(o) + f32(0.5)) - f32(0.5)
+        s = max(s, f32(0.0))
+        i0 = int(s)
+        return i0, i0 + (1 if i0 < n - 1 else 0), f32(s - f32(i0))
+
+    def src_int(o, n):
+        m, odd = o >> 1, (o & 1) == 1
+        i0 = m if odd else max(m - 1, 0)
+        return i0, min(i0 + 1, n - 1), f32(0.25 if odd else (0.0 if o == 0 else 0.75))
+
+    def adj_w(o, n, i):
+        i0, i1, l1 = src_float(o, n)
+        return (f32(1.0) - l1 if i0 == i else f32(0.0)) + (l1 if i1 == i else f32(0.0))
+
+    def adj_w4(i, n):
+        w = [0.25, 0.75, 0.75, 0.25]
+        if i == 0:
+            w[0], w[1] = 0.0, 1.0
+        if i == n - 1:
+            w[2], w[3] = 1.0, 0.0
+        return [f32(v) for v in w]
+
+    for n in range(1, 71):
+        for o in range(2 * n):
+            assert src_int(o, n) == src_float(o, n), (n, o)
+        for i in range(n):
+            w4 = adj_w4(i, n)
+            for d in range(4):
+                o = 2 * i - 1 + d
+                ref = adj_w(o, n, i) if 0 <= o < 2 * n else f32(0.0)
+                assert w4[d] == ref, (n, i, d)
