@@ -946,6 +946,31 @@ __device__ __forceinline__ void gram_group(const float* su, int r0, int q, const
   c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, f1, c11, 0, 0, 0);
 }
 
+// the same for a group whose 32 pixels are all inside the image (every group of a full tile): no validity
+// factor, and the padding entries 9K <= j < 31 read the window corner instead of a selected zero -- they only
+// reach G's rows / columns 9K .. 30, which nothing reads (each G entry is its own dot product over the
+// pixels); the validity entry j = 31 (lanes with o1 == -2) is the constant 1.0 pair.  8 v_cvt_pk_bf16_f32
+// per group instead of a select chain per entry; the G entries that are read are the same values.
+template <int RS>
+__device__ __forceinline__ void gram_group_full(const float* su, int r0, int q, int o0, int o1, bool one,
+                                                f32x4& c00, f32x4& c01, f32x4& c11) {
+  static_assert(RS - 2 == 32, "one tile row per 32-pixel group");
+  const int base = (r0 * RS + 8 * q) * 3;
+  uint32_t w0[4], w1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = base + 6 * i;
+    w0[i] = pk_bf16(su[b + o0], su[b + 3 + o0]);
+    const uint32_t v1 = pk_bf16(su[b + o1], su[b + 3 + o1]);
+    w1[i] = one ? 0x3F803F80u : v1;
+  }
+  const bf16x8 f0 = __builtin_bit_cast(bf16x8, (u32x4){w0[0], w0[1], w0[2], w0[3]});
+  const bf16x8 f1 = __builtin_bit_cast(bf16x8, (u32x4){w1[0], w1[1], w1[2], w1[3]});
+  c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, f0, c00, 0, 0, 0);
+  c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0, f1, c01, 0, 0, 0);
+  c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1, f1, c11, 0, 0, 0);
+}
+
 // the block's three G blocks -> one partial row (fixed-order sum of the 4 waves)
 __device__ __forceinline__ void gram_store(float* red, float* row, const f32x4& c00, const f32x4& c01,
                                            const f32x4& c11) {
@@ -1031,6 +1056,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = lane >> 4, x = lane & 15;
   int o[2];
   gram_offsets<K, GR>(x, o);
+  const int o0c = o[0] < 0 ? 0 : o[0], o1c = o[1] < 0 ? 0 : o[1];
+  const bool one = o[1] == -2;
   f32x4 c00 = {0.f, 0.f, 0.f, 0.f}, c01 = c00, c11 = c00;
   const int H2 = 2 * a.h, W2 = 2 * a.w;
   float zv[Z32<K>::ZI];
@@ -1042,8 +1069,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void he
     stage_u32<K>(a, su, zs, zv, tile, oy0, ox0);
     __syncthreads();
     const int vh = min(GT, H2 - oy0), vw = min(GT, W2 - ox0);
+    if (vh == GT && vw == GT) {
 #pragma unroll 2
-    for (int rr = 0; rr < GT / 4; ++rr) gram_group<GR>(su, 8 * wv + rr, q, o, vh, vw, c00, c01, c11);
+      for (int rr = 0; rr < GT / 4; ++rr)
+        gram_group_full<GR>(su, 8 * wv + rr, q, o0c, o1c, one, c00, c01, c11);
+    } else {
+#pragma unroll 2
+      for (int rr = 0; rr < GT / 4; ++rr) gram_group<GR>(su, 8 * wv + rr, q, o, vh, vw, c00, c01, c11);
+    }
   }
   EUNET_DASSERT(a.gram != nullptr);
   gram_store(red, a.gram + (long long)blockIdx.x * GRAM_LD, c00, c01, c11);
