@@ -872,6 +872,60 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
   }
 }
 
+// bn_bwd_apply for dec1's input gradient without it in memory: g = W^T gz recomputed per pixel exactly as
+// conv1x1_bwd_kernel forms it (the same fmaf chain over k < 3 with zero weights / gz past K, then its rounding
+// to T), then the apply above.  conv1x1_bwd_bnr reduced the same rounded g' and no longer stores g: at the
+// bench shape a 64-channel bf16 tensor at 1024^2 x 4, 537 MB written there and read here (the gz read that
+// replaces it: 33 MB).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_1x1_kernel(const T* y, int yct, int yco, long long P, int C,
+                                                               const float* w, int K, const float* gz,
+                                                               const float* mean, const float* istd,
+                                                               const float* scale, const float* shift,
+                                                               const float* dbeta, const float* dgamma, T* gy, int oct,
+                                                               int oco) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E;
+  const int u = threadIdx.x % U, c = u * E;
+  const float inv_n = 1.f / (float)P;
+  float kP[E], kQ[E], k1[E], k2[E], k3[E], wk[3][E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const BnBwdCoef k = bn_bwd_coef(mean[c + j], istd[c + j], scale[c + j], shift[c + j], dbeta[c + j],
+                                    dgamma[c + j], inv_n);
+    kP[j] = k.k1;
+    kQ[j] = k.kq;
+    k1[j] = k.k1;
+    k2[j] = k.k2;
+    k3[j] = k.k3;
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) wk[kk][j] = kk < K ? w[kk * C + c + j] : 0.f;
+  }
+  const int ppb = blockDim.x / U;
+  for (long long p = (long long)blockIdx.x * ppb + threadIdx.x / U; p < P; p += (long long)gridDim.x * ppb) {
+    float gk[3];
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) gk[kk] = kk < K ? gz[p * K + kk] : 0.f;
+    float yf[E], go[E], gf[E], o[E];
+    Vec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)(y + p * yct + yco + c))), yf);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      float sv = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) sv = fmaf(wk[kk][j], gk[kk], sv);
+      go[j] = sv;
+    }
+    Vec16<T>::unpack(Vec16<T>::pack(go), gf);  // the rounding of conv1x1_bwd's store
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float gg = fmaf(yf[j], kP[j], kQ[j]) > 0.f ? gf[j] : 0.f;
+      o[j] = fmaf(k1[j], gg, fmaf(yf[j], k2[j], k3[j]));
+    }
+    EUNET_DASSERT(p < P && oco + c + E <= oct && u < U);
+    *(uint4*)(gy + p * oct + oco + c) = Vec16<T>::pack(o);
+  }
+}
+
 // Fused BN-backward reduction in a gradient producer (the reduction half of bn_bwd_reduce for
 // the block whose output gradient g the kernel writes): each thread accumulates, for its 16-byte
 // channel unit, s1 += g', s2 += g' xhat over the pixels it writes (g' = stored g where
@@ -1336,11 +1390,11 @@ __global__ __launch_bounds__(NT) void conv1x1_bwd_kernel(const T* y, long long P
           go[e] = sv;
         }
         const uint4 pk0 = Vec16<T>::pack(go);
-        *(uint4*)(ga + p * gct + gco + c) = pk0;
+        if (ga) *(uint4*)(ga + p * gct + gco + c) = pk0;  // (ga null: reduced only, eunet_bn_bwd_apply_1x1)
         uint4 pk1 = pk0;
         if constexpr (E == 4) {
           pk1 = Vec16<T>::pack(go + 4);
-          *(uint4*)(ga + p * gct + gco + c + 4) = pk1;
+          if (ga) *(uint4*)(ga + p * gct + gco + c + 4) = pk1;
         }
         if constexpr (BNR) {  // the stored (rounded) gradient, as bn_bwd_reduce would read it
           float gr[8];
@@ -1687,6 +1741,33 @@ int eunet_bn_bwd_apply(const eunet_act* g, const eunet_act* y, const float* mean
   return bn_bwd_apply_launch(g, y, mean, invstd, scale, shift, dbeta, dgamma, nullptr, gy, stream);
 }
 
+int eunet_bn_bwd_apply_1x1(const eunet_act* y, const float* w, int k, const float* gz, const float* mean,
+                           const float* invstd, const float* scale, const float* shift, const float* dbeta,
+                           const float* dgamma, const eunet_act* gy, void* stream) {
+  EUNET_REQUIRE(act_ok(y) && act_ok(gy) && vec_ok(y) && vec_ok(gy) && w && gz && mean && invstd && scale && shift &&
+                    dbeta && dgamma,
+                "bn_bwd_apply_1x1: bad args");
+  EUNET_REQUIRE(k >= 1 && k <= 3 && gy->dtype == y->dtype && gy->c == y->c && gy->n == y->n && gy->h == y->h &&
+                    gy->w == y->w,
+                "bn_bwd_apply_1x1: K <= 3, gy like y");
+  const long long P = (long long)y->n * y->h * y->w;
+  const int U = y->c / e16(y->dtype);
+  EUNET_REQUIRE(U <= 256, "bn_bwd_apply_1x1: at most 256 channel units");
+  const int bs = (256 / U) * U;
+  const long long nb = (P * U + bs - 1) / bs;
+  const unsigned gr = (unsigned)(nb < 4096 ? nb : 4096);
+  if (y->dtype == EUNET_BF16)
+    bn_bwd_apply_1x1_kernel<bf16_t><<<gr, bs, 0, (hipStream_t)stream>>>(
+        (const bf16_t*)y->ptr, y->ctot, y->coff, P, y->c, w, k, gz, mean, invstd, scale, shift, dbeta, dgamma,
+        (bf16_t*)gy->ptr, gy->ctot, gy->coff);
+  else
+    bn_bwd_apply_1x1_kernel<float><<<gr, bs, 0, (hipStream_t)stream>>>(
+        (const float*)y->ptr, y->ctot, y->coff, P, y->c, w, k, gz, mean, invstd, scale, shift, dbeta, dgamma,
+        (float*)gy->ptr, gy->ctot, gy->coff);
+  EUNET_LAUNCH_CHECK("bn_bwd_apply_1x1");
+  return EUNET_OK;
+}
+
 int eunet_bn_bwd_apply_coef(const eunet_act* g, const eunet_act* y, const float* coef, const eunet_act* gy,
                             void* stream) {
   EUNET_REQUIRE(coef, "bn_bwd_apply_coef: null coef");
@@ -1877,10 +1958,14 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
 int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* shift, const float* w, int k,
                           const float* gz, const eunet_act* gact, float* part, const float* mean, const float* invstd,
                           float* bn_part, void* stream) {
-  EUNET_REQUIRE(act_ok(y) && act_ok(gact) && vec_ok(y) && vec_ok(gact) && scale && shift && w && gz && part,
+  EUNET_REQUIRE(act_ok(y) && vec_ok(y) && (!gact || (act_ok(gact) && vec_ok(gact))) && scale && shift && w && gz &&
+                    part,
                 "conv1x1_bwd: bad args");
-  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 128 && y->c % 8 == 0 && gact->c == y->c && gact->dtype == y->dtype,
+  EUNET_REQUIRE(k >= 1 && k <= 3 && y->c <= 128 && y->c % 8 == 0 &&
+                    (!gact || (gact->c == y->c && gact->dtype == y->dtype)),
                 "conv1x1_bwd: K<=3, C<=128, C%8==0");
+  const eunet_act none{};
+  if (!gact) gact = &none;  // (a null ptr: the kernel reduces without storing)
   EUNET_REQUIRE(mean && invstd && bn_part, "conv1x1_bwd_bnr: BN args");
   const long long P = (long long)y->n * y->h * y->w;
   const unsigned tiles = (unsigned)((P + C1X_PIX - 1) / C1X_PIX);

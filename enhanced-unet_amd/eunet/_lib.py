@@ -90,6 +90,7 @@ SIGNATURES = {
     "eunet_colsum": [_f, c_int, c_int, _f, _f, c_void_p],
     "eunet_colsum_split": [_f, c_int, c_int, c_int, _f, _f, _f, c_void_p],
     "eunet_bn_bwd_apply": [_P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
+    "eunet_bn_bwd_apply_1x1": [_P, _f, c_int, _f, _f, _f, _f, _f, _f, _f, _P, c_void_p],
     "eunet_bn_bwd_coef": [_f, _f, _f, _f, _f, _f, c_int64, c_int, _f, c_void_p],
     "eunet_bn_bwd_apply_coef": [_P, _P, _f, _P, c_void_p],
     "eunet_pool_bwd_add": [_P, _P, _P, _P, c_void_p],

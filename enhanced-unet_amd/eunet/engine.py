@@ -30,6 +30,13 @@ from ._lib import EunetError
 BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+class Grad1x1:
+    """A gradient w.r.t. relu(bn(y)) held as dec1's W^T g_z instead of a tensor (UNetEngine.dec1_recompute)."""
+
+    def __init__(self, w, k, gz):
+        self.w, self.k, self.gz = w, k, gz
+
+
 class GradSink:
     """Default sink: a fresh fp32 tensor per parameter gradient."""
 
@@ -116,6 +123,11 @@ class UNetEngine:
     # next level's HBM-bound upsample / max-pool adjoints instead of the dgrad (they ran 2.7x longer:
     # +0.85 ms/step in a same-box A/B, profiles/r03_ab.txt)
     fuse_bn_apply_a = False
+    # dec1_recompute -- dec1's input gradient W^T g_z (64 channels at H) is not stored: conv1x1_bwd only
+    # reduces it for dec2's second BatchNorm, and that BatchNorm's apply recomputes it per pixel from g_z
+    # (eunet_bn_bwd_apply_1x1: the same gy bit for bit, 2 x 537 MB less HBM traffic at the bench shape).
+    # Needs fuse_bn_reduce and dec2 outside fuse_bn_apply (whose fused dgrad reads the stored gradient).
+    dec1_recompute = True
     # dgrad_first -- after a DoubleConv's BN-a backward, conv .0's data gradient is issued on the launch
     # stream before the side-stream weight gradients (which wait on an event recorded right after the
     # apply, not on the launch stream's tail).  Closes half of the ~24 us apply -> dgrad launch-stream gap
@@ -302,7 +314,8 @@ class UNetEngine:
         return S
 
     # --------------------------------------------------------------- backward
-    def _block_bwd(self, nm, G: torch.Tensor, S, P, sink: GradSink, need_gx: bool, small: bool, gred=(None, 0)):
+    def _block_bwd(self, nm, G: "torch.Tensor | Grad1x1", S, P, sink: GradSink, need_gx: bool, small: bool,
+                   gred=(None, 0)):
         """gred: (part, rows) of the block's BN-b backward reduction when G's producer fused it."""
         p = f"{self.prefix}{nm}"
         s = S[nm]
@@ -311,6 +324,13 @@ class UNetEngine:
         dev, dt = yb.device, self.dtype
 
         def bn_back(prefix, g, y, bn, part=None, tiles=0):
+            if isinstance(g, Grad1x1):  # reduced by conv1x1_bwd_bnr, recomputed by the apply
+                dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
+                ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
+                gy = torch.empty_like(y)
+                ops.bn_bwd_apply_1x1(ops.act(y), g.w, g.k, g.gz, bn["mean"], bn["invstd"], bn["scale"],
+                                     bn["shift"], dbeta, dgamma, ops.act(gy))
+                return gy
             if part is None:  # reduction not fused into the producer of g
                 tiles = ops.bn_bwd_tiles(ops.act(y))
                 part = _e(tiles * 2 * C, torch.float32, dev)
@@ -545,7 +565,6 @@ class UNetEngine:
 
         # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))
         s2 = S["dec2"]
-        gd2 = torch.empty_like(s2["yb"])
         yb_act = ops.act(s2["yb"])
         tiles = ops.conv1x1_bwd_tiles(yb_act)
         part = _e(tiles * (K * b + K), torch.float32, dev)
@@ -554,10 +573,17 @@ class UNetEngine:
         red2 = (None, 0)
         if self.fuse_bn_reduce:
             bpart = _e(tiles * 2 * b, torch.float32, dev)
-            ops.conv1x1_bwd_bnr(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part,
-                                bnb2["mean"], bnb2["invstd"], bpart)
+            if self.dec1_recompute and not _per_block(self.fuse_bn_apply, "dec2"):
+                gd2 = Grad1x1(w1, K, gz)
+                ops.conv1x1_bwd_bnr(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, None, part,
+                                    bnb2["mean"], bnb2["invstd"], bpart)
+            else:
+                gd2 = torch.empty_like(s2["yb"])
+                ops.conv1x1_bwd_bnr(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part,
+                                    bnb2["mean"], bnb2["invstd"], bpart)
             red2 = (bpart, tiles)
         else:
+            gd2 = torch.empty_like(s2["yb"])
             ops.conv1x1_bwd(yb_act, bnb2["scale"], bnb2["shift"], w1, K, gz, ops.act(gd2), part)
         # the column sums go straight into the two gradient slots (colsum's split output)
         ops.colsum(part, tiles, K * b + K, sink.slot(pre + "dec1.weight", (K, b, 1, 1)), split=K * b,

@@ -462,11 +462,20 @@ def conv1x1_bwd(y: Act, scale, shift, w, k, gz, gact: Act, part):
          ctypes.byref(gact), _ptr(part), _stream())
 
 
-@_dispatched("A T T T i T A! T!? T T T!")
-def conv1x1_bwd_bnr(y: Act, scale, shift, w, k, gz, gact: Act, part, mean, invstd, bn_part):
-    """conv1x1_bwd + the BN-backward partial sums [tiles][2][C] of y's BatchNorm over gact."""
+@_dispatched("A T T T i T A!? T!? T T T!")
+def conv1x1_bwd_bnr(y: Act, scale, shift, w, k, gz, gact: Act | None, part, mean, invstd, bn_part):
+    """conv1x1_bwd + the BN-backward partial sums [tiles][2][C] of y's BatchNorm over gact (gact None: the
+    gradient is reduced, not stored -- bn_bwd_apply_1x1 recomputes it)."""
     call("eunet_conv1x1_bwd_bnr", ctypes.byref(y), _ptr(scale), _ptr(shift), _ptr(w), k, _ptr(gz),
-         ctypes.byref(gact), _ptr(part), _ptr(mean), _ptr(invstd), _ptr(bn_part), _stream())
+         _ref(gact), _ptr(part), _ptr(mean), _ptr(invstd), _ptr(bn_part), _stream())
+
+
+@_dispatched("A T i T T T T T T T A!")
+def bn_bwd_apply_1x1(y: Act, w, k, gz, mean, invstd, scale, shift, dbeta, dgamma, gy: Act):
+    """bn_bwd_apply of the gradient W^T gz that conv1x1_bwd_bnr reduced without storing (recomputed per pixel
+    with its arithmetic and rounding: the same gy bit for bit)."""
+    call("eunet_bn_bwd_apply_1x1", ctypes.byref(y), _ptr(w), k, _ptr(gz), _ptr(mean), _ptr(invstd), _ptr(scale),
+         _ptr(shift), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
 
 
 # ---- evaluation path (evalpath.hip) ------------------------------------------------

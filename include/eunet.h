@@ -294,10 +294,20 @@ int eunet_conv1x1_bwd(const eunet_act* y, const float* scale, const float* shift
                       void* stream);
 /* the same, also writing the BN-backward partial sums of y's BatchNorm over the gradient it
  * produces (what eunet_bn_bwd_reduce would compute from gact): bn_part [tiles][2][C] = per-tile
- * (sum g', sum g' xhat), g' = gact where relu(bn(y)) > 0 (scale/shift are that BN's affine form). */
+ * (sum g', sum g' xhat), g' = gact where relu(bn(y)) > 0 (scale/shift are that BN's affine form).
+ * gact may be NULL: the gradient is then only reduced, not stored, and eunet_bn_bwd_apply_1x1
+ * recomputes it for the apply. */
 int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* shift,
                           const float* w, int k, const float* gz, const eunet_act* gact, float* part,
                           const float* mean, const float* invstd, float* bn_part, void* stream);
+/* eunet_bn_bwd_apply for the gradient eunet_conv1x1_bwd_bnr produced without storing it: g = W^T gz
+ * (w [K][C], gz [N*H*W][K] fp32) recomputed per pixel with conv1x1_bwd's arithmetic and rounding to
+ * y's dtype, then gy = scale (g' - dbeta/n - xhat dgamma/n) as eunet_bn_bwd_apply -- the same gy bit for
+ * bit, without the C-channel gradient's write and read.  Reference: the autograd of models.py:336-337
+ * (dec1 = Conv2d 1x1 on relu(bn(dec2's conv .3 output)), models.py:220-223). */
+int eunet_bn_bwd_apply_1x1(const eunet_act* y, const float* w, int k, const float* gz, const float* mean,
+                           const float* invstd, const float* scale, const float* shift, const float* dbeta,
+                           const float* dgamma, const eunet_act* gy, void* stream);
 
 /* ---- optimizer tail of the Trainer step (optim.hip; train_eval.py:341-343, AdamW from :120)
  * clip_grad_norm_(max_norm) + AdamW (decoupled weight decay) over every parameter tensor in three
