@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void po
 #pragma unroll
       for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
       const uint4 packed = Vec16<T>::pack(o);
-      *(uint4*)(go + pix[k] * goct + goco + c) = packed;
+      if (go) *(uint4*)(go + pix[k] * goct + goco + c) = packed;  // (go null: reduced only, bn_bwd_apply_pool)
       if constexpr (RED) {
         float gr[E], yv[E];
         Vec16<T>::unpack(packed, gr);
@@ -1059,6 +1059,81 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void po
     }
   }
   if constexpr (RED) bnred_block<T>(br, C, s1, s2);
+}
+
+// bn_bwd_apply for the max-pool adjoint's gradient without it in memory: per 2x2 window and channel unit the
+// gradient gout = gs + scatter(gp) is recomputed exactly as pool_bwd_add_kernel<T, true> forms and rounds it
+// (argmax over round(relu(y scale + shift)), first maximum, NaN wins), then the BN-backward apply of the block's
+// second BatchNorm.  pool_bwd_add_bnr reduced the same g' and no longer stores gout: the apply reads gs and the
+// quarter-size gp instead of gout -- 0.75 C per pixel less traffic (gout's write and read, gp's re-read).  The
+// block size is a multiple of the channel units (bnr_block), so a thread keeps one unit's constants.
+template <typename T>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void bn_bwd_apply_pool_kernel(
+    const T* gp, int gpct, int gpco, const T* gs, int gsct, int gsco, const T* y, int yct, int yco, const float* mean,
+    const float* istd, const float* scale, const float* shift, const float* dbeta, const float* dgamma, T* gy, int oct,
+    int oco, int N, int H, int W, int C) {
+  constexpr int E = Vec16<T>::N;
+  const int U = C / E, Ho = H / 2, Wo = W / 2;
+  const float inv_n = 1.f / (float)((long long)N * H * W);
+  const long long id0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(id0 % U) * E;
+  float kP[E], kQ[E], k1[E], k2[E], k3[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const BnBwdCoef k = bn_bwd_coef(mean[c + j], istd[c + j], scale[c + j], shift[c + j], dbeta[c + j],
+                                    dgamma[c + j], inv_n);
+    kP[j] = k.k1;
+    kQ[j] = k.kq;
+    k1[j] = k.k1;
+    k2[j] = k.k2;
+    k3[j] = k.k3;
+  }
+  auto ldnt = [](const T* q) { return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)q)); };
+  for (long long id = id0; id < (long long)N * Ho * Wo * U; id += (long long)gridDim.x * blockDim.x) {
+    long long p = id / U;
+    const int xo = (int)(p % Wo); p /= Wo;
+    const int yo = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    long long pix[4];
+    uint4 ra[4], rs[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pix[k] = (long long)(n * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+      ra[k] = ldnt(y + pix[k] * yct + yco + c);
+    }
+    const uint4 rg = ldnt(gp + ((long long)(n * Ho + yo) * Wo + xo) * gpct + gpco + c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rs[k] = gs != nullptr ? ldnt(gs + pix[k] * gsct + gsco + c) : make_uint4(0, 0, 0, 0);
+    float best[E], gpv[E];
+    int arg[E];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float a[E];
+      Vec16<T>::unpack(ra[k], a);
+#pragma unroll
+      for (int j = 0; j < E; ++j) a[j] = fmaxf(fmaf(a[j], kP[j], kQ[j]), 0.f);
+      Vec16<T>::unpack(Vec16<T>::pack(a), a);
+#pragma unroll
+      for (int j = 0; j < E; ++j)
+        if (k == 0 || a[j] > best[j] || (a[j] != a[j])) { best[j] = a[j]; arg[j] = k; }
+    }
+    Vec16<T>::unpack(rg, gpv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[E], gr[E], yv[E], out[E];
+      Vec16<T>::unpack(rs[k], o);
+#pragma unroll
+      for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
+      Vec16<T>::unpack(Vec16<T>::pack(o), gr);  // the rounding of pool_bwd_add's store
+      Vec16<T>::unpack(ra[k], yv);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float gg = fmaf(yv[j], kP[j], kQ[j]) > 0.f ? gr[j] : 0.f;
+        out[j] = fmaf(k1[j], gg, fmaf(yv[j], k2[j], k3[j]));
+      }
+      *(uint4*)(gy + pix[k] * oct + oco + c) = Vec16<T>::pack(out);
+    }
+  }
 }
 
 
@@ -1874,7 +1949,16 @@ int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows) {
 int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
                            const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
                            const float* scale, const float* shift, float* part, void* stream) {
-  EUNET_REQUIRE(act_ok(act) && act_ok(gpool) && act_ok(gout) && vec_ok(act) && vec_ok(gpool) && vec_ok(gout),
+  EUNET_REQUIRE(act_ok(act) && vec_ok(act), "pool_bwd_add_bnr: bad act");
+  eunet_act none;
+  if (!gout) {  // reduce only (the apply recomputes gout: eunet_bn_bwd_apply_pool)
+    none = *act;
+    none.ptr = nullptr;
+    none.ctot = act->c;
+    none.coff = 0;
+    gout = &none;
+  }
+  EUNET_REQUIRE(act_ok(gpool) && vec_ok(gpool) && (!gout->ptr || (act_ok(gout) && vec_ok(gout))),
                 "pool_bwd_add_bnr: bad tensors");
   if (gskip) EUNET_REQUIRE(act_ok(gskip) && vec_ok(gskip) && gskip->c == act->c, "pool_bwd_add_bnr: gskip");
   EUNET_REQUIRE(gpool->h * 2 == act->h && gpool->w * 2 == act->w && gout->h == act->h && gout->w == act->w &&
@@ -1894,6 +1978,35 @@ int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const e
   else PBA(float);
 #undef PBA
   EUNET_LAUNCH_CHECK("pool_bwd_add_bnr");
+  return EUNET_OK;
+}
+
+int eunet_bn_bwd_apply_pool(const eunet_act* gpool, const eunet_act* gskip, const eunet_act* y, const float* mean,
+                            const float* invstd, const float* scale, const float* shift, const float* dbeta,
+                            const float* dgamma, const eunet_act* gy, void* stream) {
+  EUNET_REQUIRE(act_ok(gpool) && vec_ok(gpool) && act_ok(y) && vec_ok(y) && act_ok(gy) && vec_ok(gy) && mean &&
+                    invstd && scale && shift && dbeta && dgamma,
+                "bn_bwd_apply_pool: bad args");
+  if (gskip) EUNET_REQUIRE(act_ok(gskip) && vec_ok(gskip) && gskip->c == y->c && gskip->n == y->n &&
+                               gskip->h == y->h && gskip->w == y->w && gskip->dtype == y->dtype,
+                           "bn_bwd_apply_pool: gskip");
+  EUNET_REQUIRE(gpool->h * 2 == y->h && gpool->w * 2 == y->w && gpool->n == y->n && gpool->c == y->c &&
+                    gpool->dtype == y->dtype && gy->n == y->n && gy->h == y->h && gy->w == y->w && gy->c == y->c &&
+                    gy->dtype == y->dtype,
+                "bn_bwd_apply_pool: shapes (even H and W: every pixel in a 2x2 window)");
+  const int bs = bnr_block(y);
+  EUNET_REQUIRE(bs > 0, "bn_bwd_apply_pool: 256 or 192 %% channel units == 0");
+  const long long th = pool_threads(y);
+  const unsigned gr = (unsigned)std::min<long long>((th + bs - 1) / bs, 8192);
+#define BAP(T)                                                                                                       \
+  bn_bwd_apply_pool_kernel<T><<<gr, bs, 0, (hipStream_t)stream>>>(                                                   \
+      (const T*)gpool->ptr, gpool->ctot, gpool->coff, gskip ? (const T*)gskip->ptr : nullptr, gskip ? gskip->ctot : 0, \
+      gskip ? gskip->coff : 0, (const T*)y->ptr, y->ctot, y->coff, mean, invstd, scale, shift, dbeta, dgamma,          \
+      (T*)gy->ptr, gy->ctot, gy->coff, y->n, y->h, y->w, y->c)
+  if (y->dtype == EUNET_BF16) BAP(bf16_t);
+  else BAP(float);
+#undef BAP
+  EUNET_LAUNCH_CHECK("bn_bwd_apply_pool");
   return EUNET_OK;
 }
 

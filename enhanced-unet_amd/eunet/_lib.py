@@ -97,6 +97,7 @@ SIGNATURES = {
     "eunet_upsample_bwd": [_P, _P, c_void_p],
     "eunet_pool_bwd_add_bnr_rows": [_P, POINTER(c_int)],
     "eunet_pool_bwd_add_bnr": [_P, _P, _P, _P, _P, _f, _f, _f, _f, _f, c_void_p],
+    "eunet_bn_bwd_apply_pool": [_P, _P, _P, _f, _f, _f, _f, _f, _f, _P, c_void_p],
     "eunet_upsample_bwd_bnr_rows": [_P, POINTER(c_int)],
     "eunet_upsample_bwd_bnr": [_P, _P, _P, _f, _f, _f, _f, _f, c_void_p],
     "eunet_conv1x1_bwd_tiles": [_P, POINTER(c_int)],

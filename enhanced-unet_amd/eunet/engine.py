@@ -37,6 +37,13 @@ class Grad1x1:
         self.w, self.k, self.gz = w, k, gz
 
 
+class GradPool:
+    """A gradient w.r.t. relu(bn(y)) held as gskip + maxpool-adjoint(gpool) (UNetEngine.pool_recompute)."""
+
+    def __init__(self, gpool, gskip):
+        self.gpool, self.gskip = gpool, gskip
+
+
 class GradSink:
     """Default sink: a fresh fp32 tensor per parameter gradient."""
 
@@ -128,6 +135,13 @@ class UNetEngine:
     # (eunet_bn_bwd_apply_1x1: the same gy bit for bit, 2 x 537 MB less HBM traffic at the bench shape).
     # Needs fuse_bn_reduce and dec2 outside fuse_bn_apply (whose fused dgrad reads the stored gradient).
     dec1_recompute = True
+    # pool_recompute -- the same for the encoders' output gradients gskip + maxpool-adjoint(gpool):
+    # pool_bwd_add_bnr only reduces them, the block's apply recomputes them per 2x2 window
+    # (eunet_bn_bwd_apply_pool: the same gy bit for bit, 0.75 C per pixel less traffic).  Needs
+    # fuse_bn_reduce, the block outside fuse_bn_apply, and even H and W at the level.  Measured equal
+    # (182.4 vs 182.7 img/s over three alternating pairs, profiles/r05_ab.txt r5pr: the apply's window
+    # loads and argmax cost what the saved traffic gives): off
+    pool_recompute = False
     # dgrad_first -- after a DoubleConv's BN-a backward, conv .0's data gradient is issued on the launch
     # stream before the side-stream weight gradients (which wait on an event recorded right after the
     # apply, not on the launch stream's tail).  Closes half of the ~24 us apply -> dgrad launch-stream gap
@@ -314,7 +328,7 @@ class UNetEngine:
         return S
 
     # --------------------------------------------------------------- backward
-    def _block_bwd(self, nm, G: "torch.Tensor | Grad1x1", S, P, sink: GradSink, need_gx: bool, small: bool,
+    def _block_bwd(self, nm, G: "torch.Tensor | Grad1x1 | GradPool", S, P, sink: GradSink, need_gx: bool, small: bool,
                    gred=(None, 0)):
         """gred: (part, rows) of the block's BN-b backward reduction when G's producer fused it."""
         p = f"{self.prefix}{nm}"
@@ -324,12 +338,16 @@ class UNetEngine:
         dev, dt = yb.device, self.dtype
 
         def bn_back(prefix, g, y, bn, part=None, tiles=0):
-            if isinstance(g, Grad1x1):  # reduced by conv1x1_bwd_bnr, recomputed by the apply
+            if isinstance(g, (Grad1x1, GradPool)):  # reduced by its producer, recomputed by the apply
                 dbeta, dgamma = sink.slot(prefix + ".bias", (C,)), sink.slot(prefix + ".weight", (C,))
                 ops.colsum(part, tiles, 2 * C, dbeta, split=C, out_hi=dgamma)
                 gy = torch.empty_like(y)
-                ops.bn_bwd_apply_1x1(ops.act(y), g.w, g.k, g.gz, bn["mean"], bn["invstd"], bn["scale"],
-                                     bn["shift"], dbeta, dgamma, ops.act(gy))
+                if isinstance(g, Grad1x1):
+                    ops.bn_bwd_apply_1x1(ops.act(y), g.w, g.k, g.gz, bn["mean"], bn["invstd"], bn["scale"],
+                                         bn["shift"], dbeta, dgamma, ops.act(gy))
+                else:
+                    ops.bn_bwd_apply_pool(g.gpool, g.gskip, ops.act(y), bn["mean"], bn["invstd"], bn["scale"],
+                                          bn["shift"], dbeta, dgamma, ops.act(gy))
                 return gy
             if part is None:  # reduction not fused into the producer of g
                 tiles = ops.bn_bwd_tiles(ops.act(y))
@@ -554,14 +572,22 @@ class UNetEngine:
             ops.upsample_bwd_bnr(ghi, ops.act(glo), *bnr_args(nm), part)
             return part, rows
 
-        def pool_bwd(act_saved: ops.Act, gpool: ops.Act, gskip: ops.Act, gout: torch.Tensor, nm):
-            rows = ops.pool_bwd_add_bnr_rows(ops.act(gout)) if self.fuse_bn_reduce else 0
+        def pool_bwd(act_saved: ops.Act, gpool: ops.Act, gskip: ops.Act, shape, nm):
+            """block nm's output gradient (a tensor, or GradPool when the apply recomputes it) and the
+            (part, rows) of its fused BN-b reduction."""
+            rows = ops.pool_bwd_add_bnr_rows(act_saved) if self.fuse_bn_reduce else 0  # (gout's shape)
             if not rows:
+                gout = _e(shape, dt, dev)
                 ops.pool_bwd_add(act_saved, gpool, gskip, ops.act(gout))
-                return None, 0
-            part = _e(rows * 2 * gout.shape[3], torch.float32, dev)
+                return gout, (None, 0)
+            part = _e(rows * 2 * shape[3], torch.float32, dev)
+            if (self.pool_recompute and not _per_block(self.fuse_bn_apply, nm) and shape[1] % 2 == 0
+                    and shape[2] % 2 == 0):
+                ops.pool_bwd_add_bnr(act_saved, gpool, gskip, None, *bnr_args(nm), part)
+                return GradPool(gpool, gskip), (part, rows)
+            gout = _e(shape, dt, dev)
             ops.pool_bwd_add_bnr(act_saved, gpool, gskip, ops.act(gout), *bnr_args(nm), part)
-            return part, rows
+            return gout, (part, rows)
 
         # ---- dec1 (1x1) -> gradient w.r.t. d2 = relu(bn(y_b of dec2))
         s2 = S["dec2"]
@@ -605,18 +631,18 @@ class UNetEngine:
         # ---- encoder (skip gradients + max-pool backward)
         g_p3 = self._block_bwd("enc4", g_e4, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e4
-        g_e3 = _e((N, H >> 2, W >> 2, ch[2]), dt, dev)
-        red = pool_bwd(ops.act(S["cat4"], ch[3], ch[2]), ops.act(g_p3), ops.act(g_cat4, ch[3], ch[2]), g_e3, "enc3")
+        g_e3, red = pool_bwd(ops.act(S["cat4"], ch[3], ch[2]), ops.act(g_p3), ops.act(g_cat4, ch[3], ch[2]),
+                             (N, H >> 2, W >> 2, ch[2]), "enc3")
         del g_p3, g_cat4
         g_p2 = self._block_bwd("enc3", g_e3, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e3
-        g_e2 = _e((N, H >> 1, W >> 1, ch[1]), dt, dev)
-        red = pool_bwd(ops.act(S["cat3"], ch[2], ch[1]), ops.act(g_p2), ops.act(g_cat3, ch[2], ch[1]), g_e2, "enc2")
+        g_e2, red = pool_bwd(ops.act(S["cat3"], ch[2], ch[1]), ops.act(g_p2), ops.act(g_cat3, ch[2], ch[1]),
+                             (N, H >> 1, W >> 1, ch[1]), "enc2")
         del g_p2, g_cat3
         g_p1 = self._block_bwd("enc2", g_e2, S, P, sink, need_gx=True, small=False, gred=red)
         del g_e2
-        g_e1 = _e((N, H, W, ch[0]), dt, dev)
-        red = pool_bwd(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]), g_e1, "enc1")
+        g_e1, red = pool_bwd(ops.act(S["cat2"], ch[1], ch[0]), ops.act(g_p1), ops.act(g_cat2, ch[1], ch[0]),
+                             (N, H, W, ch[0]), "enc1")
         del g_p1, g_cat2
         self._block_bwd("enc1", g_e1, S, P, sink, need_gx=False, small=True, gred=red)
         if self.overlap_wgrad:

@@ -429,12 +429,21 @@ def pool_bwd_add_bnr_rows(gout: Act) -> int:
     return r.value
 
 
-@_dispatched("A A A? A! A T T T T T!")
-def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act, y: Act, mean, invstd, scale, shift,
-                     part):
-    """pool_bwd_add + the BN-backward partial sums of the block whose output gradient gout is."""
-    call("eunet_pool_bwd_add_bnr", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), ctypes.byref(gout),
+@_dispatched("A A A? A!? A T T T T T!")
+def pool_bwd_add_bnr(act_saved: Act, gpool: Act, gskip: Act | None, gout: Act | None, y: Act, mean, invstd, scale,
+                     shift, part):
+    """pool_bwd_add + the BN-backward partial sums of the block whose output gradient gout is (gout None: reduced
+    only, bn_bwd_apply_pool recomputes it)."""
+    call("eunet_pool_bwd_add_bnr", ctypes.byref(act_saved), ctypes.byref(gpool), _ref(gskip), _ref(gout),
          ctypes.byref(y), _ptr(mean), _ptr(invstd), _ptr(scale), _ptr(shift), _ptr(part), _stream())
+
+
+@_dispatched("A A? A T T T T T T A!")
+def bn_bwd_apply_pool(gpool: Act, gskip: Act | None, y: Act, mean, invstd, scale, shift, dbeta, dgamma, gy: Act):
+    """bn_bwd_apply of gout = gskip + scatter(gpool) that pool_bwd_add_bnr reduced without storing (recomputed per
+    2x2 window with its arithmetic and rounding: the same gy bit for bit)."""
+    call("eunet_bn_bwd_apply_pool", ctypes.byref(gpool), _ref(gskip), ctypes.byref(y), _ptr(mean), _ptr(invstd),
+         _ptr(scale), _ptr(shift), _ptr(dbeta), _ptr(dgamma), ctypes.byref(gy), _stream())
 
 
 def upsample_bwd_bnr_rows(glo: Act) -> int:

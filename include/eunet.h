@@ -283,6 +283,14 @@ int eunet_pool_bwd_add_bnr_rows(const eunet_act* gout, int* rows);
 int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const eunet_act* gskip,
                            const eunet_act* gout, const eunet_act* y, const float* mean, const float* invstd,
                            const float* scale, const float* shift, float* part, void* stream);
+/* gout may be NULL in eunet_pool_bwd_add_bnr: the gradient is then only reduced, and the block's apply
+ * recomputes it -- eunet_bn_bwd_apply_pool = eunet_bn_bwd_apply on gout = gskip + scatter(gpool), formed and
+ * rounded per 2x2 window as eunet_pool_bwd_add_bnr forms it (the same gy bit for bit, without gout's write and
+ * read; even H and W).  Reference: the autograd of models.py:226-229 (MaxPool2d(2) after each encoder block, its
+ * output also the skip input of the decoder concat) and models.py:222-223 (the block's second BatchNorm). */
+int eunet_bn_bwd_apply_pool(const eunet_act* gpool, const eunet_act* gskip, const eunet_act* y, const float* mean,
+                            const float* invstd, const float* scale, const float* shift, const float* dbeta,
+                            const float* dgamma, const eunet_act* gy, void* stream);
 int eunet_upsample_bwd_bnr_rows(const eunet_act* glo, int* rows);
 int eunet_upsample_bwd_bnr(const eunet_act* ghi, const eunet_act* glo, const eunet_act* y, const float* mean,
                            const float* invstd, const float* scale, const float* shift, float* part, void* stream);

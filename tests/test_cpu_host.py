@@ -234,7 +234,8 @@ def test_network_ops_registered_with_the_dispatcher():
     expect = {"conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bnbwd", "conv3x3_dgrad_fused", "conv3x3_wgrad",
               "wgrad_reduce", "conv_small_fwd", "conv_small_wgrad", "bn_finalize", "bnrelu_pool", "bnrelu_upsample",
               "bnrelu_conv1x1", "head_fwd", "head_bwd", "bn_bwd_apply", "bn_bwd_coef", "bn_bwd_apply_coef",
-              "pool_bwd_add_bnr", "upsample_bwd_bnr", "conv1x1_bwd_bnr", "bn_bwd_apply_1x1", "colsum", "conv3x3_pack"}
+              "pool_bwd_add_bnr", "upsample_bwd_bnr", "conv1x1_bwd_bnr", "bn_bwd_apply_1x1", "bn_bwd_apply_pool",
+              "colsum", "conv3x3_pack"}
     assert expect <= set(ops.DISPATCHED)
     sch = str(torch.ops.eunet.conv3x3_fwd.default._schema)
     assert sch.startswith("eunet::conv3x3_fwd(Tensor x, int x_coff, int x_c, Tensor wp, Tensor(a!) y,"), sch

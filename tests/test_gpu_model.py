@@ -347,25 +347,29 @@ def test_backward_stream_schedules_are_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("dt,base", [("bf16", 16), ("fp32", 16), ("bf16", 64)])
-def test_dec1_recomputed_gradient_is_exact(monkeypatch, dt, base):
-    """dec1's input gradient recomputed inside dec2's BN-backward apply (UNetEngine.dec1_recompute:
-    conv1x1_bwd_bnr reduces W^T g_z without storing it, eunet_bn_bwd_apply_1x1 recomputes it with the same
-    arithmetic and rounding) against the stored-gradient path: every gradient bit for bit (base 64: the
-    J = 1 channel-half kernels; base 16: C = 16)."""
+def test_recomputed_block_gradients_are_exact(monkeypatch, dt, base):
+    """Block output gradients recomputed inside their BatchNorm's backward apply instead of stored: dec1's
+    W^T g_z (UNetEngine.dec1_recompute, eunet_bn_bwd_apply_1x1) and the encoders' gskip + maxpool-adjoint
+    (UNetEngine.pool_recompute, eunet_bn_bwd_apply_pool), each producer reducing without storing -- against
+    the stored-gradient path: every gradient bit for bit, each switch alone and both (base 64: the bench's
+    channel counts; base 16: C = 16 / 32 / 64)."""
     from eunet import engine, synth
     from eunet.losses import combined_loss
     x, msk = synth.batch(2, 64, 96, start_index=9, num_classes=2, in_channels=1)
     out = {}
-    for rec in (True, False):
-        monkeypatch.setattr(engine.UNetEngine, "dec1_recompute", rec)
+    for dec1, pool in ((False, False), (True, False), (False, True), (True, True)):
+        monkeypatch.setattr(engine.UNetEngine, "dec1_recompute", dec1)
+        monkeypatch.setattr(engine.UNetEngine, "pool_recompute", pool)
         m = _model(base, 1, 2, dt)
         m.train()
         loss = combined_loss(m.forward_lowres(x.to(DEV)), msk.to(DEV))
         loss.backward()
         torch.cuda.synchronize()
-        out[rec] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
-    for k, g in out[True].items():
-        assert torch.equal(g, out[False][k]), k
+        out[(dec1, pool)] = {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+    ref = out[(False, False)]
+    for key, grads in out.items():
+        for k, g in grads.items():
+            assert torch.equal(g, ref[k]), (key, k)
 
 
 def test_train_epoch_device_loss_sum():
