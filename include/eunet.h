@@ -286,8 +286,9 @@ int eunet_pool_bwd_add_bnr(const eunet_act* act, const eunet_act* gpool, const e
 /* gout may be NULL in eunet_pool_bwd_add_bnr: the gradient is then only reduced, and the block's apply
  * recomputes it -- eunet_bn_bwd_apply_pool = eunet_bn_bwd_apply on gout = gskip + scatter(gpool), formed and
  * rounded per 2x2 window as eunet_pool_bwd_add_bnr forms it (the same gy bit for bit, without gout's write and
- * read; even H and W).  Reference: the autograd of models.py:226-229 (MaxPool2d(2) after each encoder block, its
- * output also the skip input of the decoder concat) and models.py:222-223 (the block's second BatchNorm). */
+ * read; even H and W).  Reference: the autograd of models.py:214, 228-230 (MaxPool2d(2) after each encoder block,
+ * its input also the skip input of the decoder concat, :232-234) and models.py:222-223 (the block's second
+ * BatchNorm). */
 int eunet_bn_bwd_apply_pool(const eunet_act* gpool, const eunet_act* gskip, const eunet_act* y, const float* mean,
                             const float* invstd, const float* scale, const float* shift, const float* dbeta,
                             const float* dgamma, const eunet_act* gy, void* stream);
@@ -311,7 +312,7 @@ int eunet_conv1x1_bwd_bnr(const eunet_act* y, const float* scale, const float* s
 /* eunet_bn_bwd_apply for the gradient eunet_conv1x1_bwd_bnr produced without storing it: g = W^T gz
  * (w [K][C], gz [N*H*W][K] fp32) recomputed per pixel with conv1x1_bwd's arithmetic and rounding to
  * y's dtype, then gy = scale (g' - dbeta/n - xhat dgamma/n) as eunet_bn_bwd_apply -- the same gy bit for
- * bit, without the C-channel gradient's write and read.  Reference: the autograd of models.py:336-337
+ * bit, without the C-channel gradient's write and read.  Reference: the autograd of models.py:212, 236
  * (dec1 = Conv2d 1x1 on relu(bn(dec2's conv .3 output)), models.py:220-223). */
 int eunet_bn_bwd_apply_1x1(const eunet_act* y, const float* w, int k, const float* gz, const float* mean,
                            const float* invstd, const float* scale, const float* shift, const float* dbeta,
