@@ -115,9 +115,9 @@ __global__ __launch_bounds__(NT) void conv_small_fwd_kernel(SmallArgs a) {
       }
     }
     T* yp = (T*)a.y + ((long long)(n * a.H + yy) * a.W + xx) * a.yct + a.yco + co0 + 8 * g;
-    if (full) {
-      *(uint4*)yp = Vec16<T>::pack(acc);
-      if constexpr (E == 4) *(uint4*)(yp + 4) = Vec16<T>::pack(acc + 4);
+    if (full) {  // (non-temporal: y is read back by the next conv well after it has left L2)
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(acc)), (u32x4*)yp);
+      if constexpr (E == 4) __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(acc + 4)), (u32x4*)(yp + 4));
     } else {
       for (int e = 0; e < 8; ++e)
         if (co0 + 8 * g + e < a.cout) Elem<T>::st(yp + e, acc[e]);

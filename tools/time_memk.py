@@ -61,3 +61,12 @@ for h, c in ((128, 512), (256, 256), (512, 128)):
     tot += ms
     print(f"upsample_bwd_bnr {h:4d}^2 x {c:3d} {ms * 1e3:7.1f} us  {glo.numel() * 2 * 6 / ms / 1e9:5.2f} TB/s")
 print(f"upsample_bwd_bnr total {tot * 1e3:7.1f} us")
+
+# enc1.0: the 1-input-channel direct conv (conv_small_fwd, 1024^2 x 4 -> 64 channels bf16, BN partials), HBM-write-bound
+xs1 = torch.randn(N, H, H, 1, device=dev).bfloat16()
+w1s, b1s = torch.randn(64, 1, 3, 3, device=dev) * 0.3, torch.randn(64, device=dev) * 0.1
+ys1 = torch.empty(N, H, H, 64, device=dev).bfloat16()
+tiles1 = N * (H // 16) * (H // 32)
+st1 = torch.empty(tiles1 * 2 * 64 + tiles1, device=dev)
+ms = timeit(lambda: ops.conv_small_fwd(ops.act(xs1), w1s, b1s, ops.act(ys1), st1))
+print(f"conv_small_fwd enc1.0 {ms * 1e3:7.1f} us  {(ys1.numel() * 2 + xs1.numel() * 2) / ms / 1e9:5.2f} TB/s")
