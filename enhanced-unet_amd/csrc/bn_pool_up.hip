@@ -453,13 +453,16 @@ __global__ void bnrelu_pool_kernel(const T* y, int N, int H, int W, int C, int y
     for (int dx = 0; dx < 2; ++dx) {
       const long long pix = (long long)(n * H + 2 * yo + dy) * W + 2 * xo + dx;
       float f[E];
-      Vec16<T>::unpack(*(const uint4*)(y + pix * yct + yco + c), f);
+      // y is read once here (disjoint windows) and the skip activation is next read by the decoder, long
+      // after: both non-temporal; the pooled output, read by the next encoder conv, is cached normally
+      Vec16<T>::unpack(__builtin_bit_cast(uint4, __builtin_nontemporal_load((const u32x4*)(y + pix * yct + yco + c))), f);
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         f[j] = fmaxf(fmaf(f[j], s[j], t[j]), 0.f);
         m[j] = fmaxf(m[j], f[j]);
       }
-      if (act != nullptr) *(uint4*)(act + pix * act_ct + act_co + c) = Vec16<T>::pack(f);
+      if (act != nullptr)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(f)), (u32x4*)(act + pix * act_ct + act_co + c));
     }
   const long long po = (long long)(n * Ho + yo) * Wo + xo;
   *(uint4*)(pool + po * pct + pco + c) = Vec16<T>::pack(m);
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(256) void bnrelu_up_rows_kernel(const T* y, int N, 
       float f[E];
 #pragma unroll
       for (int e = 0; e < E2; ++e) { f[2 * e] = o[b][e].x; f[2 * e + 1] = o[b][e].y; }
-      *(uint4*)(out + (po + b) * oct + oco + c) = Vec16<T>::pack(f);
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(f)), (u32x4*)(out + (po + b) * oct + oco + c));
     }
   };
   f32x2 xp[4][E2], xc[4][E2], xn[4][E2];

@@ -70,3 +70,15 @@ tiles1 = N * (H // 16) * (H // 32)
 st1 = torch.empty(tiles1 * 2 * 64 + tiles1, device=dev)
 ms = timeit(lambda: ops.conv_small_fwd(ops.act(xs1), w1s, b1s, ops.act(ys1), st1))
 print(f"conv_small_fwd enc1.0 {ms * 1e3:7.1f} us  {(ys1.numel() * 2 + xs1.numel() * 2) / ms / 1e9:5.2f} TB/s")
+
+# BN+ReLU -> skip activation + 2x2 max-pool (the bench's three launches: 1024^2 x 64, 512^2 x 128, 256^2 x 256)
+tot = 0.0
+for h, c in ((1024, 64), (512, 128), (256, 256)):
+    yp_ = torch.randn(N, h, h, c, device=dev).bfloat16()
+    catp = torch.empty(N, h, h, 2 * c, device=dev).bfloat16()
+    pooled = torch.empty(N, h // 2, h // 2, c, device=dev).bfloat16()
+    sc, sh = torch.rand(c, device=dev) + 0.5, torch.randn(c, device=dev) * 0.3
+    ms = timeit(lambda: ops.bnrelu_pool(ops.act(yp_), sc, sh, ops.act(catp, c, c), ops.act(pooled)))
+    tot += ms
+    print(f"bnrelu_pool {h:5d}^2 x {c:3d} {ms * 1e3:7.1f} us  {yp_.numel() * 2 * 2.25 / ms / 1e9:5.2f} TB/s")
+print(f"bnrelu_pool total {tot * 1e3:7.1f} us")
