@@ -871,7 +871,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* g, int gct, 
       o[j] = fmaf(k1[j], gg, fmaf(yf[j], k2[j], k3[j]));
     }
     EUNET_DASSERT(p < P && oco + c + E <= oct && u < U);
-    *(uint4*)(gy + p * oct + oco + c) = Vec16<TO>::pack(o);
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<TO>::pack(o)), (u32x4*)(gy + p * oct + oco + c));
   }
 }
 
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_1x1_kernel(const T* y, int y
       o[j] = fmaf(k1[j], gg, fmaf(yf[j], k2[j], k3[j]));
     }
     EUNET_DASSERT(p < P && oco + c + E <= oct && u < U);
-    *(uint4*)(gy + p * oct + oco + c) = Vec16<T>::pack(o);
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(o)), (u32x4*)(gy + p * oct + oco + c));
   }
 }
 
@@ -1052,7 +1052,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void po
 #pragma unroll
       for (int j = 0; j < E; ++j) o[j] += (arg[j] == k) ? gpv[j] : 0.f;
       const uint4 packed = Vec16<T>::pack(o);
-      if (go) *(uint4*)(go + pix[k] * goct + goco + c) = packed;  // (go null: reduced only, bn_bwd_apply_pool)
+      if (go)  // (go null: reduced only, bn_bwd_apply_pool)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(go + pix[k] * goct + goco + c));
       if constexpr (RED) {
         float gr[E], yv[E];
         Vec16<T>::unpack(packed, gr);
@@ -1134,7 +1135,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1))) void bn
         const float gg = fmaf(yv[j], kP[j], kQ[j]) > 0.f ? gr[j] : 0.f;
         out[j] = fmaf(k1[j], gg, fmaf(yv[j], k2[j], k3[j]));
       }
-      *(uint4*)(gy + pix[k] * oct + oco + c) = Vec16<T>::pack(out);
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, Vec16<T>::pack(out)), (u32x4*)(gy + pix[k] * oct + oco + c));
     }
   }
 }
@@ -1286,7 +1287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void u
 #pragma unroll
         for (int j = 0; j < E2; ++j) { ac[2 * j] = acur[b][j].x; ac[2 * j + 1] = acur[b][j].y; }
         const uint4 packed = Vec16<TO>::pack(ac);
-        *(uint4*)(o + pix * oct + oco + c) = packed;
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(o + pix * oct + oco + c));
         if constexpr (RED) {
           float gr[E], yv[E];
           Vec16<TO>::unpack(packed, gr);
