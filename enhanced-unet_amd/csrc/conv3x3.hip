@@ -715,8 +715,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         EUNET_DASSERT(tile_px + (long long)r * a.W + c < (long long)a.N * a.H * a.W && co + E <= a.cout &&
                       a.yco + co + E <= a.yct);
         const uint4 packed = Vec16<T>::pack(f);
-        if constexpr (sizeof(TO) == sizeof(T)) {
-          *(uint4*)(ybase + off) = packed;
+        if constexpr (sizeof(TO) == sizeof(T)) {  // (non-temporal: the output is read back after it left L2)
+          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(ybase + off));
         } else {  // fp32 output of a bf16 kernel: E = 8 floats, two 16-byte stores
           float* yo = yfbase + off;
           *(float4*)yo = make_float4(f[0], f[1], f[2], f[3]);
