@@ -305,6 +305,9 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
         # (graph steps: deferred-loss warm-up steps, so the graph is captured before the timed region)
         tr.step(x, m, sync_loss=not graph)
     torch.cuda.synchronize()
+    dp = getattr(tr, "dp", None)
+    if dp is not None:
+        dp.start_timing()
     if world > 1:
         dist.barrier()
     # one event per step boundary on the launch stream (K+1 markers, no per-kernel cost): the
@@ -322,6 +325,8 @@ def timed_steps(tr, x, m, steps, warmup, world, dev):
             host.append(time.perf_counter())
         torch.cuda.synchronize()
         t1 = time.perf_counter()
+    timer.dp = dp.stop_timing() if dp is not None else None
+    timer.local_s = t1 - t0
     if world > 1:
         dist.barrier()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
@@ -435,6 +440,18 @@ def conv_roofline(args, timer, steps, step_flops, elapsed, dtype):
                                "launches_per_step": en["launches"] // max(1, steps),
                                "covers": "forward launches of enc1.3 and enc2-4 .0/.3 (enc1.0, Cin=1, runs on the "
                                          "HBM-bound conv_small kernel)"}
+    if "conv3x3.encoder_train" in ks:  # the same convs' forward + data + weight gradients, over their union wall
+        et = ks["conv3x3.encoder_train"]
+        wall = timer.union_ms(["conv3x3.encoder_train"])
+        et_tf = et["flops"] / (wall * 1e-3) / 1e12 if wall else None
+        roof["encoder_train"] = {"achieved": round(et_tf, 2) if et_tf else None,
+                                 "frac": round(et_tf / peak, 4) if et_tf else None,
+                                 "wall_ms_per_step": round(wall / steps, 3),
+                                 "spans_ms_per_step": round(et["ms"] / steps, 3),
+                                 "launches_per_step": et["launches"] // max(1, steps),
+                                 "covers": "every conv3x3 MFMA launch of the encoder blocks (enc1.3, enc2-4 .0/.3): "
+                                           "forward, data gradient and weight gradient (side stream included); "
+                                           "FLOPs over the union of their HIP-event intervals"}
     return roof
 
 
@@ -523,6 +540,7 @@ def dual_configs4_leg(args, dev):
     a4.size, a4.batch, a4.dtype, a4.base, a4.dual = size, batch, "bf16", base, True
     roof = conv_roofline(a4, timer, args.steps, sf, el, "bf16")
     roof.pop("encoder_fwd", None)
+    roof.pop("encoder_train", None)
     out = {"value": round(batch * args.steps / el, 3), "unit": "img/s", "ms_per_step": round(1e3 * el / args.steps, 3),
            "workload": "dual-branch + deep supervision, base_ch=96, 1x2048x2048 1-ch->2-cls, batch 2/GPU, bf16 "
                        "(BASELINE configs[4] per GPU)",
@@ -569,6 +587,11 @@ def main():
     x, m = synth.batch(args.batch, args.size, args.size, start_index=rank * args.batch, num_classes=2,
                        in_channels=1, device=dev)
     elapsed, timer = timed_steps(tr, x, m, args.steps, args.warmup, world, dev)
+    per_rank = None
+    if world > 1:  # every rank's own step time and exposed communication (train_eval.py:337-343 per rank)
+        mine = {"rank": rank, "ms_per_step": round(1e3 * timer.local_s / args.steps, 3), **(timer.dp or {})}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     diag = step_record(timer, tr, x, m)
     if rank != 0:
         if world > 1:
@@ -605,7 +628,8 @@ def main():
         "unit": "img/s",
         "n_gpus": world,
         "world": {"size": dist.get_world_size() if world > 1 else 1,
-                  "backend": backend + (" (RCCL)" if backend == "nccl" else "") if world > 1 else None},
+                  "backend": backend + (" (RCCL)" if backend == "nccl" else "") if world > 1 else None,
+                  "per_rank": per_rank},
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_plain, 3),

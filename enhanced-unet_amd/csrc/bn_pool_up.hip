@@ -356,7 +356,7 @@ constexpr int FNT = 1024;  // threads per channel block of bn_finalize (8 tiles 
 __global__ __launch_bounds__(FNT) void bn_finalize_kernel(const float* st, int tiles, int C, const float* gamma,
                                                          const float* beta, float eps, float mom, float* rm,
                                                          float* rv, float* mean_o, float* invstd_o, float* scale_o,
-                                                         float* shift_o, long long* nbt) {
+                                                         float* shift_o, long long* nbt, const double* guard) {
   __shared__ double shn[FNT], shm[FNT], shq[FNT];
   const int c = blockIdx.x, tid = threadIdx.x;
   const float* cnt = st + (long long)2 * C * tiles;
@@ -403,6 +403,9 @@ __global__ __launch_bounds__(FNT) void bn_finalize_kernel(const float* st, int t
     __syncthreads();
   }
   n = shn[0]; mean = shm[0]; m2 = shq[0];
+  // the running statistics stay as they are while the update guard is raised (eunet_set_update_guard)
+  const bool keep = guard != nullptr && *guard != 0.0;
+  if (keep) { rm = nullptr; rv = nullptr; nbt = nullptr; }
   if (tid == 0 && c == 0 && nbt != nullptr) *nbt += 1;  // BatchNorm2d.num_batches_tracked
   if (tid == 0) {
     const double var_b = m2 / n;
@@ -1640,7 +1643,7 @@ int eunet_bn_finalize(const float* stats, int tiles, int c, const float* gamma, 
   EUNET_REQUIRE(stats && tiles > 0 && c > 0 && gamma && beta, "bn_finalize: bad args");
   bn_finalize_kernel<<<c, FNT, 0, (hipStream_t)stream>>>(stats, tiles, c, gamma, beta, eps, momentum, run_mean,
                                                         run_var, mean, invstd, scale, shift,
-                                                        (long long*)num_batches_tracked);
+                                                        (long long*)num_batches_tracked, eunet::update_guard());
   EUNET_LAUNCH_CHECK("bn_finalize");
   return EUNET_OK;
 }

@@ -110,7 +110,13 @@ int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream) {
   return EUNET_OK;
 }
 
-// Stream-to-stream ordering on the current device: `to` waits for the work enqueued on `from` so far.  The
+int eunet_set_update_guard(int device, const double* guard) {
+  EUNET_REQUIRE(device >= 0 && device < eunet::GUARD_NDEV, "set_update_guard: device index %d out of range", device);
+  eunet::update_guard_slot(device) = guard;
+  return EUNET_OK;
+}
+
+// Stream-to-stream ordering on the streams' device: `to` waits for the work enqueued on `from` so far.  The
 // events have a device-scope release and no timing (torch's Stream.wait_stream records an event with the
 // default system-scope release, whose cache writeback / invalidate sits between the producing kernel and
 // the recording stream's next kernel).  A ring of events per device; re-recording one whose wait is
@@ -120,18 +126,28 @@ int eunet_stream_wait(void* from, void* to) {
   static std::mutex mu;
   static hipEvent_t ring[NDEV][RING];
   static unsigned next[NDEV];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= NDEV) {
-    eunet::set_error("stream_wait: no current device (or device index >= %d)", NDEV);
+  // the device of the streams, not the calling thread's current device (a DataParallel replica or an
+  // autograd thread need not have entered it); both streams must be on it
+  int dev = 0, dev_to = 0;
+  if (hipStreamGetDevice((hipStream_t)from, &dev) != hipSuccess ||
+      hipStreamGetDevice((hipStream_t)to, &dev_to) != hipSuccess || dev < 0 || dev >= NDEV) {
+    eunet::set_error("stream_wait: cannot query the streams' device (or device index >= %d)", NDEV);
     return EUNET_ERR_HIP;
   }
+  EUNET_REQUIRE(dev == dev_to, "stream_wait: streams on devices %d and %d", dev, dev_to);
   std::lock_guard<std::mutex> lock(mu);
   hipEvent_t& e = ring[dev][next[dev]++ % RING];
-  if (e == nullptr &&
-      hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
-    e = nullptr;
-    eunet::set_error("stream_wait: hipEventCreateWithFlags failed");
-    return EUNET_ERR_HIP;
+  if (e == nullptr) {
+    int cur = 0;
+    const bool sw = hipGetDevice(&cur) == hipSuccess && cur != dev;
+    if (sw) (void)hipSetDevice(dev);  // the event belongs to the device current at its creation
+    const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice);
+    if (sw) (void)hipSetDevice(cur);
+    if (rc != hipSuccess) {
+      e = nullptr;
+      eunet::set_error("stream_wait: hipEventCreateWithFlags failed");
+      return EUNET_ERR_HIP;
+    }
   }
   if (hipEventRecord(e, (hipStream_t)from) != hipSuccess || hipStreamWaitEvent((hipStream_t)to, e, 0) != hipSuccess) {
     eunet::set_error("stream_wait: record / wait failed");

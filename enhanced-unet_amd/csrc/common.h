@@ -33,6 +33,20 @@ __device__ __forceinline__ bf16x8 cat_bf16x4(s16x4 lo, s16x4 hi) {
 namespace eunet {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+
+// The update guard of the current device (eunet_set_update_guard): a device fp64 word; while it is
+// nonzero the persistent-state writes of eunet_bn_finalize and eunet_clip_adamw are skipped.  Read
+// on the host at launch, so a captured graph keeps the pointer it was captured with.
+constexpr int GUARD_NDEV = 64;
+inline const double*& update_guard_slot(int dev) {
+  static const double* slots[GUARD_NDEV] = {};
+  return slots[dev];
+}
+inline const double* update_guard() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= GUARD_NDEV) return nullptr;
+  return update_guard_slot(d);
+}
 }  // namespace eunet
 
 #define EUNET_REQUIRE(cond, ...)                    \

@@ -94,16 +94,25 @@ constexpr int FHPXP = 640;                   // halo pixel slots (612 used), 4 c
 // fragment reads) and 6 % with the quarter XOR-swizzle that removes them (its per-read address VALU), the
 // DMA-staged data gradient gains 6 %, the DMA-staged untransformed forward 5-13 % -- so the layout follows the
 // staging.
+// Round 6: the pixel-major slots are split into two channel halves, [q >> 1][hp][q & 1] (a pixel's quarters
+// 2h, 2h + 1 -- 32 contiguous bytes -- adjacent, the halves 2 * FHPXP slots apart).  A ds_read_b128 lane
+// group of the A fragments (lanes 0-3 / 12-15 at quarter q, 4-11 at q + 1, or the reverse, over 16
+// consecutive halo pixels) then covers 16 distinct 16-byte slots of a bank row for any first pixel, where
+// [hp][q] put pixels 4 apart on one slot (2-way: SQ_LDS_BANK_CONFLICT 0.35-0.39 of the LDS cycles of every
+// DMA-staged forward / data gradient, profiles/r06_sq_layers.txt); a DMA wave-instruction reads 32 pixels x
+// 32 contiguous bytes.
+constexpr int FHALF = 2 * FHPXP;  // slots per channel half
 template <bool PIX>
 __device__ __forceinline__ int fslot(int hp, int q) {
-  return PIX ? hp * 4 + q : q * FHPXP + hp;
+  return PIX ? (q >> 1) * FHALF + hp * 2 + (q & 1) : q * FHPXP + hp;
 }
 // inverse for slot s: (halo pixel, quarter)
 template <bool PIX>
 __device__ __forceinline__ void fslot_inv(int s, int& hp, int& q) {
   if (PIX) {
-    hp = s >> 2;
-    q = s & 3;
+    const int h = s / FHALF, r = s - h * FHALF;
+    hp = r >> 1;
+    q = 2 * h + (r & 1);
   } else {
     q = s / FHPXP;
     hp = s - q * FHPXP;
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   // this thread's halo quarter (fwd_unit), the same for every unit (ids tid + FT i)
   constexpr bool PIX = ((DG && !BT) || PF) && sizeof(T) == 2;  // halo layout / staging (fslot)
-  const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
+  const int sq = PIX ? tid & 1 : (tid >> 3) & 3;  // (PIX: the quarter of unit tid; PIX stages by dma_a only)
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const T*)a.x + (long long)ns * a.H * a.W * a.xct), 0,
@@ -370,9 +379,11 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
     const bool full = (kc + 1) * KC <= a.cin;  // else: quarters past cin read as zeros
 #pragma unroll
+    static_assert(FHALF % FT == 0, "dma_a: a wave-instruction stays inside one channel half");
     for (int i = 0; i < A_IT; ++i) {
       uint32_t off = aoff[i];
-      if (!full && kc * KC + (tid & 3) * E >= a.cin) off = FWD_OOB;  // (quarter of slot tid + FT i)
+      // quarter of slot tid + FT i: half (FT i) / FHALF (tid < FT), then the slot's parity
+      if (!full && kc * KC + (2 * (i * FT / FHALF) + (tid & 1)) * E >= a.cin) off = FWD_OOB;
       EUNET_DASSERT(off == FWD_OOB || off + cadd + 16u <= slice_bytes);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + (i * FT + wvs * 64) * 16),
                                                16, off, cadd, 0, 0);
@@ -1008,9 +1019,13 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
                                                16, ok ? off : FWD_OOB, 0, 0, 0);
     }
   };
-  // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t & 7 and
-  // halo pixels (t >> 3) + 32 i (i < 11): its 8 scales / shifts are read once per tile.
-  const int xo = tid & 7;
+  // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t >> 5 and
+  // halo pixels (t & 31) + 32 i (i < 11): its 8 scales / shifts are read once per tile.  A wave covers 32
+  // consecutive pixels of two octants, so the 16 lanes of a ds_read_b128 group and the 8 of a
+  // ds_write_b128 group address distinct 16-byte slots of a bank row (octant-fastest lanes, as before
+  // round 6, put 2 - 4 lanes on one slot: SQ_LDS_BANK_CONFLICT 0.34 of the LDS cycles, wgrad +35 % with
+  // the transform on the 64-channel layers).
+  const int xo = tid >> 5;
   auto bnrelu_x = [&](int y0, int x0) {
     if (kc * KCW + xo * 8 >= a.cin) return;
     const f32x4 s0 = *(const f32x4*)(lsc + xo * 8), s1 = *(const f32x4*)(lsc + xo * 8 + 4);
@@ -1029,14 +1044,14 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       bool ok[G];
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        const int hp = (tid >> 3) + 32 * (i0 + j), hy = hp / HW_, hx = hp - hy * HW_;
+        const int hp = (tid & 31) + 32 * (i0 + j), hy = hp / HW_, hx = hp - hy * HW_;
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
         ok[j] = (hp < HPX) & ((uint32_t)yy < (uint32_t)a.H) & ((uint32_t)xx < (uint32_t)a.W);
         w[j] = *(const u32x4*)(plane + hp * 16);
       }
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        const int hp = (tid >> 3) + 32 * (i0 + j);
+        const int hp = (tid & 31) + 32 * (i0 + j);
         u32x4 o;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {  // packed fp32 FMA, round to bf16, ReLU on the bf16 pair (sign bit)

@@ -50,7 +50,7 @@ __device__ __forceinline__ OptRow opt_row(const long long* tab, int nt, int blk,
 }
 
 __global__ __launch_bounds__(OPT_NT) void opt_sumsq_kernel(const long long* tab, int nt, double* partial,
-                                                           GradPtrs gp) {
+                                                           GradPtrs gp, const double* guard) {
   __shared__ double red[OPT_NT / 64];
   const int tid = threadIdx.x, blk = blockIdx.x;
   const OptRow r = opt_row(tab, nt, blk, gp);
@@ -71,7 +71,8 @@ __global__ __launch_bounds__(OPT_NT) void opt_sumsq_kernel(const long long* tab,
   __syncthreads();
   if (tid == 0) {
     partial[blk] = (red[0] + red[1]) + (red[2] + red[3]);
-    if (blk == r.b0) *r.step += 1.f;  // AdamW state_steps += 1 (torch increments before the update)
+    // AdamW state_steps += 1 (torch increments before the update); not while the update guard is raised
+    if (blk == r.b0 && (guard == nullptr || *guard == 0.0)) *r.step += 1.f;
   }
 }
 
@@ -97,7 +98,11 @@ __global__ __launch_bounds__(1024) void opt_norm_kernel(const double* partial, i
 }
 
 __global__ __launch_bounds__(OPT_NT) void opt_adamw_kernel(const long long* tab, int nt, const float* coefp, double lr,
-                                                           double b1, double b2, double eps, double wd, GradPtrs gp) {
+                                                           double b1, double b2, double eps, double wd, GradPtrs gp,
+                                                           const double* guard) {
+  // a raised update guard (eunet_set_update_guard: a loss of this step saw an out-of-range target)
+  // leaves parameters, gradients and moments as they are -- the reference raises before this update
+  if (guard != nullptr && *guard != 0.0) return;
   const int tid = threadIdx.x, blk = blockIdx.x;
   const OptRow r = opt_row(tab, nt, blk, gp);
   const long long e0 = (blk - r.b0) * (long long)OPT_EPB + tid;
@@ -166,10 +171,11 @@ int eunet_clip_adamw(const int64_t* table, int nt, int nblocks, float* const* gr
                   EUNET_OPT_KARG_MAX);
   }
   hipStream_t s = (hipStream_t)stream;
-  opt_sumsq_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, partial, gp);
+  const double* guard = eunet::update_guard();
+  opt_sumsq_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, partial, gp, guard);
   opt_norm_kernel<<<1, 1024, 0, s>>>(partial, nblocks, max_norm, coef, total_norm);
   opt_adamw_kernel<<<nblocks, OPT_NT, 0, s>>>((const long long*)table, nt, coef, lr, beta1, beta2, eps,
-                                              weight_decay, gp);
+                                              weight_decay, gp, guard);
   EUNET_LAUNCH_CHECK("clip_adamw");
   return EUNET_OK;
 }

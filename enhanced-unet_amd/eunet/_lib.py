@@ -51,6 +51,7 @@ _f = c_void_p  # float* / void* device pointers are passed as integers
 SIGNATURES = {
     "eunet_nchw_to_nhwc": [_f, _P, c_void_p],
     "eunet_stream_wait": [c_void_p, c_void_p],
+    "eunet_set_update_guard": [c_int, c_void_p],
     "eunet_conv3x3_packed_bytes": [c_int, c_int, c_int, POINTER(c_size_t)],
     "eunet_conv3x3_pack": [_f, c_int, c_int, c_int, _f, c_int, c_void_p],
     "eunet_conv3x3_pack_many": [c_void_p, c_int, c_int, c_void_p],

@@ -52,6 +52,7 @@ class BucketSink:
         self.launched = [False] * len(dp.buckets)
         self.works = []
         self.grads: Dict[str, torch.Tensor] = {}
+        self.last_issue = None  # DataParallel.timing: event at the last bucket's issue (on the issuing stream)
 
     def slot(self, name, shape):
         off, numel = self.dp.offsets[name]
@@ -64,6 +65,9 @@ class BucketSink:
         for i, (lo, hi, members) in enumerate(self.dp.buckets):
             if not self.launched[i] and all(m in self.done for m in members):
                 self.launched[i] = True
+                if self.dp.timing and all(self.launched):
+                    self.last_issue = torch.cuda.Event(enable_timing=True)
+                    self.last_issue.record()
                 self.works.append(dist.all_reduce(self.dp.flat[lo:hi], group=self.dp.group, async_op=True))
 
     def finish(self):
@@ -71,9 +75,17 @@ class BucketSink:
         for i, lo_hi in enumerate(self.dp.buckets):
             if not self.launched[i]:
                 raise RuntimeError(f"bucket {i} never completed: missing gradients")
+        e0 = None
+        if self.dp.timing:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()  # the launch stream is done with the backward's own kernels here
         for w in self.works:
             w.wait()
         self.dp.flat.mul_(1.0 / self.dp.world)
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.dp._timings.append((self.last_issue, e0, e1))
         return self.grads
 
 
@@ -109,7 +121,31 @@ class DataParallel:
                 dist.broadcast(params[n].data, src=0, group=group)
         self.flat_buffers, self._buffer_views = self._flatten_buffers(model)
         self._sync_buffers()
+        # timing (bench.py): per step, HIP events at the last bucket's issue and around the sink's final wait
+        self.timing = False
+        self._timings = []
         model.grad_sink_factory = lambda: BucketSink(self)
+
+    def start_timing(self):
+        self._timings = []
+        self.timing = True
+
+    def stop_timing(self):
+        """Per-step means over the steps since start_timing(): exposed_ms = the launch stream's time from the
+        end of its backward kernels to the gradients being reduced and scaled (waiting for the side stream's
+        last weight gradients, the outstanding bucket all-reduces and the 1/N scale: the communication the
+        backward did not hide); last_bucket_ms = the last bucket from its issue to that point (its
+        all-reduce and anything queued before it)."""
+        self.timing = False
+        torch.cuda.synchronize()
+        ts, self._timings = self._timings, []
+        if not ts:
+            return {"buckets": len(self.buckets), "steps": 0}
+        exposed = sum(e0.elapsed_time(e1) for _, e0, e1 in ts) / len(ts)
+        last = [li.elapsed_time(e1) for li, _, e1 in ts if li is not None]
+        return {"buckets": len(self.buckets), "bucket_mb": round(self.flat.numel() * 4 / 2 ** 20, 2), "steps": len(ts),
+                "exposed_comm_ms": round(exposed, 4),
+                "last_bucket_ms": round(sum(last) / len(last), 4) if last else None}
 
     @staticmethod
     def _flatten_buffers(model):

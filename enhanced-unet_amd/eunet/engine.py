@@ -24,8 +24,10 @@ from typing import Dict, Optional
 
 import torch
 
-from . import ops
+from . import kprof, ops
 from ._lib import EunetError
+
+ENCODER_SCOPE = "conv3x3.encoder_train"  # kprof family of every encoder conv3x3 launch (fwd, dgrad, wgrad)
 
 BLOCKS = ("enc1", "enc2", "enc3", "enc4", "dec4", "dec3", "dec2")
 BN_EPS = 1e-5
@@ -79,8 +81,11 @@ def side_stream(device) -> torch.cuda.Stream:
 
 
 def _per_block(flag, nm) -> bool:
-    """An engine knob that is a bool (every block) or a collection of block names."""
-    return bool(flag) if isinstance(flag, bool) else nm in flag
+    """An engine knob that is a collection of block names, or any other value taken as a bool (every
+    block or none: True / False / 0 / 1)."""
+    if isinstance(flag, (set, frozenset, list, tuple)):
+        return nm in flag
+    return bool(flag)
 
 
 class UNetEngine:
@@ -222,6 +227,10 @@ class UNetEngine:
         return dict(zip(names, ops.conv3x3_pack_many(items, self.dtype)))
 
     def _block_fwd(self, nm, X: ops.Act, training, P, B, small: bool, wps=None):
+        with kprof.scope(ENCODER_SCOPE if nm.startswith("enc") else None):
+            return self._block_fwd_impl(nm, X, training, P, B, small, wps)
+
+    def _block_fwd_impl(self, nm, X: ops.Act, training, P, B, small: bool, wps=None):
         p = f"{self.prefix}{nm}"
         N, H, W = X.n, X.h, X.w
         C = P[p + ".0.weight"].shape[0]
@@ -266,7 +275,11 @@ class UNetEngine:
                      training, BN_EPS, BN_MOMENTUM, B["enhance.1.running_mean"], B["enhance.1.running_var"],
                      hmean, hinv, out2h, logits, hws, dtype=self.dtype)
         if training:
-            B["enhance.1.num_batches_tracked"].add_(1)
+            guard = ops.update_guard(dev)  # eunet_bn_finalize counts the other BNs' batches under it
+            if guard is None:
+                B["enhance.1.num_batches_tracked"].add_(1)
+            else:
+                B["enhance.1.num_batches_tracked"].add_(guard.eq(0).long().reshape(()))
         S.update(hmean=hmean, hinv=hinv, want=want)
         return (logits if want == "logits" else out2h), S
 
@@ -328,8 +341,12 @@ class UNetEngine:
         return S
 
     # --------------------------------------------------------------- backward
-    def _block_bwd(self, nm, G: "torch.Tensor | Grad1x1 | GradPool", S, P, sink: GradSink, need_gx: bool, small: bool,
-                   gred=(None, 0)):
+    def _block_bwd(self, nm, G, S, P, sink, need_gx: bool, small: bool, gred=(None, 0)):
+        with kprof.scope(ENCODER_SCOPE if nm.startswith("enc") else None):
+            return self._block_bwd_impl(nm, G, S, P, sink, need_gx, small, gred)
+
+    def _block_bwd_impl(self, nm, G: "torch.Tensor | Grad1x1 | GradPool", S, P, sink: GradSink, need_gx: bool,
+                        small: bool, gred=(None, 0)):
         """gred: (part, rows) of the block's BN-b backward reduction when G's producer fused it."""
         p = f"{self.prefix}{nm}"
         s = S[nm]

@@ -102,6 +102,30 @@ class BusyTimer:
 
 
 _OFF = os.environ.get("EUNET_KPROF", "1") == "0"  # diagnostic: measure the event overhead itself
+_scope = None  # while set: every timed conv3x3 launch is credited to this family too (scope())
+
+
+class scope:
+    """Credit every conv3x3 launch timed inside the block to `family` as well (None: no-op).  The engine
+    wraps the encoder blocks' forward and backward in it, so bench.py can report the north-star's "3x3
+    encoder convs" over forward, data and weight gradients (the weight gradients issued on the side stream
+    from inside the block included)."""
+    __slots__ = ("family", "prev")
+
+    def __init__(self, family):
+        self.family = family
+
+    def __enter__(self):
+        global _scope
+        self.prev = _scope
+        if self.family is not None:
+            _scope = self.family
+        return self
+
+    def __exit__(self, *exc):
+        global _scope
+        _scope = self.prev
+        return False
 
 
 def timed(family: str, flops: float, nbytes: float = 0.0, sub: str | None = None):
@@ -110,7 +134,7 @@ def timed(family: str, flops: float, nbytes: float = 0.0, sub: str | None = None
     t = _active
     if t is None or _OFF:
         return _Null
-    return _Rec(t, family, flops, nbytes, sub)
+    return _Rec(t, family, flops, nbytes, sub, _scope if family.startswith("conv3x3") else None)
 
 
 class _NullCtx:
@@ -125,10 +149,10 @@ _Null = _NullCtx()
 
 
 class _Rec:
-    __slots__ = ("t", "fam", "flops", "nbytes", "e0", "sub")
+    __slots__ = ("t", "fam", "flops", "nbytes", "e0", "sub", "scope")
 
-    def __init__(self, t, fam, flops, nbytes, sub=None):
-        self.t, self.fam, self.flops, self.nbytes, self.sub = t, fam, flops, nbytes, sub
+    def __init__(self, t, fam, flops, nbytes, sub=None, scope=None):
+        self.t, self.fam, self.flops, self.nbytes, self.sub, self.scope = t, fam, flops, nbytes, sub, scope
 
     def __enter__(self):
         self.e0 = torch.cuda.Event(enable_timing=True)
@@ -141,4 +165,6 @@ class _Rec:
         self.t.records.setdefault(self.fam, []).append((self.e0, e1, self.flops, self.nbytes))
         if self.sub is not None:
             self.t.records.setdefault(self.sub, []).append((self.e0, e1, self.flops, self.nbytes))
+        if self.scope is not None:
+            self.t.records.setdefault(self.scope, []).append((self.e0, e1, self.flops, self.nbytes))
         return False

@@ -107,6 +107,31 @@ def stream_wait(frm: torch.cuda.Stream, to: torch.cuda.Stream):
     call("eunet_stream_wait", ctypes.c_void_p(frm.cuda_stream), ctypes.c_void_p(to.cuda_stream))
 
 
+_guards = {}  # device index -> the fp64 [1] tensor eunet_set_update_guard points at (kept alive here)
+
+
+def set_update_guard(device, guard):
+    """eunet_set_update_guard: while guard (a device fp64 [1] tensor, or None) is nonzero, BN running
+    statistics and the native clip + AdamW leave the persistent state untouched."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if guard is not None and (guard.dtype != torch.float64 or guard.device.type != "cuda" or guard.device.index != idx):
+        raise ValueError("update guard: an fp64 tensor on the guarded device")
+    if _guards.get(idx) is guard:
+        return
+    call("eunet_set_update_guard", idx, None if guard is None else ctypes.c_void_p(guard.data_ptr()))
+    if guard is None:
+        _guards.pop(idx, None)
+    else:
+        _guards[idx] = guard
+
+
+def update_guard(device):
+    """The tensor eunet_set_update_guard currently points at for device (None: no guard)."""
+    dev = torch.device(device)
+    return _guards.get(dev.index if dev.index is not None else torch.cuda.current_device())
+
+
 def _ptr(t):
     if t is None:
         return None

@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import losses as L
+from . import ops
 from .losses import CrossEntropyLoss, FocalLoss, check_targets, combined_loss, consistency_loss  # noqa: F401
 from .models import EnhancedUNet
 
@@ -145,7 +146,16 @@ class Trainer:
         """One optimisation step on device-resident images [B,C,H,W] / masks [B,H,W].
 
         With self.step_graph set, a deferred-loss step (sync_loss=False, no DataParallel) replays a
-        captured HIP graph of this same step (StepGraph): same kernels, same bits, one launch."""
+        captured HIP graph of this same step (StepGraph): same kernels, same bits, one launch.
+
+        A target outside [0, K) leaves the model as the reference leaves it when its loss raises
+        (train_eval.py:325 -> FocalLoss:39, before backward and optimizer.step()): with sync_loss the
+        step raises before its update; deferred, the update guard (ops.set_update_guard, pointed at the
+        loss's device-side count of such targets) keeps this step and every later one from touching
+        the parameters, the optimizer state and the BN running statistics until check_targets()
+        raises at the next host synchronisation."""
+        if images.is_cuda:
+            ops.set_update_guard(images.device, L.bad_target_accumulator(images.device))
         if self.step_graph and not sync_loss and self.dp is None and images.is_cuda:
             out = self._graphed_step(images, masks)
         else:
@@ -248,22 +258,29 @@ class Trainer:
         return loss
 
     def train_epoch(self, dataloader):
-        """Mean loss over the epoch with one host sync at its end.  Out-of-range targets are counted
-        on the device and raise ValueError at that sync -- after the epoch's updates, including the
-        offending batches' (with their bad pixels dropped from the loss).  Trainer.step(...,
-        sync_loss=True) raises before the update instead."""
+        """Mean loss over the epoch (train_eval.py:236-353).  A target outside [0, K) raises ValueError
+        with the model in the state the reference's raise at that batch leaves it (train_eval.py:325 ->
+        FocalLoss:39, before that batch's backward and optimizer.step()): the earlier batches' updates
+        applied, that batch's and later ones' not (parameters, AdamW state, BN running statistics --
+        that batch's forward did update them, as there).  On the native optimizer path the steps are
+        deferred (one host sync per epoch): the update guard (Trainer.step) holds the state from the
+        offending loss on, the remaining batches run without effect and the error is raised at the
+        epoch's sync.  With torch's optimizer every step synchronises and raises before its update."""
         self.model.train()
+        deferred = str(self.device).startswith("cuda") and self._native_opt()
         total = None  # device-side running sum: one host sync per epoch, not per step
         n = 0
         for batch in dataloader:
             images = batch["images"].to(self.device, non_blocking=True)
             masks = self._masks(batch, self.device, 0, 0)
-            loss = self.step(images, masks, sync_loss=False).double()
+            if deferred:
+                loss = self.step(images, masks, sync_loss=False).double()
+            else:
+                loss = self.step(images, masks, sync_loss=True)
             total = loss if total is None else total + loss
             n += 1
-        value = float(total.item()) / n if n else 0.0
         check_targets()
-        return value
+        return float(total) / n if n else 0.0
 
     def epoch_lr_step(self, epoch: int) -> float:
         """train_model's per-epoch stepping (train_eval.py:1104-1111).  The reference steps the
@@ -279,7 +296,15 @@ class Trainer:
 
 
 ENGINE_KNOBS = ("overlap_wgrad", "materialize_za", "fuse_bn_reduce", "wg3_late", "fuse_bn_apply", "fuse_bn_apply_a",
-                "dgrad_first", "wg3_early_last", "fork_once")
+                "dgrad_first", "wg3_early_last", "fork_once", "dec1_recompute", "pool_recompute", "device_fence_forks",
+                "narrow_mfma")
+
+
+def _engine_knobs(eng):
+    """Every schedule knob a captured step depends on: the engine's, and for the dual-branch engine its
+    two trunk engines' too (their knobs are UNetEngine class attributes unless set per instance)."""
+    engines = [eng] + [getattr(eng, n) for n in ("ea", "eb") if hasattr(eng, n)]
+    return tuple(tuple(_hashable(getattr(e, k, None)) for k in ENGINE_KNOBS) for e in engines)
 
 
 def _hashable(v):
@@ -352,8 +377,7 @@ class StepGraph:
             raise RuntimeError("Trainer.step_graph: fixed dropout keep masks (a test hook) are host inputs")
         # the compute dtype is baked into the captured kernels and buffers: EnhancedUNet.set_dtype
         # (which only changes the engine's dtype) must re-capture
-        knobs = tuple(_hashable(getattr(eng, k, None)) for k in ENGINE_KNOBS) + (
-            str(getattr(eng, "dtype", None)), str(getattr(trainer.model, "compute_dtype", None)))
+        knobs = _engine_knobs(eng) + (str(getattr(eng, "dtype", None)), str(getattr(trainer.model, "compute_dtype", None)))
         ps = [p for g in trainer.optimizer.param_groups for p in g["params"]]
         store = (id(trainer.optimizer), ps[0].data_ptr(), ps[-1].data_ptr(), len(ps))
         lossp = (bytes(trainer.loss_params()), tuple(trainer.aux_branch_weights.items()), trainer.consistency_weight,

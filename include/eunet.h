@@ -52,8 +52,20 @@ int eunet_nchw_to_nhwc(const float* x, const eunet_act* out, void* stream);
 
 /* ---- stream ordering (the backward's weight-gradient side stream; no reference counterpart: the
  * reference's backward is one stream, train_eval.py:230-243) -------------------------------------
- * `to` waits for everything enqueued on `from` so far (device-scope event release, no timing). */
+ * `to` waits for everything enqueued on `from` so far (device-scope event release, no timing).  Both
+ * streams must be on one device (any current device of the calling thread). */
 int eunet_stream_wait(void* from, void* to);
+
+/* ---- update guard (train_eval.py:325 -> FocalLoss:39: an out-of-range target raises inside the
+ * loss of that batch, before its backward and optimizer.step(), so neither that batch nor any later
+ * one updates the model) ----------------------------------------------------------------------------
+ * guard: a device fp64 word on `device` (null: no guard).  While *guard != 0 at kernel time,
+ * eunet_bn_finalize leaves the running statistics and num_batches_tracked untouched and
+ * eunet_clip_adamw leaves parameters, gradients, moments and step counters untouched.  The Trainer
+ * points it at the loss's out-of-range target counter, so a deferred (sync-free) epoch keeps the
+ * reference's state at the raise and raises at its next host synchronisation.  The pointer is read
+ * at launch (a captured graph keeps the one it was captured with). */
+int eunet_set_update_guard(int device, const double* guard);
 
 /* ---- Conv2d 3x3, padding 1 (models.py:219,222 / autograd) -----------------
  * Weights are re-packed every step from the fp32 torch parameter

@@ -12,7 +12,8 @@ What is restated (all citations into /root/reference):
   * Trainer.dice_loss       train_eval.py:134-157 (class weights [1,15,8], eps 1e-6)
   * Trainer.tversky_loss    train_eval.py:159-181 (class weights [1,12,6], alpha 0.7)
   * _compute_combined_loss  train_eval.py:183-197 (2.5*focal + 2.5*dice + 1.0*tversky, :82-85)
-  * Trainer.train_epoch     train_eval.py:236-353 (per-sample bilinear resize :306-310, /B,
+  * Trainer.train_epoch     train_eval.py:236-353 (reflect / zero pad to /32 :248-253, 276-296,
+                                                  per-sample bilinear resize :306-310, /B,
                                                   clip_grad_norm_(1.0) :341, AdamW :120,343)
   * LR schedule             train_eval.py:122-132 + stepping train_eval.py:1103-1111
 
@@ -256,6 +257,17 @@ def tversky_loss(pred, target, num_classes=3, alpha=0.7):
     return sum(out) / len(out)
 
 
+def pad32(images: torch.Tensor, masks: torch.Tensor):
+    """train_eval.py:248-253 + 276-296: images reflect-padded and masks zero-padded at the bottom /
+    right to the next multiple of 32 before the forward and the loss."""
+    h, w = images.shape[-2:]
+    h_pad, w_pad = (32 - h % 32) % 32, (32 - w % 32) % 32
+    if h_pad or w_pad:
+        images = F.pad(images, (0, w_pad, 0, h_pad), mode="reflect")
+        masks = F.pad(masks[:, None], (0, w_pad, 0, h_pad), mode="constant", value=0)[:, 0]
+    return images, masks
+
+
 def batch_loss(out2h: torch.Tensor, target: torch.Tensor):
     """train_eval.py:262-337: per-sample resize 2H->H (bilinear) + combined loss, /B."""
     B = out2h.shape[0]
@@ -298,6 +310,7 @@ class OracleTrainer:
 
     def step(self, images: torch.Tensor, masks: torch.Tensor, clip: bool = True):
         self.optimizer.zero_grad()
+        images, masks = pad32(images, masks)
         out = forward(self.S, images, training=True)
         loss = batch_loss(out, masks)
         loss.backward()
@@ -335,6 +348,6 @@ def avgpool_equals_resize(out2h: torch.Tensor) -> float:
     return float((a - b).abs().max())
 
 
-__all__ = ["state_spec", "formula_weights", "forward", "combined_loss", "batch_loss", "focal_loss", "dice_loss",
+__all__ = ["state_spec", "formula_weights", "forward", "combined_loss", "batch_loss", "pad32", "focal_loss", "dice_loss",
            "tversky_loss",
            "OracleTrainer", "lr_trajectory", "block_table", "flops_per_pixel", "math"]

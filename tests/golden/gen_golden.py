@@ -16,6 +16,8 @@ Fixtures (all with formula weights, oracle/weights.py):
   loss_k3.npz      Trainer._compute_combined_loss (+parts) and d loss / d logits, K=3
   loss_k2.npz      K=2 via a -inf third logit fed to the reference loss
   step_c3k3.npz    one Trainer.train_epoch (warmup-stepped LR, clip, AdamW) on a B=2 batch
+  step_pad_c3k3.npz  the same on a 40x56 batch: train_epoch's reflect pad of the images and zero
+                   pad of the masks to /32 (train_eval.py:248-253, 276-296) exercised
   lr_traj.npz      train_model's per-epoch LR for E in {6, 50}
   metrics.npz      metrics.calculate_semantic_metrics / calculate_iou / calculate_dice on
                    mask pairs incl. empty classes and out-of-range labels
@@ -204,10 +206,10 @@ def gen_loss_api(ref_te):
     np.savez_compressed(os.path.join(HERE, "loss_api.npz"), **out)
 
 
-def gen_step(ref_models, ref_te):
+def gen_step(ref_models, ref_te, H=32, W=32, fname="step_c3k3.npz", seed=41):
     model = ref_models.get_model("enhanced_unet", num_classes=3, device="cpu")
     _load_formula(model, 64, 3, 3)
-    x, m = _inputs(2, 3, 32, 32, 3, seed=41)
+    x, m = _inputs(2, 3, H, W, 3, seed=seed)
     batch = {"images": x, "batch_items": [{"semantic_mask": m[i]} for i in range(2)]}
     tr = ref_te.Trainer(model, "cpu", "enhanced_unet", total_epochs=50)
     tr.warmup_scheduler.step()  # train_model epoch 0 (train_eval.py:1104-1105)
@@ -215,7 +217,7 @@ def gen_step(ref_models, ref_te):
     loss = tr.train_epoch([batch])
     sd = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
     grads = {k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()}
-    np.savez_compressed(os.path.join(HERE, "step_c3k3.npz"), x=x.numpy(), m=m.numpy(), lr=lr,
+    np.savez_compressed(os.path.join(HERE, fname), x=x.numpy(), m=m.numpy(), lr=lr,
                         loss=loss, **_summaries("post", sd), **_summaries("grad", grads))
 
 
@@ -421,6 +423,7 @@ def main(only=()):
         "loss_k2": lambda: gen_loss(ref_te, 2, "loss_k2.npz"),
         "loss_api": lambda: gen_loss_api(ref_te),
         "step_c3k3": lambda: gen_step(ref_models, ref_te),
+        "step_pad_c3k3": lambda: gen_step(ref_models, ref_te, 40, 56, "step_pad_c3k3.npz", seed=43),
         "lr_traj": lambda: gen_lr(ref_te),
         "metrics": gen_metrics,
         "probs_mask": lambda: gen_probs_mask(ref_te),

@@ -3,6 +3,7 @@ driver's command shape), each timing the per-rank workload with max-over-ranks t
 one JSON line that reports the real process-group size (BASELINE configs[3]: train_eval.py:337-343 per
 rank).  gloo carries the collectives so that two ranks can share the one GPU of the box."""
 import json
+import math
 import os
 import subprocess
 import sys
@@ -31,6 +32,14 @@ def test_bench_gpus2_runs_two_ranks():
     assert d["steps"] == 2 and d["value"] > 0
     # value = images of all ranks / the max-over-ranks time
     assert abs(d["value"] - 2 * 1 * 2 / (d["ms_per_step"] * 2e-3)) / d["value"] < 1e-2
+    # per rank: its own step time, the communication its backward left exposed, the bucket count
+    pr = d["world"]["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1], pr
+    for r in pr:
+        assert r["steps"] == 2 and r["buckets"] >= 1, r
+        for k in ("ms_per_step", "exposed_comm_ms", "last_bucket_ms"):
+            assert isinstance(r[k], float) and math.isfinite(r[k]) and r[k] >= 0.0, (k, r)
+    assert max(r["ms_per_step"] for r in pr) <= d["ms_per_step"] * 1.01
 
 
 def test_bench_rejects_world_size_mismatch():

@@ -3,6 +3,9 @@
 configs[1]: base 64, 1 x 512^2 -> 2 classes, batch 8, fp32 (models.py:217-238, train_eval.py:236-353):
   logits per pixel and the loss vs the fp64 oracle, every parameter gradient vs the fp32 CPU oracle --
   both evaluated on the branch configuration the GPU took (tests/_pins.py).
+configs[2]: base 64, 1 x 1024^2 -> 2 classes, batch 4, bf16 -- the bench workload: the configs[4] properties
+  below at this size (determinism, exact schedules, BN statistics of three layers vs the recomputed conv,
+  loss decrease, a 256^2 slice vs the fp64 oracle).
 configs[4]: dual-branch base 96 + deep supervision, 2048^2, batch 2, bf16 (models.py:253-333,
   train_eval.py:199-234): an fp64 oracle at this size is out of reach of the host, so full-size
   properties -- finite loss; two runs bit-identical; the side-stream and the serial weight-gradient
@@ -244,6 +247,145 @@ def test_configs4_256_slice_vs_oracle(cfg4_batch):
     agree = float((out.argmax(1) == ref.argmax(1)).double().mean())
     agree_ac = float((ac.argmax(1) == ref.argmax(1)).double().mean())
     print("configs[4] 256^2 slice bf16 relL2 ours", ours, "autocast", auto, "argmax agreement", agree, agree_ac)
+    assert torch.isfinite(out).all()
+    assert ours < max(2.0 * auto, 0.02), (ours, auto)
+    assert agree > min(0.97, agree_ac - 0.02), (agree, agree_ac)
+
+
+# ---- configs[2]: base 64, 1 x 1024^2 -> 2 classes, batch 4, bf16 (the bench workload) ----------------------
+# The headline config at its own size (models.py:217-238, train_eval.py:236-353).  An fp64 oracle of the full
+# step is out of reach of the host here too, so the configs[4] suite's full-size properties are applied to it:
+# determinism and the exact schedules, BN statistics against the conv recomputed from the kernels' own bf16
+# operands at three layers (64 -> 64 at 1024^2, 512 -> 512 at 128^2, the 192 -> 64 concat input of dec2.0),
+# the loss decreasing over three Trainer steps, and a 256^2 slice of the same model against the fp64 oracle.
+B2, H2 = 4, 1024
+
+
+def _base64(dtype="bf16"):
+    from eunet.models import EnhancedUNet
+    m = EnhancedUNet(num_classes=2, in_channels=1, base_ch=64, dtype=dtype)
+    m.load_state_dict({k: (v.float() if v.is_floating_point() else v) for k, v in R.formula_weights(64, 1, 2).items()})
+    return m.to(DEV).train()
+
+
+@pytest.fixture(scope="module")
+def cfg2_batch():
+    from eunet import synth
+    x, msk = synth.batch(B2, H2, H2, start_index=71, num_classes=2, in_channels=1)
+    return x.to(DEV), msk.to(DEV)
+
+
+def _grads2(m, x, msk):
+    from eunet.losses import combined_loss
+    loss = combined_loss(m.forward_lowres(x), msk)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+
+def test_configs2_deterministic_and_schedules_exact(cfg2_batch, monkeypatch):
+    """configs[2] workload: finite loss and gradients; a second run from the same weights is bit-identical,
+    and so is the serial schedule (weight gradients on the launch stream: UNetEngine.overlap_wgrad = False)."""
+    from eunet import engine
+    x, msk = cfg2_batch
+    l1, g1 = _grads2(_base64(), x, msk)
+    assert torch.isfinite(l1).all()
+    assert all(torch.isfinite(g).all() for g in g1.values())
+    l2, g2 = _grads2(_base64(), x, msk)
+    assert torch.equal(l1, l2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), ("rerun", k)
+    del g2
+    monkeypatch.setattr(engine.UNetEngine, "overlap_wgrad", False)
+    l3, g3 = _grads2(_base64(), x, msk)
+    assert torch.equal(l1, l3)
+    for k in g1:
+        assert torch.equal(g1[k], g3[k]), ("serial schedule", k)
+
+
+def test_configs2_bn_running_stats_match_recomputed_conv(cfg2_batch):
+    """One training forward at the configs[2] size from fresh running statistics: the batch mean / 1/std and
+    the running statistics of model.enc1.4 (enc1.3: 64 -> 64 at 1024^2), model.enc4.4 (enc4.3: 512 -> 512 at
+    128^2) and model.dec2.1 (dec2.0 over the 192-channel concat buffer [skip | upsampled], 1024^2) against the
+    statistics of the pre-BN conv output recomputed from the kernels' own operands: the bf16 operand as staged
+    (bf16(relu(fmaf(ya, scale, shift))) for a .3 conv, the stored concat buffer for dec2.0) and the bf16
+    weights, conv in fp32 (TF32 off) -- the kernels take the statistics from their fp32 accumulators."""
+    import _pins
+    import torch.nn.functional as F
+    x, _ = cfg2_batch
+    m = _pins.keep(_base64())
+    with torch.enable_grad():
+        m.forward_lowres(x)
+    S = m._engine.last_state
+    sd = m.state_dict()
+    P = dict(m.named_parameters())
+    tf32 = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = False
+    try:
+        for key, blk, conv in (("model.enc1.4", "enc1", "model.enc1.3"), ("model.enc4.4", "enc4", "model.enc4.3"),
+                               ("model.dec2.1", "dec2", "model.dec2.0")):
+            s = S[blk]
+            if conv.endswith(".3"):
+                ya, bna = s["ya"], s["bna"]
+                inp = torch.relu(torch.addcmul(bna["shift"], ya.float(), bna["scale"]))  # fmaf, as the kernels
+                inp = inp.bfloat16().float().permute(0, 3, 1, 2)
+                bn = s["bnb"]
+            else:
+                X = s["X"]
+                inp = X._keep[..., X.coff:X.coff + X.c].float().permute(0, 3, 1, 2)
+                bn = s["bna"]
+            y = F.conv2d(inp, P[conv + ".weight"].bfloat16().float(), P[conv + ".bias"].float(), padding=1)
+            del inp
+            yd = y.transpose(0, 1).reshape(y.shape[1], -1).double()
+            del y
+            n = yd.shape[1]
+            mean, var = yd.mean(1), yd.var(1, unbiased=True)
+            del yd
+            std = var.sqrt()
+            vb = var * (n - 1) / n
+            em = float(((bn["mean"].double() - mean).abs() / std).max())
+            ei = float(((bn["invstd"].double() - 1.0 / torch.sqrt(vb + 1e-5)).abs() * torch.sqrt(vb + 1e-5)).max())
+            rm, rv = sd[key + ".running_mean"].double(), sd[key + ".running_var"].double()
+            ref_rv = 0.9 + 0.1 * var
+            erm = float(((rm - 0.1 * mean).abs() / (0.1 * std)).max())
+            erv = float(((rv - ref_rv).abs() / (1e-4 * 0.1 * var + 2.0 ** -23 * ref_rv)).max())
+            print(f"configs[2] {key} ({n} px): batch mean err / std {em:.2e}, 1/std rel err {ei:.2e}; running mean "
+                  f"err / std {erm:.2e}, running var err / (1e-4 x 0.1 var + fp32 ulp) {erv:.2f}")
+            assert em < 1e-4 and ei < 1e-4 and erm < 1e-4 and erv < 1.0, (key, em, ei, erm, erv)
+    finally:
+        torch.backends.cudnn.allow_tf32 = tf32
+        m._engine.last_state = None
+
+
+def test_configs2_loss_decreases_over_three_steps(cfg2_batch):
+    """Three Trainer.steps (clip, native AdamW at lr 1e-3) on the configs[2] batch: the loss decreases."""
+    from eunet.train_eval import Trainer
+    x, msk = cfg2_batch
+    tr = Trainer(_base64(), DEV, "enhanced_unet")
+    for g in tr.optimizer.param_groups:
+        g["lr"] = 1e-3
+    losses = [tr.step(x, msk) for _ in range(4)]
+    print("configs[2] losses:", losses)
+    assert all(b < a for a, b in zip(losses, losses[1:])), losses
+
+
+def test_configs2_256_slice_vs_oracle(cfg2_batch):
+    """A 256^2 crop of the configs[2] batch through the same bf16 base-64 model (train mode) vs the fp64
+    oracle, gated by what CPU bf16 autocast of the oracle achieves on the same crop, plus argmax agreement."""
+    x, _ = cfg2_batch
+    xs = x[:, :, 512:768, 256:512].contiguous()
+    m = _base64()
+    with torch.no_grad():
+        out = m(xs).double().cpu()
+    xc = xs.cpu()
+    with torch.no_grad():
+        ref = R.forward(R.formula_weights(64, 1, 2), xc.double(), training=True)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ac = R.forward(R.formula_weights(64, 1, 2, dtype=torch.float32), xc, training=True).float()
+    ours, auto = _rel_l2(out, ref), _rel_l2(ac, ref)
+    agree = float((out.argmax(1) == ref.argmax(1)).double().mean())
+    agree_ac = float((ac.argmax(1) == ref.argmax(1)).double().mean())
+    print("configs[2] 256^2 slice bf16 relL2 ours", ours, "autocast", auto, "argmax agreement", agree, agree_ac)
     assert torch.isfinite(out).all()
     assert ours < max(2.0 * auto, 0.02), (ours, auto)
     assert agree > min(0.97, agree_ac - 0.02), (agree, agree_ac)

@@ -106,3 +106,52 @@ def test_out_of_range_target_is_reported():
     with pytest.raises(ValueError):
         tr.train_epoch([{"images": x.cpu(), "batch_items": [{"semantic_mask": bad[i].cpu()} for i in range(2)]}])
     check_targets()  # nothing pending
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_train_epoch_bad_target_leaves_reference_state(graph):
+    """train_eval.py:325 -> FocalLoss:39: the reference raises inside the offending batch's loss, after
+    its forward (BN running statistics updated) and before its backward / optimizer.step(); later
+    batches never run.  A deferred train_epoch (the update guard holds the state from that loss on, the
+    error is raised at the epoch's sync) must leave parameters, BN buffers and the AdamW state exactly
+    as a trainer that ran the earlier batches and then that batch's forward."""
+    from eunet import synth
+    from eunet.models import EnhancedUNet
+    from eunet.train_eval import Trainer
+    xs, ms = [], []
+    for i in range(4):
+        x, m = synth.batch(2, 64, 64, start_index=10 + 2 * i, num_classes=2, in_channels=1, device=DEV)
+        xs.append(x)
+        ms.append(m)
+    ms[2] = ms[2].clone()
+    ms[2][1, 7, 9] = 5
+    batches = [{"images": x, "batch_items": [{"semantic_mask": mm} for mm in m]} for x, m in zip(xs, ms)]
+
+    def trainer():
+        torch.manual_seed(3)
+        return Trainer(EnhancedUNet(num_classes=2, in_channels=1, base_ch=16).to(DEV), DEV, "enhanced_unet",
+                       total_epochs=12)
+
+    ta, tb = trainer(), trainer()
+    ta.step_graph = graph
+    ta.graph_warmup = 1
+    ta.epoch_lr_step(0)
+    tb.epoch_lr_step(0)
+    with pytest.raises(ValueError, match="1 target"):
+        ta.train_epoch(batches)
+    tb.step(xs[0], ms[0])
+    tb.step(xs[1], ms[1])
+    with pytest.raises(ValueError, match="1 target"):
+        tb.step(xs[2], ms[2])  # forward (BN running stats) then the raise, before backward / update
+    sa, sb = ta.model.state_dict(), tb.model.state_dict()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    for pa, pb in zip(ta.model.parameters(), tb.model.parameters()):
+        for key in ("exp_avg", "exp_avg_sq", "step"):
+            assert torch.equal(ta.optimizer.state[pa][key], tb.optimizer.state[pb][key]), key
+    # the guard drops with the raise: the next epoch trains again (both trainers step alike)
+    ta.train_epoch(batches[:2])
+    tb.step(xs[0], ms[0])
+    tb.step(xs[1], ms[1])
+    for (k, pa), pb in zip(ta.model.named_parameters(), tb.model.parameters()):
+        assert torch.equal(pa, pb), k

@@ -179,10 +179,13 @@ def test_train_grads_match_oracle(base, cin, K, H):
             assert _rel(v, S[k]) < 1e-3, k
 
 
-def test_trainer_step_matches_reference_fixture(golden_dir):
-    """Trainer.step on the fixture batch: loss and the post-AdamW parameters."""
+@pytest.mark.parametrize("fname", ["step_c3k3.npz", "step_pad_c3k3.npz"])
+def test_trainer_step_matches_reference_fixture(golden_dir, fname):
+    """Trainer.step on the fixture batch: loss and the post-AdamW parameters.  step_pad_c3k3 is a
+    40x56 batch: the Trainer's reflect pad of the images and zero pad of the masks to 64x64
+    (train_eval.py:248-253, 276-296) is part of what the reference's step pins."""
     from eunet.train_eval import Trainer
-    g = _load(golden_dir, "step_c3k3.npz")
+    g = _load(golden_dir, fname)
     m = _model(64, 3, 3)
     tr = Trainer(m, DEV, "enhanced_unet", total_epochs=50)
     lr = tr.epoch_lr_step(0)

@@ -1,7 +1,15 @@
 """Per-kernel numerics through the C-ABI vs plain PyTorch fp64 references (GPU only).
 
-fp32 kernels (exact-fp32 MFMA / VALU) are held to 1e-4 relative; bf16
-kernels (bf16 operands, fp32 accumulation) to 2e-2 relative of the output scale.
+fp32 kernels (exact-fp32 MFMA / VALU) are held to 1e-4 relative.  The bf16 conv3x3 / conv_small
+kernels (bf16 operands, fp32 accumulation, one rounding of a bf16 output) are held to an
+operand-exact bound (gate()): the fp64 reference is evaluated on the kernel's own bf16 operands --
+the inputs and weights as rounded, and the BN+ReLU operand transform as the kernels form it
+(relu(fmaf(x, scale, shift)) of the fp32 constants, then rounded to bf16: tf()) -- so what remains is
+the fp32 accumulation and the output rounding, and every element must satisfy
+    |got - ref| <= 2^-8 |ref| + 1e-5 max|ref|
+(2^-8 = twice the round-to-nearest bound of a bf16 output).  A dropped K-chunk, a mis-indexed co-block
+or a shifted tap moves elements by O(|ref|) and fails it.  The other bf16 kernels (BN+ReLU / pool /
+upsample / 1x1 producers, whose references are not operand-exact) keep 2e-2 of the output scale.
 """
 import pytest
 import torch
@@ -24,6 +32,25 @@ def rel(a, b):
 
 
 TOL = {torch.float32: 1e-4, torch.bfloat16: 2e-2}
+
+
+def gate(got, ref, dt):
+    """Worst element's error over its bound (passes at <= 1).  fp32: max|got - ref| <= 1e-4 max|ref|;
+    bf16 (operand-exact reference, module docstring): |got - ref| <= 2^-8 |ref| + 1e-5 max|ref| per element."""
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    mx = float(ref.abs().max().clamp_min(1e-30))
+    if dt == torch.float32:
+        return float((got - ref).abs().max()) / (1e-4 * mx)
+    return float(((got - ref).abs() / (2.0 ** -8 * ref.abs() + 1e-5 * mx)).max())
+
+
+def tf(x, sc, sh, dt):
+    """The conv kernels' BN+ReLU operand transform: relu(fmaf(x, sc, sh)) with the fp32 constants (the
+    fp64 product and sum of these operands are exact, then rounded once to fp32 as the fused multiply-add
+    rounds), rounded to the staged operand's dtype."""
+    v = (x * sc.float().double() + sh.float().double()).float().double().clamp_min(0.0)
+    return v.to(torch.bfloat16).double() if dt == torch.bfloat16 else v
 
 
 def nhwc(t):
@@ -49,11 +76,9 @@ def test_conv3x3_fwd_stats(dt, transform):
     xq = xd.double().cpu()[..., CO:CO + Cin]  # rounded input the kernel sees
     xt = nchw(xq)
     if transform:
-        xt = torch.relu(xt * sc[None, :, None, None] + sh[None, :, None, None])
-        if dt == torch.bfloat16:
-            xt = xt.to(torch.bfloat16).double()
+        xt = tf(xt, sc[None, :, None, None], sh[None, :, None, None], dt)
     wq = w.to(dt).double()
-    ref = nhwc(F.conv2d(xt, wq, b, padding=1))
+    ref = nhwc(F.conv2d(xt, wq, b.float().double(), padding=1))
     y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
     tiles = ops.conv3x3_tiles(ops.act(y))
@@ -62,7 +87,7 @@ def test_conv3x3_fwd_stats(dt, transform):
                     scale=sc.float().to(DEV) if transform else None,
                     shift=sh.float().to(DEV) if transform else None, stats=st)
     torch.cuda.synchronize()
-    assert rel(y, ref) < TOL[dt]
+    assert gate(y, ref, dt) <= 1.0, gate(y, ref, dt)
     # BN statistics via finalize
     gamma = torch.ones(Cout, device=DEV)
     beta = torch.zeros(Cout, device=DEV)
@@ -140,7 +165,7 @@ def test_conv3x3_fwd_large_sample_slice():
                     patch[dy, dx] = x[0, sy, sx].double().cpu()
         ref = torch.einsum("oiyx,yxi->o", w, patch) + b
         got = y[0, yy, xx].double().cpu()
-        assert rel(got, ref) < 2e-2, (yy, xx, rel(got, ref))
+        assert gate(got, ref, torch.bfloat16) <= 1.0, (yy, xx, gate(got, ref, torch.bfloat16))
     assert (1900 * W + 1500) * Cin * 2 > 2 ** 31  # the checked halos sit beyond 2 GiB
     del x, y
 
@@ -157,7 +182,7 @@ def test_conv3x3_dgrad_wgrad(dt):
     sh = torch.randn(Cin, generator=g, dtype=torch.float64) * 0.3
     xt = nchw(x).requires_grad_(True)
     xa = torch.relu(xt * sc[None, :, None, None] + sh[None, :, None, None])
-    xa_q = xa.to(dt).double() if dt == torch.bfloat16 else xa
+    xa_q = tf(xt.detach(), sc[None, :, None, None], sh[None, :, None, None], dt) if dt == torch.bfloat16 else xa
     wt = w.clone().requires_grad_(True)
     y = F.conv2d(xa_q.detach() if dt == torch.bfloat16 else xa, wt, None, padding=1)
     y.backward(nchw(gy))
@@ -180,9 +205,9 @@ def test_conv3x3_dgrad_wgrad(dt):
     ops.wgrad_reduce(dwp, dbp, ns, Cout, Cin, 9, dw, db)
     torch.cuda.synchronize()
     assert torch.equal(gxd, gxd2)
-    assert rel(gxd, gx_ref) < TOL[dt]
-    assert rel(dw, wt.grad) < TOL[dt]
-    assert rel(db, gy.sum(dim=(0, 1, 2))) < TOL[dt]
+    assert gate(gxd, gx_ref, dt) <= 1.0, gate(gxd, gx_ref, dt)
+    assert gate(dw, wt.grad, dt) <= 1.0, gate(dw, wt.grad, dt)
+    assert gate(db, gy.sum(dim=(0, 1, 2)), dt) <= 1.0
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
@@ -233,7 +258,7 @@ def test_conv_small(dt, cin):
     x = torch.rand(N, H, W, cin, generator=g, dtype=torch.float64).to(dt).double()
     w = torch.randn(Cout, cin, 3, 3, generator=g, dtype=torch.float64) / 3
     b = torch.randn(Cout, generator=g, dtype=torch.float64)
-    ref = nhwc(F.conv2d(nchw(x), w, b, padding=1))
+    ref = nhwc(F.conv2d(nchw(x), w.float().double(), b.float().double(), padding=1))
     y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     tiles = ops.conv3x3_tiles(ops.act(y))
     st = torch.empty(tiles * (2 * Cout + 1), device=DEV)
@@ -249,7 +274,7 @@ def test_conv_small(dt, cin):
     wt = w.clone().requires_grad_(True)
     F.conv2d(nchw(x), wt, None, padding=1).backward(nchw(gy))
     torch.cuda.synchronize()
-    assert rel(y, ref) < TOL[dt]
+    assert gate(y, ref, dt) <= 1.0, gate(y, ref, dt)
     assert rel(dw, wt.grad) < 1e-4
     assert rel(db, gy.sum(dim=(0, 1, 2))) < 1e-4
     gamma, beta = torch.ones(Cout, device=DEV), torch.zeros(Cout, device=DEV)
@@ -704,16 +729,14 @@ def test_conv3x3_per_sample_affine_and_gscale(dt):
     sh = torch.randn(N, Cin, generator=g, dtype=torch.float64) * 0.3
     keep = (torch.rand(N, Cin, generator=g) > 0.3).double()
     scn, shn = sc * keep / 0.7, sh * keep / 0.7
-    xt = torch.relu(x * scn[:, None, None, :] + shn[:, None, None, :])
-    if dt == torch.bfloat16:
-        xt = xt.to(torch.bfloat16).double()
+    xt = tf(x, scn[:, None, None, :], shn[:, None, None, :], dt)
     ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), None, padding=1))
     y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
     ops.conv3x3_fwd(ops.act(x.to(DEV, dt)), wp, ops.act(y), scale=scn.float().to(DEV), shift=shn.float().to(DEV),
                     nstride=Cin)
     torch.cuda.synchronize()
-    assert rel(y, ref) < TOL[dt]
+    assert gate(y, ref, dt) <= 1.0, gate(y, ref, dt)
     gy = torch.randn(N, H, W, Cout, generator=g).to(dt).double()
     ns = ops.conv3x3_wgrad_splits(ops.act(gy.to(DEV, dt)), Cin, dt)
     dwp = torch.empty(ns * Cout * 9 * Cin, device=DEV)
@@ -724,7 +747,7 @@ def test_conv3x3_per_sample_affine_and_gscale(dt):
     wt = w.clone().requires_grad_(True)
     F.conv2d(nchw(xt), wt, None, padding=1).backward(nchw(gy))
     torch.cuda.synchronize()
-    assert rel(dw, wt.grad) < (1e-4 if dt == torch.float32 else 1e-2)
+    assert gate(dw, wt.grad, dt) <= 1.0, gate(dw, wt.grad, dt)
     # dgrad with gscale: gx = conv_transpose(gy) * gs[n][c]
     gs = (keep / 0.7).float().to(DEV)
     wpt = ops.conv3x3_pack(w.float().to(DEV), dt, flip=True)
@@ -740,6 +763,8 @@ def test_conv3x3_per_sample_affine_and_gscale(dt):
     torch.cuda.synchronize()
     exp = (gx0.double() * gs.double()[:, None, None, :]).to(dt).double()
     assert rel(gx, exp) < (1e-6 if dt == torch.float32 else 1e-2)
+    gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w.to(dt).double(), padding=1)) * gs.double().cpu()[:, None, None, :]
+    assert gate(gx, gx_ref, dt) <= 1.0, gate(gx, gx_ref, dt)
 
 
 def test_conv3x3_cin64_ragged_slice():
@@ -757,8 +782,8 @@ def test_conv3x3_cin64_ragged_slice():
     sc = torch.rand(N, Cin, generator=g, dtype=torch.float64) + 0.5
     sh = torch.randn(N, Cin, generator=g, dtype=torch.float64) * 0.3
     x = buf.double().cpu()[..., CO:CO + Cin]
-    xt = torch.relu(x * sc[:, None, None, :] + sh[:, None, None, :]).to(dt).double()
-    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), b, padding=1))
+    xt = tf(x, sc[:, None, None, :], sh[:, None, None, :], dt)
+    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), b.float().double(), padding=1))
     y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
     tiles = ops.conv3x3_tiles(ops.act(y))
@@ -771,7 +796,7 @@ def test_conv3x3_cin64_ragged_slice():
     s1, s2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
     ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, rm, rv, mean, inv, s1, s2)
     torch.cuda.synchronize()
-    assert rel(y, ref) < TOL[dt]
+    assert gate(y, ref, dt) <= 1.0, gate(y, ref, dt)
     assert rel(mean, ref.mean(dim=(0, 1, 2))) < 1e-2
     assert rel(1.0 / inv ** 2 - 1e-5, ref.var(dim=(0, 1, 2), unbiased=False)) < 1e-1
     # dgrad of a 136 -> 64 conv (Cin of the dgrad = 64): gx = conv_transpose(gy) * gs, fused BN-bwd sums
@@ -791,8 +816,8 @@ def test_conv3x3_cin64_ragged_slice():
     red = torch.empty(2 * Cout, device=DEV)
     ops.colsum(part, tiles, 2 * Cout, red)
     torch.cuda.synchronize()
-    gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w2.to(dt).double(), padding=1)) * gs[:, None, None, :]
-    assert rel(gx, gx_ref) < TOL[dt]
+    gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w2.to(dt).double(), padding=1)) * gs.float().double()[:, None, None, :]
+    assert gate(gx, gx_ref, dt) <= 1.0, gate(gx, gx_ref, dt)
     xh = (yb.double() - bm.double()) * bi.double()
     gp = torch.where(bgam.double() * xh + bbet.double() > 0, gx.double(), torch.zeros_like(xh))
     assert rel(red[:Cout], gp.sum(dim=(0, 1, 2))) < 1e-5
@@ -814,8 +839,8 @@ def test_conv3x3_deep_layer_shapes():
     sc = torch.rand(N, Cin, generator=g, dtype=torch.float64) + 0.5
     sh = torch.randn(N, Cin, generator=g, dtype=torch.float64) * 0.3
     x = buf.double().cpu()[..., CO:CO + Cin]
-    xt = torch.relu(x * sc[:, None, None, :] + sh[:, None, None, :]).to(dt).double()
-    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), b, padding=1))
+    xt = tf(x, sc[:, None, None, :], sh[:, None, None, :], dt)
+    ref = nhwc(F.conv2d(nchw(xt), w.to(dt).double(), b.float().double(), padding=1))
     y = torch.empty(N, H, W, Cout, dtype=dt, device=DEV)
     wp = ops.conv3x3_pack(w.float().to(DEV), dt, flip=False)
     tiles = ops.conv3x3_tiles(ops.act(y))
@@ -828,7 +853,7 @@ def test_conv3x3_deep_layer_shapes():
     s1, s2 = torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
     ops.bn_finalize(st, tiles, Cout, gamma, beta, 1e-5, 0.1, rm, rv, mean, inv, s1, s2)
     torch.cuda.synchronize()
-    assert rel(y, ref) < TOL[dt]
+    assert gate(y, ref, dt) <= 1.0, gate(y, ref, dt)
     yr = y.double().cpu()  # the stored outputs (stats are taken from the fp32 accumulators)
     assert rel(mean, yr.mean(dim=(0, 1, 2))) < 1e-2
     assert rel(1.0 / inv ** 2 - 1e-5, yr.var(dim=(0, 1, 2), unbiased=False)) < 2e-2
@@ -853,8 +878,8 @@ def test_conv3x3_deep_layer_shapes():
     ops.colsum(part, tiles, 2 * Cout, red)
     torch.cuda.synchronize()
     gx_ref = nhwc(F.conv_transpose2d(nchw(gy), w2.to(dt).double(), padding=1))
-    assert rel(gx_plain, gx_ref) < TOL[dt]
-    assert rel(gx, gx_ref * gs[:, None, None, :]) < TOL[dt]
+    assert gate(gx_plain, gx_ref, dt) <= 1.0, gate(gx_plain, gx_ref, dt)
+    assert gate(gx, gx_ref * gs.float().double()[:, None, None, :], dt) <= 1.0
     xh = (yb.double() - bm.double()) * bi.double()
     gp = torch.where(bgam.double() * xh + bbet.double() > 0, gx.double(), torch.zeros_like(xh))
     assert rel(red[:Cout], gp.sum(dim=(0, 1, 2))) < 1e-5

@@ -98,8 +98,11 @@ def test_loss_api_restatements_match_reference(golden_dir):
     check("tversky_a05", lambda x, tt: R.tversky_loss(x, tt, 3, 0.5), t)
 
 
-def test_train_step_matches_reference(golden_dir):
-    g = _load(golden_dir, "step_c3k3.npz")
+@pytest.mark.parametrize("fname", ["step_c3k3.npz", "step_pad_c3k3.npz"])
+def test_train_step_matches_reference(golden_dir, fname):
+    """One train_epoch step; step_pad_c3k3 is a 40x56 batch, so the reference's reflect pad of the
+    images and zero pad of the masks to /32 (train_eval.py:248-253, 276-296) are in the fixture."""
+    g = _load(golden_dir, fname)
     S = R.formula_weights(64, 3, 3, dtype=torch.float32)
     tr = R.OracleTrainer(S, total_epochs=50)
     lr = tr.epoch_lr_step(0)
@@ -416,6 +419,22 @@ def test_fillpoly_restatement_known_answers_and_per_pixel_form():
     pt = O.fill_poly_u8([[3, 4]], 6, 6)
     assert pt.sum() == 1 and pt[4, 3] == 1
     assert O.fill_poly_u8([[-9, -9], [-1, -3], [-5, -1]], 6, 6).sum() == 0
+    # border-crossing polygons (clipLine + the re-projected PolyEdge path), answers derived by hand from
+    # the geometry: exact-integer edges leave no rounding choice, so any OpenCV >= 4.5.2 (requirements.txt:
+    # opencv-python>=4.5.0) fills these pixels
+    rect = O.fill_poly_u8([[-3, 1], [3, 1], [3, 4], [-3, 4]], 6, 6)  # left half outside
+    exp = np.zeros((6, 6), np.uint8)
+    exp[1:5, 0:4] = 1
+    assert np.array_equal(rect, exp)
+    diag = O.fill_poly_u8([[2, 0], [9, 0], [2, 7]], 6, 6)  # hypotenuse x + y = 9 leaves right and bottom
+    exp = np.zeros((6, 6), np.uint8)
+    for r in range(6):
+        exp[r, 2:min(5, 9 - r) + 1] = 1
+    assert np.array_equal(diag, exp)
+    top = O.fill_poly_u8([[1, -4], [4, -4], [4, 2], [1, 2]], 6, 6)  # top edge above the image
+    exp = np.zeros((6, 6), np.uint8)
+    exp[0:3, 1:5] = 1
+    assert np.array_equal(top, exp)
     rng = np.random.default_rng(0)
     for t in range(300):
         h, w = int(rng.integers(4, 20)), int(rng.integers(4, 20))
