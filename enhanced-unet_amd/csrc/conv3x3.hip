@@ -378,8 +378,8 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   auto dma_a = [&](int kc) {
     const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
     const bool full = (kc + 1) * KC <= a.cin;  // else: quarters past cin read as zeros
-#pragma unroll
     static_assert(FHALF % FT == 0, "dma_a: a wave-instruction stays inside one channel half");
+#pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       uint32_t off = aoff[i];
       // quarter of slot tid + FT i: half (FT i) / FHALF (tid < FT), then the slot's parity
