@@ -94,25 +94,23 @@ constexpr int FHPXP = 640;                   // halo pixel slots (612 used), 4 c
 // fragment reads) and 6 % with the quarter XOR-swizzle that removes them (its per-read address VALU), the
 // DMA-staged data gradient gains 6 %, the DMA-staged untransformed forward 5-13 % -- so the layout follows the
 // staging.
-// Round 6: the pixel-major slots are split into two channel halves, [q >> 1][hp][q & 1] (a pixel's quarters
-// 2h, 2h + 1 -- 32 contiguous bytes -- adjacent, the halves 2 * FHPXP slots apart).  A ds_read_b128 lane
-// group of the A fragments (lanes 0-3 / 12-15 at quarter q, 4-11 at q + 1, or the reverse, over 16
-// consecutive halo pixels) then covers 16 distinct 16-byte slots of a bank row for any first pixel, where
-// [hp][q] put pixels 4 apart on one slot (2-way: SQ_LDS_BANK_CONFLICT 0.35-0.39 of the LDS cycles of every
-// DMA-staged forward / data gradient, profiles/r06_sq_layers.txt); a DMA wave-instruction reads 32 pixels x
-// 32 contiguous bytes.
-constexpr int FHALF = 2 * FHPXP;  // slots per channel half
+// The pixel-major fragment reads are 2-way bank conflicted: a ds_read_b128 lane group (lanes 0-3 / 12-15 at
+// quarter q, 4-11 at q + 1 over 16 consecutive halo pixels) puts pixels 4 apart on one 16-byte slot of the
+// 256-byte bank row (SQ_LDS_BANK_CONFLICT 0.35-0.39 of the LDS cycles of every DMA-staged forward / data
+// gradient, profiles/r06_sq_layers.txt).  Round 6 measured the conflict-free alternative that keeps the DMA
+// contiguous, channel halves [q >> 1][hp][q & 1] (a DMA wave-instruction then reads 32 pixels x 32 B): 13-layer
+// data gradient 5.95 vs 5.77 ms, untransformed forwards +3 %, bench -1.2 % (profiles/r06_ab.txt r6hp) -- the
+// halved DMA contiguity costs more than the conflicts, which the MFMA phase's LDS headroom absorbs.
 template <bool PIX>
 __device__ __forceinline__ int fslot(int hp, int q) {
-  return PIX ? (q >> 1) * FHALF + hp * 2 + (q & 1) : q * FHPXP + hp;
+  return PIX ? hp * 4 + q : q * FHPXP + hp;
 }
 // inverse for slot s: (halo pixel, quarter)
 template <bool PIX>
 __device__ __forceinline__ void fslot_inv(int s, int& hp, int& q) {
   if (PIX) {
-    const int h = s / FHALF, r = s - h * FHALF;
-    hp = r >> 1;
-    q = 2 * h + (r & 1);
+    hp = s >> 2;
+    q = s & 3;
   } else {
     q = s / FHPXP;
     hp = s - q * FHPXP;
@@ -238,7 +236,7 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   // this thread's halo quarter (fwd_unit), the same for every unit (ids tid + FT i)
   constexpr bool PIX = ((DG && !BT) || PF) && sizeof(T) == 2;  // halo layout / staging (fslot)
-  const int sq = PIX ? tid & 1 : (tid >> 3) & 3;  // (PIX: the quarter of unit tid; PIX stages by dma_a only)
+  const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)((const T*)a.x + (long long)ns * a.H * a.W * a.xct), 0,
@@ -378,12 +376,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   auto dma_a = [&](int kc) {
     const uint32_t cadd = (uint32_t)(kc * KC * (int)sizeof(T));
     const bool full = (kc + 1) * KC <= a.cin;  // else: quarters past cin read as zeros
-    static_assert(FHALF % FT == 0, "dma_a: a wave-instruction stays inside one channel half");
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
       uint32_t off = aoff[i];
-      // quarter of slot tid + FT i: half (FT i) / FHALF (tid < FT), then the slot's parity
-      if (!full && kc * KC + (2 * (i * FT / FHALF) + (tid & 1)) * E >= a.cin) off = FWD_OOB;
+      if (!full && kc * KC + (tid & 3) * E >= a.cin) off = FWD_OOB;  // (quarter of slot tid + FT i)
       EUNET_DASSERT(off == FWD_OOB || off + cadd + 16u <= slice_bytes);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(As + (i * FT + wvs * 64) * 16),
                                                16, off, cadd, 0, 0);
