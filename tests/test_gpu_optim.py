@@ -140,6 +140,16 @@ def test_capturable_adamw_after_torch_step_and_cpu_state():
         for p, q, gr in zip(pa, pb, grads):
             p.grad, q.grad = gr.to(DEV), gr.to(DEV)
         torch.nn.utils.clip_grad_norm_(pa, max_norm=1.0, foreach=True)
+        if it == 1:
+            # the native step restates torch's FUSED AdamW (bias corrections and hyper-parameter products in
+            # double, narrowed to fp32).  capturable foreach AdamW forms the bias corrections as fp32 tensor
+            # ops instead, so it differs from both in the step size's last bits (1.1e-6 relative after two
+            # steps, round 5).  The reference therefore continues from the capturable optimizer's state with a
+            # fused AdamW, which computes exactly what the native step computes.
+            fused = torch.optim.AdamW(pa, lr=4e-3, weight_decay=1e-4, fused=True)
+            for p in pa:  # (the state only: load_state_dict would also restore the param-group flags)
+                fused.state[p] = {k: v.clone() for k, v in oa.state[p].items()}
+            oa = fused
         oa.step()
         if it == 0:  # torch's own first step on ob, then a CPU step counter on one tensor
             torch.nn.utils.clip_grad_norm_(pb, max_norm=1.0, foreach=True)
@@ -150,9 +160,7 @@ def test_capturable_adamw_after_torch_step_and_cpu_state():
             native.step(1.0)
         torch.cuda.synchronize()
         for p, q in zip(pa, pb):
-            # capturable AdamW (foreach) forms its bias corrections as fp32 tensors, the native step (like
-            # the fused one) in double: last-bit differences in the step size
-            assert rel(q, p) < 1e-5, (it, p.shape)
+            assert rel(q, p) < 1e-6, (it, p.shape)
             assert ob.state[q]["step"].is_cuda or it == 0
             assert float(ob.state[q]["step"]) == it + 1
 
