@@ -357,16 +357,27 @@ def test_configs2_bn_running_stats_match_recomputed_conv(cfg2_batch):
         m._engine.last_state = None
 
 
-def test_configs2_loss_decreases_over_three_steps(cfg2_batch):
-    """Three Trainer.steps (clip, native AdamW at lr 1e-3) on the configs[2] batch: the loss decreases."""
+def test_configs2_loss_decreases_bf16_tracks_fp32(cfg2_batch):
+    """Five Trainer.steps (clip, native AdamW at lr 3e-4) on the configs[2] batch in bf16 and in fp32 (the
+    precision the oracle tests pin at configs[1]): the loss decreases at every step in both, and the bf16 loss
+    trajectory stays within 2e-3 relative of the fp32 one (measured 2.6e-4 .. 4.8e-4).  At lr 1e-3 both
+    precisions rise after the first step alike (14.30 -> 14.90 bf16, 14.30 -> 14.90 fp32:
+    tools/cfg2_loss_probe.py) -- optimisation dynamics, not a precision effect."""
     from eunet.train_eval import Trainer
     x, msk = cfg2_batch
-    tr = Trainer(_base64(), DEV, "enhanced_unet")
-    for g in tr.optimizer.param_groups:
-        g["lr"] = 1e-3
-    losses = [tr.step(x, msk) for _ in range(4)]
-    print("configs[2] losses:", losses)
-    assert all(b < a for a, b in zip(losses, losses[1:])), losses
+    traj = {}
+    for dt in ("bf16", "fp32"):
+        tr = Trainer(_base64(dt), DEV, "enhanced_unet")
+        for g in tr.optimizer.param_groups:
+            g["lr"] = 3e-4
+        traj[dt] = [tr.step(x, msk) for _ in range(5)]
+        del tr
+        torch.cuda.empty_cache()
+    print("configs[2] losses bf16:", traj["bf16"], "fp32:", traj["fp32"])
+    for dt in traj:
+        assert all(b < a for a, b in zip(traj[dt], traj[dt][1:])), (dt, traj[dt])
+    rel = max(abs(a - b) / abs(b) for a, b in zip(traj["bf16"], traj["fp32"]))
+    assert rel < 2e-3, (rel, traj)
 
 
 def test_configs2_256_slice_vs_oracle(cfg2_batch):
