@@ -231,7 +231,7 @@ def dice_vs_cpu_ref(model, args, dev):
 # rocprofv3 --pmc summaries of the default bench command (tools/gpu_pmc.sh, tools/gpu_pmc_mfma.sh);
 # the newest round's file that exists is used
 def _profile(name):
-    for r in ("r05", "r04", "r03", "r02"):
+    for r in ("r06", "r05", "r04", "r03", "r02"):
         f = os.path.join(ROOT, "profiles", f"{r}_{name}")
         if os.path.exists(f):
             return f
