@@ -36,10 +36,6 @@ EUNET_DEBUG_UNIT(conv3x3)
 
 namespace {
 
-constexpr int TH = 8, TW = 32;            // wgrad output tile (pixels)
-constexpr int HW_ = TW + 2, HH_ = TH + 2;  // halo tile
-constexpr int HPX = HH_ * HW_;            // 340 halo pixels
-constexpr int HPXP = 352;                 // padded plane (multiple of 16)
 constexpr int BN = 64;                    // output channels per block
 constexpr int NTHR = 256;
 constexpr int B_UNITS = 4 * BN * 9;       // 2304
@@ -887,31 +883,14 @@ struct WgArgs {
   int tx, ty, ntiles, per_split, nsplit;
 };
 
-__device__ uint4 g_conv_zero;  // 16 zero bytes (static storage is zero-initialised): LDS-DMA source of padding
-
 // LDS bank spreading of the wgrad stages (ds_read_b64_tr_b16 serves 2 x 32 lanes; a wave's
 // fragment reads were 4-way (dY) / 2-way (X) conflicted):
-//  - dY tile [256 px][8 units of 16 B]: pixel p's channel unit u is stored at unit u ^ wd_swz(p),
+//  - dY tile [128 px][8 units of 16 B]: pixel p's channel unit u is stored at unit u ^ wd_swz(p),
 //    so the 32 lanes of a transposed read (8 pixels x 4 channel quads) hit 64 distinct banks;
-//  - X halo [8 octants][HPXP]: odd channel octants start 4 slots (64 B) later, so the two octants
+//  - X halo [8 octants][DHPXP]: odd channel octants start 4 slots (64 B) later, so the two octants
 //    a read spans fall in different banks.
 __device__ __forceinline__ int wd_swz(int p) { return (p & 3) ^ (((p >> 3) & 1) << 2); }
 __device__ __forceinline__ int wx_shift(int oc) { return (oc & 1) * 4; }
-// last slot a bnrelu_x group of ni slots per thread reads (octant 7, thread pixel 31)
-constexpr int xo_max_slot(int ni) { return 7 * HPXP + 4 + 31 + 32 * (ni - 1); }
-
-// bf16 wgrad v2: block = (pixel-tile split, 64 co, 64 ci).  Wave w owns ci tile
-// w (16 channels) for all 9 taps x 4 co tiles (36 accumulators), so one
-// 32-pixel k-step costs 8 + 18 transposed fragment reads for 36 MFMAs.
-constexpr int KCW = 64;                        // ci channels per wgrad block (bf16)
-constexpr int WX_LDS = 8 * HPXP * 16;          // X halo [8 octants][HPXP][16 B]
-constexpr int WD_LDS = TH * TW * 64 * 2;       // dY tile [256 px][64 co] bf16
-constexpr int WSTAGE = WX_LDS + WD_LDS;        // 77824
-constexpr int WG_LDS = WSTAGE + 4 * 64 * 4;      // one stage + 1 KB (transform scales; 2 blocks / CU)
-constexpr int WX_IDS = ((HPX + 7) / 8) * 64;   // 2752: X unit ids (8 pixels x 8 octants per 64)
-constexpr int WX_ITERS = (WX_IDS + NTHR - 1) / NTHR;  // 11
-constexpr int WD_ITERS = TH * TW * 8 / NTHR;   // 8
-static_assert(WG_LDS <= 160 * 1024, "wgrad LDS");
 
 // Block order: logical L = (split, co-block, ci-block), ci fastest, XCD-contiguous
 // (see xcd_map): the blocks sharing a split's X / dY tiles share one L2.
@@ -924,19 +903,55 @@ __device__ __forceinline__ void wg_map(int b, int nsplit, int ncob, int ncib, in
   split = r / ncob;
 }
 
-// Pixels are the GEMM K: dW[co][t][ci] += dY^T[co][px] * X~[px + d_t][ci].
-// 4 waves, wave w owns ci 16w..16w+15 of the block's 64, all 64 co and 9 taps
-// (36 accumulators).  Two blocks per CU: a tile's X halo / dY loads are all
-// issued before the barrier that ends the previous tile's MFMAs, then written
-// to LDS (BN+ReLU applied to X there); the other block computes meanwhile.
-// Tile staging: X halo and dY both by LDS-DMA (global_load_lds, no staging VGPRs), then
-// BN+ReLU applied to the halo in place; one global round trip per tile (register-staged
-// variants measured slower: profiles/r01_ab_wgrad_pf.txt).  Holding the next tile in
-// registers across the k-loop (tried) spills: the 36 accumulators take 144 of the 256
-// VGPRs two blocks per CU leave each wave.
+// bf16 wgrad: pixels are the GEMM K.  Block = (pixel split, 64 co, 64 ci); wave w owns ci 16w..16w+15 for all
+// 64 co and 9 taps (36 accumulators): a 32-pixel k-step is 8 dY^T + 18 X transposed fragment reads
+// (ds_read_b64_tr_b16) for 36 MFMAs.  Two blocks per CU.  Split partials are reduced in fixed order in fp64
+// (wgrad_reduce).  Round 6: double-buffered over 8 x 16-pixel tiles, whose X halo + dY tile (40 KB) fit twice
+// in a block's 80 KB of LDS, so tile t + 1 is copied by LDS-DMA while tile t's MFMAs run (the round-5 kernel
+// staged 8 x 32 tiles into one stage: with its copies skipped after a split's first tile -- a diagnostic with
+// wrong results -- the 13 layers ran 3.72 vs 4.86 ms, profiles/r06_ab.txt r6wn).  The copies are issued by inline asm (buffer_load_dwordx4 ... lds, M0 = the
+// LDS destination), so the compiler sees no LDS-DMA: it would otherwise order every LDS read of the current
+// stage behind the other stage's copy in flight (vmcnt(0)).  The waits are explicit instead: vmcnt(0) before
+// the barrier that opens a tile (its copy, issued one tile earlier, has landed), and the barrier after the
+// in-place BN+ReLU pass is lgkmcnt(0) + s_barrier (no fence: __syncthreads' would wait for the copy).
+constexpr int KCW = 64;                         // ci channels per block
+constexpr int DTH = 8, DTW = 16;                // pixel tile
+constexpr int DHW = DTW + 2;                    // 18
+constexpr int DHPX = (DTH + 2) * DHW;           // 180 halo pixels
+constexpr int DHPXP = 192;                      // octant plane (slots): 3072 B = 12 bank rows
+constexpr int DWX = 8 * DHPXP * 16;             // X halo [8 octants][DHPXP][16 B]
+constexpr int DWD = DTH * DTW * 64 * 2;         // dY tile [128 px][64 co] bf16
+constexpr int DSTAGE = DWX + DWD;               // 40960
+constexpr int DWX_ITERS = 8 * DHPXP / NTHR;     // 6 wave-instructions per wave
+constexpr int DWD_ITERS = DTH * DTW * 8 / NTHR; // 4
+static_assert(8 * DHPXP == NTHR * DWX_ITERS && DTH * DTW * 8 == NTHR * DWD_ITERS, "whole wave-instructions");
+static_assert(7 * DHPXP + 4 + DHPX <= 8 * DHPXP, "the shifted last octant plane fits");
+static_assert(2 * DSTAGE <= 80 * 1024, "two stages per block, two blocks per CU");
+constexpr bool one_octant_boundary() {  // each 256-slot DMA range crosses one octant boundary at most
+  for (int i = 0; i < DWX_ITERS; ++i) {
+    int nb = 0;
+    for (int k = 1; k < 8; ++k) nb += (k * DHPXP > NTHR * i && k * DHPXP < NTHR * (i + 1)) ? 1 : 0;
+    if (nb > 1) return false;
+  }
+  return true;
+}
+static_assert(one_octant_boundary(), "dma_x: one octant boundary per wave-instruction range at most");
+
+// 16 bytes per lane from buffer rsrc at byte offset voff (range-checked: out of range reads zeros) into LDS at
+// M0 + 16 lane; lds must be wave-uniform
+__device__ __forceinline__ void dma16_lds(u32x4 rsrc, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(lds), "v"(voff), "s"(rsrc) : "memory", "m0");
+}
+__device__ __forceinline__ u32x4 rsrc_of(const void* base, uint32_t bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  return (u32x4){(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)),
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000u};
+}
+
 __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* lsc = (float*)(smem + WSTAGE);  // [scale | shift][KCW] of the current tile
+  __shared__ __attribute__((aligned(16))) char wst[2 * DSTAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   int split, cob, kc;
   wg_map(blockIdx.x, a.nsplit, cdiv(a.cout, 64), cdiv(a.cin, KCW), split, cob, kc);
@@ -946,9 +961,6 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   EUNET_DASSERT(split < a.nsplit && co0 < a.cout && kc * KCW < a.cin && t_begin < a.ntiles);
   const int tpi = a.tx * a.ty;
   const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  // this lane's dY read offset within a pixel row, less the 2ct units: wd_swz(pxa) is q4 ^ 4 (g & 1)
-  // for every k-step (pxa = 32 ks + 8 g + q4), and XOR-ing 2ct (even) into the unit index
-  // commutes with the low bit and the byte offset of the half
   const int sw16 = (((p4 >> 1) ^ wd_swz(8 * g + q4)) * 8 + 4 * (p4 & 1)) * 2;
 
   f32x4 acc[9][4];
@@ -956,93 +968,84 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[t][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // bias gradient: thread owns channels co0 + 8 (tid & 7) .. +7 over pixels (tid >> 3) + 32 i, as
-  // (even, odd) channel pairs summed in packed fp32
   f32x2 dbv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) dbv[e] = (f32x2){0.f, 0.f};
   if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(40);  // phase offset (conv3x3_fwd_kernel)
 
-  // Tile staging by buffer LDS-DMA (buffer_load ... lds) through per-sample descriptors: one 32-bit
-  // byte offset per lane, padding / out-of-range units at FWD_OOB (the range check reads zeros), the
-  // wave-instructions unrolled so that every per-lane term below is tile-invariant or a compile-time
-  // constant (the per-tile part is scalar).
-  const int wvs = __builtin_amdgcn_readfirstlane(wv);
-  // dY unit tid + 256 i = tile pixel (row i, column tid >> 3), LDS unit tid & 7 holding channel unit du
-  const int dcol = tid >> 3, du = (tid & 7) ^ wd_swz(dcol);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)wst;  // LDS byte address
+  const uint32_t wlds = lds0 + (uint32_t)__builtin_amdgcn_readfirstlane(wv) * 1024u;    // + this wave's 1 KB
+  // dY unit tid + 256 i = tile pixel p = (tid >> 3) + 32 i (row 2 i + (tid >> 7), column (tid >> 3) & 15),
+  // LDS unit tid & 7 holding channel unit du
+  const int dp = tid >> 3, dcol = dp & (DTW - 1), drow = dp >> 4, du = (tid & 7) ^ wd_swz(dp);
   const bool dch_ok = co0 + du * 8 < a.cout;
-  const uint32_t dlane = (uint32_t)((dcol * a.dct + a.dco + co0 + du * 8) * 2);
+  const uint32_t rstep = (uint32_t)(a.W * a.dct) * 2u;
+  const uint32_t dlane = (uint32_t)((dcol * a.dct + a.dco + co0 + du * 8) * 2) + (uint32_t)drow * rstep;
   const uint32_t dslice = (uint32_t)(a.H * a.W * a.dct) * 2u, xslice = (uint32_t)(a.H * a.W * a.xct) * 2u;
-  auto dma_d = [&](int n, int y0, int x0) {
-    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const bf16_t*)a.dy + (long long)n * a.H * a.W * a.dct), 0, (int)dslice, 0x00020000);
+  auto dma_d = [&](int st, int n, int y0, int x0) {
+    const u32x4 dr = rsrc_of((const bf16_t*)a.dy + (long long)n * a.H * a.W * a.dct, dslice);
     const bool xok = dch_ok & (dcol < a.W - x0);
-    const uint32_t rb = (uint32_t)((y0 * a.W + x0) * a.dct) * 2u, rstep = (uint32_t)(a.W * a.dct) * 2u;
-    char* Ds = smem + WX_LDS;
+    const uint32_t rb = (uint32_t)((y0 * a.W + x0) * a.dct) * 2u;
+    const uint32_t l = wlds + (uint32_t)(st * DSTAGE + DWX);
 #pragma unroll
-    for (int i = 0; i < TH; ++i) {
-      const bool ok = xok & (y0 + i < a.H);
-      const uint32_t off = dlane + rb + i * rstep;
+    for (int i = 0; i < DWD_ITERS; ++i) {
+      const bool ok = xok & (y0 + 2 * i + drow < a.H);
+      const uint32_t off = dlane + rb + 2u * i * rstep;
       EUNET_DASSERT(!ok || off + 16u <= dslice);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (__attribute__((address_space(3))) void*)(Ds + (wvs + 4 * i) * 1024),
-                                               16, ok ? off : FWD_OOB, 0, 0, 0);
+      dma16_lds(dr, ok ? off : FWD_OOB, l + 4096u * i);
     }
   };
-  static_assert(WD_ITERS == TH && TW * 8 == NTHR, "dma_d: one tile row per wave-instruction group");
-  // X halo raw into LDS: slot s = tid + 256 i = oc * HPXP + wx_shift(oc) + hp
-  static_assert(8 * HPXP == 4 * 64 * WX_ITERS, "dma_x: 11 wave-instructions per wave");
-  auto dma_x = [&](int n, int y0, int x0) {
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)((const bf16_t*)a.x + (long long)n * a.H * a.W * a.xct), 0, (int)xslice, 0x00020000);
+  // X halo raw into LDS: slot s = tid + 256 i = oc * DHPXP + wx_shift(oc) + hp
+  auto dma_x = [&](int st, int n, int y0, int x0) {
+    const u32x4 xr = rsrc_of((const bf16_t*)a.x + (long long)n * a.H * a.W * a.xct, xslice);
     const int tb = ((y0 - 1) * a.W + (x0 - 1)) * a.xct + a.xco + kc * KCW;  // element (y0 - 1, x0 - 1)
-    // recomputed per tile: hoisted out of the tile loop, the 11 lanes' offsets and masks would be
-    // live across the k-loop and spill
+    const uint32_t l = wlds + (uint32_t)(st * DSTAGE);
     int t = tid;
-    asm volatile("" : "+v"(t));
+    asm volatile("" : "+v"(t));  // per tile: hoisted, the 6 lanes' offsets and masks would be live across the k-loop
 #pragma unroll
-    for (int i = 0; i < WX_ITERS; ++i) {
-      // octant of slot tid + 256 i: k, or k + 1 from lane tid >= tk on (256 < HPXP: one boundary at most)
-      const int k = 256 * i / HPXP, tk = HPXP * (k + 1) - 256 * i;
-      const bool bump = tk < 256 && t >= tk;
+    for (int i = 0; i < DWX_ITERS; ++i) {
+      const int k = NTHR * i / DHPXP, tk = DHPXP * (k + 1) - NTHR * i;
+      const bool bump = tk < NTHR && t >= tk;
       const int oc = k + bump;
-      const int hp = t + 256 * i - HPXP * oc - wx_shift(oc);
-      const int hy = (int)((uint32_t)hp / HW_), hx = hp - hy * HW_;
-      const bool ok = ((uint32_t)hp < (uint32_t)HPX) & ((uint32_t)(y0 - 1 + hy) < (uint32_t)a.H) &
+      const int hp = t + NTHR * i - DHPXP * oc - wx_shift(oc);
+      const int hy = (int)((uint32_t)hp / DHW), hx = hp - hy * DHW;
+      const bool ok = ((uint32_t)hp < (uint32_t)DHPX) & ((uint32_t)(y0 - 1 + hy) < (uint32_t)a.H) &
                       ((uint32_t)(x0 - 1 + hx) < (uint32_t)a.W) & (kc * KCW + oc * 8 < a.cin);
       const uint32_t off = (uint32_t)(tb + (hy * a.W + hx) * a.xct + oc * 8) * 2u;
       EUNET_DASSERT(!ok || off + 16u <= xslice);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(smem + (wvs + 4 * i) * 1024),
-                                               16, ok ? off : FWD_OOB, 0, 0, 0);
+      dma16_lds(xr, ok ? off : FWD_OOB, l + 4096u * i);
     }
   };
-  // BN+ReLU of the staged halo in place; padding stays 0.  Thread t owns channel octant t >> 5 and
-  // halo pixels (t & 31) + 32 i (i < 11): its 8 scales / shifts are read once per tile.  A wave covers 32
-  // consecutive pixels of two octants, so the 16 lanes of a ds_read_b128 group and the 8 of a
-  // ds_write_b128 group address distinct 16-byte slots of a bank row (octant-fastest lanes, as before
-  // round 6, put 2 - 4 lanes on one slot: SQ_LDS_BANK_CONFLICT 0.34 of the LDS cycles, wgrad +35 % with
-  // the transform on the 64-channel layers).
+  // BN+ReLU of the staged halo in place (padding stays 0): thread = (octant tid >> 5, pixels (tid & 31) + 32 i);
+  // its octant's 8 scales / shifts are loaded before the tile's opening barrier
   const int xo = tid >> 5;
-  auto bnrelu_x = [&](int y0, int x0) {
-    if (kc * KCW + xo * 8 >= a.cin) return;
-    const f32x4 s0 = *(const f32x4*)(lsc + xo * 8), s1 = *(const f32x4*)(lsc + xo * 8 + 4);
-    const f32x4 h0 = *(const f32x4*)(lsc + KCW + xo * 8), h1 = *(const f32x4*)(lsc + KCW + xo * 8 + 4);
-    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-    char* const plane = smem + (xo * HPXP + wx_shift(xo)) * 16;
-    // groups of G slots: all G reads issued before the first write (the reads of padding / past-the-halo
-    // slots are harmless -- they stay inside the stage -- and only valid slots are written back)
-    // NI = 12 >= 11 whole groups: slot 352 + 31 of the last plane still lies inside the stage (in the dY tile)
-    constexpr int G = 4, NI = ((HPX + 31) / 32 + G - 1) / G * G;
-    static_assert((xo_max_slot(NI) + 1) * 16 <= WSTAGE, "bnrelu_x: group reads stay inside the stage");
+  const bool xo_ok = kc * KCW + xo * 8 < a.cin;
+  auto load_aff = [&](int n, f32x4* sc) {
+    const float* ps = a.isc + (long long)n * a.iss + kc * KCW + xo * 8;
+    const float* ph = a.ish + (long long)n * a.iss + kc * KCW + xo * 8;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    sc[0] = xo_ok ? *(const f32x4*)ps : z;
+    sc[1] = xo_ok ? *(const f32x4*)(ps + 4) : z;
+    sc[2] = xo_ok ? *(const f32x4*)ph : z;
+    sc[3] = xo_ok ? *(const f32x4*)(ph + 4) : z;
+  };
+  auto bnrelu_x = [&](char* S, int y0, int x0, const f32x4* sc) {
+    if (!xo_ok) return;
+    const float scv[8] = {sc[0][0], sc[0][1], sc[0][2], sc[0][3], sc[1][0], sc[1][1], sc[1][2], sc[1][3]};
+    const float shv[8] = {sc[2][0], sc[2][1], sc[2][2], sc[2][3], sc[3][0], sc[3][1], sc[3][2], sc[3][3]};
+    char* const plane = S + (xo * DHPXP + wx_shift(xo)) * 16;
+    constexpr int G = 3, NI = (DHPX + 31) / 32;  // 6 pixel rounds in 2 groups of 3
+    static_assert(NI % G == 0, "bnrelu_x groups");
+    static_assert((7 * DHPXP + 4 + 31 + 32 * (NI - 1) + 1) * 16 <= DSTAGE, "bnrelu_x: group reads stay inside the stage");
 #pragma unroll 1
-    for (int i0 = 0; i0 < NI; i0 += G) {  // (unrolled, the groups' registers spill)
+    for (int i0 = 0; i0 < NI; i0 += G) {
       u32x4 w[G];
       bool ok[G];
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        const int hp = (tid & 31) + 32 * (i0 + j), hy = hp / HW_, hx = hp - hy * HW_;
+        const int hp = (tid & 31) + 32 * (i0 + j), hy = hp / DHW, hx = hp - hy * DHW;
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        ok[j] = (hp < HPX) & ((uint32_t)yy < (uint32_t)a.H) & ((uint32_t)xx < (uint32_t)a.W);
+        ok[j] = (hp < DHPX) & ((uint32_t)yy < (uint32_t)a.H) & ((uint32_t)xx < (uint32_t)a.W);
         w[j] = *(const u32x4*)(plane + hp * 16);
       }
 #pragma unroll
@@ -1050,9 +1053,9 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         const int hp = (tid & 31) + 32 * (i0 + j);
         u32x4 o;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {  // packed fp32 FMA, round to bf16, ReLU on the bf16 pair (sign bit)
+        for (int d = 0; d < 4; ++d) {
           const f32x2 x = {__uint_as_float(w[j][d] << 16), __uint_as_float(w[j][d] & 0xFFFF0000u)};
-          const f32x2 r = __builtin_elementwise_fma(x, (f32x2){sc[2 * d], sc[2 * d + 1]}, (f32x2){sh[2 * d], sh[2 * d + 1]});
+          const f32x2 r = __builtin_elementwise_fma(x, (f32x2){scv[2 * d], scv[2 * d + 1]}, (f32x2){shv[2 * d], shv[2 * d + 1]});
           const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(r[0], r[1]));
           o[d] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
         }
@@ -1062,73 +1065,78 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   };
   // tile coordinates advance incrementally (scalar): sample tn, tile row tyi, tile column txi
   int tn = t_begin / tpi, tyi = (t_begin - tn * tpi) / a.tx, txi = t_begin - tn * tpi - tyi * a.tx;
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  const bool tf = a.isc != nullptr;
+  {  // the split's first tile into stage 0
     const int n = __builtin_amdgcn_readfirstlane(tn);
-    const int y0 = __builtin_amdgcn_readfirstlane(tyi) * TH, x0 = __builtin_amdgcn_readfirstlane(txi) * TW;
+    dma_x(0, n, __builtin_amdgcn_readfirstlane(tyi) * DTH, __builtin_amdgcn_readfirstlane(txi) * DTW);
+    dma_d(0, n, __builtin_amdgcn_readfirstlane(tyi) * DTH, __builtin_amdgcn_readfirstlane(txi) * DTW);
+  }
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int st = (tile - t_begin) & 1;
+    char* const S = wst + st * DSTAGE;
+    const int n = __builtin_amdgcn_readfirstlane(tn);
+    const int y0 = __builtin_amdgcn_readfirstlane(tyi) * DTH, x0 = __builtin_amdgcn_readfirstlane(txi) * DTW;
     if (++txi == a.tx) {
       txi = 0;
       if (++tyi == a.ty) { tyi = 0; ++tn; }
     }
-    {  // X halo and dY both by LDS-DMA
-      // the block's 64 input channels' BN scale / shift for this tile's sample: one load per thread
-      // (tid < 128) instead of 16 per halo slot in the transform pass
-      float rsc = 0.f;
-      if (a.isc != nullptr && tid < 2 * KCW) {
-        const int c = kc * KCW + (tid % KCW);
-        if (c < a.cin) rsc = (tid < KCW ? a.isc : a.ish)[c + n * a.iss];
-      }
-      __syncthreads();  // previous tile's LDS reads are done
-      dma_x(n, y0, x0);
-      dma_d(n, y0, x0);
-      if (a.isc != nullptr && tid < 2 * KCW) lsc[tid] = rsc;
-      __syncthreads();  // (its fence waits for the DMA)
-      if (a.isc != nullptr) {
-        bnrelu_x(y0, x0);
-        __syncthreads();
-      }
+    f32x4 sc[4];
+    if (tf) load_aff(n, sc);
+    // this tile's copy (issued a tile earlier) has landed; every wave is done reading the other stage.  The
+    // wait is the builtin, so the compiler knows its own loads (the scales) are complete too and puts no
+    // vmcnt(0) before their use -- which would wait for the next tile's copy
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    if (tile + 1 < t_end) {
+      const int n1 = __builtin_amdgcn_readfirstlane(tn);
+      const int y1 = __builtin_amdgcn_readfirstlane(tyi) * DTH, x1 = __builtin_amdgcn_readfirstlane(txi) * DTW;
+      dma_x(st ^ 1, n1, y1, x1);
+      dma_d(st ^ 1, n1, y1, x1);
     }
-    const char* Xs = smem;
-    const char* Ds = Xs + WX_LDS;
+    if (tf) {
+      bnrelu_x(S, y0, x0, sc);
+      // every wave's transformed slots are written before any wave reads them (a raw barrier: the other
+      // stage's copy stays in flight)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    const char* const Xs = S;
+    const char* const Ds = S + DWX;
     if (a.db != nullptr && kc == 0) {
       const bf16_t* d = (const bf16_t*)Ds;
 #pragma unroll
-      for (int i = 0; i < TH * TW / 32; ++i) {  // independent 16-B reads, no per-read wait
+      for (int i = 0; i < DTH * DTW / 32; ++i) {
         const int px = (tid >> 3) + 32 * i;
         const u32x4 w = *(const u32x4*)(d + px * 64 + ((tid & 7) ^ wd_swz(px)) * 8);
 #pragma unroll
         for (int e = 0; e < 4; ++e) dbv[e] += (f32x2){__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xFFFF0000u)};
       }
     }
-    // dY^T fragments of k-step ks (32 pixels x 4 co tiles); channel unit 2ct + (p4 >> 1) of pixel
-    // pxa (and pxa + 4: same wd_swz) sits at LDS unit (2ct + (p4 >> 1)) ^ wd_swz(pxa)
-    auto load_af = [&](int ks, bf16x8* f) {
-      const int pxa = ks * TW + 8 * g + q4;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int uo = (32 * ct) ^ sw16;  // byte offset of unit (2ct + (p4 >> 1)) ^ wd_swz(pxa), + the half
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + pxa * 128 + uo));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa + 4) * 128 + uo));
-        f[ct] = cat_bf16x4(lo, hi);
-      }
-    };
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
-    for (int ks = 0; ks < TH; ++ks) {
+    for (int ks = 0; ks < DTH * DTW / 32; ++ks) {
+      // k-step ks: tile pixels 32 ks .. 32 ks + 31 = rows 2 ks, 2 ks + 1 (lane groups g = 0, 1 / 2, 3)
       bf16x8 af[4];
-      load_af(ks, af);
+      const int pxa = ks * 32 + 8 * g + q4;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int uo = (32 * ct) ^ sw16;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + pxa * 128 + uo));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa + 4) * 128 + uo));
+        af[ct] = cat_bf16x4(lo, hi);
+      }
       const int oc = 2 * wv + (p4 >> 1);
+      const int hrow = 2 * ks + (g >> 1), hcol = 8 * (g & 1) + q4;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
-        const int hp = (ks + ky) * HW_ + 8 * g + q4 + kx;
-        const char* base = Xs + (oc * HPXP + wx_shift(oc) + hp) * 16 + (p4 & 1) * 8;
+        const int hp = (hrow + ky) * DHW + hcol + kx;
+        const char* base = Xs + (oc * DHPXP + wx_shift(oc) + hp) * 16 + (p4 & 1) * 8;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
         const bf16x8 bfr = cat_bf16x4(lo, hi);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
+        for (int ct = 0; ct < 4; ++ct)
           acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ct], bfr, acc[t][ct], 0, 0, 0);
-        }
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1148,7 +1156,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
         }
       }
   if (a.db != nullptr && kc == 0) {
-    float* dbred = (float*)smem;  // [32 pixel groups][64 co], over the finished tile stage
+    float* dbred = (float*)wst;  // [32 pixel groups][64 co]
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) dbred[(tid >> 3) * 64 + (tid & 7) * 8 + e] = dbv[e >> 1][e & 1];
@@ -1160,7 +1168,6 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     }
   }
 }
-
 
 // fp32 wgrad (exact fp32: v_mfma_f32_16x16x4_f32, 64 FLOP/clk/SIMD).  Pixels are the GEMM K.
 // Block = (pixel split, 64 co, 32 ci) over 4 x 32 pixel tiles; wave w owns ci tile w & 1 and
@@ -1591,7 +1598,7 @@ constexpr int WG_BLOCKS = 512;  // weight-gradient blocks per launch (two per CU
 int eunet_conv3x3_wgrad_splits(const eunet_act* dy, int cin, int dtype, int* nsplit) {
   EUNET_REQUIRE(act_ok(dy) && nsplit && cin > 0, "conv3x3_wgrad_splits: bad args");
   const bool bf = dtype == EUNET_BF16;
-  const int ntiles = dy->n * cdiv(dy->h, bf ? TH : WF_TH) * cdiv(dy->w, bf ? TW : WF_TW);
+  const int ntiles = dy->n * cdiv(dy->h, bf ? DTH : WF_TH) * cdiv(dy->w, bf ? DTW : WF_TW);
   const int blocks = cdiv(dy->c, 64) * cdiv(cin, bf ? KCW : WF_CI);
   int s = cdiv(WG_BLOCKS, blocks);
   {
@@ -1644,14 +1651,13 @@ int eunet_conv3x3_wgrad(const eunet_act* x, const float* in_scale, const float* 
   EUNET_REQUIRE(!bf || ((long long)a.H * a.W * a.xct * 2 < (long long)FWD_OOB &&
                         (long long)a.H * a.W * a.dct * 2 < (long long)FWD_OOB),
                 "conv3x3_wgrad: sample slice >= 3 GiB");
-  a.tx = cdiv(x->w, bf ? TW : WF_TW); a.ty = cdiv(x->h, bf ? TH : WF_TH); a.ntiles = x->n * a.tx * a.ty;
+  a.tx = cdiv(x->w, bf ? DTW : WF_TW); a.ty = cdiv(x->h, bf ? DTH : WF_TH); a.ntiles = x->n * a.tx * a.ty;
   a.per_split = cdiv(a.ntiles, nsplit);
   a.nsplit = nsplit;
   EUNET_REQUIRE(cdiv(a.ntiles, a.per_split) == nsplit, "conv3x3_wgrad: nsplit not from wgrad_splits");
   if (x->dtype == EUNET_BF16) {
     dim3 grid(nsplit * cdiv(dy->c, 64) * cdiv(x->c, KCW));
-    allow_lds(conv3x3_wgrad_bf16_kernel, WG_LDS);
-    conv3x3_wgrad_bf16_kernel<<<grid, NTHR, WG_LDS, (hipStream_t)stream>>>(a);
+    conv3x3_wgrad_bf16_kernel<<<grid, NTHR, 0, (hipStream_t)stream>>>(a);
   } else {
     dim3 grid(nsplit * cdiv(dy->c, WF_CO) * cdiv(x->c, WF_CI));
     allow_lds(conv3x3_wgrad_f32_kernel, WF_LDS);

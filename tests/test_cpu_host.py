@@ -42,7 +42,7 @@ def test_wgrad_split_count_fills_launch_waves(n, hw, cout, cin, dtype):
     assert lib.eunet_conv3x3_wgrad_splits(ctypes.byref(dy), cin, dtc, ctypes.byref(s)) == 0
     ns = s.value
     bf = dtype == "bf16"
-    th, tw, kc = (8, 32, 64) if bf else (4, 32, 32)
+    th, tw, kc = (8, 16, 64) if bf else (4, 32, 32)  # bf16: the double-buffered 8 x 16 tiles (round 6)
     ntiles = n * -(-hw // th) * -(-hw // tw)
     blocks = -(-cout // 64) * -(-cin // kc)
     assert 1 <= ns <= ntiles

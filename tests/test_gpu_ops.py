@@ -231,8 +231,8 @@ def test_conv3x3_wgrad_ragged_slots(dt):
         xa = xa.float().bfloat16().double()
     wt = torch.zeros(Cout, Cin, 3, 3, dtype=torch.float64, requires_grad=True)
     F.conv2d(nchw(xa), wt, None, padding=1).backward(nchw(dy))
-    th = 8 if dt == torch.bfloat16 else 4
-    ntiles = N * -(-H // th) * -(-W // 32)
+    th, tw = (8, 16) if dt == torch.bfloat16 else (4, 32)  # the kernels' pixel tiles
+    ntiles = N * -(-H // th) * -(-W // tw)
     tpi = ntiles // N
     crossing = [s for s in range(2, ntiles) if -(-ntiles // -(-ntiles // s)) == s and (-(-ntiles // s)) % tpi]
     assert crossing
