@@ -1016,8 +1016,9 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       dma16_lds(xr, ok ? off : FWD_OOB, l + 4096u * i);
     }
   };
-  // BN+ReLU of the staged halo in place (padding stays 0): thread = (octant tid >> 5, pixels (tid & 31) + 32 i);
-  // its octant's 8 scales / shifts are loaded before the tile's opening barrier
+  // BN+ReLU of the staged halo in place (padding stays 0): thread = (octant tid >> 5, pixels (tid & 31) + 32 i) --
+  // wave w owns octants 2w, 2w + 1, the ones its fragment reads use; its octant's 8 scales / shifts are loaded
+  // before the tile's opening barrier
   const int xo = tid >> 5;
   const bool xo_ok = kc * KCW + xo * 8 < a.cin;
   auto load_aff = [&](int n, f32x4* sc) {
@@ -1094,10 +1095,11 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       dma_d(st ^ 1, n1, y1, x1);
     }
     if (tf) {
+      // wave w transforms octants 2w, 2w + 1 (threads tid >> 5), which are exactly the X octants its own
+      // fragment reads use (oc = 2 wv + (p4 >> 1)): its LDS writes precede its reads in program order, so no
+      // block barrier -- each wave starts its MFMAs when its own octants are done
       bnrelu_x(S, y0, x0, sc);
-      // every wave's transformed slots are written before any wave reads them (a raw barrier: the other
-      // stage's copy stays in flight)
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const char* const Xs = S;
     const char* const Ds = S + DWX;

@@ -143,10 +143,10 @@ class UNetEngine:
     # pool_recompute -- the same for the encoders' output gradients gskip + maxpool-adjoint(gpool):
     # pool_bwd_add_bnr only reduces them, the block's apply recomputes them per 2x2 window
     # (eunet_bn_bwd_apply_pool: the same gy bit for bit, 0.75 C per pixel less traffic).  Needs
-    # fuse_bn_reduce, the block outside fuse_bn_apply, and even H and W at the level.  Measured equal
-    # (182.4 vs 182.7 img/s over three alternating pairs, profiles/r05_ab.txt r5pr: the apply's window
-    # loads and argmax cost what the saved traffic gives): off
-    pool_recompute = False
+    # fuse_bn_reduce, the block outside fuse_bn_apply, and even H and W at the level.  Round 5 measured it
+    # equal (182.4 vs 182.7 img/s, profiles/r05_ab.txt r5pr); with round 6's weight gradient it is +0.3 / +1.0 %
+    # in two same-box runs of three alternating rounds each (profiles/r06_ab.txt r6pr): on
+    pool_recompute = True
     # dgrad_first -- after a DoubleConv's BN-a backward, conv .0's data gradient is issued on the launch
     # stream before the side-stream weight gradients (which wait on an event recorded right after the
     # apply, not on the launch stream's tail).  Closes half of the ~24 us apply -> dgrad launch-stream gap

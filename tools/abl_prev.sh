@@ -10,7 +10,7 @@ objs=$(ls enhanced-unet_amd/build/*.o)
 prev=""
 for src in "$@"; do
   git show ${REV:-HEAD}:enhanced-unet_amd/csrc/$src.hip > abl/${src}_prev.hip
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -Wno-unused-variable -Wno-inline-asm \
     -Ienhanced-unet_amd/csrc -c abl/${src}_prev.hip -o abl/${src}_prev.o
   objs=$(echo "$objs" | grep -v "/$src.o")
   prev="$prev abl/${src}_prev.o"
