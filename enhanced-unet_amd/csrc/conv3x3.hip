@@ -883,14 +883,15 @@ struct WgArgs {
   int tx, ty, ntiles, per_split, nsplit;
 };
 
-// LDS bank spreading of the wgrad stages (ds_read_b64_tr_b16 serves 2 x 32 lanes; a wave's
-// fragment reads were 4-way (dY) / 2-way (X) conflicted):
-//  - dY tile [128 px][8 units of 16 B]: pixel p's channel unit u is stored at unit u ^ wd_swz(p),
-//    so the 32 lanes of a transposed read (8 pixels x 4 channel quads) hit 64 distinct banks;
-//  - X halo [8 octants][DHPXP]: odd channel octants start 4 slots (64 B) later, so the two octants
-//    a read spans fall in different banks.
-__device__ __forceinline__ int wd_swz(int p) { return (p & 3) ^ (((p >> 3) & 1) << 2); }
-__device__ __forceinline__ int wx_shift(int oc) { return (oc & 1) * 4; }
+// LDS layout of the wgrad stages.  A ds_read_b64_tr_b16 serves 2 x 32 lanes; a 32-lane half reads 8
+// consecutive pixels of one tile row (lo: columns 0-7, hi: 8-15 of the k-step's row) x 2 channel groups x 2
+// 8-byte halves -- 256 bytes that must cover the 64 banks once:
+//  - dY tile [128 px][8 units of 16 B]: pixel p's channel unit u is stored at unit u ^ wd_swz(p), p & 6: the
+//    4 same-parity pixels of a read (one 256-byte row holds 2 pixels) take 4 distinct unit rotations;
+//  - X halo [4 octant pairs][DPL][2 octants x 16 B]: a read's 8 pixels x 2 octants of its wave's pair are 16
+//    consecutive 16-byte slots.  A pixel's octant pair is 32 contiguous bytes in global memory, so a DMA
+//    wave-instruction touches 32 lines (octant planes: 64, round-6 r6wc).
+__device__ __forceinline__ int wd_swz(int p) { return p & 6; }
 
 // Block order: logical L = (split, co-block, ci-block), ci fastest, XCD-contiguous
 // (see xcd_map): the blocks sharing a split's X / dY tiles share one L2.
@@ -918,24 +919,16 @@ constexpr int KCW = 64;                         // ci channels per block
 constexpr int DTH = 8, DTW = 16;                // pixel tile
 constexpr int DHW = DTW + 2;                    // 18
 constexpr int DHPX = (DTH + 2) * DHW;           // 180 halo pixels
-constexpr int DHPXP = 192;                      // octant plane (slots): 3072 B = 12 bank rows
-constexpr int DWX = 8 * DHPXP * 16;             // X halo [8 octants][DHPXP][16 B]
+constexpr int DPL = 384;                        // octant-pair plane (slots): 2 x 180 used, 6144 B = 24 bank rows
+constexpr int DWX = 4 * DPL * 16;               // X halo [4 pairs][DPL][16 B]
 constexpr int DWD = DTH * DTW * 64 * 2;         // dY tile [128 px][64 co] bf16
 constexpr int DSTAGE = DWX + DWD;               // 40960
-constexpr int DWX_ITERS = 8 * DHPXP / NTHR;     // 6 wave-instructions per wave
+constexpr int DWX_ITERS = 4 * DPL / NTHR;       // 6 wave-instructions per wave
 constexpr int DWD_ITERS = DTH * DTW * 8 / NTHR; // 4
-static_assert(8 * DHPXP == NTHR * DWX_ITERS && DTH * DTW * 8 == NTHR * DWD_ITERS, "whole wave-instructions");
-static_assert(7 * DHPXP + 4 + DHPX <= 8 * DHPXP, "the shifted last octant plane fits");
+static_assert(4 * DPL == NTHR * DWX_ITERS && DTH * DTW * 8 == NTHR * DWD_ITERS, "whole wave-instructions");
+static_assert(2 * DHPX <= DPL && DPL % 16 == 0, "a pair plane holds the halo, bank-row aligned");
 static_assert(2 * DSTAGE <= 80 * 1024, "two stages per block, two blocks per CU");
-constexpr bool one_octant_boundary() {  // each 256-slot DMA range crosses one octant boundary at most
-  for (int i = 0; i < DWX_ITERS; ++i) {
-    int nb = 0;
-    for (int k = 1; k < 8; ++k) nb += (k * DHPXP > NTHR * i && k * DHPXP < NTHR * (i + 1)) ? 1 : 0;
-    if (nb > 1) return false;
-  }
-  return true;
-}
-static_assert(one_octant_boundary(), "dma_x: one octant boundary per wave-instruction range at most");
+static_assert(DPL > NTHR, "dma_x: one pair-plane boundary per wave-instruction range at most");
 
 // 16 bytes per lane from buffer rsrc at byte offset voff (range-checked: out of range reads zeros) into LDS at
 // M0 + 16 lane; lds must be wave-uniform
@@ -961,7 +954,9 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
   EUNET_DASSERT(split < a.nsplit && co0 < a.cout && kc * KCW < a.cin && t_begin < a.ntiles);
   const int tpi = a.tx * a.ty;
   const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-  const int sw16 = (((p4 >> 1) ^ wd_swz(8 * g + q4)) * 8 + 4 * (p4 & 1)) * 2;
+  // a lane's k-step pixels: lo = row 2 ks + (g >> 1), column 4 (g & 1) + q4; hi = 8 columns on (same wd_swz)
+  const int pcol = 4 * (g & 1) + q4;
+  const int sw16 = (((p4 >> 1) ^ wd_swz(pcol)) * 8 + 4 * (p4 & 1)) * 2;
 
   f32x4 acc[9][4];
 #pragma unroll
@@ -995,7 +990,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       dma16_lds(dr, ok ? off : FWD_OOB, l + 4096u * i);
     }
   };
-  // X halo raw into LDS: slot s = tid + 256 i = oc * DHPXP + wx_shift(oc) + hp
+  // X halo raw into LDS: slot s = tid + 256 i = (oc >> 1) * DPL + 2 hp + (oc & 1)
   auto dma_x = [&](int st, int n, int y0, int x0) {
     const u32x4 xr = rsrc_of((const bf16_t*)a.x + (long long)n * a.H * a.W * a.xct, xslice);
     const int tb = ((y0 - 1) * a.W + (x0 - 1)) * a.xct + a.xco + kc * KCW;  // element (y0 - 1, x0 - 1)
@@ -1004,10 +999,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     asm volatile("" : "+v"(t));  // per tile: hoisted, the 6 lanes' offsets and masks would be live across the k-loop
 #pragma unroll
     for (int i = 0; i < DWX_ITERS; ++i) {
-      const int k = NTHR * i / DHPXP, tk = DHPXP * (k + 1) - NTHR * i;
+      const int k = NTHR * i / DPL, tk = DPL * (k + 1) - NTHR * i;
       const bool bump = tk < NTHR && t >= tk;
-      const int oc = k + bump;
-      const int hp = t + NTHR * i - DHPXP * oc - wx_shift(oc);
+      const int pr = k + bump, r = t + NTHR * i - DPL * pr;
+      const int oc = 2 * pr + (r & 1), hp = r >> 1;
       const int hy = (int)((uint32_t)hp / DHW), hx = hp - hy * DHW;
       const bool ok = ((uint32_t)hp < (uint32_t)DHPX) & ((uint32_t)(y0 - 1 + hy) < (uint32_t)a.H) &
                       ((uint32_t)(x0 - 1 + hx) < (uint32_t)a.W) & (kc * KCW + oc * 8 < a.cin);
@@ -1016,10 +1011,10 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
       dma16_lds(xr, ok ? off : FWD_OOB, l + 4096u * i);
     }
   };
-  // BN+ReLU of the staged halo in place (padding stays 0): thread = (octant tid >> 5, pixels (tid & 31) + 32 i) --
-  // wave w owns octants 2w, 2w + 1, the ones its fragment reads use; its octant's 8 scales / shifts are loaded
-  // before the tile's opening barrier
-  const int xo = tid >> 5;
+  // BN+ReLU of the staged halo in place (padding stays 0): wave w owns pair plane w -- octants 2w, 2w + 1, the
+  // ones its fragment reads use -- lane l its slots l + 64 j (octant 2w + (l & 1), pixel (l >> 1) + 32 j); the
+  // octant's 8 scales / shifts are loaded before the tile's opening barrier
+  const int xo = 2 * wv + (lane & 1);
   const bool xo_ok = kc * KCW + xo * 8 < a.cin;
   auto load_aff = [&](int n, f32x4* sc) {
     const float* ps = a.isc + (long long)n * a.iss + kc * KCW + xo * 8;
@@ -1034,24 +1029,23 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     if (!xo_ok) return;
     const float scv[8] = {sc[0][0], sc[0][1], sc[0][2], sc[0][3], sc[1][0], sc[1][1], sc[1][2], sc[1][3]};
     const float shv[8] = {sc[2][0], sc[2][1], sc[2][2], sc[2][3], sc[3][0], sc[3][1], sc[3][2], sc[3][3]};
-    char* const plane = S + (xo * DHPXP + wx_shift(xo)) * 16;
-    constexpr int G = 3, NI = (DHPX + 31) / 32;  // 6 pixel rounds in 2 groups of 3
+    char* const plane = S + (wv * DPL + lane) * 16;
+    constexpr int G = 3, NI = (2 * DHPX + 63) / 64;  // 6 slot rounds in 2 groups of 3
     static_assert(NI % G == 0, "bnrelu_x groups");
-    static_assert((7 * DHPXP + 4 + 31 + 32 * (NI - 1) + 1) * 16 <= DSTAGE, "bnrelu_x: group reads stay inside the stage");
+    static_assert((3 * DPL + 63 + 64 * (NI - 1) + 1) * 16 <= DSTAGE, "bnrelu_x: group reads stay inside the stage");
 #pragma unroll 1
     for (int i0 = 0; i0 < NI; i0 += G) {
       u32x4 w[G];
       bool ok[G];
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        const int hp = (tid & 31) + 32 * (i0 + j), hy = hp / DHW, hx = hp - hy * DHW;
+        const int hp = (lane >> 1) + 32 * (i0 + j), hy = hp / DHW, hx = hp - hy * DHW;
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
         ok[j] = (hp < DHPX) & ((uint32_t)yy < (uint32_t)a.H) & ((uint32_t)xx < (uint32_t)a.W);
-        w[j] = *(const u32x4*)(plane + hp * 16);
+        w[j] = *(const u32x4*)(plane + 64 * (i0 + j) * 16);
       }
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        const int hp = (tid & 31) + 32 * (i0 + j);
         u32x4 o;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -1060,7 +1054,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
           const s16x2 b = __builtin_bit_cast(s16x2, pk_bf16(r[0], r[1]));
           o[d] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(b, (s16x2){0, 0}));
         }
-        if (ok[j]) *(u32x4*)(plane + hp * 16) = o;
+        if (ok[j]) *(u32x4*)(plane + 64 * (i0 + j) * 16) = o;
       }
     }
   };
@@ -1118,23 +1112,22 @@ __global__ __launch_bounds__(NTHR, 2) void conv3x3_wgrad_bf16_kernel(WgArgs a) {
     for (int ks = 0; ks < DTH * DTW / 32; ++ks) {
       // k-step ks: tile pixels 32 ks .. 32 ks + 31 = rows 2 ks, 2 ks + 1 (lane groups g = 0, 1 / 2, 3)
       bf16x8 af[4];
-      const int pxa = ks * 32 + 8 * g + q4;
+      const int pxa = ks * 32 + 16 * (g >> 1) + pcol;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         const int uo = (32 * ct) ^ sw16;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + pxa * 128 + uo));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa + 4) * 128 + uo));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + (pxa + 8) * 128 + uo));
         af[ct] = cat_bf16x4(lo, hi);
       }
-      const int oc = 2 * wv + (p4 >> 1);
-      const int hrow = 2 * ks + (g >> 1), hcol = 8 * (g & 1) + q4;
+      const int hrow = 2 * ks + (g >> 1);  // X octants 2 wv + (p4 >> 1): the wave's pair plane
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int ky = t / 3, kx = t - ky * 3;
-        const int hp = (hrow + ky) * DHW + hcol + kx;
-        const char* base = Xs + (oc * DHPXP + wx_shift(oc) + hp) * 16 + (p4 & 1) * 8;
+        const int hp = (hrow + ky) * DHW + pcol + kx;
+        const char* base = Xs + (wv * DPL + 2 * hp + (p4 >> 1)) * 16 + (p4 & 1) * 8;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 4 * 16));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, base + 16 * 16));
         const bf16x8 bfr = cat_bf16x4(lo, hi);
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
