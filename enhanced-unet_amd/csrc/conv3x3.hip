@@ -232,6 +232,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr int E = Vec16<T>::N, KC = KCh<T>::v;
   // this thread's halo quarter (fwd_unit), the same for every unit (ids tid + FT i)
   constexpr bool PIX = ((DG && !BT) || PF) && sizeof(T) == 2;  // halo layout / staging (fslot)
+  // CTE: a bf16 data gradient with a bf16 output (the plain and the BN-reducing ones) accumulates C^T (the MFMA
+  // operands swapped: a lane holds 4 consecutive channels of one pixel) and stages its tile as bf16 in one pass
+  // (not the CT tail instantiation: already at 254 VGPRs, the C^T epilogue spills it)
+  constexpr bool CTE = DG && !BT && !CT && sizeof(T) == 2 && sizeof(TO) == 2;
   const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
   const int ns = __builtin_amdgcn_readfirstlane(n);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -398,7 +402,10 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
           const uint4 fa = *(const uint4*)(As + fslot<PIX>(hp, q) * 16);
 #pragma unroll
           for (int nt = 0; nt < NTC; ++nt) {
-            if constexpr (sizeof(T) == 2) {
+            if constexpr (CTE) {
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16x8, fb[nt]), __builtin_bit_cast(bf16x8, fa), acc[mt][nt], 0, 0, 0);
+            } else if constexpr (sizeof(T) == 2) {
               acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                   __builtin_bit_cast(bf16x8, fa), __builtin_bit_cast(bf16x8, fb[nt]), acc[mt][nt], 0, 0, 0);
             } else {
@@ -509,227 +516,107 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
 #endif
   }
 
-  // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
-  constexpr int NCW = NW, NTH = FT;
-  const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
-  // Bias (and, dgrad only, the Dropout2d scale) in packed fp32; on a partial tile the accumulators of
-  // pixels outside the image are zeroed afterwards (a uniform branch), so the BN sums below need no
-  // per-element masks: the sum over all 128 values of a wave's rows is the sum over its valid ones, and
-  // its M2 about the valid mean is the all-element M2 less (invalid count) x mean^2.  Two packed ops per
-  // pair of values instead of six scalar ops per value (SQ: 5.1 VALU instructions per MFMA on the
-  // 64-channel layers, profiles/r04_sq_layers.txt).
+  // ---- epilogue ----
+  constexpr int NTH = FT;
+  constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
+  static_assert(NTH % UPX == 0, "a thread's channel unit must be fixed across store iterations");
+  constexpr bool bnb = BNB;
+  const int ucol = tid % UPX;
+  f32x2 bp1[E / 2], bp2[E / 2];  // the fused BN-backward reduction's per-thread sums (dgrad)
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int co = co0 + nt * 16 + li;
-    const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
-    const f32x2 b2 = {bv, bv};
-    if constexpr (DG) {
-      const float gv = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
-      const f32x2 g2 = {gv, gv};
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2) * g2;
-        const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2) * g2;
-        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
-      }
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x2 lo = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2;
-        const f32x2 hi = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2;
-        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
-      }
-    }
-  }
-  if (vh < FTH || vw < FTW) {  // partial tile (image edge): zero the pixels outside the image
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt][i] = ok ? acc[mt][nt][i] : 0.f;
-      }
-  }
-  constexpr int PASS_PX = PROWS * FTW;
-  float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
-  float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NCW][64] x 2
-  float* bprm = red + 2 * NCW * 64;                             // [4][64] BN-backward constants
-  static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= FWD_LDS, "epilogue LDS");
-  __syncthreads();  // all waves are done with the K loop's LDS
-  if (a.stats != nullptr) {
-    // per wave: its rows' channel sums and M2 about the wave's own mean, both from the fp32
-    // accumulators (two register passes, lane sums by the permlane swaps); the 4 waves are then
-    // Chan-combined by 64 threads -- one barrier, one LDS round trip
-    const int nw = max(0, min(RPW, vh - RPW * wv)) * vw;  // valid pixels in this wave's rows
-    const float inv_nw = nw > 0 ? 1.f / (float)nw : 0.f;
-    const bool part = vh < FTH || vw < FTW;                 // block-uniform: an edge tile
-    float s1[4], s2[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      f32x2 v = {0.f, 0.f};
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) v += (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){acc[mt][nt][2], acc[mt][nt][3]};
-      s1[nt] = xor32_sum(xor16_sum(v.x + v.y));
-    }
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const float mw = s1[nt] * inv_nw;
-      const f32x2 m2 = {-mw, -mw};
-      f32x2 v = {0.f, 0.f};
-      if (!part) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
-          const f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
-          v = __builtin_elementwise_fma(d0, d0, v);
-          v = __builtin_elementwise_fma(d1, d1, v);
-        }
-      } else {  // the pixels outside the image contribute nothing (no (0 - mw)^2 to cancel afterwards)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const bool rok = RPW * wv + (mt >> 1) < vh;
-          const int c0 = (mt & 1) * 16 + q * 4;
-          f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
-          f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
-          d0.x = rok && c0 + 0 < vw ? d0.x : 0.f;
-          d0.y = rok && c0 + 1 < vw ? d0.y : 0.f;
-          d1.x = rok && c0 + 2 < vw ? d1.x : 0.f;
-          d1.y = rok && c0 + 3 < vw ? d1.y : 0.f;
-          v = __builtin_elementwise_fma(d0, d0, v);
-          v = __builtin_elementwise_fma(d1, d1, v);
-        }
-      }
-      s2[nt] = xor32_sum(xor16_sum(v.x + v.y));
-    }
-    if (q == 0)
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        red[wv * 64 + nt * 16 + li] = s1[nt];
-        red[NCW * 64 + wv * 64 + nt * 16 + li] = s2[nt];
-      }
-    __syncthreads();
-    const float cnt = (float)(vh * vw);
-    if (tid < 64 && co0 + tid < a.cout) {
-      float sum = 0.f, m2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < NCW; ++w) sum += red[w * 64 + tid];
-      const float mean = sum / cnt;
-#pragma unroll
-      for (int w = 0; w < NCW; ++w) {
-        const int nwv = max(0, min(RPW, vh - RPW * w)) * vw;
-        if (nwv > 0) {
-          const float d = red[w * 64 + tid] / (float)nwv - mean;
-          m2 += red[NCW * 64 + w * 64 + tid] + (float)nwv * d * d;
-        }
-      }
-      a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
-      a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
-    }
-    if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
-  }
+  for (int e = 0; e < E / 2; ++e) { bp1[e] = (f32x2){0.f, 0.f}; bp2[e] = (f32x2){0.f, 0.f}; }
 #if CONV_STAMP
   unsigned long long st_ep[6] = {conv_stamp(), 0, 0, 0, 0, 0};
 #endif
-  constexpr int UPX = 64 / E;  // 16-byte units per pixel row of the tile
-  static_assert(NTH % UPX == 0, "a thread's channel unit must be fixed across store iterations");
-  T* yp = (T*)a.y;
-  constexpr bool bnb = BNB;
-  const int ucol = tid % UPX;
-  f32x2 bp1[E / 2], bp2[E / 2];
-  f32x2 km[E / 2], ki[E / 2], ks[E / 2], kh[E / 2];  // BN-backward mean, istd, scale, shift of the unit
+  if constexpr (CTE) {
+    EUNET_DASSERT(a.stats == nullptr);
+    // C^T accumulators: lane (q, li) holds, per (mt, nt), channels co0 + 16 nt + 4 q .. + 3 of the pixel in
+    // m-tile mt, column li.  The tile is staged as bf16 [512 px][CLD] in ONE pass (4 channels = one 8-byte
+    // LDS store: 32 per thread, where the fp32 [px][OUT_LD] staging took 128 4-byte stores in two passes),
+    // then each thread stores 16 whole 16-byte units (and, BNB, reduces them with y).  No forward BN
+    // statistics in a data gradient.
+    constexpr int CLD = 72;  // bf16 per staged pixel row (144 B: 16-byte aligned unit reads)
+    constexpr int SJ1 = FTH * FTW * UPX / NTH;  // 16 units per thread
+    static_assert(FTH * FTW * CLD * 2 + 4 * BN * 4 <= FWD_LDS, "C^T epilogue LDS");
+    static_assert(NTH / UPX == FTW, "unit step j = tile row j");
+    bf16_t* const stgb = (bf16_t*)smem;
+    float* const bprm2 = (float*)(smem + FTH * FTW * CLD * 2);
+    const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
 #pragma unroll
-  for (int e = 0; e < E / 2; ++e) { bp1[e] = (f32x2){0.f, 0.f}; bp2[e] = (f32x2){0.f, 0.f}; }
-  if (bnb && tid < BN) {
-    const bool ok = co0 + tid < a.cout;
-    bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
-    bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
-    bprm[2 * BN + tid] = ok ? a.bsc[co0 + tid] : 0.f;
-    bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
-  }
-  constexpr int SJ = PASS_PX * UPX / NTH;      // output units per thread per pass
-  constexpr int PXJ = NTH / UPX;                // pixels per unit step
-  static_assert(FTW % PXJ == 0, "a unit step covers a fraction of one tile row (row compile-time per step)");
-  const int tu = tid;
-  // output / y addresses: a block-uniform base (the tile's corner) + row x row stride + the thread's
-  // (column, unit) offset, instead of a 64-bit pixel index per unit
-  const long long yrs = (long long)a.W * a.yct;
-  const long long tile_px = (long long)(n * a.H + y0) * a.W + x0;
-  T* const ybase = yp + tile_px * a.yct + a.yco + co0;
-  float* const yfbase = (float*)a.y + tile_px * a.yct + a.yco + co0;
-  const long long brs = (long long)a.W * a.byct;
-  const T* const bybase = BNB ? (const T*)a.by + tile_px * a.byct + a.byco + co0 : nullptr;
-  constexpr bool PRE = sizeof(T) == 2;         // bf16: prefetch the pass's y (BN-backward input)
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 b4, g4;
 #pragma unroll
-  for (int pass = 0; pass < NPASS; ++pass) {
-    // the fused BN-backward reduction reads y at every output unit: issue those loads before the
-    // staging barrier so their latency overlaps it (the stores below would otherwise serialise
-    // each load behind the previous unit's store)
-    uint4 ryb[PRE ? SJ : 1];
-    if constexpr (PRE) {
-      if (bnb) {
+      for (int i = 0; i < 4; ++i) {
+        const int co = co0 + nt * 16 + 4 * q + i;
+        b4[i] = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
+        g4[i] = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
+      }
 #pragma unroll
-        for (int j = 0; j < SJ; ++j) {
-          const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
-          const int co = co0 + u * E;
-          ryb[j] = make_uint4(0, 0, 0, 0);
-          if (r < vh && c < vw && co < a.cout)
-            ryb[j] = *(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E));
-        }
+      for (int mt = 0; mt < MT; ++mt) {
+        const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){b4[0], b4[1]}) * (f32x2){g4[0], g4[1]};
+        const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + (f32x2){b4[2], b4[3]}) * (f32x2){g4[2], g4[3]};
+        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
       }
     }
-    if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
+    // (pixels outside the image are staged but never stored or reduced: no masking of the accumulators)
+    const long long yrs = (long long)a.W * a.yct;
+    const long long tile_px = (long long)(n * a.H + y0) * a.W + x0;
+    T* const ybase = (T*)a.y + tile_px * a.yct + a.yco + co0;
+    const long long brs = (long long)a.W * a.byct;
+    const T* const bybase = BNB ? (const T*)a.by + tile_px * a.byct + a.byco + co0 : nullptr;
+    const int c = tid / UPX, cu = co0 + ucol * E;
+    uint4 ryb[BNB ? SJ1 : 1];
+    auto load_y = [&](int j0, int j1) {  // y of this thread's units j0..j1-1 (BN-backward input)
+      if constexpr (BNB) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int px = (RPW * wv - pass * PROWS + (mt >> 1)) * FTW + (mt & 1) * 16 + q * 4 + i;
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) stg[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
+        for (int j = j0; j < j1; ++j) {
+          ryb[j] = make_uint4(0, 0, 0, 0);
+          if (j < vh && c < vw && cu < a.cout) ryb[j] = *(const uint4*)(bybase + (long long)j * brs + (c * a.byct + ucol * E));
         }
+      }
+    };
+    load_y(0, SJ1 / 2);  // (the accumulators are still live: half now, half after they are staged)
+    __syncthreads();  // all waves are done with the K loop's LDS
+    if (bnb && tid < BN) {
+      const bool ok = co0 + tid < a.cout;
+      bprm2[tid] = ok ? a.bmean[co0 + tid] : 0.f;
+      bprm2[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
+      bprm2[2 * BN + tid] = ok ? a.bsc[co0 + tid] : 0.f;
+      bprm2[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
     }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int px = (RPW * wv + (mt >> 1)) * FTW + (mt & 1) * 16 + li;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        *(uint2*)(stgb + px * CLD + nt * 16 + 4 * q) =
+            make_uint2(pk_bf16(acc[mt][nt][0], acc[mt][nt][1]), pk_bf16(acc[mt][nt][2], acc[mt][nt][3]));
+    }
+    load_y(SJ1 / 2, SJ1);
     __syncthreads();
-#if CONV_STAMP
-    st_ep[1 + 2 * pass] = conv_stamp();
-#endif
-    if (BNB && pass == 0) {  // this thread's channel unit is fixed: its BN-backward constants into registers
+    f32x2 km[E / 2], ki[E / 2], ks[E / 2], kh[E / 2];  // BN-backward mean, istd, scale, shift of the unit
+    if constexpr (BNB) {
 #pragma unroll
       for (int e = 0; e < E / 2; ++e) {
         const int cc = ucol * E + 2 * e;
-        km[e] = *(const f32x2*)(bprm + cc);
-        ki[e] = *(const f32x2*)(bprm + BN + cc);
-        ks[e] = *(const f32x2*)(bprm + 2 * BN + cc);
-        kh[e] = *(const f32x2*)(bprm + 3 * BN + cc);
+        km[e] = *(const f32x2*)(bprm2 + cc);
+        ki[e] = *(const f32x2*)(bprm2 + BN + cc);
+        ks[e] = *(const f32x2*)(bprm2 + 2 * BN + cc);
+        kh[e] = *(const f32x2*)(bprm2 + 3 * BN + cc);
       }
     }
 #pragma unroll
-    for (int j = 0; j < SJ; ++j) {
-      // unit tid + j NTH = (pixel px, channel unit u): u = tid mod UPX, px = tid / UPX + PXJ j, and since
-      // PXJ divides FTW the row of px is compile-time per (pass, j)
-      const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
-      const int px = (r - pass * PROWS) * FTW + c;
-      const int co = co0 + u * E;
-      if (r < vh && c < vw && co < a.cout) {
-        const float* sp = stg + px * OUT_LD + u * E;
-        float f[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) f[e] = sp[e];
-        const long long off = (long long)r * yrs + (c * a.yct + u * E);
-        EUNET_DASSERT(tile_px + (long long)r * a.W + c < (long long)a.N * a.H * a.W && co + E <= a.cout &&
-                      a.yco + co + E <= a.yct);
-        const uint4 packed = Vec16<T>::pack(f);
-        if constexpr (sizeof(TO) == sizeof(T)) {  // (non-temporal: the output is read back after it left L2)
-          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(ybase + off));
-        } else {  // fp32 output of a bf16 kernel: E = 8 floats, two 16-byte stores
-          float* yo = yfbase + off;
-          *(float4*)yo = make_float4(f[0], f[1], f[2], f[3]);
-          *(float4*)(yo + 4) = make_float4(f[4], f[5], f[6], f[7]);
-        }
+    for (int j = 0; j < SJ1; ++j) {  // unit (pixel row j, column c, channel unit ucol)
+      if (j < vh && c < vw && cu < a.cout) {
+        const uint4 packed = *(const uint4*)(stgb + (j * FTW + c) * CLD + ucol * E);
+        const long long off = (long long)j * yrs + (c * a.yct + ucol * E);
+        EUNET_DASSERT(tile_px + (long long)j * a.W + c < (long long)a.N * a.H * a.W && cu + E <= a.cout &&
+                      a.yco + cu + E <= a.yct);
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(ybase + off));
         if constexpr (BNB) {
           float gr[E], yv[E];
           Vec16<T>::unpack(packed, gr);
-          if constexpr (PRE) Vec16<T>::unpack(ryb[j], yv);
-          else Vec16<T>::unpack(*(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E)), yv);
+          Vec16<T>::unpack(ryb[j], yv);
 #pragma unroll
           for (int e = 0; e < E; e += 2) {  // packed fp32: each element rounded as the scalar ops round it
             const f32x2 y2 = {yv[e], yv[e + 1]};
@@ -742,10 +629,238 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
         }
       }
     }
-#if CONV_STAMP
-    st_ep[2 + 2 * pass] = conv_stamp();
-#endif
-    if (pass + 1 < NPASS) __syncthreads();
+  } else {
+    // ---- epilogue: bias, BN partials, LDS-staged vector stores (NPASS row bands) ----
+    constexpr int NCW = NW;
+    const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
+    // Bias (and, dgrad only, the Dropout2d scale) in packed fp32; on a partial tile the accumulators of
+    // pixels outside the image are zeroed afterwards (a uniform branch), so the BN sums below need no
+    // per-element masks: the sum over all 128 values of a wave's rows is the sum over its valid ones, and
+    // its M2 about the valid mean is the all-element M2 less (invalid count) x mean^2.  Two packed ops per
+    // pair of values instead of six scalar ops per value (SQ: 5.1 VALU instructions per MFMA on the
+    // 64-channel layers, profiles/r04_sq_layers.txt).
+  #pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int co = co0 + nt * 16 + li;
+      const float bv = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
+      const f32x2 b2 = {bv, bv};
+      if constexpr (DG) {
+        const float gv = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
+        const f32x2 g2 = {gv, gv};
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2) * g2;
+          const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2) * g2;
+          acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+        }
+      } else {
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x2 lo = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + b2;
+          const f32x2 hi = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + b2;
+          acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+        }
+      }
+    }
+    if (vh < FTH || vw < FTW) {  // partial tile (image edge): zero the pixels outside the image
+  #pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = RPW * wv + (mt >> 1) < vh && (mt & 1) * 16 + q * 4 + i < vw;
+  #pragma unroll
+          for (int nt = 0; nt < 4; ++nt) acc[mt][nt][i] = ok ? acc[mt][nt][i] : 0.f;
+        }
+    }
+    constexpr int PASS_PX = PROWS * FTW;
+    float* stg = (float*)smem;                                    // [PASS_PX][OUT_LD]
+    float* red = (float*)(smem + PASS_PX * OUT_LD * 4);           // [NCW][64] x 2
+    float* bprm = red + 2 * NCW * 64;                             // [4][64] BN-backward constants
+    static_assert(PASS_PX * OUT_LD * 4 + (2 * NCW + 4) * 64 * 4 <= FWD_LDS, "epilogue LDS");
+    __syncthreads();  // all waves are done with the K loop's LDS
+    if (a.stats != nullptr) {
+      // per wave: its rows' channel sums and M2 about the wave's own mean, both from the fp32
+      // accumulators (two register passes, lane sums by the permlane swaps); the 4 waves are then
+      // Chan-combined by 64 threads -- one barrier, one LDS round trip
+      const int nw = max(0, min(RPW, vh - RPW * wv)) * vw;  // valid pixels in this wave's rows
+      const float inv_nw = nw > 0 ? 1.f / (float)nw : 0.f;
+      const bool part = vh < FTH || vw < FTW;                 // block-uniform: an edge tile
+      float s1[4], s2[4];
+  #pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x2 v = {0.f, 0.f};
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt) v += (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){acc[mt][nt][2], acc[mt][nt][3]};
+        s1[nt] = xor32_sum(xor16_sum(v.x + v.y));
+      }
+  #pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float mw = s1[nt] * inv_nw;
+        const f32x2 m2 = {-mw, -mw};
+        f32x2 v = {0.f, 0.f};
+        if (!part) {
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
+            const f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
+            v = __builtin_elementwise_fma(d0, d0, v);
+            v = __builtin_elementwise_fma(d1, d1, v);
+          }
+        } else {  // the pixels outside the image contribute nothing (no (0 - mw)^2 to cancel afterwards)
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bool rok = RPW * wv + (mt >> 1) < vh;
+            const int c0 = (mt & 1) * 16 + q * 4;
+            f32x2 d0 = (f32x2){acc[mt][nt][0], acc[mt][nt][1]} + m2;
+            f32x2 d1 = (f32x2){acc[mt][nt][2], acc[mt][nt][3]} + m2;
+            d0.x = rok && c0 + 0 < vw ? d0.x : 0.f;
+            d0.y = rok && c0 + 1 < vw ? d0.y : 0.f;
+            d1.x = rok && c0 + 2 < vw ? d1.x : 0.f;
+            d1.y = rok && c0 + 3 < vw ? d1.y : 0.f;
+            v = __builtin_elementwise_fma(d0, d0, v);
+            v = __builtin_elementwise_fma(d1, d1, v);
+          }
+        }
+        s2[nt] = xor32_sum(xor16_sum(v.x + v.y));
+      }
+      if (q == 0)
+  #pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          red[wv * 64 + nt * 16 + li] = s1[nt];
+          red[NCW * 64 + wv * 64 + nt * 16 + li] = s2[nt];
+        }
+      __syncthreads();
+      const float cnt = (float)(vh * vw);
+      if (tid < 64 && co0 + tid < a.cout) {
+        float sum = 0.f, m2 = 0.f;
+  #pragma unroll
+        for (int w = 0; w < NCW; ++w) sum += red[w * 64 + tid];
+        const float mean = sum / cnt;
+  #pragma unroll
+        for (int w = 0; w < NCW; ++w) {
+          const int nwv = max(0, min(RPW, vh - RPW * w)) * vw;
+          if (nwv > 0) {
+            const float d = red[w * 64 + tid] / (float)nwv - mean;
+            m2 += red[NCW * 64 + w * 64 + tid] + (float)nwv * d * d;
+          }
+        }
+        a.stats[((long long)tile * 2 + 0) * a.cout + co0 + tid] = sum;
+        a.stats[((long long)tile * 2 + 1) * a.cout + co0 + tid] = m2;
+      }
+      if (cob == 0 && tid == 0) a.stats[(long long)2 * a.cout * a.ntiles + tile] = cnt;
+    }
+  #if CONV_STAMP
+    st_ep[0] = conv_stamp();
+  #endif
+    T* yp = (T*)a.y;
+    f32x2 km[E / 2], ki[E / 2], ks[E / 2], kh[E / 2];  // BN-backward mean, istd, scale, shift of the unit
+    if (bnb && tid < BN) {
+      const bool ok = co0 + tid < a.cout;
+      bprm[tid] = ok ? a.bmean[co0 + tid] : 0.f;
+      bprm[BN + tid] = ok ? a.bistd[co0 + tid] : 0.f;
+      bprm[2 * BN + tid] = ok ? a.bsc[co0 + tid] : 0.f;
+      bprm[3 * BN + tid] = ok ? a.bsh[co0 + tid] : 0.f;
+    }
+    constexpr int SJ = PASS_PX * UPX / NTH;      // output units per thread per pass
+    constexpr int PXJ = NTH / UPX;                // pixels per unit step
+    static_assert(FTW % PXJ == 0, "a unit step covers a fraction of one tile row (row compile-time per step)");
+    const int tu = tid;
+    // output / y addresses: a block-uniform base (the tile's corner) + row x row stride + the thread's
+    // (column, unit) offset, instead of a 64-bit pixel index per unit
+    const long long yrs = (long long)a.W * a.yct;
+    const long long tile_px = (long long)(n * a.H + y0) * a.W + x0;
+    T* const ybase = yp + tile_px * a.yct + a.yco + co0;
+    float* const yfbase = (float*)a.y + tile_px * a.yct + a.yco + co0;
+    const long long brs = (long long)a.W * a.byct;
+    const T* const bybase = BNB ? (const T*)a.by + tile_px * a.byct + a.byco + co0 : nullptr;
+    constexpr bool PRE = sizeof(T) == 2;         // bf16: prefetch the pass's y (BN-backward input)
+  #pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+      // the fused BN-backward reduction reads y at every output unit: issue those loads before the
+      // staging barrier so their latency overlaps it (the stores below would otherwise serialise
+      // each load behind the previous unit's store)
+      uint4 ryb[PRE ? SJ : 1];
+      if constexpr (PRE) {
+        if (bnb) {
+  #pragma unroll
+          for (int j = 0; j < SJ; ++j) {
+            const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
+            const int co = co0 + u * E;
+            ryb[j] = make_uint4(0, 0, 0, 0);
+            if (r < vh && c < vw && co < a.cout)
+              ryb[j] = *(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E));
+          }
+        }
+      }
+      if (RPW * wv >= pass * PROWS && RPW * wv < (pass + 1) * PROWS) {
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int px = (RPW * wv - pass * PROWS + (mt >> 1)) * FTW + (mt & 1) * 16 + q * 4 + i;
+  #pragma unroll
+            for (int nt = 0; nt < 4; ++nt) stg[px * OUT_LD + nt * 16 + li] = acc[mt][nt][i];
+          }
+      }
+      __syncthreads();
+  #if CONV_STAMP
+      st_ep[1 + 2 * pass] = conv_stamp();
+  #endif
+      if (BNB && pass == 0) {  // this thread's channel unit is fixed: its BN-backward constants into registers
+  #pragma unroll
+        for (int e = 0; e < E / 2; ++e) {
+          const int cc = ucol * E + 2 * e;
+          km[e] = *(const f32x2*)(bprm + cc);
+          ki[e] = *(const f32x2*)(bprm + BN + cc);
+          ks[e] = *(const f32x2*)(bprm + 2 * BN + cc);
+          kh[e] = *(const f32x2*)(bprm + 3 * BN + cc);
+        }
+      }
+  #pragma unroll
+      for (int j = 0; j < SJ; ++j) {
+        // unit tid + j NTH = (pixel px, channel unit u): u = tid mod UPX, px = tid / UPX + PXJ j, and since
+        // PXJ divides FTW the row of px is compile-time per (pass, j)
+        const int r = pass * PROWS + (PXJ * j) / FTW, c = tu / UPX + (PXJ * j) % FTW, u = ucol;
+        const int px = (r - pass * PROWS) * FTW + c;
+        const int co = co0 + u * E;
+        if (r < vh && c < vw && co < a.cout) {
+          const float* sp = stg + px * OUT_LD + u * E;
+          float f[E];
+  #pragma unroll
+          for (int e = 0; e < E; ++e) f[e] = sp[e];
+          const long long off = (long long)r * yrs + (c * a.yct + u * E);
+          EUNET_DASSERT(tile_px + (long long)r * a.W + c < (long long)a.N * a.H * a.W && co + E <= a.cout &&
+                        a.yco + co + E <= a.yct);
+          const uint4 packed = Vec16<T>::pack(f);
+          if constexpr (sizeof(TO) == sizeof(T)) {  // (non-temporal: the output is read back after it left L2)
+            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, packed), (u32x4*)(ybase + off));
+          } else {  // fp32 output of a bf16 kernel: E = 8 floats, two 16-byte stores
+            float* yo = yfbase + off;
+            *(float4*)yo = make_float4(f[0], f[1], f[2], f[3]);
+            *(float4*)(yo + 4) = make_float4(f[4], f[5], f[6], f[7]);
+          }
+          if constexpr (BNB) {
+            float gr[E], yv[E];
+            Vec16<T>::unpack(packed, gr);
+            if constexpr (PRE) Vec16<T>::unpack(ryb[j], yv);
+            else Vec16<T>::unpack(*(const uint4*)(bybase + (long long)r * brs + (c * a.byct + u * E)), yv);
+  #pragma unroll
+            for (int e = 0; e < E; e += 2) {  // packed fp32: each element rounded as the scalar ops round it
+              const f32x2 y2 = {yv[e], yv[e + 1]};
+              const f32x2 xh = (y2 - km[e >> 1]) * ki[e >> 1];
+              const f32x2 pre = __builtin_elementwise_fma(y2, ks[e >> 1], kh[e >> 1]);
+              const f32x2 gp = {pre.x > 0.f ? gr[e] : 0.f, pre.y > 0.f ? gr[e + 1] : 0.f};
+              bp1[e >> 1] += gp;
+              bp2[e >> 1] = __builtin_elementwise_fma(gp, xh, bp2[e >> 1]);
+            }
+          }
+        }
+      }
+  #if CONV_STAMP
+      st_ep[2 + 2 * pass] = conv_stamp();
+  #endif
+      if (pass + 1 < NPASS) __syncthreads();
+    }
   }
   if (bnb) {  // fixed-order reduction of the per-thread channel sums: the lanes of a wave that share a
              // channel unit (lane = ucol mod UPX) by DPP / permlane xor sums, then the 4 waves through LDS
