@@ -234,7 +234,9 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
   constexpr bool PIX = ((DG && !BT) || PF) && sizeof(T) == 2;  // halo layout / staging (fslot)
   // CTE: a bf16 data gradient with a bf16 output (the plain and the BN-reducing ones) accumulates C^T (the MFMA
   // operands swapped: a lane holds 4 consecutive channels of one pixel) and stages its tile as bf16 in one pass
-  // (not the CT tail instantiation: already at 254 VGPRs, the C^T epilogue spills it)
+  // (not the CT tail instantiation: already at 254 VGPRs, the C^T epilogue spills it).  The forwards keep the C
+  // layout: with C^T and their BN partials summed by DPP over a lane row the 13 standalone forwards measured
+  // 0.6 % faster but the step 0.9 % slower in three alternating pairs (profiles/r06_ab.txt r6n / r6p; code in git)
   constexpr bool CTE = DG && !BT && !CT && sizeof(T) == 2 && sizeof(TO) == 2;
   const int sq = PIX ? tid & 3 : (tid >> 3) & 3;
   const int ns = __builtin_amdgcn_readfirstlane(n);
