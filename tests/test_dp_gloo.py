@@ -1,4 +1,4 @@
-"""Data-parallel path on CPU: world_size 2 over gloo (SURVEY.md §8e DP oracle).
+"""Data-parallel path on CPU: world sizes 2 and 4 over gloo (SURVEY.md §8e DP oracle).
 
 Each rank computes its shard's gradients with the oracle (the HIP engine needs
 a GPU) and feeds them to eunet.dp's BucketSink exactly as the engine does
@@ -81,11 +81,13 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_dp_world2_gloo_bucketed_allreduce():
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_world2_gloo_bucketed_allreduce(world):
+    """(world 4 rehearses the ring over more ranks than the GPU tests can place on one card with RCCL)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
