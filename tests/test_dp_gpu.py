@@ -272,8 +272,10 @@ def _trainer_worker(rank, world, port, q, cfg):
             gs = [torch.zeros_like(t) for t in (params, pre, post) for _ in range(world)]
             for i, t in enumerate((params, pre, post)):
                 dist.all_gather(gs[i * world:(i + 1) * world], t)
-            rec = dict(loss=loss, params_equal=torch.equal(gs[0], gs[1]), pre_differ=not torch.equal(gs[2], gs[3]),
-                       post_equal=torch.equal(gs[4], gs[5]))
+            P, B0, B1 = gs[:world], gs[world:2 * world], gs[2 * world:]
+            rec = dict(loss=loss, params_equal=all(torch.equal(P[0], t) for t in P[1:]),
+                       pre_differ=not all(torch.equal(B0[0], t) for t in B0[1:]),
+                       post_equal=all(torch.equal(B1[0], t) for t in B1[1:]))
             if cfg == "fp32" and step == 0:
                 pins = _pins.model_pins(mod)
                 # numpy arrays travel through the queue by value (torch CPU tensors would be shared through
@@ -287,7 +289,7 @@ def _trainer_worker(rank, world, port, q, cfg):
                     orec = {} if odt == torch.float64 else None
                     R.batch_loss(R.forward(S, x.cpu().to(odt), True, pins=pins, record=orec), m.cpu()).backward()
                     if orec is not None:  # every disputed branch within rounding of its kink / tie
-                        rec["pin_audit"] = _pins.audit(pins, orec, "fp32", label=f"world-2 rank {rank}")
+                        rec["pin_audit"] = _pins.audit(pins, orec, "fp32", label=f"world-{world} rank {rank}")
                     rec[key] = {k: S[k].grad.double().numpy() for k in rec["grads"]}
             out["steps"].append(rec)
         q.put(out)
@@ -298,11 +300,11 @@ def _trainer_worker(rank, world, port, q, cfg):
         dist.destroy_process_group()
 
 
-def _run_world2(cfg):
+def _run_world2(cfg, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, q, cfg)) for r in range(2)]
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q, cfg)) for r in range(world)]
     for p in procs:
         p.start()
     res = []
@@ -342,22 +344,25 @@ def test_dp_world2_trainer_steps_keep_replicas_identical(cfg):
 
 
 @pytest.mark.timeout(600)
-def test_dp_world2_step_is_mean_of_shards_oracle():
-    """fp32 world-2 step (base 16, 64^2, B 2 per rank): the all-reduced, clipped gradients every rank
-    applies equal the oracle's mean over the two shards of each shard's branch-pinned gradient (its
-    own BatchNorm statistics, as per-replica BN under DDP), clipped to total norm 1.0
-    (train_eval.py:341), within max(1e-3, 3x the fp32 oracle's error) relative L2 per tensor."""
-    res = _run_world2("fp32")
-    s0, s1 = res[0]["steps"][0], res[1]["steps"][0]
-    for s in (s0, s1):
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_world2_step_is_mean_of_shards_oracle(world):
+    """fp32 step at world size 2 and 4 (base 16, 64^2, B 2 per rank; all ranks share the one GPU, gloo
+    carries the collectives): the all-reduced, clipped gradients every rank applies equal the oracle's
+    mean over the shards of each shard's branch-pinned gradient (its own BatchNorm statistics, as
+    per-replica BN under DDP), clipped to total norm 1.0 (train_eval.py:341), within max(1e-3, 3x the
+    fp32 oracle's error) relative L2 per tensor."""
+    res = _run_world2("fp32", world)
+    st = [r["steps"][0] for r in res]
+    s0 = st[0]
+    for s in st:
         assert s["params_equal"] and s["post_equal"]
 
-    for s in (s0, s1):
+    for s in st:
         for key in ("grads", "oracle64", "oracle32"):
             s[key] = {k: torch.from_numpy(v) for k, v in s[key].items()}
 
     def mean_clipped(key):
-        g = {k: 0.5 * (s0[key][k] + s1[key][k]) for k in s0[key]}
+        g = {k: sum(s[key][k] for s in st) / world for k in s0[key]}
         norm = float(torch.sqrt(sum((v ** 2).sum() for v in g.values())))
         c = min(1.0, 1.0 / (norm + 1e-6))
         return {k: v * c for k, v in g.items()}
@@ -366,7 +371,7 @@ def test_dp_world2_step_is_mean_of_shards_oracle():
     scale = max(float(v.abs().max()) for v in ref.values())
     rows = []
     for k, g in s0["grads"].items():
-        assert torch.equal(g, s1["grads"][k]), k
+        assert all(torch.equal(g, s["grads"][k]) for s in st[1:]), k
         if k.endswith((".0.bias", ".3.bias")) and not k.startswith("enhance.3"):
             assert float((g - ref[k]).abs().max()) < 1e-4 * scale, k
             continue
@@ -374,5 +379,5 @@ def test_dp_world2_step_is_mean_of_shards_oracle():
         tol = max(1e-3, 3 * float((ref32[k] - ref[k]).norm() / ref[k].norm().clamp_min(1e-30)))
         rows.append((err / tol, k, err, tol))
     for r in sorted(rows, reverse=True)[:4]:
-        print("world-2 mean-of-shards grad (ratio, name, err, tol):", r)
+        print(f"world-{world} mean-of-shards grad (ratio, name, err, tol):", r)
     assert all(r[0] < 1.0 for r in rows), sorted(rows, reverse=True)[:3]
