@@ -544,20 +544,22 @@ __global__ __launch_bounds__(FT, 2) void conv3x3_fwd_kernel(FwdArgs a) {
     bf16_t* const stgb = (bf16_t*)smem;
     float* const bprm2 = (float*)(smem + FTH * FTW * CLD * 2);
     const int vh = min(FTH, a.H - y0), vw = min(FTW, a.W - x0);
+    if (a.bias != nullptr || a.gsc != nullptr) {  // (uniform: most data gradients have neither)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      f32x4 b4, g4;
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4 b4, g4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = co0 + nt * 16 + 4 * q + i;
-        b4[i] = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
-        g4[i] = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
-      }
+        for (int i = 0; i < 4; ++i) {
+          const int co = co0 + nt * 16 + 4 * q + i;
+          b4[i] = (a.bias != nullptr && co < a.cout) ? a.bias[co] : 0.f;
+          g4[i] = (a.gsc != nullptr && co < a.cout) ? a.gsc[(long long)n * a.cout + co] : 1.f;
+        }
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){b4[0], b4[1]}) * (f32x2){g4[0], g4[1]};
-        const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + (f32x2){b4[2], b4[3]}) * (f32x2){g4[2], g4[3]};
-        acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+        for (int mt = 0; mt < MT; ++mt) {
+          const f32x2 lo = ((f32x2){acc[mt][nt][0], acc[mt][nt][1]} + (f32x2){b4[0], b4[1]}) * (f32x2){g4[0], g4[1]};
+          const f32x2 hi = ((f32x2){acc[mt][nt][2], acc[mt][nt][3]} + (f32x2){b4[2], b4[3]}) * (f32x2){g4[2], g4[3]};
+          acc[mt][nt] = (f32x4){lo.x, lo.y, hi.x, hi.y};
+        }
       }
     }
     // (pixels outside the image are staged but never stored or reduced: no masking of the accumulators)
